@@ -1,0 +1,93 @@
+// C ABI of libadvdiff: hand-written gfx950 (CDNA4) HIP stencil kernels.
+//
+// Every entry point enqueues work on the given HIP stream (nullptr = legacy default
+// stream), never synchronises, never allocates, and returns a hipError_t value
+// (0 = success) so it can be captured into a hipGraph and called from Python
+// (ctypes) or from the native C++ apps alike.
+//
+// Array layout (all kernels): x fastest.  Element (i, j, k) lives at
+//     k*sz + j*sy + i
+// where sy >= nx is the row pitch and sz >= ny*sy the plane pitch (elements).
+// 2-D arrays use (i, j) -> j*sy + i.
+//
+// dtype codes: 0 = float32, 1 = float64.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum advdiff_dtype { ADVDIFF_F32 = 0, ADVDIFF_F64 = 1 };
+
+// ---------------------------------------------------------------------------------
+// Heat equation u_t = K ∇²u : ONE fused SSP-RK3 stage
+//     out = a*u0 + b*(in + dt*L(in)),   L = FD4 (13-pt) or FD2 (7-pt) Laplacian
+// on cells i in [border, nx-border), j in [border, ny-border), k in [k0, k1).
+// cx = K/dx², cy = K/dy², cz = K/dz²  (the kernel applies the 1/12 of FD4).
+// Reads planes k0-R .. k1-1+R of `in` (R = order/2), which must be allocated.
+// a == 0 skips reading u0 (stage 1). `out` may alias `u0` (in-place stage 3),
+// never `in`.
+int advdiff_diffusion3d_stage(int dtype, const void* in, const void* u0, void* out,
+                              int nx, int ny, int64_t sy, int64_t sz, int k0, int k1,
+                              int border, int order, double cx, double cy, double cz,
+                              double dt, double a, double b, void* stream);
+
+// 2-D heat stage, rows j in [j0, j1), columns i in [border, nx-border).
+int advdiff_diffusion2d_stage(int dtype, const void* in, const void* u0, void* out,
+                              int nx, int64_t sy, int j0, int j1, int border, int order,
+                              double cx, double cy, double dt, double a, double b,
+                              void* stream);
+
+// ---------------------------------------------------------------------------------
+// Burgers u_t + Σ_d ∂_d(u²/2) = C ∇²u : ONE fused SSP-RK3 stage
+//     L(u) = -Σ_d (F_{+½} - F_{-½}) * rd_d  +  C ∇²u (FD4)
+// WENO5 (JS when weno_z == 0, Z otherwise) with local Lax-Friedrichs splitting.
+// rdx = 1/dx ...; vx = C/dx² ... (all zero = inviscid, the viscous path is not
+// compiled in).  Reads planes k0-3 .. k1+2.
+int advdiff_burgers3d_stage(int dtype, const void* in, const void* u0, void* out,
+                            int nx, int ny, int64_t sy, int64_t sz, int k0, int k1,
+                            int border, int weno_z, double rdx, double rdy, double rdz,
+                            double vx, double vy, double vz, double dt, double a,
+                            double b, void* stream);
+
+int advdiff_burgers2d_stage(int dtype, const void* in, const void* u0, void* out,
+                            int nx, int64_t sy, int j0, int j1, int border, int weno_z,
+                            double rdx, double rdy, double vx, double vy, double dt,
+                            double a, double b, void* stream);
+
+// ---------------------------------------------------------------------------------
+// Reductions over the box [i0,i1)x[j0,j1)x[k0,k1):
+//     result[0] = Σ|x - y|, result[1] = Σ(x - y)², result[2] = max|x - y|
+// (y == nullptr means y = 0, i.e. norms / max|u| of x).  `result` is a DEVICE
+// pointer to 3 doubles.  `workspace` must hold advdiff_reduce_workspace_bytes().
+size_t advdiff_reduce_workspace_bytes(void);
+int advdiff_reduce_norms(int dtype, const void* x, const void* y, int64_t sy, int64_t sz,
+                         int i0, int i1, int j0, int j1, int k0, int k1, void* workspace,
+                         double* result, void* stream);
+
+// ---------------------------------------------------------------------------------
+// Device-side initial conditions (no host staging, each rank builds its own slab).
+// ic codes (see multigpu_advectiondiffusion_amd/utils/ics.py for the formulas):
+//   0 zero, 1 square jump, 2 sine (zero faces), 3 heat kernel (zero faces),
+//   4 Burgers Gaussian, 5 hot plates, 6 disc (2-D)
+// The array holds global planes kg0 .. kg0+nzl-1; in 2-D (NZ <= 1) it holds the
+// global rows kg0 .. kg0+ny-1 (nzl = 1).
+// p0, p1: IC parameters (heat kernel: d, t0; Gaussian: width; others ignored).
+int advdiff_init_ic(int dtype, int ic, void* u, int nx, int ny, int nzl, int64_t sy,
+                    int64_t sz, int kg0, int NX, int NY, int NZ, double dx, double dy,
+                    double dz, double p0, double p1, void* stream);
+
+// Copy planes (contiguous z-slabs) — a strided 3-D copy for halo staging and
+// x/y-face pack/unpack of a Cartesian decomposition:
+//   dst[(k)*dsz + j*dsy + i] = src[(k)*ssz + j*ssy + i], (i,j,k) in [0,ni)x[0,nj)x[0,nk)
+int advdiff_copy_box(int dtype, void* dst, int64_t dsy, int64_t dsz, const void* src,
+                     int64_t ssy, int64_t ssz, int ni, int nj, int nk, void* stream);
+
+// Library identification (build flags, arch) for diagnostics.
+const char* advdiff_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif

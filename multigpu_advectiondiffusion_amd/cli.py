@@ -1,0 +1,179 @@
+"""Command-line front end with the reference's positional argument layouts.
+
+Reference CLIs:
+
+    diffusion2d  C|K L W Nx Ny iters [bx by]            (SingleGPU/Diffusion2d/main.cpp:32-47,
+                                                         MultiGPU/Diffusion2d_Baseline/main.c:36-51)
+    diffusion3d  C|K L W H Nx Ny Nz iters [bx by bz]    (SingleGPU/Diffusion3d_*/main.cpp:32-50,
+                                                         MultiGPU/Diffusion3d_Baseline/main.c:36-54)
+    burgers2d    tEnd CFL L W Nx Ny [bx by]             (MultiGPU/Burgers2d_Baseline/main.c:36-51)
+    burgers3d    tEnd CFL L W H Nx Ny Nz [bx by bz]     (SingleGPU/Burgers3d_WENO5/main.cpp:32-50,
+                                                         MultiGPU/Burgers3d_Baseline/main.c:36-54)
+
+Block sizes are accepted for compatibility and ignored (the gfx950 tiles are fixed:
+64-wide wave rows).  Everything the reference hard-codes at compile time is a runtime
+flag here: --ic, --order, --weno, --viscosity, --dtype, --overlap,
+--write, --checkpoint/--restart, --config (JSON/TOML/YAML file of the same keys).
+
+Multi-GPU: run under torchrun (one process per GPU), e.g.
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        -m multigpu_advectiondiffusion_amd diffusion3d 1 2 2 2 1024 1024 1024 100
+or with the bundled launcher:  python -m multigpu_advectiondiffusion_amd.launch -np 8 diffusion3d ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+APPS = {
+    "diffusion2d": ["K", "L", "W", "Nx", "Ny", "iters"],
+    "diffusion3d": ["K", "L", "W", "H", "Nx", "Ny", "Nz", "iters"],
+    "burgers2d": ["tEnd", "CFL", "L", "W", "Nx", "Ny"],
+    "burgers3d": ["tEnd", "CFL", "L", "W", "H", "Nx", "Ny", "Nz"],
+}
+_INT = {"Nx", "Ny", "Nz", "iters"}
+
+
+def _load_config(path):
+    p = Path(path)
+    text = p.read_text()
+    if p.suffix in (".toml",):
+        try:
+            import tomllib
+        except ImportError:  # py3.10
+            import tomli as tomllib
+        return tomllib.loads(text)
+    if p.suffix in (".yaml", ".yml"):
+        import yaml
+        return yaml.safe_load(text)
+    return json.loads(text)
+
+
+def build_parser():
+    ap = argparse.ArgumentParser(prog="multigpu_advectiondiffusion_amd",
+                                 description="MI355X-native advection-diffusion stencil solvers")
+    ap.add_argument("app", choices=sorted(APPS))
+    ap.add_argument("args", nargs="*", help="reference positional arguments (see module doc)")
+    ap.add_argument("--config", help="JSON/TOML/YAML file with any of the named options")
+    ap.add_argument("--ic", help="initial condition: zero|square|sine|heat|gaussian|plates|disc")
+    ap.add_argument("--order", type=int, default=4, help="diffusion FD order: 4 (13-pt) or 2 (7-pt)")
+    ap.add_argument("--safety", type=float, default=0.9, help="diffusion dt safety factor (MG used 0.8)")
+    ap.add_argument("--weno", choices=["js", "z"], default="z")
+    ap.add_argument("--viscosity", type=float, default=1e-5, help="Burgers C (0 = inviscid)")
+    ap.add_argument("--cfl-mode", choices=["fixed", "adaptive"], default="fixed")
+    ap.add_argument("--dtype", choices=["fp64", "fp32"], default="fp64")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default=None)
+    ap.add_argument("--no-overlap", action="store_true", help="disable halo/compute overlap")
+    ap.add_argument("--write", default=None, help="write float32 result.bin to this path")
+    ap.add_argument("--initial", default=None, help="write float32 initial.bin to this path")
+    ap.add_argument("--checkpoint", default=None, help="write fp64 checkpoint shards to PREFIX")
+    ap.add_argument("--restart", default=None, help="restart from checkpoint PREFIX")
+    ap.add_argument("--style", choices=["multigpu", "singlegpu"], default="multigpu",
+                    help="summary block layout / GFLOPs formula of the reference")
+    ap.add_argument("--error-norms", action="store_true",
+                    help="print L1/L2/Linf vs the exact solution (sine/heat ICs)")
+    ap.add_argument("--check-every", type=int, default=0, help="NaN/Inf watchdog period (steps)")
+    ap.add_argument("--json", action="store_true", help="also print one JSON metrics line")
+    ap.add_argument("--warmup", type=int, default=0, help="untimed warm-up steps")
+    return ap
+
+
+def parse(argv=None):
+    ap = build_parser()
+    ns = ap.parse_args(argv)
+    if ns.config:
+        cfg = _load_config(ns.config)
+        for k, v in cfg.items():
+            k2 = k.replace("-", "_")
+            if k2 == "args":
+                ns.args = [str(x) for x in v]
+            elif hasattr(ns, k2):
+                setattr(ns, k2, v)
+            else:
+                ap.error(f"unknown config key {k!r}")
+    names = APPS[ns.app]
+    if len(ns.args) < len(names):
+        ap.error(f"{ns.app} needs positional args: {' '.join(names)} [block sizes]")
+    pos = {}
+    for n, v in zip(names, ns.args):
+        pos[n] = int(v) if n in _INT else float(v)
+    ns.pos = pos
+    ns.blocks = ns.args[len(names):]
+    return ns
+
+
+def make_problem(ns):
+    """Return (model, grid, ic, run_kwargs) from parsed args."""
+    from .models import Burgers, Diffusion, Grid
+    p = ns.pos
+    if ns.app.startswith("diffusion"):
+        model = Diffusion(K=p["K"], order=ns.order, safety=ns.safety)
+        if ns.app == "diffusion3d":
+            grid = Grid((p["Nx"], p["Ny"], p["Nz"]), (p["L"], p["W"], p["H"]))
+        else:
+            grid = Grid((p["Nx"], p["Ny"]), (p["L"], p["W"]))
+        ic = ns.ic or "heat"
+        run = {"iters": p["iters"]}
+    else:
+        model = Burgers(viscosity=ns.viscosity, weno=ns.weno, cfl=p["CFL"], cfl_mode=ns.cfl_mode)
+        if ns.app == "burgers3d":
+            grid = Grid((p["Nx"], p["Ny"], p["Nz"]), (p["L"], p["W"], p["H"]))
+        else:
+            grid = Grid((p["Nx"], p["Ny"]), (p["L"], p["W"]))
+        ic = ns.ic or "gaussian"
+        run = {"t_end": p["tEnd"]}
+    return model, grid, ic, run
+
+
+def main(argv=None) -> int:
+    import torch
+
+    from .parallel.comm import Comm
+    from .solver import Solver
+    from .utils import metrics
+
+    ns = parse(argv)
+    model, grid, ic, run = make_problem(ns)
+    comm = Comm.from_env(device=ns.device)
+    dtype = torch.float64 if ns.dtype == "fp64" else torch.float32
+    t0 = 0.1 if (ic == "heat") else 0.0  # heat kernel IC is the exact solution at t0
+    solver = Solver(model, grid, comm, dtype=dtype, ic=ic, overlap=not ns.no_overlap, t0=t0,
+                    check_every=ns.check_every)
+    if ns.restart:
+        solver.load_checkpoint(ns.restart)
+    if ns.initial:
+        solver.save_result(ns.initial)
+    if ns.warmup:
+        wt, wi = solver.t, solver.it
+        saved = [f.clone() for f in solver.fields()]
+        solver.run(iters=ns.warmup)
+        for f, s in zip(solver.fields(), saved):
+            f.copy_(s)
+        solver.t, solver.it = wt, wi
+    if "t_end" in run:
+        run = {"t_end": run["t_end"] + (t0 if ic == "heat" else 0.0)}
+    stats = solver.run(**run)
+    extra = {}
+    if ns.error_norms and ic in ("sine", "heat"):
+        l1, l2, li = solver.error_norms()
+        extra = {"L1 norm": f"{l1:e}", "L2 norm": f"{l2:e}", "Linf norm": f"{li:e}"}
+    text = solver.summary(stats, style=ns.style, extra=extra)
+    if ns.write:
+        solver.save_result(ns.write)
+    if ns.checkpoint:
+        solver.save_checkpoint(ns.checkpoint)
+    if comm.rank == 0:
+        if ns.blocks:
+            print(f"(block sizes {' '.join(ns.blocks)} ignored: gfx950 tiles are fixed)")
+        print(text)
+        if ns.json:
+            print(json.dumps({
+                "app": ns.app, "grid": list(grid.shape), "steps": stats.steps,
+                "seconds": stats.compute_s,
+                "mlups": metrics.mlups(stats.compute_s, stats.steps, grid.cells),
+                "n_procs": comm.size, "dtype": ns.dtype, "t": stats.t}))
+    sys.stdout.flush()
+    comm.finalize()
+    return 0

@@ -1,0 +1,84 @@
+"""Burgers u_t + Σ_d ∂_d(u²/2) = C ∇²u (2-D / 3-D) with WENO5 flux splitting.
+
+Reference apps: MultiGPU Burgers2d/3d_Baseline (inviscid, WENO5-JS), SingleGPU
+Burgers3d_WENO5{,_PitchedMem,_SharedMem,_TextureMem,_Hybrid,_Hybrid2} (viscous C=1e-5,
+WENO5-Z), Matlab_Prototipes/InviscidBurgersNd (WENO5-JS).  One fused HIP kernel per
+dimensionality (``csrc/kernels/burgers.hip``) covers all of them: ``weno="js"|"z"``,
+``viscosity=0`` compiles the viscous term out.
+
+Time step (`SingleGPU/Burgers3d_WENO5/main.cpp:130-133`, `MultiGPU/Burgers3d_Baseline/main.c:193`):
+    dt = min(CFL·min(d)/umax, 0.9 / (2C Σ 1/d²))
+The reference hard-codes umax = 1 (no reduction).  ``cfl_mode="fixed"``
+keeps that (default: matches the reference step count); ``"adaptive"`` uses the true
+global max|u| (device reduction + allreduce every step, as the MATLAB prototype
+`LFWENO5FDM3d.m:71`).
+
+Deltas by design: each face flux is computed once (the reference's MultiGPU x-sweep
+starts at i=2 with a zero "old" flux — quirk #8 — and the SingleGPU y-sweep covers
+i < Ny only — quirk #6); frozen Dirichlet border of 3 cells on every face.
+"""
+from __future__ import annotations
+
+from ..ops import stencil
+from .base import Model
+
+
+class Burgers(Model):
+    name = "burgers"
+
+    def __init__(self, viscosity: float = 0.0, weno: str = "z", cfl: float = 0.3,
+                 cfl_mode: str = "fixed", umax: float = 1.0, border: int = 3):
+        if weno not in ("js", "z"):
+            raise ValueError("weno must be 'js' (Jiang-Shu) or 'z' (Borges)")
+        if cfl_mode not in ("fixed", "adaptive"):
+            raise ValueError("cfl_mode must be 'fixed' or 'adaptive'")
+        self.C = float(viscosity)
+        self.weno = weno
+        self.cfl = float(cfl)
+        self.cfl_mode = cfl_mode
+        self.umax = float(umax)
+        self.radius = 3
+        self.border = int(border)
+        if self.border < 3:
+            raise ValueError("WENO5 needs a frozen border >= 3")
+        self.needs_umax = cfl_mode == "adaptive"
+
+    def bind(self, grid):
+        super().bind(grid)
+        d = grid.spacing
+        self.dims = grid.dims
+        self.rd = tuple(1.0 / h for h in d)
+        self.visc = tuple(self.C / (h * h) for h in d)
+        kind = "WENO5-Z" if self.weno == "z" else "WENO5-JS"
+        self.title = f"Burgers-{grid.dims}D MI355X-{kind}"
+
+    @property
+    def bytes_per_cell_step(self):
+        return 64.0
+
+    def stable_dt(self, umax=None) -> float:
+        u = self.umax if (umax is None or self.cfl_mode == "fixed") else max(umax, 1e-300)
+        dt = self.cfl * min(self.grid.spacing) / u
+        if self.C > 0:
+            dt = min(dt, 0.9 / (2.0 * sum(self.visc)))
+        return dt
+
+    def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None):
+        g = self.grid
+        z = self.weno == "z"
+        if self.dims == 3:
+            stencil.burgers3d_stage(inp, u0, out, nx=g.nx, ny=g.ny, k0=lo, k1=hi,
+                                    border=self.border, weno_z=z, rdx=self.rd[0],
+                                    rdy=self.rd[1], rdz=self.rd[2], vx=self.visc[0],
+                                    vy=self.visc[1], vz=self.visc[2], dt=dt, a=a, b=b,
+                                    stream=stream)
+        else:
+            stencil.burgers2d_stage(inp, u0, out, nx=g.nx, j0=lo, j1=hi, border=self.border,
+                                    weno_z=z, rdx=self.rd[0], rdy=self.rd[1], vx=self.visc[0],
+                                    vy=self.visc[1], dt=dt, a=a, b=b, stream=stream)
+
+    def describe(self):
+        d = super().describe()
+        d.update({"viscosity": self.C, "weno": self.weno, "cfl": self.cfl,
+                  "cfl_mode": self.cfl_mode})
+        return d

@@ -1,0 +1,65 @@
+"""Heat equation u_t = K ∇²u (2-D / 3-D), FD4 (13-point in 3-D, 9-point in 2-D) or FD2.
+
+Reference apps: MultiGPU Diffusion2d/3d_Baseline, SingleGPU
+Diffusion2d{,_PitchedMem,_TextureMem}, Diffusion3d_{baselineCode,PitchedMem,Blocking},
+Matlab_Prototipes/DiffusionNd.  All memory variants collapse into one fused kernel
+(``csrc/kernels/diffusion.hip``).
+
+Deliberate deltas from the reference:
+* every axis uses its own coefficient K/(12 d²) (the MultiGPU 3-D kernel used
+  ``diff_x/12`` for all axes, an effective K/12 — quirk #2);
+* the fixed time step is ``safety / (2K Σ 1/d²)`` with safety 0.9 (SingleGPU,
+  `SingleGPU/Diffusion3d_baselineCode/main.cpp:58`) by default; ``safety=0.8``
+  reproduces the MultiGPU choice (`MultiGPU/Diffusion3d_Baseline/main.c:64`);
+* iteration counts are exact (the MultiGPU ``while t < dt*iters`` loop ran iters+1).
+"""
+from __future__ import annotations
+
+from ..ops import stencil
+from .base import Model
+
+
+class Diffusion(Model):
+    name = "diffusion"
+
+    def __init__(self, K: float = 1.0, order: int = 4, safety: float = 0.9, border=None):
+        if order not in (2, 4):
+            raise ValueError("order must be 2 (7-pt) or 4 (13-pt)")
+        self.K = float(K)
+        self.order = order
+        self.safety = float(safety)
+        self.radius = order // 2
+        self.border = self.radius if border is None else int(border)
+        if self.border < self.radius:
+            raise ValueError("frozen border must be >= stencil radius")
+
+    def bind(self, grid):
+        super().bind(grid)
+        d = grid.spacing
+        self.coef = tuple(self.K / (h * h) for h in d)
+        self.dims = grid.dims
+        self.title = f"Diffusion-{grid.dims}D MI355X-FD{self.order}"
+
+    @property
+    def bytes_per_cell_step(self):
+        return 64.0  # stage 1: 16 B, stages 2/3: 24 B (read in, read u0, write out)
+
+    def stable_dt(self, umax=None) -> float:
+        return self.safety / (2.0 * sum(self.coef))
+
+    def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None):
+        g = self.grid
+        if self.dims == 3:
+            stencil.diffusion3d_stage(inp, u0, out, nx=g.nx, ny=g.ny, k0=lo, k1=hi,
+                                      border=self.border, order=self.order, cx=self.coef[0],
+                                      cy=self.coef[1], cz=self.coef[2], dt=dt, a=a, b=b,
+                                      stream=stream)
+        else:
+            stencil.diffusion2d_stage(inp, u0, out, nx=g.nx, j0=lo, j1=hi, border=self.border,
+                                      order=self.order, cx=self.coef[0], cy=self.coef[1],
+                                      dt=dt, a=a, b=b, stream=stream)
+
+    def describe(self):
+        d = super().describe()
+        d.update({"K": self.K, "order": self.order, "safety": self.safety})
+        return d

@@ -1,0 +1,179 @@
+"""Device-dispatching stencil ops.
+
+``cuda`` (HIP) tensors run the hand-written gfx950 kernels of ``libadvdiff.so``; CPU
+tensors run the PyTorch reference (``ops/reference.py``).  There is deliberately NO silent
+fallback for device tensors: if the native library is missing on a GPU box the op raises.
+
+All ops enqueue on the current HIP stream (``torch.cuda.current_stream()``) unless a
+``stream`` is given, and never synchronise, so they can be captured into a hipGraph.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from . import reference as ref
+
+_DT = {torch.float32: 0, torch.float64: 1}
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype} (float32/float64 only)") from None
+
+
+def _stream_ptr(stream) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _check_layout(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if t.stride(-1) != 1:
+            raise ValueError("x (last axis) must be contiguous")
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def diffusion3d_stage(inp, u0, out, *, nx, ny, k0, k1, border, order, cx, cy, cz, dt, a, b,
+                      stream=None):
+    """out[k0:k1] = a*u0 + b*(inp + dt*K∇²inp) on the interior box (see kernels.h)."""
+    _check_layout(inp, u0, out)
+    if inp.is_cuda:
+        lib = _lib.require()
+        R = order // 2
+        assert k0 >= R and k1 + R <= inp.shape[0], "stencil planes out of bounds"
+        assert nx <= inp.shape[2] and ny <= inp.shape[1]
+        code = lib.advdiff_diffusion3d_stage(
+            _dtype_code(inp), _ptr(inp), _ptr(u0) if a != 0 else None, _ptr(out), nx, ny,
+            inp.stride(1), inp.stride(0), k0, k1, border, order, cx, cy, cz, dt, a, b,
+            _stream_ptr(stream))
+        _lib.check(code, "diffusion3d_stage")
+    else:
+        ref.diffusion3d_stage(inp, u0, out, nx, ny, k0, k1, border, order, cx, cy, cz, dt, a, b)
+
+
+def diffusion2d_stage(inp, u0, out, *, nx, j0, j1, border, order, cx, cy, dt, a, b,
+                      stream=None):
+    _check_layout(inp, u0, out)
+    if inp.is_cuda:
+        lib = _lib.require()
+        R = order // 2
+        assert j0 >= R and j1 + R <= inp.shape[0], "stencil rows out of bounds"
+        code = lib.advdiff_diffusion2d_stage(
+            _dtype_code(inp), _ptr(inp), _ptr(u0) if a != 0 else None, _ptr(out), nx,
+            inp.stride(0), j0, j1, border, order, cx, cy, dt, a, b, _stream_ptr(stream))
+        _lib.check(code, "diffusion2d_stage")
+    else:
+        ref.diffusion2d_stage(inp, u0, out, nx, j0, j1, border, order, cx, cy, dt, a, b)
+
+
+def burgers3d_stage(inp, u0, out, *, nx, ny, k0, k1, border, weno_z, rdx, rdy, rdz,
+                    vx=0.0, vy=0.0, vz=0.0, dt, a, b, stream=None):
+    _check_layout(inp, u0, out)
+    if border < 3:
+        raise ValueError("WENO5 needs a frozen border of at least 3 cells")
+    if inp.is_cuda:
+        lib = _lib.require()
+        assert k0 >= 3 and k1 + 3 <= inp.shape[0], "stencil planes out of bounds"
+        code = lib.advdiff_burgers3d_stage(
+            _dtype_code(inp), _ptr(inp), _ptr(u0) if a != 0 else None, _ptr(out), nx, ny,
+            inp.stride(1), inp.stride(0), k0, k1, border, int(bool(weno_z)), rdx, rdy, rdz,
+            vx, vy, vz, dt, a, b, _stream_ptr(stream))
+        _lib.check(code, "burgers3d_stage")
+    else:
+        ref.burgers3d_stage(inp, u0, out, nx, ny, k0, k1, border, bool(weno_z), rdx, rdy, rdz,
+                            vx, vy, vz, dt, a, b)
+
+
+def burgers2d_stage(inp, u0, out, *, nx, j0, j1, border, weno_z, rdx, rdy, vx=0.0, vy=0.0,
+                    dt, a, b, stream=None):
+    _check_layout(inp, u0, out)
+    if border < 3:
+        raise ValueError("WENO5 needs a frozen border of at least 3 cells")
+    if inp.is_cuda:
+        lib = _lib.require()
+        assert j0 >= 3 and j1 + 3 <= inp.shape[0], "stencil rows out of bounds"
+        code = lib.advdiff_burgers2d_stage(
+            _dtype_code(inp), _ptr(inp), _ptr(u0) if a != 0 else None, _ptr(out), nx,
+            inp.stride(0), j0, j1, border, int(bool(weno_z)), rdx, rdy, vx, vy, dt, a, b,
+            _stream_ptr(stream))
+        _lib.check(code, "burgers2d_stage")
+    else:
+        ref.burgers2d_stage(inp, u0, out, nx, j0, j1, border, bool(weno_z), rdx, rdy, vx, vy,
+                            dt, a, b)
+
+
+class NormReducer:
+    """Σ|x-y|, Σ(x-y)², max|x-y| over a box, on device (two-pass deterministic tree)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        if self.device.type == "cuda":
+            lib = _lib.require()
+            nbytes = lib.advdiff_reduce_workspace_bytes()
+            self.ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self.res = torch.empty(3, dtype=torch.float64, device=self.device)
+
+    def __call__(self, x, y=None, box=None, stream=None, sync=True):
+        """box = ((i0,i1),(j0,j1),(k0,k1)) in array coordinates (3-D) or
+        ((i0,i1),(j0,j1)) (2-D).  Returns a float64 tensor [3] (device) or tuple."""
+        if x.dim() == 2:
+            xs = x.unsqueeze(0)
+            ys = None if y is None else y.unsqueeze(0)
+            if box is None:
+                box = ((0, x.shape[1]), (0, x.shape[0]))
+            box = (box[0], box[1], (0, 1))
+        else:
+            xs, ys = x, y
+            if box is None:
+                box = ((0, x.shape[2]), (0, x.shape[1]), (0, x.shape[0]))
+        (i0, i1), (j0, j1), (k0, k1) = box
+        if not x.is_cuda:
+            sub = xs[k0:k1, j0:j1, i0:i1]
+            suby = None if ys is None else ys[k0:k1, j0:j1, i0:i1]
+            r = ref.norms(sub, suby)
+            return torch.tensor(r, dtype=torch.float64) if not sync else r
+        lib = _lib.require()
+        code = lib.advdiff_reduce_norms(
+            _dtype_code(x), xs.data_ptr(), None if ys is None else ys.data_ptr(),
+            xs.stride(1), xs.stride(0), i0, i1, j0, j1, k0, k1, self.ws.data_ptr(),
+            self.res.data_ptr(), _stream_ptr(stream))
+        _lib.check(code, "reduce_norms")
+        if sync:
+            return tuple(float(v) for v in self.res.cpu())
+        return self.res
+
+
+def copy_box(dst, src, ni, nj, nk, stream=None):
+    """Strided 3-D box copy dst[k, j, i] = src[k, j, i] (halo pack/unpack)."""
+    if dst.is_cuda:
+        lib = _lib.require()
+        d3 = dst if dst.dim() == 3 else dst.unsqueeze(0)
+        s3 = src if src.dim() == 3 else src.unsqueeze(0)
+        code = lib.advdiff_copy_box(_dtype_code(dst), d3.data_ptr(), d3.stride(1),
+                                    d3.stride(0), s3.data_ptr(), s3.stride(1), s3.stride(0),
+                                    ni, nj, nk, _stream_ptr(stream))
+        _lib.check(code, "copy_box")
+    else:
+        if dst.dim() == 3:
+            dst[:nk, :nj, :ni].copy_(src[:nk, :nj, :ni])
+        else:
+            dst[:nj, :ni].copy_(src[:nj, :ni])
+
+
+def init_ic_device(u, ic_code, *, nx, ny, nzl, kg0, NX, NY, NZ, dx, dy, dz, p0=0.0, p1=0.0,
+                   stream=None):
+    """Fill a local slab with a built-in IC on the device (see kernels.h codes)."""
+    lib = _lib.require()
+    u3 = u if u.dim() == 3 else u.unsqueeze(0)
+    code = lib.advdiff_init_ic(_dtype_code(u), ic_code, u3.data_ptr(), nx, ny, nzl,
+                               u3.stride(1), u3.stride(0), kg0, NX, NY, NZ, dx, dy, dz, p0,
+                               p1, _stream_ptr(stream))
+    _lib.check(code, "init_ic")

@@ -1,0 +1,139 @@
+"""Process-group bootstrap and collectives: one process per GPU over torch.distributed.
+
+Replaces the reference's MPI layer (`MultiGPU/Diffusion3d_Baseline/Tools.c:228-242`
+InitializeMPI/FinalizeMPI, `Util.cu:66-93` AssignDevices/ECCCheck, and the hand-rolled
+Isend/Recv gather at `main.c:327-335`).
+
+* Backend ``nccl`` (= RCCL on ROCm, point-to-point over xGMI) for device tensors,
+  ``gloo`` for CPU runs and the CPU multi-process tests.
+* Rendezvous from the standard torchrun environment (RANK, WORLD_SIZE, LOCAL_RANK,
+  MASTER_ADDR, MASTER_PORT).  A single process needs no rendezvous at all.
+* Device binding: ``cuda:LOCAL_RANK`` (the reference's ``rank % ndev``; here more ranks
+  than GPUs is refused rather than silently oversubscribed — RCCL forbids two ranks on
+  one GPU anyway).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    def __init__(self, rank=0, size=1, local_rank=0, device=None, backend=None, group=None):
+        self.rank = rank
+        self.size = size
+        self.local_rank = local_rank
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.backend = backend
+        self.group = group
+        self._owns_pg = False
+
+    # ------------------------------------------------------------------------------
+    @classmethod
+    def from_env(cls, device: str | None = None, backend: str | None = None,
+                 timeout_s: float = 600.0) -> "Comm":
+        """Create (or attach to) the default process group from torchrun env vars.
+
+        device: "cuda", "cpu" or None (= cuda if available).  backend defaults to
+        nccl for cuda, gloo for cpu.
+        """
+        size = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        if device.startswith("cuda"):
+            ndev = torch.cuda.device_count()
+            if ndev == 0:
+                raise RuntimeError("device=cuda requested but no GPU is visible")
+            if size > 1 and local_rank >= ndev:
+                raise RuntimeError(f"local rank {local_rank} >= {ndev} visible GPUs "
+                                   "(one process per GPU; oversubscription is refused)")
+            torch.cuda.set_device(local_rank % ndev)
+            dev = torch.device("cuda", local_rank % ndev)
+        else:
+            dev = torch.device("cpu")
+        c = cls(rank, size, local_rank, dev)
+        if size > 1:
+            c.backend = backend or ("nccl" if dev.type == "cuda" else "gloo")
+            if not dist.is_initialized():
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                kw = dict(backend=c.backend, rank=rank, world_size=size,
+                          timeout=datetime.timedelta(seconds=timeout_s))
+                if dev.type == "cuda" and c.backend == "nccl":
+                    kw["device_id"] = dev  # eager communicator init: no lazy P2P setup
+                dist.init_process_group(**kw)
+                c._owns_pg = True
+            c.group = dist.group.WORLD
+        return c
+
+    @property
+    def distributed(self) -> bool:
+        return self.size > 1
+
+    # ---- collectives ---------------------------------------------------------------
+    def barrier(self):
+        if self.size > 1:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def _scalar(self, v: float, op):
+        if self.size == 1:
+            return float(v)
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self._coll_device())
+        dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    def _coll_device(self):
+        return self.device if self.backend == "nccl" else torch.device("cpu")
+
+    def allreduce_max(self, v: float) -> float:
+        return self._scalar(v, dist.ReduceOp.MAX)
+
+    def allreduce_min(self, v: float) -> float:
+        return self._scalar(v, dist.ReduceOp.MIN)
+
+    def allreduce_sum(self, v: float) -> float:
+        return self._scalar(v, dist.ReduceOp.SUM)
+
+    def allreduce_tensor(self, t: torch.Tensor, op="sum") -> torch.Tensor:
+        if self.size == 1:
+            return t
+        ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+        x = t.to(self._coll_device())
+        dist.all_reduce(x, op=ops[op])
+        return x.to(t.device)
+
+    def gather_planes(self, local: torch.Tensor, counts: list[int]) -> torch.Tensor | None:
+        """Gather per-rank slabs (axis 0) to rank 0 (returned on CPU; None elsewhere).
+        Point-to-point so uneven slabs need no padding."""
+        if self.size == 1:
+            return local.detach().cpu()
+        dev = self._coll_device()
+        if self.rank == 0:
+            parts = [local.detach().cpu()]
+            for r in range(1, self.size):
+                buf = torch.empty((counts[r],) + tuple(local.shape[1:]), dtype=local.dtype,
+                                  device=dev)
+                dist.recv(buf, src=r)
+                parts.append(buf.cpu())
+            return torch.cat(parts, 0)
+        dist.send(local.detach().contiguous().to(dev), dst=0)
+        return None
+
+    def broadcast_object(self, obj):
+        if self.size == 1:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=0)
+        return lst[0]
+
+    def finalize(self):
+        if self._owns_pg and dist.is_initialized():
+            dist.destroy_process_group()
+            self._owns_pg = False
