@@ -31,8 +31,9 @@ __global__ __launch_bounds__(TX* TY) void diffusion3d_stage_kernel(
     const T* __restrict__ in, const T* u0, T* out, int nx, int ny, int64_t sy, int64_t sz,
     int k0, int k1, int zchunk, int border, T cx, T cy, T cz, T dt, T a, T b) {
   constexpr int R = FD<ORDER>::R;
-  constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NS = R + 2, NT = TX * TY;
-  __shared__ T ring[NS][LY * LX];
+  constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NS = R + 2, NT = TX * TY, NE = LX * LY;
+  constexpr int NPT = (NE + NT - 1) / NT;  // tile elements staged per thread and plane
+  __shared__ T ring[NS][NE];
 
   const int tx = threadIdx.x, ty = threadIdx.y, tid = ty * TX + tx;
   const int i0 = blockIdx.x * TX, j0 = blockIdx.y * TY;
@@ -40,32 +41,46 @@ __global__ __launch_bounds__(TX* TY) void diffusion3d_stage_kernel(
   const int kc0 = k0 + (int)blockIdx.z * zchunk;
   const int kc1 = min(kc0 + zchunk, k1);
   const bool active = i >= border && i < nx - border && j >= border && j < ny - border;
-  const int64_t own = (int64_t)min(j, ny - 1) * sy + min(i, nx - 1);
+  const int own = min(j, ny - 1) * (int)sy + min(i, nx - 1);  // plane-relative
   const int lc = (ty + R) * LX + tx + R;
 
-  auto load_plane = [&](int k) {
-    T* s = ring[k % NS];
-    const T* src = in + (int64_t)k * sz;
-    constexpr int NPT = (LX * LY + NT - 1) / NT;
+  // Plane-relative gather offsets of this thread's tile elements (clamped at the array
+  // edge: those values only feed cells that are never written).
+  int toff[NPT];
 #pragma unroll
-    for (int r = 0; r < NPT; ++r) {
-      const int idx = tid + r * NT;
-      if (NPT * NT != LX * LY && idx >= LX * LY) break;
-      const int ly = idx / LX, lx = idx - ly * LX;
-      const int gi = clampi(i0 - R + lx, 0, nx - 1);
-      const int gj = clampi(j0 - R + ly, 0, ny - 1);
-      s[idx] = src[(int64_t)gj * sy + gi];
-    }
+  for (int r = 0; r < NPT; ++r) {
+    const int idx = min(tid + r * NT, NE - 1);
+    const int ly = idx / LX, lx = idx - ly * LX;
+    toff[r] = clampi(j0 - R + ly, 0, ny - 1) * (int)sy + clampi(i0 - R + lx, 0, nx - 1);
+  }
+  T pre[NPT];
+  auto fetch = [&](int k) {
+    const T* src = in + (int64_t)k * sz;
+#pragma unroll
+    for (int r = 0; r < NPT; ++r) pre[r] = src[toff[r]];
+  };
+  auto stash = [&](int k) {
+    T* s = ring[k % NS];
+#pragma unroll
+    for (int r = 0; r < NPT; ++r)
+      if (NPT * NT == NE || tid + r * NT < NE) s[tid + r * NT] = pre[r];
   };
 
   T zw[2 * R + 1];
 #pragma unroll
   for (int q = 0; q < 2 * R; ++q) zw[q] = in[(int64_t)(kc0 - R + q) * sz + own];
 #pragma unroll
-  for (int q = 0; q < R; ++q) load_plane(kc0 + q);
+  for (int q = 0; q < R; ++q) {
+    fetch(kc0 + q);
+    stash(kc0 + q);
+  }
+  fetch(kc0 + R);
 
   for (int k = kc0; k < kc1; ++k) {
-    load_plane(k + R);
+    stash(k + R);                       // plane k+R: loaded one iteration ago
+    if (k + 1 < kc1) fetch(k + R + 1);  // keep the next plane's loads in flight
+    T uo = T(0);
+    if constexpr (USE_U0) uo = u0[(int64_t)k * sz + own];
     __syncthreads();
     zw[2 * R] = ring[(k + R) % NS][lc];
     const T* c = ring[k % NS];
@@ -80,8 +95,9 @@ __global__ __launch_bounds__(TX* TY) void diffusion3d_stage_kernel(
             cy * FD<2>::d2(c[lc - LX], ctr, c[lc + LX]) + cz * FD<2>::d2(zw[0], ctr, zw[2]);
     }
     if (active) {
-      const int64_t o = (int64_t)k * sz + own;
-      out[o] = rk_combine<T, USE_U0>(u0, o, ctr, lap, dt, a, b);
+      T v = b * (ctr + dt * lap);
+      if constexpr (USE_U0) v = a * uo + v;
+      out[(int64_t)k * sz + own] = v;
     }
 #pragma unroll
     for (int q = 0; q < 2 * R; ++q) zw[q] = zw[q + 1];
@@ -103,25 +119,39 @@ __global__ __launch_bounds__(TX) void diffusion2d_stage_kernel(
   const bool active = i >= border && i < nx - border;
   const int ic = min(i, nx - 1);
   const int lc = tx + R;
+  const int g0 = clampi(i0 - R + tx, 0, nx - 1);
+  const int g1 = clampi(i0 - R + TX + tx, 0, nx - 1);
 
-  auto load_row = [&](int j) {
-    T* s = ring[j % NS];
-    const T* src = in + (int64_t)j * sy;
-    s[tx] = src[clampi(i0 - R + tx, 0, nx - 1)];
-    if (tx < 2 * R) s[TX + tx] = src[clampi(i0 - R + TX + tx, 0, nx - 1)];
+  T p0, p1 = T(0);
+  auto fetch = [&](int jj) {
+    const T* src = in + (int64_t)jj * sy;
+    p0 = src[g0];
+    if (tx < 2 * R) p1 = src[g1];
+  };
+  auto stash = [&](int jj) {
+    T* s = ring[jj % NS];
+    s[tx] = p0;
+    if (tx < 2 * R) s[TX + tx] = p1;
   };
 
   T yw[2 * R + 1];
 #pragma unroll
   for (int q = 0; q < 2 * R; ++q) yw[q] = in[(int64_t)(jc0 - R + q) * sy + ic];
 #pragma unroll
-  for (int q = 0; q < R; ++q) load_row(jc0 + q);
+  for (int q = 0; q < R; ++q) {
+    fetch(jc0 + q);
+    stash(jc0 + q);
+  }
+  fetch(jc0 + R);
 
-  for (int j = jc0; j < jc1; ++j) {
-    load_row(j + R);
+  for (int jj = jc0; jj < jc1; ++jj) {
+    stash(jj + R);
+    if (jj + 1 < jc1) fetch(jj + R + 1);
+    T uo = T(0);
+    if constexpr (USE_U0) uo = u0[(int64_t)jj * sy + ic];
     __syncthreads();
-    yw[2 * R] = ring[(j + R) % NS][lc];
-    const T* c = ring[j % NS];
+    yw[2 * R] = ring[(jj + R) % NS][lc];
+    const T* c = ring[jj % NS];
     const T ctr = yw[R];
     T lap;
     if constexpr (ORDER == 4) {
@@ -131,8 +161,9 @@ __global__ __launch_bounds__(TX) void diffusion2d_stage_kernel(
       lap = cx * FD<2>::d2(c[lc - 1], ctr, c[lc + 1]) + cy * FD<2>::d2(yw[0], ctr, yw[2]);
     }
     if (active) {
-      const int64_t o = (int64_t)j * sy + i;
-      out[o] = rk_combine<T, USE_U0>(u0, o, ctr, lap, dt, a, b);
+      T v = b * (ctr + dt * lap);
+      if constexpr (USE_U0) v = a * uo + v;
+      out[(int64_t)jj * sy + i] = v;
     }
 #pragma unroll
     for (int q = 0; q < 2 * R; ++q) yw[q] = yw[q + 1];
@@ -142,23 +173,38 @@ __global__ __launch_bounds__(TX) void diffusion2d_stage_kernel(
 // ------------------------------------------------------------------------------
 // Host launchers
 // ------------------------------------------------------------------------------
-constexpr int kTX3 = 64, kTY3 = 4;  // 256-thread groups: one wave per tile row
+constexpr int kTX3 = 64, kTY3 = 16;  // 1024-thread groups: one wave per tile row (A/B: profiles/)
 constexpr int kTX2 = 256;
+
+template <typename T, int ORDER, int TY, bool USE_U0>
+static hipError_t launch_d3_ty(const void* in, const void* u0, void* out, int nx, int ny,
+                               int64_t sy, int64_t sz, int k0, int k1, int border, double cx,
+                               double cy, double cz, double dt, double a, double b,
+                               hipStream_t st) {
+  const int gx = div_up(nx, kTX3), gy = div_up(ny, TY);
+  const int zc = pick_chunk(k1 - k0, (long long)gx * gy, 8, 256);
+  const int gz = div_up(k1 - k0, zc);
+  const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
+  hipLaunchKernelGGL((diffusion3d_stage_kernel<T, ORDER, kTX3, TY, USE_U0>), dim3(gx, gy, gz),
+                     dim3(kTX3, TY, 1), 0, st, (const T*)in, (const T*)u0, (T*)out, nx, ny, sy,
+                     sz, k0, k1, zc, border, T(cx * s), T(cy * s), T(cz * s), T(dt), T(a), T(b));
+  return hipGetLastError();
+}
 
 template <typename T, int ORDER, bool USE_U0>
 static hipError_t launch_d3(const void* in, const void* u0, void* out, int nx, int ny,
                             int64_t sy, int64_t sz, int k0, int k1, int border, double cx,
                             double cy, double cz, double dt, double a, double b,
                             hipStream_t st) {
-  const int gx = div_up(nx, kTX3), gy = div_up(ny, kTY3);
-  const int zc = pick_chunk(k1 - k0, (long long)gx * gy, 8, 256);
-  const int gz = div_up(k1 - k0, zc);
-  const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
-  hipLaunchKernelGGL((diffusion3d_stage_kernel<T, ORDER, kTX3, kTY3, USE_U0>),
-                     dim3(gx, gy, gz), dim3(kTX3, kTY3, 1), 0, st, (const T*)in,
-                     (const T*)u0, (T*)out, nx, ny, sy, sz, k0, k1, zc, border, T(cx * s),
-                     T(cy * s), T(cz * s), T(dt), T(a), T(b));
-  return hipGetLastError();
+  static const int ty = knob("D3_TY", kTY3);
+#define TYL(TY) \
+  return launch_d3_ty<T, ORDER, TY, USE_U0>(in, u0, out, nx, ny, sy, sz, k0, k1, border, cx, cy, cz, dt, a, b, st)
+  switch (ty) {
+    case 4: TYL(4);
+    case 16: TYL(16);
+    default: TYL(8);
+  }
+#undef TYL
 }
 
 template <typename T, int ORDER, bool USE_U0>
@@ -218,6 +264,7 @@ extern "C" int advdiff_diffusion3d_stage(int dtype, const void* in, const void* 
   if (k1 <= k0) return hipSuccess;
   const int R = order / 2;
   if (k0 < R || nx <= 0 || ny <= 0 || in == out) return hipErrorInvalidValue;
+  if (sy * (int64_t)ny >= (int64_t(1) << 31)) return hipErrorInvalidValue;  // 32-bit plane offsets
   hipStream_t st = (hipStream_t)stream;
   if (dtype == ADVDIFF_F64)
     return dispatch_d3<double>(in, u0, out, nx, ny, sy, sz, k0, k1, border, order, cx, cy,

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <stdint.h>
 
 namespace advdiff {
@@ -14,9 +16,12 @@ constexpr long long kTargetBlocks = 2048;
 // Length of the marching chunk (planes per workgroup) so that the launch has at
 // least kTargetBlocks groups while each group marches far enough to amortise the
 // 2R-plane prologue of its register window.
+inline int knob(const char* name, int def);
+
 inline int pick_chunk(int nrange, long long xyblocks, int minc, int maxc) {
   if (nrange <= 0) return 1;
-  long long want_chunks = (kTargetBlocks + xyblocks - 1) / std::max<long long>(xyblocks, 1);
+  static const long long target = knob("TARGET_BLOCKS", (int)kTargetBlocks);
+  long long want_chunks = (target + xyblocks - 1) / std::max<long long>(xyblocks, 1);
   long long c = (nrange + want_chunks - 1) / std::max<long long>(want_chunks, 1);
   c = std::max<long long>(c, minc);
   c = std::min<long long>(c, maxc);
@@ -24,5 +29,14 @@ inline int pick_chunk(int nrange, long long xyblocks, int minc, int maxc) {
 }
 
 inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// Tuning knobs read once from the environment (ADVDIFF_<NAME>), for A/B experiments
+// inside one process; the defaults are the tuned gfx950 choices.
+inline int knob(const char* name, int def) {
+  char key[64];
+  std::snprintf(key, sizeof(key), "ADVDIFF_%s", name);
+  const char* v = std::getenv(key);
+  return v ? std::atoi(v) : def;
+}
 
 }  // namespace advdiff

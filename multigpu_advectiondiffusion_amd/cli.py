@@ -136,7 +136,8 @@ def main(argv=None) -> int:
 
     ns = parse(argv)
     model, grid, ic, run = make_problem(ns)
-    comm = Comm.from_env(device=ns.device)
+    import os
+    comm = Comm.from_env(device=ns.device or os.environ.get("ADVDIFF_DEVICE"))
     dtype = torch.float64 if ns.dtype == "fp64" else torch.float32
     t0 = 0.1 if (ic == "heat") else 0.0  # heat kernel IC is the exact solution at t0
     solver = Solver(model, grid, comm, dtype=dtype, ic=ic, overlap=not ns.no_overlap, t0=t0,

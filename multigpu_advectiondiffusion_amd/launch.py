@@ -1,0 +1,123 @@
+"""Local multi-process launcher (the reference's ``mpirun -np P``, `MultiGPU/*/run.sh`).
+
+Two entry points:
+
+* CLI: ``python -m multigpu_advectiondiffusion_amd.launch -np 8 diffusion3d 1 2 2 2 512 512 512 100``
+  starts P child processes of ``python -m multigpu_advectiondiffusion_amd`` with the
+  torchrun environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1,
+  MASTER_PORT) — one process per GPU; ``--cpu`` runs P gloo ranks on the CPU (the
+  oversubscription / no-cluster test mode of SURVEY.md §4, done properly).
+* API: ``spawn_local(world, fn, *args)`` runs ``fn(comm, *args)`` in `world` fresh
+  processes with an initialised process group and returns the per-rank results — used
+  by the multi-rank tests.
+
+Children are started as subprocesses (never exec'd from a process that touched the GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import socket
+import subprocess
+import sys
+import traceback
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _child_env(rank: int, world: int, port: int, cpu: bool) -> dict:
+    env = dict(os.environ)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
+                "MASTER_PORT": str(port)})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if cpu:
+        env["ADVDIFF_DEVICE"] = "cpu"
+    return env
+
+
+def launch(np_: int, argv: list[str], cpu: bool = False, timeout: float | None = None) -> int:
+    port = free_port()
+    cmd = [sys.executable, "-m", "multigpu_advectiondiffusion_amd"] + argv
+    if cpu and "--device" not in argv:
+        cmd += ["--device", "cpu"]
+    procs = [subprocess.Popen(cmd, env=_child_env(r, np_, port, cpu)) for r in range(np_)]
+    rc = 0
+    try:
+        for p in procs:
+            code = p.wait(timeout=timeout)
+            rc = rc or code
+    except subprocess.TimeoutExpired:
+        rc = 124
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+# ----------------------------------------------------------------------------------
+# in-process API for tests
+# ----------------------------------------------------------------------------------
+def _spawn_entry(rank, world, port, device, fn, args, queue):
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    try:
+        import torch
+        torch.set_num_threads(1)
+        from .parallel.comm import Comm
+        comm = Comm.from_env(device=device)
+        try:
+            res = fn(comm, *args)
+        finally:
+            comm.finalize()
+        queue.put((rank, "ok", res))
+    except BaseException as e:  # report instead of hanging the parent
+        queue.put((rank, "err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+
+
+def spawn_local(world: int, fn, *args, device: str = "cpu", timeout: float = 300.0):
+    """Run fn(comm, *args) on `world` local ranks; return [result_rank0, ...]."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_spawn_entry, args=(r, world, port, device, fn, args, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [None] * world
+    errors = []
+    try:
+        for _ in range(world):
+            rank, status, payload = q.get(timeout=timeout)
+            if status == "ok":
+                results[rank] = payload
+            else:
+                errors.append(f"rank {rank}: {payload}")
+    finally:
+        for p in procs:
+            p.join(timeout=10)
+            if p.is_alive():
+                p.kill()
+    if errors:
+        raise RuntimeError("\n".join(errors))
+    return results
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="launch P local ranks (one per GPU)")
+    ap.add_argument("-np", "--nproc", type=int, required=True)
+    ap.add_argument("--cpu", action="store_true", help="gloo ranks on the CPU")
+    ap.add_argument("--timeout", type=float, default=None)
+    ap.add_argument("rest", nargs=argparse.REMAINDER)
+    ns = ap.parse_args(argv)
+    return launch(ns.nproc, ns.rest, cpu=ns.cpu, timeout=ns.timeout)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
