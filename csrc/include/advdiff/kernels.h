@@ -85,6 +85,9 @@ int advdiff_init_ic(int dtype, int ic, void* u, int nx, int ny, int nzl, int64_t
 int advdiff_copy_box(int dtype, void* dst, int64_t dsy, int64_t dsz, const void* src,
                      int64_t ssy, int64_t ssz, int ni, int nj, int nk, void* stream);
 
+// x[0:n] *= s (contiguous), e.g. to scale a device-generated IC into an exact solution.
+int advdiff_scale(int dtype, void* x, int64_t n, double s, void* stream);
+
 // Library identification (build flags, arch) for diagnostics.
 const char* advdiff_build_info(void);
 

@@ -159,7 +159,28 @@ __global__ void copy_box_kernel(T* __restrict__ dst, int64_t dsy, int64_t dsz,
   dst[(int64_t)k * dsz + (int64_t)j * dsy + i] = src[(int64_t)k * ssz + (int64_t)j * ssy + i];
 }
 
+template <typename T>
+__global__ void scale_kernel(T* __restrict__ x, int64_t n, T s) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x)
+    x[q] *= s;
+}
+
 }  // namespace advdiff
+
+extern "C" int advdiff_scale(int dtype, void* x, int64_t n, double s, void* stream) {
+  using namespace advdiff;
+  if (n <= 0) return hipSuccess;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  if (dtype == ADVDIFF_F64)
+    hipLaunchKernelGGL(scale_kernel<double>, dim3(nb), dim3(256), 0, st, (double*)x, n, s);
+  else if (dtype == ADVDIFF_F32)
+    hipLaunchKernelGGL(scale_kernel<float>, dim3(nb), dim3(256), 0, st, (float*)x, n, (float)s);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
 
 extern "C" size_t advdiff_reduce_workspace_bytes(void) {
   return sizeof(advdiff::Norm3) * advdiff::kRedBlocks;

@@ -56,12 +56,17 @@ struct FD<2> {
 
 // Burgers flux f(u) = u²/2, local Lax-Friedrichs split  f± = ½(f(u) ± |u|·u).
 // (reference: MultiGPU/Burgers3d_Baseline/Kernels.cu:256-264)
+//
+// Determinism: the split and the WENO reconstruction are written with explicit fma()
+// and FP contraction disabled inside, so a face flux is bit-identical wherever it is
+// evaluated (the z-face of a chunk's prologue vs. the same face inside the march).
+// That makes a P-rank run bitwise equal to the 1-rank run whatever the chunking.
 template <typename T>
 __device__ __forceinline__ void lf_split(T u, T& fp, T& fm) {
-  const T q = T(0.25) * u * u;  // ½·f(u)
-  const T s = T(0.5) * fabs(u) * u;
-  fp = q + s;
-  fm = q - s;
+#pragma clang fp contract(off)
+  const T s = (T(0.5) * fabs(u)) * u;
+  fp = fma(T(0.25) * u, u, s);
+  fm = fma(T(0.25) * u, u, -s);
 }
 
 // Left-biased WENO5 reconstruction of the value at the right face of v2 from the
@@ -72,37 +77,37 @@ __device__ __forceinline__ void lf_split(T u, T& fp, T& fm) {
 //                 tau5 = |beta_0 - beta_2|
 template <typename T, bool ZVARIANT>
 __device__ __forceinline__ T weno5(T v0, T v1, T v2, T v3, T v4) {
+#pragma clang fp contract(off)
   constexpr T c1312 = T(13.0 / 12.0);
   constexpr T eps = T(1e-6);
-  const T t0a = v0 - T(2) * v1 + v2, t0b = v0 - T(4) * v1 + T(3) * v2;
-  const T t1a = v1 - T(2) * v2 + v3, t1b = v1 - v3;
-  const T t2a = v2 - T(2) * v3 + v4, t2b = T(3) * v2 - T(4) * v3 + v4;
-  const T b0 = c1312 * t0a * t0a + T(0.25) * t0b * t0b;
-  const T b1 = c1312 * t1a * t1a + T(0.25) * t1b * t1b;
-  const T b2 = c1312 * t2a * t2a + T(0.25) * t2b * t2b;
+  const T t0a = fma(T(-2), v1, v0 + v2), t0b = fma(T(3), v2, fma(T(-4), v1, v0));
+  const T t1a = fma(T(-2), v2, v1 + v3), t1b = v1 - v3;
+  const T t2a = fma(T(-2), v3, v2 + v4), t2b = fma(T(3), v2, fma(T(-4), v3, v4));
+  const T b0 = fma(c1312 * t0a, t0a, (T(0.25) * t0b) * t0b);
+  const T b1 = fma(c1312 * t1a, t1a, (T(0.25) * t1b) * t1b);
+  const T b2 = fma(c1312 * t2a, t2a, (T(0.25) * t2b) * t2b);
   // candidate polynomials (times 6)
-  const T q0 = T(2) * v0 - T(7) * v1 + T(11) * v2;
-  const T q1 = -v1 + T(5) * v2 + T(2) * v3;
-  const T q2 = T(2) * v2 + T(5) * v3 - v4;
+  const T q0 = fma(T(11), v2, fma(T(-7), v1, T(2) * v0));
+  const T q1 = fma(T(5), v2, fma(T(2), v3, -v1));
+  const T q2 = fma(T(5), v3, fma(T(2), v2, -v4));
   T w0, w1, w2;
   if constexpr (ZVARIANT) {
     const T tau = fabs(b0 - b2);
     const T e0 = b0 + eps, e1 = b1 + eps, e2 = b2 + eps;
     // alpha_k ∝ d_k (e_k + tau) * e_j * e_l
-    w0 = T(0.1) * (e0 + tau) * (e1 * e2);
-    w1 = T(0.6) * (e1 + tau) * (e0 * e2);
-    w2 = T(0.3) * (e2 + tau) * (e0 * e1);
+    w0 = (T(0.1) * (e0 + tau)) * (e1 * e2);
+    w1 = (T(0.6) * (e1 + tau)) * (e0 * e2);
+    w2 = (T(0.3) * (e2 + tau)) * (e0 * e1);
   } else {
-    const T s0 = (eps + b0) * (eps + b0);
-    const T s1 = (eps + b1) * (eps + b1);
-    const T s2 = (eps + b2) * (eps + b2);
+    const T e0 = eps + b0, e1 = eps + b1, e2 = eps + b2;
+    const T s0 = e0 * e0, s1 = e1 * e1, s2 = e2 * e2;
     // alpha_k ∝ d_k * s_j * s_l
     w0 = T(0.1) * (s1 * s2);
     w1 = T(0.6) * (s0 * s2);
     w2 = T(0.3) * (s0 * s1);
   }
-  const T num = w0 * q0 + w1 * q1 + w2 * q2;
-  const T den = T(6) * (w0 + w1 + w2);
+  const T num = fma(w0, q0, fma(w1, q1, w2 * q2));
+  const T den = T(6) * ((w0 + w1) + w2);
   return num / den;
 }
 
@@ -110,6 +115,7 @@ __device__ __forceinline__ T weno5(T v0, T v1, T v2, T v3, T v4) {
 template <typename T, bool ZVARIANT>
 __device__ __forceinline__ T weno5_face(T p0, T p1, T p2, T p3, T p4,   // fp i-2..i+2
                                         T m0, T m1, T m2, T m3, T m4) {  // fm i-1..i+3
+#pragma clang fp contract(off)
   return weno5<T, ZVARIANT>(p0, p1, p2, p3, p4) + weno5<T, ZVARIANT>(m4, m3, m2, m1, m0);
 }
 

@@ -1,0 +1,133 @@
+// Shared driver of the native executables (bin/diffusion2d, diffusion3d, burgers2d,
+// burgers3d) with the reference's positional command lines:
+//
+//   diffusion2d  K L W Nx Ny iters [bx by]           (MultiGPU/Diffusion2d_Baseline/main.c:36-51)
+//   diffusion3d  K L W H Nx Ny Nz iters [bx by bz]   (MultiGPU/Diffusion3d_Baseline/main.c:36-54)
+//   burgers2d    tEnd CFL L W Nx Ny [bx by]          (MultiGPU/Burgers2d_Baseline/main.c:36-51)
+//   burgers3d    tEnd CFL L W H Nx Ny Nz [bx by bz]  (MultiGPU/Burgers3d_Baseline/main.c:36-54)
+//
+// plus named options (runtime replacements of the reference's #defines, §2.7):
+//   --ic NAME  --order 2|4  --safety S  --weno js|z  --visc C  --fp32  --no-overlap
+//   --transport rccl|socket  --write FILE  --error-norms
+// Launch one process per GPU with torchrun-style env vars (RANK/WORLD_SIZE/LOCAL_RANK/
+// MASTER_ADDR/MASTER_PORT), e.g. via `python -m multigpu_advectiondiffusion_amd.launch`.
+#include <chrono>
+#include <cstring>
+#include <iostream>
+#include <map>
+#include <string>
+
+#include "runtime.hpp"
+
+namespace advdiff::rt {
+
+static int ic_code(const std::string& s) {
+  static const std::map<std::string, int> m = {{"zero", 0},  {"square", 1},   {"sine", 2},
+                                               {"heat", 3},  {"gaussian", 4}, {"plates", 5},
+                                               {"disc", 6}};
+  auto it = m.find(s);
+  if (it == m.end()) throw std::runtime_error("unknown IC " + s);
+  return it->second;
+}
+
+int run_app(int argc, char** argv, Physics phys, int dims) {
+  std::vector<std::string> pos;
+  std::map<std::string, std::string> opt;
+  for (int q = 1; q < argc; ++q) {
+    std::string a = argv[q];
+    if (a.rfind("--", 0) == 0) {
+      const bool flag = a == "--fp32" || a == "--no-overlap" || a == "--error-norms";
+      if (flag || q + 1 >= argc) {
+        opt[a] = "1";
+      } else {
+        opt[a] = argv[++q];
+      }
+    } else {
+      pos.push_back(a);
+    }
+  }
+  const bool diff = phys == Physics::Diffusion;
+  const size_t need = diff ? (dims == 3 ? 8 : 6) : (dims == 3 ? 8 : 6);
+  if (pos.size() < need) {
+    std::cerr << "usage: " << argv[0]
+              << (diff ? (dims == 3 ? " K L W H Nx Ny Nz iters [bx by bz]" : " K L W Nx Ny iters [bx by]")
+                       : (dims == 3 ? " tEnd CFL L W H Nx Ny Nz [bx by bz]" : " tEnd CFL L W Nx Ny [bx by]"))
+              << " [--ic NAME] [--order 2|4] [--weno js|z] [--visc C] [--fp32] [--no-overlap]"
+                 " [--transport rccl|socket] [--write FILE] [--error-norms]\n";
+    return 1;
+  }
+  Problem p;
+  p.physics = phys;
+  p.dims = dims;
+  size_t k = 0;
+  double tEnd = 0;
+  int iters = 0;
+  if (diff) {
+    p.K = std::stod(pos[k++]);
+  } else {
+    tEnd = std::stod(pos[k++]);
+    p.cfl = std::stod(pos[k++]);
+  }
+  p.L = std::stod(pos[k++]);
+  p.W = std::stod(pos[k++]);
+  if (dims == 3) p.H = std::stod(pos[k++]);
+  p.nx = std::stoi(pos[k++]);
+  p.ny = std::stoi(pos[k++]);
+  if (dims == 3) p.nz = std::stoi(pos[k++]);
+  if (diff) iters = std::stoi(pos[k++]);
+  if (opt.count("--order")) p.order = std::stoi(opt["--order"]);
+  if (opt.count("--safety")) p.safety = std::stod(opt["--safety"]);
+  if (opt.count("--weno")) p.weno_z = opt["--weno"] == "z";
+  if (opt.count("--visc")) p.C = std::stod(opt["--visc"]);
+  if (opt.count("--fp32")) p.dtype = ADVDIFF_F32;
+  if (opt.count("--no-overlap")) p.overlap = false;
+  std::string ic = opt.count("--ic") ? opt["--ic"] : (diff ? "heat" : "gaussian");
+  p.ic = ic_code(ic);
+  if (p.ic == 3) {
+    p.ic_p0 = p.K;
+    p.ic_p1 = 0.1;
+    p.t0 = 0.1;
+  } else if (p.ic == 4) {
+    p.ic_p0 = 0.1;
+  } else if (p.ic == 6) {
+    p.ic_p0 = 0.2;
+  }
+
+  ProcEnv env = ProcEnv::from_env();
+  int ndev = 0;
+  HIP_CHECK(hipGetDeviceCount(&ndev));
+  if (ndev == 0) throw std::runtime_error("no HIP device");
+  const std::string tk = opt.count("--transport") ? opt["--transport"] : "rccl";
+  if (env.size > ndev && tk != "socket")
+    throw std::runtime_error("more ranks than GPUs: one process per GPU (or --transport socket)");
+  HIP_CHECK(hipSetDevice(env.local_rank % ndev));
+  auto tr = make_transport(env, tk);
+  Engine eng(p, tr.get(), env);
+  Stats st = diff ? eng.run_iters(iters) : eng.run_until(tEnd + p.t0);
+  std::string title =
+      std::string(diff ? "Diffusion-" : "Burgers-") + (dims == 3 ? "3D" : "2D") +
+      (diff ? (p.order == 4 ? " MI355X-FD4" : " MI355X-FD2") : (p.weno_z ? " MI355X-WENO5Z" : " MI355X-WENO5JS"));
+  std::string optname = std::string("Fused LDS z-march + RK3 (gfx950), transport=") + tr->name();
+  double l1 = 0, l2 = 0, li = 0;
+  const bool norms = opt.count("--error-norms") && (p.ic == 2 || p.ic == 3);
+  if (norms) eng.error_norms(l1, l2, li);
+  const double tw = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  std::vector<float> g;
+  if (opt.count("--write")) g = eng.gather_float32();
+  st.dtoh = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() - tw;
+  if (env.rank == 0) {
+    if (pos.size() > need) std::cout << "(block sizes ignored: gfx950 tiles are fixed)\n";
+    std::cout << summary_multigpu(title, optname, st, p, env.size);
+    if (norms) {
+      std::printf("L1 norm                                       :  %e\n", l1);
+      std::printf("L2 norm                                       :  %e\n", l2);
+      std::printf("Linf norm                                     :  %e\n", li);
+    }
+    if (opt.count("--write")) write_binary(opt["--write"], g);
+    std::cout.flush();
+  }
+  tr->barrier();
+  return 0;
+}
+
+}  // namespace advdiff::rt

@@ -1,0 +1,334 @@
+// SSP-RK3 engine of the native runtime (mirror of multigpu_advectiondiffusion_amd/solver.py).
+//
+// Per stage, on the compute stream:  interior(in->out)  -> wait(halo of in) ->
+// boundary(in->out) -> event -> [comm stream] exchange of out's ghost planes, which
+// overlaps the next stage's interior.  Buffers u -> A -> B -> u (stage 3 in place), no
+// Lu array, no uo copy.  Reference: MultiGPU/Diffusion3d_Baseline/main.c:189-303.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <sstream>
+
+#include "runtime.hpp"
+
+namespace advdiff::rt {
+
+Range Slab::compute_range(int border) const {
+  const int lo = std::max(start(), border);
+  const int hi = std::min(start() + count(), n - border);
+  if (hi <= lo) return {ghost, ghost};
+  return {to_local(lo), to_local(hi)};
+}
+
+void Slab::split(int border, int radius, Range& interior, Range& blo, Range& bhi) const {
+  Range r = compute_range(border);
+  const int o0 = ghost, o1 = ghost + count();
+  if (r.empty()) {
+    interior = blo = bhi = {r.lo, r.lo};
+    return;
+  }
+  const int blo_end = lower() >= 0 ? std::min(r.hi, o0 + radius) : r.lo;
+  const int bhi_start = upper() >= 0 ? std::max(r.lo, o1 - radius) : r.hi;
+  blo = {r.lo, std::max(r.lo, blo_end)};
+  if (bhi_start < blo.hi) {
+    interior = {blo.hi, blo.hi};
+    blo = r;
+    bhi = {r.hi, r.hi};
+    return;
+  }
+  bhi = {bhi_start, r.hi};
+  interior = {blo.hi, bhi_start};
+}
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_(tr), env_(env) {
+  slab_.n = p.n_decomposed();
+  slab_.size = env.size;
+  slab_.rank = env.rank;
+  slab_.ghost = p.radius();
+  if (slab_.n < slab_.size * slab_.ghost)
+    throw std::runtime_error("slab thinner than the ghost width: use fewer ranks");
+  elem_ = p.dtype == ADVDIFF_F64 ? 8 : 4;
+  const int per = 256 / (int)elem_;
+  const int sx = (p.nx + per - 1) / per * per;  // 256-B row pitch
+  sy_ = sx;
+  if (p.dims == 3) {
+    sz_ = (int64_t)p.ny * sx;
+    plane_bytes_ = (size_t)sz_ * elem_;
+  } else {
+    sz_ = sx;
+    plane_bytes_ = (size_t)sx * elem_;
+  }
+  field_bytes_ = plane_bytes_ * (size_t)slab_.alloc();
+  HIP_CHECK(hipMalloc(&u_, field_bytes_));
+  HIP_CHECK(hipMalloc(&A_, field_bytes_));
+  HIP_CHECK(hipMalloc(&B_, field_bytes_));
+  HIP_CHECK(hipMemset(u_, 0, field_bytes_));
+  int lo_pri = 0, hi_pri = 0;
+  HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri));
+  HIP_CHECK(hipStreamCreateWithPriority(&compute_, hipStreamNonBlocking, lo_pri));
+  HIP_CHECK(hipStreamCreateWithPriority(&comm_, hipStreamNonBlocking, hi_pri));
+  HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&halo_done_, hipEventDisableTiming));
+  // initial condition on the device, ghosts included (they equal the neighbours' planes)
+  const int kg0 = slab_.start() - slab_.ghost;
+  if (p.dims == 3)
+    KERNEL_CHECK(advdiff_init_ic(p.dtype, p.ic, u_, p.nx, p.ny, slab_.alloc(), sy_, sz_, kg0,
+                                 p.nx, p.ny, p.nz, p.dx(), p.dy(), p.dz(), p.ic_p0, p.ic_p1,
+                                 compute_));
+  else
+    KERNEL_CHECK(advdiff_init_ic(p.dtype, p.ic, u_, p.nx, slab_.alloc(), 1, sy_, sz_, kg0, p.nx,
+                                 p.ny, 1, p.dx(), p.dy(), 0.0, p.ic_p0, p.ic_p1, compute_));
+  HIP_CHECK(hipMemcpyAsync(A_, u_, field_bytes_, hipMemcpyDeviceToDevice, compute_));
+  HIP_CHECK(hipMemcpyAsync(B_, u_, field_bytes_, hipMemcpyDeviceToDevice, compute_));
+  HIP_CHECK(hipStreamSynchronize(compute_));
+  full_ = slab_.compute_range(p.border());
+  slab_.split(p.border(), p.radius(), interior_, blo_, bhi_);
+  t_ = p.t0;
+}
+
+Engine::~Engine() {
+  (void)hipStreamSynchronize(compute_);
+  (void)hipStreamSynchronize(comm_);
+  (void)hipEventDestroy(ready_);
+  (void)hipEventDestroy(halo_done_);
+  (void)hipStreamDestroy(compute_);
+  (void)hipStreamDestroy(comm_);
+  (void)hipFree(u_);
+  (void)hipFree(A_);
+  (void)hipFree(B_);
+}
+
+double Engine::stable_dt() const {
+  // same operation order as models/*.stable_dt so Python and C++ runs are bitwise equal
+  const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
+  auto coef_sum = [&](double c) {
+    double s = c / (dx * dx) + c / (dy * dy);
+    if (p_.dims == 3) s += c / (dz * dz);
+    return s;
+  };
+  if (p_.physics == Physics::Diffusion) return p_.safety / (2.0 * coef_sum(p_.K));
+  double h = std::min(dx, dy);
+  if (p_.dims == 3) h = std::min(h, dz);
+  double dt = p_.cfl * h / 1.0;  // reference: max|u| assumed 1 (main.cpp:130-133)
+  if (p_.C > 0) dt = std::min(dt, 0.9 / (2.0 * coef_sum(p_.C)));
+  return dt;
+}
+
+void Engine::launch(const void* in, const void* u0, void* out, Range r, double dt, double a,
+                    double b) {
+  if (r.empty()) return;
+  const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
+  const int B = p_.border();
+  if (p_.physics == Physics::Diffusion) {
+    const double cx = p_.K / (dx * dx), cy = p_.K / (dy * dy);
+    if (p_.dims == 3)
+      KERNEL_CHECK(advdiff_diffusion3d_stage(p_.dtype, in, u0, out, p_.nx, p_.ny, sy_, sz_, r.lo,
+                                             r.hi, B, p_.order, cx, cy, p_.K / (dz * dz), dt, a,
+                                             b, compute_));
+    else
+      KERNEL_CHECK(advdiff_diffusion2d_stage(p_.dtype, in, u0, out, p_.nx, sy_, r.lo, r.hi, B,
+                                             p_.order, cx, cy, dt, a, b, compute_));
+  } else {
+    if (p_.dims == 3)
+      KERNEL_CHECK(advdiff_burgers3d_stage(
+          p_.dtype, in, u0, out, p_.nx, p_.ny, sy_, sz_, r.lo, r.hi, B, p_.weno_z, 1.0 / dx,
+          1.0 / dy, 1.0 / dz, p_.C / (dx * dx), p_.C / (dy * dy), p_.C / (dz * dz), dt, a, b,
+          compute_));
+    else
+      KERNEL_CHECK(advdiff_burgers2d_stage(p_.dtype, in, u0, out, p_.nx, sy_, r.lo, r.hi, B,
+                                           p_.weno_z, 1.0 / dx, 1.0 / dy, p_.C / (dx * dx),
+                                           p_.C / (dy * dy), dt, a, b, compute_));
+  }
+}
+
+void Engine::start_halo(void* field) {
+  if (env_.size == 1) return;
+  const int G = slab_.ghost, c = slab_.count();
+  HIP_CHECK(hipEventRecord(ready_, compute_));
+  HIP_CHECK(hipStreamWaitEvent(comm_, ready_, 0));
+  tr_->halo(plane(field, G), plane(field, 0), plane(field, G + c - G), plane(field, G + c),
+            (size_t)G * plane_bytes_, slab_.lower(), slab_.upper(), comm_);
+  HIP_CHECK(hipEventRecord(halo_done_, comm_));
+  halo_pending_ = true;
+}
+
+void Engine::stage(void* in, void* u0, void* out, double a, double b, double dt) {
+  if (env_.size == 1) {
+    launch(in, u0, out, full_, dt, a, b);
+    return;
+  }
+  if (p_.overlap) {
+    launch(in, u0, out, interior_, dt, a, b);
+    if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
+    launch(in, u0, out, blo_, dt, a, b);
+    launch(in, u0, out, bhi_, dt, a, b);
+  } else {
+    if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
+    launch(in, u0, out, full_, dt, a, b);
+  }
+  halo_pending_ = false;
+  start_halo(out);
+}
+
+void Engine::step(double dt) {
+  stage(u_, nullptr, A_, 0.0, 1.0, dt);
+  stage(A_, u_, B_, 0.75, 0.25, dt);
+  stage(B_, u_, u_, 1.0 / 3.0, 2.0 / 3.0, dt);
+  t_ += dt;
+  ++it_;
+}
+
+Stats Engine::run_iters(int iters) {
+  const double dt = stable_dt();
+  HIP_CHECK(hipDeviceSynchronize());
+  tr_->barrier();
+  const double t0 = now_s();
+  for (int q = 0; q < iters; ++q) step(dt);
+  HIP_CHECK(hipStreamSynchronize(compute_));
+  HIP_CHECK(hipStreamSynchronize(comm_));
+  tr_->barrier();
+  Stats s;
+  s.seconds = tr_->allreduce_max(now_s() - t0);
+  s.steps = iters;
+  s.t = t_;
+  return s;
+}
+
+Stats Engine::run_until(double t_end) {
+  const double dt0 = stable_dt();
+  HIP_CHECK(hipDeviceSynchronize());
+  tr_->barrier();
+  const double t0 = now_s();
+  int n = 0;
+  while (t_ < t_end * (1 - 1e-14)) {
+    double dt = dt0;
+    if (t_ + dt > t_end) dt = t_end - t_;
+    step(dt);
+    ++n;
+  }
+  HIP_CHECK(hipStreamSynchronize(compute_));
+  HIP_CHECK(hipStreamSynchronize(comm_));
+  tr_->barrier();
+  Stats s;
+  s.seconds = tr_->allreduce_max(now_s() - t0);
+  s.steps = n;
+  s.t = t_;
+  return s;
+}
+
+void Engine::error_norms(double& l1, double& l2, double& linf) {
+  const int G = slab_.ghost, c = slab_.count();
+  void* ex = nullptr;
+  HIP_CHECK(hipMalloc(&ex, plane_bytes_ * c));
+  double scale = 1.0;
+  const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
+  if (p_.ic == 2) {  // sine: separable decay
+    const double Lx = (p_.nx - 1) * dx, Ly = (p_.ny - 1) * dy;
+    double lam = 1.0 / (Lx * Lx) + 1.0 / (Ly * Ly);
+    if (p_.dims == 3) lam += 1.0 / std::pow((p_.nz - 1) * dz, 2);
+    scale = std::exp(-p_.K * M_PI * M_PI * lam * t_);
+  } else if (p_.ic == 3) {  // heat kernel from t0 = ic_p1
+    scale = std::pow(p_.ic_p1 / t_, p_.dims / 2.0);
+  }
+  const double p0 = p_.ic == 3 ? p_.K : p_.ic_p0, p1 = p_.ic == 3 ? t_ : p_.ic_p1;
+  if (p_.dims == 3)
+    KERNEL_CHECK(advdiff_init_ic(p_.dtype, p_.ic, ex, p_.nx, p_.ny, c, sy_, sz_, slab_.start(),
+                                 p_.nx, p_.ny, p_.nz, dx, dy, dz, p0, p1, compute_));
+  else
+    KERNEL_CHECK(advdiff_init_ic(p_.dtype, p_.ic, ex, p_.nx, c, 1, sy_, sz_, slab_.start(), p_.nx,
+                                 p_.ny, 1, dx, dy, 0.0, p0, p1, compute_));
+  KERNEL_CHECK(advdiff_scale(p_.dtype, ex, (int64_t)(plane_bytes_ / elem_) * c, scale, compute_));
+  void* ws = nullptr;
+  double* res = nullptr;
+  HIP_CHECK(hipMalloc(&ws, advdiff_reduce_workspace_bytes()));
+  HIP_CHECK(hipMalloc(&res, 3 * sizeof(double)));
+  if (p_.dims == 3)
+    KERNEL_CHECK(advdiff_reduce_norms(p_.dtype, plane(u_, G), ex, sy_, sz_, 0, p_.nx, 0, p_.ny,
+                                      0, c, ws, res, compute_));
+  else
+    KERNEL_CHECK(advdiff_reduce_norms(p_.dtype, plane(u_, G), ex, sy_, sz_ * c, 0, p_.nx, 0, c,
+                                      0, 1, ws, res, compute_));
+  double h[3];
+  HIP_CHECK(hipMemcpyAsync(h, res, sizeof(h), hipMemcpyDeviceToHost, compute_));
+  HIP_CHECK(hipStreamSynchronize(compute_));
+  (void)hipFree(ws);
+  (void)hipFree(res);
+  (void)hipFree(ex);
+  const double vol = dx * dy * (p_.dims == 3 ? dz : 1.0);
+  l1 = vol * tr_->allreduce_sum(h[0]);
+  l2 = std::sqrt(vol * tr_->allreduce_sum(h[1]));
+  linf = tr_->allreduce_max(h[2]);
+}
+
+std::vector<float> Engine::gather_float32() {
+  HIP_CHECK(hipStreamSynchronize(comm_));
+  HIP_CHECK(hipStreamSynchronize(compute_));
+  const int G = slab_.ghost, c = slab_.count();
+  std::vector<char> raw(plane_bytes_ * c);
+  HIP_CHECK(hipMemcpy(raw.data(), plane(u_, G), raw.size(), hipMemcpyDeviceToHost));
+  const int rows = p_.dims == 3 ? c * p_.ny : c;
+  std::vector<char> packed((size_t)rows * p_.nx * sizeof(float));
+  float* dst = (float*)packed.data();
+  for (int r = 0; r < rows; ++r)
+    for (int i = 0; i < p_.nx; ++i) {
+      const size_t src = (size_t)r * sy_ + i;
+      dst[(size_t)r * p_.nx + i] = elem_ == 8 ? (float)((const double*)raw.data())[src]
+                                              : ((const float*)raw.data())[src];
+    }
+  std::vector<char> all = tr_->gather(packed);
+  std::vector<float> out(all.size() / sizeof(float));
+  if (!all.empty()) std::memcpy(out.data(), all.data(), all.size());
+  return out;
+}
+
+static std::string fmt(const char* f, double v) {
+  char b[128];
+  std::snprintf(b, sizeof(b), f, v);
+  return b;
+}
+
+std::string summary_multigpu(const std::string& title, const std::string& opt, const Stats& s,
+                             const Problem& p, int nprocs) {
+  const std::string sep(67, '=');
+  const double gflops = s.seconds > 0 ? 3.0 * s.steps * p.cells() * 1e-9 * 8.0 / s.seconds : 0;
+  const double mlups = s.seconds > 0 ? p.cells() * (double)s.steps / s.seconds / 1e6 : 0;
+  std::ostringstream o;
+  o << "=======================" << title << "=====================\n";
+  o << "Optimization                                 :  " << opt << "\n";
+  o << "Kernel time ex. data transfers               :  " << fmt("%lf", s.seconds) << " seconds\n";
+  o << "Data transfer(s) HtD                         :  " << fmt("%lf", s.htod) << " seconds\n";
+  o << "Data transfer(s) DtH                         :  " << fmt("%lf", s.dtoh) << " seconds\n";
+  o << sep << "\n";
+  o << "Total effective GFLOPs                       :  " << fmt("%lf", gflops) << "\n";
+  o << sep << "\n";
+  if (p.dims == 3)
+    o << "3D Grid Size                                 :  " << p.nx << " x " << p.ny << " x "
+      << p.nz << "\n";
+  else
+    o << "2D Grid Size                                 :  " << p.nx << " x " << p.ny << "\n";
+  o << "Iterations                                   :  " << s.steps << " x 3 RK steps\n";
+  o << sep << "\n";
+  o << "MLUPS (cells x RK3 steps / s)                :  " << fmt("%.1f", mlups) << "\n";
+  o << "Stage-MLUPS                                  :  " << fmt("%.1f", 3 * mlups) << "\n";
+  o << "Processes / devices                          :  " << nprocs << " x gfx950\n";
+  o << sep << "\n";
+  return o.str();
+}
+
+void write_binary(const std::string& path, const std::vector<float>& data) {
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) {
+    std::perror(path.c_str());
+    return;
+  }
+  std::fwrite(data.data(), sizeof(float), data.size(), f);
+  std::fclose(f);
+}
+
+}  // namespace advdiff::rt

@@ -63,14 +63,14 @@ def launch(np_: int, argv: list[str], cpu: bool = False, timeout: float | None =
 # ----------------------------------------------------------------------------------
 # in-process API for tests
 # ----------------------------------------------------------------------------------
-def _spawn_entry(rank, world, port, device, fn, args, queue):
+def _spawn_entry(rank, world, port, device, backend, fn, args, queue):
     os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     try:
         import torch
         torch.set_num_threads(1)
         from .parallel.comm import Comm
-        comm = Comm.from_env(device=device)
+        comm = Comm.from_env(device=device, backend=backend)
         try:
             res = fn(comm, *args)
         finally:
@@ -80,13 +80,14 @@ def _spawn_entry(rank, world, port, device, fn, args, queue):
         queue.put((rank, "err", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
 
 
-def spawn_local(world: int, fn, *args, device: str = "cpu", timeout: float = 300.0):
+def spawn_local(world: int, fn, *args, device: str = "cpu", backend: str | None = None,
+                timeout: float = 300.0):
     """Run fn(comm, *args) on `world` local ranks; return [result_rank0, ...]."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_spawn_entry, args=(r, world, port, device, fn, args, q))
+    procs = [ctx.Process(target=_spawn_entry, args=(r, world, port, device, backend, fn, args, q))
              for r in range(world)]
     for p in procs:
         p.start()

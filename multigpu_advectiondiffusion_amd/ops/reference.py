@@ -37,7 +37,7 @@ def d2_fd2(m1, c, p1):
 def lf_split(u):
     """Local Lax-Friedrichs split of the Burgers flux: f± = ½(u²/2 ± |u|u)."""
     q = 0.25 * u * u
-    s = 0.5 * u.abs() * u
+    s = (0.5 * u.abs()) * u
     return q + s, q - s
 
 

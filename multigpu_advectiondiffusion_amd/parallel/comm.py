@@ -49,9 +49,11 @@ class Comm:
             ndev = torch.cuda.device_count()
             if ndev == 0:
                 raise RuntimeError("device=cuda requested but no GPU is visible")
-            if size > 1 and local_rank >= ndev:
+            share = os.environ.get("ADVDIFF_SHARE_GPU", "0") == "1"
+            if size > 1 and local_rank >= ndev and not (share and backend == "gloo"):
                 raise RuntimeError(f"local rank {local_rank} >= {ndev} visible GPUs "
-                                   "(one process per GPU; oversubscription is refused)")
+                                   "(one process per GPU; oversubscription is refused — "
+                                   "only gloo test runs may share with ADVDIFF_SHARE_GPU=1)")
             torch.cuda.set_device(local_rank % ndev)
             dev = torch.device("cuda", local_rank % ndev)
         else:

@@ -28,15 +28,19 @@ from .decomposition import SlabDecomposition
 class PendingExchange:
     """Handle of an in-flight halo exchange."""
 
-    def __init__(self, works, stream=None):
+    def __init__(self, works, stream=None, finish=None):
         self.works = works
         self.stream = stream
+        self.finish = finish
 
     def wait(self):
         """Make the CURRENT stream wait for completion (device); block on CPU/gloo."""
         for w in self.works:
             w.wait()
         self.works = []
+        if self.finish is not None:
+            self.finish()
+            self.finish = None
 
 
 class SlabHalo:
@@ -60,6 +64,49 @@ class SlabHalo:
             ops.append(dist.P2POp(dist.irecv, field[r0:r1], d.upper))
         return ops
 
+    def _start_host_staged(self, field: torch.Tensor, after_event=None) -> PendingExchange:
+        """Device tensors over a CPU-only backend (gloo): stage the G-plane slabs through
+        pinned host buffers on the comm stream — the reference's scheme
+        (`MultiGPU/Diffusion3d_Baseline/main.c:209-288`).  Used to run multi-process
+        tests on ONE GPU (RCCL refuses two ranks per device) and as a fallback transport;
+        the production path is RCCL (zero copy)."""
+        d = self.d
+        cur = torch.cuda.current_stream()
+        cs = self.comm_stream or cur
+        if after_event is None:
+            after_event = torch.cuda.Event()
+            after_event.record(cur)
+        cs.wait_event(after_event)
+        sends, recvs, ops = [], [], []
+        with torch.cuda.stream(cs):
+            for peer, (s0, s1), (r0, r1) in ((d.lower, d.send_lower(), d.recv_lower()),
+                                              (d.upper, d.send_upper(), d.recv_upper())):
+                if peer is None:
+                    continue
+                hs = torch.empty(field[s0:s1].shape, dtype=field.dtype, pin_memory=True)
+                hs.copy_(field[s0:s1], non_blocking=True)
+                hr = torch.empty_like(hs, pin_memory=True)
+                sends.append((peer, hs))
+                recvs.append((peer, hr, (r0, r1)))
+        cs.synchronize()  # host buffers filled before gloo reads them
+        for peer, hs in sends:
+            ops.append(dist.P2POp(dist.isend, hs, peer))
+        for peer, hr, _ in recvs:
+            ops.append(dist.P2POp(dist.irecv, hr, peer))
+        works = dist.batch_isend_irecv(ops)
+
+        def finish():
+            with torch.cuda.stream(cs):
+                for _, hr, (r0, r1) in recvs:
+                    field[r0:r1].copy_(hr, non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(cs)
+            torch.cuda.current_stream().wait_event(done)
+            # keep the pinned buffers alive until the copies have run
+            cs.synchronize()
+
+        return PendingExchange(works, cs, finish)
+
     def start(self, field: torch.Tensor, after_event=None) -> PendingExchange | None:
         """Begin exchanging the ghost planes of `field` (axis 0).
 
@@ -70,6 +117,8 @@ class SlabHalo:
         ops = self._ops(field)
         if not ops:
             return None
+        if field.is_cuda and self.comm.backend != "nccl":
+            return self._start_host_staged(field, after_event)
         if field.is_cuda and self.comm_stream is not None:
             cur = torch.cuda.current_stream()
             if after_event is None:

@@ -63,8 +63,7 @@ class Solver:
         elem = torch.empty((), dtype=dtype).element_size()
         self.sx = _row_pitch(grid.nx, elem) if pad_rows else grid.nx
         self.ic_name, self.ic_params = ic, ic_params
-        self.u = ics.evaluate(ic, grid.shape, grid.spacing, self.d.start - G, self.d.alloc,
-                              self.sx, dtype, self.device, ic_params)
+        self.u = self._initial_field(ic, ic_params)
         self.A = self.u.clone()
         self.B = self.u.clone()
         self.t = float(t0)
@@ -78,6 +77,28 @@ class Solver:
         self.interior, self.blo, self.bhi = self.d.split_ranges(model.border, model.radius)
         self._pending = {}
         self._reducer = None
+
+    def _initial_field(self, ic, params):
+        """IC of the local slab incl. ghosts (ghosts = the neighbours' planes at t0).
+        On the GPU the native init kernel fills it in place (no host array, no torch
+        temporaries); on the CPU the torch formulas of utils/ics.py."""
+        g, G = self.grid, self.model.radius
+        if self.device.type == "cuda":
+            p = params if params is not None else ics.IC_DEFAULT_PARAMS.get(ic, (0.0, 0.0))
+            if g.dims == 3:
+                u = torch.zeros((self.d.alloc, g.ny, self.sx), dtype=self.dtype, device=self.device)
+                stencil.init_ic_device(u, ics.ic_code(ic), nx=g.nx, ny=g.ny, nzl=self.d.alloc,
+                                       kg0=self.d.start - G, NX=g.nx, NY=g.ny, NZ=g.nz,
+                                       dx=g.spacing[0], dy=g.spacing[1], dz=g.spacing[2],
+                                       p0=p[0], p1=p[1])
+            else:
+                u = torch.zeros((self.d.alloc, self.sx), dtype=self.dtype, device=self.device)
+                stencil.init_ic_device(u, ics.ic_code(ic), nx=g.nx, ny=self.d.alloc, nzl=1,
+                                       kg0=self.d.start - G, NX=g.nx, NY=g.ny, NZ=1,
+                                       dx=g.spacing[0], dy=g.spacing[1], dz=0.0, p0=p[0], p1=p[1])
+            return u
+        return ics.evaluate(ic, g.shape, g.spacing, self.d.start - G, self.d.alloc, self.sx,
+                            self.dtype, self.device, params)
 
     # ------------------------------------------------------------------------------
     # geometry helpers

@@ -1,0 +1,99 @@
+"""The native C++ executables (bin/*, reference CLIs) on the GPU: results must be bitwise
+identical to the Python solver (same kernels, same launch geometry, same dt), and a
+2-rank run (host-staged socket transport, both ranks on the one GPU) must equal the
+1-rank run bitwise."""
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from multigpu_advectiondiffusion_amd import Burgers, Diffusion, Grid, Solver
+from multigpu_advectiondiffusion_amd.launch import free_port
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parent.parent
+BIN = ROOT / "bin"
+
+
+def _run(app, args, out, world=1, extra=()):
+    exe = BIN / app
+    assert exe.exists(), f"{exe} not built (make -C csrc apps)"
+    port = free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ADVDIFF_PORT=str(port))
+        cmd = [str(exe)] + [str(a) for a in args] + ["--write", str(out)] + list(extra)
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        so, _ = p.communicate(timeout=240)
+        outs.append(so)
+        assert p.returncode == 0, so
+    return outs[0]
+
+
+def _py(model, grid, ic, **run):
+    s = Solver(model, grid, dtype=torch.float64, device="cuda", ic=ic)
+    s.run(**run)
+    return s.gather().astype(np.float32)
+
+
+def test_diffusion3d_native_matches_python(tmp_path):
+    out = tmp_path / "d3.bin"
+    txt = _run("diffusion3d", [1.0, 1.0, 1.0, 1.0, 70, 60, 56, 20, 64, 4, 1], out,
+               extra=["--ic", "sine"])
+    assert "Total effective GFLOPs" in txt and "3D Grid Size                                 :  70 x 60 x 56" in txt
+    got = np.fromfile(out, dtype=np.float32).reshape(56, 60, 70)
+    exp = _py(Diffusion(K=1.0, order=4), Grid((70, 60, 56), (1.0, 1.0, 1.0)), "sine", iters=20)
+    assert np.array_equal(got, exp), np.abs(got - exp).max()
+
+
+def test_burgers3d_native_matches_python(tmp_path):
+    out = tmp_path / "b3.bin"
+    _run("burgers3d", [0.05, 0.3, 2.0, 2.0, 2.0, 48, 44, 40], out)
+    got = np.fromfile(out, dtype=np.float32).reshape(40, 44, 48)
+    exp = _py(Burgers(viscosity=1e-5, weno="z", cfl=0.3), Grid((48, 44, 40), (2.0, 2.0, 2.0)),
+              "gaussian", t_end=0.05)
+    assert np.array_equal(got, exp), np.abs(got - exp).max()
+
+
+def test_diffusion2d_and_burgers2d_native(tmp_path):
+    out = tmp_path / "d2.bin"
+    _run("diffusion2d", [1.0, 1.0, 1.0, 130, 90, 30], out, extra=["--ic", "disc", "--order", "2"])
+    got = np.fromfile(out, dtype=np.float32).reshape(90, 130)
+    exp = _py(Diffusion(K=1.0, order=2), Grid((130, 90), (1.0, 1.0)), "disc", iters=30)
+    assert np.array_equal(got, exp)
+    out = tmp_path / "b2.bin"
+    _run("burgers2d", [0.1, 0.4, 2.0, 2.0, 140, 100], out, extra=["--weno", "js", "--visc", "0"])
+    got = np.fromfile(out, dtype=np.float32).reshape(100, 140)
+    exp = _py(Burgers(viscosity=0.0, weno="js", cfl=0.4), Grid((140, 100), (2.0, 2.0)),
+              "gaussian", t_end=0.1)
+    assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("app,args,shape", [
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 66, 40, 45, 12], (45, 40, 66)),
+    ("burgers3d", [0.03, 0.3, 2.0, 2.0, 2.0, 40, 36, 41], (41, 36, 40)),
+])
+def test_native_multirank_socket_bitwise(tmp_path, app, args, shape):
+    one = tmp_path / "one.bin"
+    two = tmp_path / "two.bin"
+    _run(app, args, one)
+    txt = _run(app, args, two, world=2, extra=["--transport", "socket"])
+    assert "transport=socket" in txt
+    a = np.fromfile(one, dtype=np.float32).reshape(shape)
+    b = np.fromfile(two, dtype=np.float32).reshape(shape)
+    assert np.array_equal(a, b), np.abs(a - b).max()
+
+
+def test_native_error_norms_heat(tmp_path):
+    txt = _run("diffusion3d", [1.0, 10.0, 10.0, 10.0, 41, 41, 41, 30], tmp_path / "h.bin",
+               extra=["--error-norms"])
+    line = [l for l in txt.splitlines() if l.startswith("Linf norm")][0]
+    assert float(line.split(":")[1]) < 5e-2
