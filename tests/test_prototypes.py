@@ -108,7 +108,8 @@ def test_lf_weno_2d_3d_run():
     u0 = np.exp(-(X ** 2 + Y ** 2) / 0.1)
     u, t, it = P.lf_weno_fdm(u0, (x[1] - x[0],) * 2, 0.1, 0.4, "burgers", order=5)
     assert np.all(np.isfinite(u)) and it > 2
-    u3 = np.exp(-(X[:, :, None] ** 2 + Y[:, :, None] ** 2 + X[None, :, :1].T ** 2) / 0.1)
-    u, t, it = P.lf_weno_fdm(u3[:, :, :12], (x[1] - x[0],) * 3, 0.05, 0.3, "buckley", order=7,
-                             max_steps=3)
+    z = np.linspace(-1, 1, 16)
+    X3, Y3, Z3 = np.meshgrid(z, z, z, indexing="ij")
+    u3 = 0.2 + 0.5 * np.exp(-(X3 ** 2 + Y3 ** 2 + Z3 ** 2) / 0.1)
+    u, t, it = P.lf_weno_fdm(u3, (z[1] - z[0],) * 3, 0.5, 0.3, "buckley", order=7, max_steps=3)
     assert np.all(np.isfinite(u)) and it == 3
