@@ -58,6 +58,14 @@ def main():
         res[f"diffusion3d_fd{order}_stage1_TBps"] = round(2 * es * cells / t1 / 1e12, 2)
         res[f"diffusion3d_fd{order}_stage23_TBps"] = round(3 * es * cells / t2 / 1e12, 2)
         res[f"diffusion3d_fd{order}_step_mlups"] = round(cells / (t1 + 2 * t2) / 1e6, 1)
+    for order in (4, 2):
+        R = order // 2
+        kw = dict(nx=n, ny=n, k0=R, k1=n - R, zlo=R, zhi=n - R, border=R, order=order,
+                  cx=1.0, cy=1.0, cz=1.0, dt=0.01)
+        tf, _ = timeit(lambda: stencil.diffusion3d_step(u, A, **kw), args.reps)
+        res[f"diffusion3d_fd{order}_fused_step_us"] = round(tf * 1e6, 1)
+        res[f"diffusion3d_fd{order}_fused_step_mlups"] = round(cells / tf / 1e6, 1)
+        res[f"diffusion3d_fd{order}_fused_TBps_eff"] = round(2 * es * cells / tf / 1e12, 2)
     # copy roofline for reference: B <- A (16 B/cell)
     tc, _ = timeit(lambda: B.copy_(A), args.reps)
     res["copy_TBps"] = round(2 * es * cells / tc / 1e12, 2)

@@ -34,6 +34,17 @@ int advdiff_diffusion3d_stage(int dtype, const void* in, const void* u0, void* o
                               int border, int order, double cx, double cy, double cz,
                               double dt, double a, double b, void* stream);
 
+// Heat equation: ONE FULL SSP-RK3 step in one launch (temporal blocking, 16 B/cell):
+//     uout[k0:k1) = RK3(uin)  on i,j in [border, n-border).
+// Intermediate stages are evaluated on planes [zlo, zhi) (cells outside are frozen:
+// A = B = u there), so the launch reads uin planes k0-3R .. k1+3R-1 (clamped to
+// [0, nz_alloc)).  Multi-GPU: ghost width 3R, one exchange per step.  uin != uout.
+// Bit-identical to three advdiff_diffusion3d_stage launches.
+int advdiff_diffusion3d_step(int dtype, const void* uin, void* uout, int nx, int ny,
+                             int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int zlo,
+                             int zhi, int border, int order, double cx, double cy, double cz,
+                             double dt, void* stream);
+
 // 2-D heat stage, rows j in [j0, j1), columns i in [border, nx-border).
 int advdiff_diffusion2d_stage(int dtype, const void* in, const void* u0, void* out,
                               int nx, int64_t sy, int j0, int j1, int border, int order,

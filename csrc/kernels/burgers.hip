@@ -151,7 +151,9 @@ __global__ __launch_bounds__(TX* TY) void burgers3d_stage_kernel(
     }
     if (active) {
       const int64_t o = (int64_t)k * sz + own;
-      out[o] = rk_combine<T, USE_U0>(u0, o, ctr, L, dt, a, b);
+      T uo = T(0);
+      if constexpr (USE_U0) uo = u0[o];
+      out[o] = rk_stage<T, USE_U0>(uo, ctr, L, dt, a, b);
     }
     fz_lo = fz_hi;
 #pragma unroll
@@ -255,7 +257,9 @@ __global__ __launch_bounds__(TX) void burgers2d_stage_kernel(
     }
     if (active) {
       const int64_t o = (int64_t)jj * sy + i;
-      out[o] = rk_combine<T, USE_U0>(u0, o, ctr, L, dt, a, b);
+      T uo = T(0);
+      if constexpr (USE_U0) uo = u0[o];
+      out[o] = rk_stage<T, USE_U0>(uo, ctr, L, dt, a, b);
     }
     fy_lo = fy_hi;
 #pragma unroll

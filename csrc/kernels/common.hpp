@@ -32,7 +32,9 @@ __device__ __forceinline__ T clampi(T v, T lo, T hi) {
 }
 
 // Second-derivative stencils. `d2` returns the UNSCALED combination; the caller folds
-// 1/(12 dx²) (FD4) or 1/dx² (FD2) into a per-axis coefficient.
+// 1/(12 dx²) (FD4) or 1/dx² (FD2) into a per-axis coefficient.  Written with explicit
+// fma() and contraction off, so every kernel that evaluates a Laplacian (per-stage,
+// fused-step, Burgers viscous term) produces bit-identical values.
 template <int ORDER>
 struct FD;
 
@@ -41,7 +43,8 @@ struct FD<4> {
   static constexpr int R = 2;
   template <typename T>
   __device__ __forceinline__ static T d2(T m2, T m1, T c, T p1, T p2) {
-    return T(16) * (m1 + p1) - (m2 + p2) - T(30) * c;
+#pragma clang fp contract(off)
+    return fma(T(-30), c, fma(T(16), m1 + p1, -(m2 + p2)));
   }
 };
 
@@ -50,9 +53,31 @@ struct FD<2> {
   static constexpr int R = 1;
   template <typename T>
   __device__ __forceinline__ static T d2(T m1, T c, T p1) {
-    return (m1 + p1) - T(2) * c;
+#pragma clang fp contract(off)
+    return fma(T(-2), c, m1 + p1);
   }
 };
+
+// cx*d2x + cy*d2y + cz*d2z with a fixed evaluation order.
+template <typename T>
+__device__ __forceinline__ T lap3(T cx, T dxx, T cy, T dyy, T cz, T dzz) {
+#pragma clang fp contract(off)
+  return fma(cz, dzz, fma(cy, dyy, cx * dxx));
+}
+template <typename T>
+__device__ __forceinline__ T lap2(T cx, T dxx, T cy, T dyy) {
+#pragma clang fp contract(off)
+  return fma(cy, dyy, cx * dxx);
+}
+
+// SSP-RK3 stage value  a*u0 + b*(c + dt*L)  (a = 0: no u0 term), fixed evaluation order.
+template <typename T, bool USE_U0>
+__device__ __forceinline__ T rk_stage(T uo, T c, T L, T dt, T a, T b) {
+#pragma clang fp contract(off)
+  T v = b * fma(dt, L, c);
+  if constexpr (USE_U0) v = fma(a, uo, v);
+  return v;
+}
 
 // Burgers flux f(u) = u²/2, local Lax-Friedrichs split  f± = ½(f(u) ± |u|·u).
 // (reference: MultiGPU/Burgers3d_Baseline/Kernels.cu:256-264)
@@ -117,15 +142,6 @@ __device__ __forceinline__ T weno5_face(T p0, T p1, T p2, T p3, T p4,   // fp i-
                                         T m0, T m1, T m2, T m3, T m4) {  // fm i-1..i+3
 #pragma clang fp contract(off)
   return weno5<T, ZVARIANT>(p0, p1, p2, p3, p4) + weno5<T, ZVARIANT>(m4, m3, m2, m1, m0);
-}
-
-// SSP-RK3 (Shu–Osher) stage combination  out = a*u0 + b*(c + dt*L).
-// Stage coefficients (a, b): (0, 1), (3/4, 1/4), (1/3, 2/3).
-template <typename T, bool USE_U0>
-__device__ __forceinline__ T rk_combine(const T* u0, int64_t o, T c, T L, T dt, T a, T b) {
-  T v = b * (c + dt * L);
-  if constexpr (USE_U0) v = a * u0[o] + v;
-  return v;
 }
 
 }  // namespace advdiff

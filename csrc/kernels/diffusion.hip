@@ -87,18 +87,14 @@ __global__ __launch_bounds__(TX* TY) void diffusion3d_stage_kernel(
     const T ctr = zw[R];
     T lap;
     if constexpr (ORDER == 4) {
-      lap = cx * FD<4>::d2(c[lc - 2], c[lc - 1], ctr, c[lc + 1], c[lc + 2]) +
-            cy * FD<4>::d2(c[lc - 2 * LX], c[lc - LX], ctr, c[lc + LX], c[lc + 2 * LX]) +
-            cz * FD<4>::d2(zw[0], zw[1], ctr, zw[3], zw[4]);
+      lap = lap3(cx, FD<4>::d2(c[lc - 2], c[lc - 1], ctr, c[lc + 1], c[lc + 2]), cy,
+                 FD<4>::d2(c[lc - 2 * LX], c[lc - LX], ctr, c[lc + LX], c[lc + 2 * LX]), cz,
+                 FD<4>::d2(zw[0], zw[1], ctr, zw[3], zw[4]));
     } else {
-      lap = cx * FD<2>::d2(c[lc - 1], ctr, c[lc + 1]) +
-            cy * FD<2>::d2(c[lc - LX], ctr, c[lc + LX]) + cz * FD<2>::d2(zw[0], ctr, zw[2]);
+      lap = lap3(cx, FD<2>::d2(c[lc - 1], ctr, c[lc + 1]), cy,
+                 FD<2>::d2(c[lc - LX], ctr, c[lc + LX]), cz, FD<2>::d2(zw[0], ctr, zw[2]));
     }
-    if (active) {
-      T v = b * (ctr + dt * lap);
-      if constexpr (USE_U0) v = a * uo + v;
-      out[(int64_t)k * sz + own] = v;
-    }
+    if (active) out[(int64_t)k * sz + own] = rk_stage<T, USE_U0>(uo, ctr, lap, dt, a, b);
 #pragma unroll
     for (int q = 0; q < 2 * R; ++q) zw[q] = zw[q + 1];
   }
@@ -155,16 +151,12 @@ __global__ __launch_bounds__(TX) void diffusion2d_stage_kernel(
     const T ctr = yw[R];
     T lap;
     if constexpr (ORDER == 4) {
-      lap = cx * FD<4>::d2(c[lc - 2], c[lc - 1], ctr, c[lc + 1], c[lc + 2]) +
-            cy * FD<4>::d2(yw[0], yw[1], ctr, yw[3], yw[4]);
+      lap = lap2(cx, FD<4>::d2(c[lc - 2], c[lc - 1], ctr, c[lc + 1], c[lc + 2]), cy,
+                 FD<4>::d2(yw[0], yw[1], ctr, yw[3], yw[4]));
     } else {
-      lap = cx * FD<2>::d2(c[lc - 1], ctr, c[lc + 1]) + cy * FD<2>::d2(yw[0], ctr, yw[2]);
+      lap = lap2(cx, FD<2>::d2(c[lc - 1], ctr, c[lc + 1]), cy, FD<2>::d2(yw[0], ctr, yw[2]));
     }
-    if (active) {
-      T v = b * (ctr + dt * lap);
-      if constexpr (USE_U0) v = a * uo + v;
-      out[(int64_t)jj * sy + i] = v;
-    }
+    if (active) out[(int64_t)jj * sy + i] = rk_stage<T, USE_U0>(uo, ctr, lap, dt, a, b);
 #pragma unroll
     for (int q = 0; q < 2 * R; ++q) yw[q] = yw[q + 1];
   }

@@ -1,0 +1,479 @@
+// Temporally blocked heat-equation kernel: ONE launch = one FULL SSP-RK3 step.
+//
+// The per-stage kernels (diffusion.hip) move 64 B of HBM traffic per cell and step
+// (stage 1: 16 B, stages 2/3: 24 B each) and run at the HBM roof.  This kernel keeps the
+// two intermediate stage fields on chip and moves 16 B per cell and step (read u^n once,
+// write u^{n+1} once) — the reference has no counterpart; it is the MI355X-first answer
+// to a memory-bound stencil (SURVEY.md §2.5 "temporal blocking / wide halos").
+//
+// Overlapped (trapezoidal) tiling in x/y, a software pipeline in z:
+//   * A workgroup = NW waves.  Lane c of a wave is x = i0 - 2R + c (64 columns: one wave
+//     = one row of the stage-1 region); wave w owns region rows w, w+NW, ... (RPW rows).
+//   * Regions:  S1 (stage 1) = 64 x (TY+4R) points,  S2 = S1 shrunk by R,  S3 (outputs)
+//     = S1 shrunk by 2R = (64-4R) x TY.  Redundant stage-1/2 evaluations on the S1/S2
+//     rims replace any inter-workgroup communication.
+//   * z pipeline: iteration k computes A(k+2R) on S1, B(k+R) on S2 and u^{n+1}(k) on S3.
+//     z-neighbours live in per-thread register windows u(k..k+3R), A(k..k+2R),
+//     B(k-R..k+R); x/y neighbours come from three double-buffered LDS planes
+//     (u(k+2R) incl. an R-cell rim, A(k+R), B(k)) written at the top of the iteration,
+//     so ONE barrier per plane orders everything.
+//   * Frozen Dirichlet cells (outside the interior box / planes [zlo, zhi)) carry
+//     A = B = u, exactly as the per-stage path (whose A/B buffers keep the IC there).
+// Every arithmetic step uses the shared fma helpers of common.hpp, so the result is
+// BIT-IDENTICAL to three per-stage launches (tests/test_fused_step_gpu.py).
+#include "common.hpp"
+#include "launch.hpp"
+#include "advdiff/kernels.h"
+
+namespace advdiff {
+
+template <typename T, int ORDER, int NW, int RPW>
+__global__ __launch_bounds__(64 * NW) void diffusion3d_step_kernel(
+    const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
+    int nz_alloc, int k0, int k1, int zlo, int zhi, int zchunk, int border, T cx, T cy, T cz,
+    T dt) {
+  constexpr int R = FD<ORDER>::R;
+  constexpr int W = 64;             // stage-1 columns (one wave)
+  constexpr int TX = W - 4 * R;     // output columns
+  constexpr int S1R = NW * RPW;     // stage-1 rows
+  constexpr int TY = S1R - 4 * R;   // output rows
+  constexpr int UW = W + 2 * R, UH = S1R + 2 * R;
+  constexpr int NT = 64 * NW;
+  constexpr int NHALO = UW * UH - W * S1R;
+  constexpr int NH = (NHALO + NT - 1) / NT;
+  static_assert(TY > 0, "too few rows per workgroup");
+
+  __shared__ T sU[2][UH * UW];
+  __shared__ T sA[2][S1R * W];
+  __shared__ T sB[2][S1R * W];
+
+  const int lane = threadIdx.x, w = threadIdx.y, tid = w * 64 + lane;
+  const int i0 = blockIdx.x * TX, j0 = blockIdx.y * TY;
+  const int x = i0 - 2 * R + lane;
+  const int kc0 = k0 + (int)blockIdx.z * zchunk;
+  const int kc1 = min(kc0 + zchunk, k1);
+  const bool xin = x >= border && x < nx - border;
+  const bool s2c = lane >= R && lane < W - R;
+  const bool s3c = lane >= 2 * R && lane < W - 2 * R;
+  const int xc = clampi(x, 0, nx - 1);
+
+  int row[RPW], off[RPW];
+  bool inxy[RPW], s2r[RPW], s3r[RPW];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    row[q] = w + q * NW;
+    const int y = j0 - 2 * R + row[q];
+    inxy[q] = xin && y >= border && y < ny - border;
+    s2r[q] = row[q] >= R && row[q] < S1R - R;
+    s3r[q] = row[q] >= 2 * R && row[q] < S1R - 2 * R;
+    off[q] = clampi(y, 0, ny - 1) * (int)sy + xc;
+  }
+  // halo cells of the u plane (the R-wide rim around S1), precomputed per thread
+  int hl[NH], ho[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    int idx = tid + h * NT;  // enumerate the rim: top R rows, bottom R rows, left/right R cols
+    hl[h] = -1;
+    ho[h] = 0;
+    if (idx < NHALO) {
+      int ur, uc;
+      if (idx < R * UW) {  // top rows
+        ur = idx / UW;
+        uc = idx - ur * UW;
+      } else if ((idx -= R * UW) < R * UW) {  // bottom rows
+        ur = S1R + R + idx / UW;
+        uc = idx % UW;
+      } else {  // side columns of the S1 rows
+        idx -= R * UW;
+        ur = R + idx / (2 * R);
+        const int cc = idx % (2 * R);
+        uc = cc < R ? cc : W + cc;
+      }
+      hl[h] = ur * UW + uc;
+      ho[h] = clampi(j0 - 3 * R + ur, 0, ny - 1) * (int)sy + clampi(i0 - 3 * R + uc, 0, nx - 1);
+    }
+  }
+
+  auto plane = [&](int k) { return uin + (int64_t)clampi(k, 0, nz_alloc - 1) * sz; };
+
+  T uw[RPW][3 * R + 1], aw[RPW][2 * R + 1], bw[RPW][2 * R + 1];
+  const int kst = kc0 - 4 * R;
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+#pragma unroll
+    for (int s = 0; s < 3 * R; ++s) uw[q][s] = plane(kst + s)[off[q]];
+#pragma unroll
+    for (int s = 0; s <= 2 * R; ++s) aw[q][s] = bw[q][s] = T(0);
+  }
+  T hv[NH], un[RPW];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) hv[h] = plane(kst + 2 * R)[ho[h]];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) un[q] = plane(kst + 3 * R)[off[q]];
+
+  const T third = T(1.0 / 3.0), two3 = T(2.0 / 3.0);
+  for (int k = kst; k < kc1; ++k) {
+    const int set = k & 1;
+    T* pU = sU[set];
+    T* pA = sA[set];
+    T* pB = sB[set];
+    // ---- stage the planes: u(k+2R) (own + rim), A(k+R), B(k) ----
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      uw[q][3 * R] = un[q];
+      pU[(row[q] + R) * UW + lane + R] = uw[q][2 * R];
+      pA[row[q] * W + lane] = aw[q][R];
+      pB[row[q] * W + lane] = bw[q][R];
+    }
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+      if (hl[h] >= 0) pU[hl[h]] = hv[h];
+    if (k + 1 < kc1) {  // next plane's loads stay in flight across this plane's compute
+#pragma unroll
+      for (int h = 0; h < NH; ++h) hv[h] = plane(k + 1 + 2 * R)[ho[h]];
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) un[q] = plane(k + 1 + 3 * R)[off[q]];
+    }
+    __syncthreads();
+
+    // Every stage is evaluated UNCONDITIONALLY on all lanes of its (wave-uniform) rows
+    // and the frozen/rim lanes are fixed up with a select: straight-line code lets the
+    // compiler issue the LDS reads of all rows before the first FMA (latency hiding).
+    // ---- stage 1: A(k+2R) on S1 ----
+    const int p1 = k + 2 * R;
+    const bool z1 = p1 >= zlo && p1 < zhi;
+    T lapA[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const T c = uw[q][2 * R];
+      const int l = (row[q] + R) * UW + lane + R;
+      if constexpr (R == 2)
+        lapA[q] = lap3(cx, FD<4>::d2(pU[l - 2], pU[l - 1], c, pU[l + 1], pU[l + 2]), cy,
+                       FD<4>::d2(pU[l - 2 * UW], pU[l - UW], c, pU[l + UW], pU[l + 2 * UW]), cz,
+                       FD<4>::d2(uw[q][2], uw[q][3], c, uw[q][5], uw[q][6]));
+      else
+        lapA[q] = lap3(cx, FD<2>::d2(pU[l - 1], c, pU[l + 1]), cy,
+                       FD<2>::d2(pU[l - UW], c, pU[l + UW]), cz, FD<2>::d2(uw[q][1], c, uw[q][3]));
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const T c = uw[q][2 * R];
+      const T v = rk_stage<T, false>(T(0), c, lapA[q], dt, T(0), T(1));
+      aw[q][2 * R] = (z1 && inxy[q]) ? v : c;
+    }
+    // ---- stage 2: B(k+R) on S2 ----
+    if (k >= kc0 - 2 * R) {
+      const int p2 = k + R;
+      const bool z2 = p2 >= zlo && p2 < zhi;
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const T uo = uw[q][R];
+        if (!s2r[q]) {  // wave-uniform
+          bw[q][2 * R] = uo;
+          continue;
+        }
+        const int l = row[q] * W + lane;
+        const T c = aw[q][R];
+        T lap;
+        if constexpr (R == 2)
+          lap = lap3(cx, FD<4>::d2(pA[l - 2], pA[l - 1], c, pA[l + 1], pA[l + 2]), cy,
+                     FD<4>::d2(pA[l - 2 * W], pA[l - W], c, pA[l + W], pA[l + 2 * W]), cz,
+                     FD<4>::d2(aw[q][0], aw[q][1], c, aw[q][3], aw[q][4]));
+        else
+          lap = lap3(cx, FD<2>::d2(pA[l - 1], c, pA[l + 1]), cy,
+                     FD<2>::d2(pA[l - W], c, pA[l + W]), cz, FD<2>::d2(aw[q][0], c, aw[q][2]));
+        const T v = rk_stage<T, true>(uo, c, lap, dt, T(0.75), T(0.25));
+        bw[q][2 * R] = (z2 && inxy[q] && s2c) ? v : uo;
+      }
+    }
+    // ---- stage 3: u^{n+1}(k) on S3 ----
+    if (k >= kc0) {
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        if (!s3r[q]) continue;  // wave-uniform
+        const int l = row[q] * W + lane;
+        const T c = bw[q][R];
+        const T uo = uw[q][0];
+        T lap;
+        if constexpr (R == 2)
+          lap = lap3(cx, FD<4>::d2(pB[l - 2], pB[l - 1], c, pB[l + 1], pB[l + 2]), cy,
+                     FD<4>::d2(pB[l - 2 * W], pB[l - W], c, pB[l + W], pB[l + 2 * W]), cz,
+                     FD<4>::d2(bw[q][0], bw[q][1], c, bw[q][3], bw[q][4]));
+        else
+          lap = lap3(cx, FD<2>::d2(pB[l - 1], c, pB[l + 1]), cy,
+                     FD<2>::d2(pB[l - W], c, pB[l + W]), cz, FD<2>::d2(bw[q][0], c, bw[q][2]));
+        const T v = rk_stage<T, true>(uo, c, lap, dt, third, two3);
+        if (inxy[q] && s3c) uout[(int64_t)k * sz + off[q]] = v;  // k in [kc0,kc1): interior
+      }
+    }
+    // ---- advance the register windows ----
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+#pragma unroll
+      for (int s = 0; s < 3 * R; ++s) uw[q][s] = uw[q][s + 1];
+#pragma unroll
+      for (int s = 0; s < 2 * R; ++s) {
+        aw[q][s] = aw[q][s + 1];
+        bw[q][s] = bw[q][s + 1];
+      }
+    }
+  }
+}
+
+// Same algorithm with the z-windows kept as 8-slot register rings and the march
+// unrolled 8x: plane p lives in slot (p - kst) & 7, so at unrolled phase PH every
+// window index is a compile-time constant and no register is ever moved (the plain
+// version spends ~55 v_mov_b64 per plane shifting its windows).
+template <typename T, int ORDER, int NW, int RPW>
+__global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
+    const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
+    int nz_alloc, int k0, int k1, int zlo, int zhi, int zchunk, int border, T cx, T cy, T cz,
+    T dt) {
+  constexpr int R = FD<ORDER>::R;
+  constexpr int W = 64;
+  constexpr int TX = W - 4 * R;
+  constexpr int S1R = NW * RPW;
+  constexpr int TY = S1R - 4 * R;
+  constexpr int UW = W + 2 * R, UH = S1R + 2 * R;
+  constexpr int NT = 64 * NW;
+  constexpr int NHALO = UW * UH - W * S1R;
+  constexpr int NH = (NHALO + NT - 1) / NT;
+  static_assert(TY > 0 && 3 * R + 1 <= 8, "ring too small");
+
+  __shared__ T sU[2][UH * UW];
+  __shared__ T sA[2][S1R * W];
+  __shared__ T sB[2][S1R * W];
+
+  const int lane = threadIdx.x, w = threadIdx.y, tid = w * 64 + lane;
+  const int i0 = blockIdx.x * TX, j0 = blockIdx.y * TY;
+  const int x = i0 - 2 * R + lane;
+  const int kc0 = k0 + (int)blockIdx.z * zchunk;
+  const int kc1 = min(kc0 + zchunk, k1);
+  const bool xin = x >= border && x < nx - border;
+  const bool s2c = lane >= R && lane < W - R;
+  const bool s3c = lane >= 2 * R && lane < W - 2 * R;
+  const int xc = clampi(x, 0, nx - 1);
+
+  int row[RPW], off[RPW];
+  bool inxy[RPW], s2r[RPW], s3r[RPW];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    row[q] = w + q * NW;
+    const int y = j0 - 2 * R + row[q];
+    inxy[q] = xin && y >= border && y < ny - border;
+    s2r[q] = row[q] >= R && row[q] < S1R - R;
+    s3r[q] = row[q] >= 2 * R && row[q] < S1R - 2 * R;
+    off[q] = clampi(y, 0, ny - 1) * (int)sy + xc;
+  }
+  int hl[NH], ho[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    int idx = tid + h * NT;
+    hl[h] = -1;
+    ho[h] = 0;
+    if (idx < NHALO) {
+      int ur, uc;
+      if (idx < R * UW) {
+        ur = idx / UW;
+        uc = idx - ur * UW;
+      } else if ((idx -= R * UW) < R * UW) {
+        ur = S1R + R + idx / UW;
+        uc = idx % UW;
+      } else {
+        idx -= R * UW;
+        ur = R + idx / (2 * R);
+        const int cc = idx % (2 * R);
+        uc = cc < R ? cc : W + cc;
+      }
+      hl[h] = ur * UW + uc;
+      ho[h] = clampi(j0 - 3 * R + ur, 0, ny - 1) * (int)sy + clampi(i0 - 3 * R + uc, 0, nx - 1);
+    }
+  }
+  auto plane = [&](int k) { return uin + (int64_t)clampi(k, 0, nz_alloc - 1) * sz; };
+
+  T ru[RPW][8], ra[RPW][8], rb[RPW][8];  // plane p -> slot (p - kst) & 7
+  const int kst = kc0 - 4 * R;
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      ru[q][s] = s < 3 * R ? plane(kst + s)[off[q]] : T(0);
+      ra[q][s] = rb[q][s] = T(0);
+    }
+  }
+  T hv[NH], un[RPW];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) hv[h] = plane(kst + 2 * R)[ho[h]];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) un[q] = plane(kst + 3 * R)[off[q]];
+  const T third = T(1.0 / 3.0), two3 = T(2.0 / 3.0);
+
+  // one plane of the march at compile-time ring phase PH (k - kst == PH mod 8)
+  auto body = [&]<int PH>(int k) {
+    constexpr int U0 = PH & 7;            // u(k)
+    constexpr int UR = (PH + R) & 7;      // u(k+R)
+    constexpr int U2R = (PH + 2 * R) & 7; // u(k+2R)
+    constexpr int U3R = (PH + 3 * R) & 7; // u(k+3R)
+    constexpr int A0 = PH & 7, AR = (PH + R) & 7, A2R = (PH + 2 * R) & 7;  // A(k..)
+    constexpr int BM = (PH + 8 - R) & 7, B0 = PH & 7, BR = (PH + R) & 7;   // B(k-R..)
+    const int set = k & 1;
+    T* pU = sU[set];
+    T* pA = sA[set];
+    T* pB = sB[set];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      ru[q][U3R] = un[q];
+      pU[(row[q] + R) * UW + lane + R] = ru[q][U2R];
+      pA[row[q] * W + lane] = ra[q][AR];
+      pB[row[q] * W + lane] = rb[q][B0];
+    }
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+      if (hl[h] >= 0) pU[hl[h]] = hv[h];
+    if (k + 1 < kc1) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h) hv[h] = plane(k + 1 + 2 * R)[ho[h]];
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) un[q] = plane(k + 1 + 3 * R)[off[q]];
+    }
+    __syncthreads();
+    // stage 1: A(k+2R)
+    const int p1 = k + 2 * R;
+    const bool z1 = p1 >= zlo && p1 < zhi;
+    T lapA[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const T c = ru[q][U2R];
+      const int l = (row[q] + R) * UW + lane + R;
+      if constexpr (R == 2)
+        lapA[q] = lap3(cx, FD<4>::d2(pU[l - 2], pU[l - 1], c, pU[l + 1], pU[l + 2]), cy,
+                       FD<4>::d2(pU[l - 2 * UW], pU[l - UW], c, pU[l + UW], pU[l + 2 * UW]), cz,
+                       FD<4>::d2(ru[q][(PH + 2) & 7], ru[q][(PH + 3) & 7], c, ru[q][(PH + 5) & 7],
+                                 ru[q][(PH + 6) & 7]));
+      else
+        lapA[q] = lap3(cx, FD<2>::d2(pU[l - 1], c, pU[l + 1]), cy,
+                       FD<2>::d2(pU[l - UW], c, pU[l + UW]), cz,
+                       FD<2>::d2(ru[q][(PH + 1) & 7], c, ru[q][(PH + 3) & 7]));
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const T c = ru[q][U2R];
+      const T v = rk_stage<T, false>(T(0), c, lapA[q], dt, T(0), T(1));
+      ra[q][A2R] = (z1 && inxy[q]) ? v : c;
+    }
+    // stage 2: B(k+R)
+    if (k >= kc0 - 2 * R) {
+      const int p2 = k + R;
+      const bool z2 = p2 >= zlo && p2 < zhi;
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const T uo = ru[q][UR];
+        if (!s2r[q]) {
+          rb[q][BR] = uo;
+          continue;
+        }
+        const int l = row[q] * W + lane;
+        const T c = ra[q][AR];
+        T lap;
+        if constexpr (R == 2)
+          lap = lap3(cx, FD<4>::d2(pA[l - 2], pA[l - 1], c, pA[l + 1], pA[l + 2]), cy,
+                     FD<4>::d2(pA[l - 2 * W], pA[l - W], c, pA[l + W], pA[l + 2 * W]), cz,
+                     FD<4>::d2(ra[q][A0], ra[q][(PH + 1) & 7], c, ra[q][(PH + 3) & 7], ra[q][A2R]));
+        else
+          lap = lap3(cx, FD<2>::d2(pA[l - 1], c, pA[l + 1]), cy,
+                     FD<2>::d2(pA[l - W], c, pA[l + W]), cz, FD<2>::d2(ra[q][A0], c, ra[q][A2R]));
+        const T v = rk_stage<T, true>(uo, c, lap, dt, T(0.75), T(0.25));
+        rb[q][BR] = (z2 && inxy[q] && s2c) ? v : uo;
+      }
+    }
+    // stage 3: u^{n+1}(k)
+    if (k >= kc0) {
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        if (!s3r[q]) continue;
+        const int l = row[q] * W + lane;
+        const T c = rb[q][B0];
+        const T uo = ru[q][U0];
+        T lap;
+        if constexpr (R == 2)
+          lap = lap3(cx, FD<4>::d2(pB[l - 2], pB[l - 1], c, pB[l + 1], pB[l + 2]), cy,
+                     FD<4>::d2(pB[l - 2 * W], pB[l - W], c, pB[l + W], pB[l + 2 * W]), cz,
+                     FD<4>::d2(rb[q][BM], rb[q][(PH + 7) & 7], c, rb[q][(PH + 1) & 7], rb[q][BR]));
+        else
+          lap = lap3(cx, FD<2>::d2(pB[l - 1], c, pB[l + 1]), cy,
+                     FD<2>::d2(pB[l - W], c, pB[l + W]), cz, FD<2>::d2(rb[q][BM], c, rb[q][BR]));
+        const T v = rk_stage<T, true>(uo, c, lap, dt, third, two3);
+        if (inxy[q] && s3c) uout[(int64_t)k * sz + off[q]] = v;
+      }
+    }
+  };
+
+  for (int kb = kst; kb < kc1; kb += 8) {
+    body.template operator()<0>(kb);
+    if (kb + 1 < kc1) body.template operator()<1>(kb + 1);
+    if (kb + 2 < kc1) body.template operator()<2>(kb + 2);
+    if (kb + 3 < kc1) body.template operator()<3>(kb + 3);
+    if (kb + 4 < kc1) body.template operator()<4>(kb + 4);
+    if (kb + 5 < kc1) body.template operator()<5>(kb + 5);
+    if (kb + 6 < kc1) body.template operator()<6>(kb + 6);
+    if (kb + 7 < kc1) body.template operator()<7>(kb + 7);
+  }
+}
+
+template <typename T, int ORDER, int NW, int RPW>
+static hipError_t launch_step(const void* uin, void* uout, int nx, int ny, int64_t sy,
+                              int64_t sz, int nz_alloc, int k0, int k1, int zlo, int zhi,
+                              int border, double cx, double cy, double cz, double dt,
+                              hipStream_t st) {
+  constexpr int R = ORDER / 2;
+  constexpr int TX = 64 - 4 * R, TY = NW * RPW - 4 * R;
+  const int gx = div_up(nx, TX), gy = div_up(ny, TY);
+  static const int target = knob("STEP_TARGET_BLOCKS", 1280);
+  long long chunks = (target + (long long)gx * gy - 1) / ((long long)gx * gy);
+  int zc = div_up(k1 - k0, std::max<long long>(chunks, 1));
+  zc = std::max(zc, knob("STEP_MIN_CHUNK", 32));
+  const int gz = div_up(k1 - k0, zc);
+  const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
+  static const int ring = knob("STEP_RING", 1);
+  if (ring)
+    hipLaunchKernelGGL((diffusion3d_step_ring_kernel<T, ORDER, NW, RPW>), dim3(gx, gy, gz),
+                       dim3(64, NW, 1), 0, st, (const T*)uin, (T*)uout, nx, ny, sy, sz, nz_alloc,
+                       k0, k1, zlo, zhi, zc, border, T(cx * s), T(cy * s), T(cz * s), T(dt));
+  else
+    hipLaunchKernelGGL((diffusion3d_step_kernel<T, ORDER, NW, RPW>), dim3(gx, gy, gz),
+                       dim3(64, NW, 1), 0, st, (const T*)uin, (T*)uout, nx, ny, sy, sz, nz_alloc,
+                       k0, k1, zlo, zhi, zc, border, T(cx * s), T(cy * s), T(cz * s), T(dt));
+  return hipGetLastError();
+}
+
+}  // namespace advdiff
+
+extern "C" int advdiff_diffusion3d_step(int dtype, const void* uin, void* uout, int nx, int ny,
+                                        int64_t sy, int64_t sz, int nz_alloc, int k0, int k1,
+                                        int zlo, int zhi, int border, int order, double cx,
+                                        double cy, double cz, double dt, void* stream) {
+  using namespace advdiff;
+  if (k1 <= k0) return hipSuccess;
+  if (nx <= 0 || ny <= 0 || uin == uout || k0 < 0 || k1 > nz_alloc) return hipErrorInvalidValue;
+  if (sy * (int64_t)ny >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  static const int rpw = knob("STEP_RPW", 2);
+  if (dtype == ADVDIFF_F64) {
+    if (order == 4)
+      return rpw == 3 ? launch_step<double, 4, 8, 3>(uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1,
+                                                     zlo, zhi, border, cx, cy, cz, dt, st)
+                      : launch_step<double, 4, 12, 2>(uin, uout, nx, ny, sy, sz, nz_alloc, k0,
+                                                      k1, zlo, zhi, border, cx, cy, cz, dt, st);
+    if (order == 2)
+      return launch_step<double, 2, 12, 2>(uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
+                                           border, cx, cy, cz, dt, st);
+  } else if (dtype == ADVDIFF_F32) {
+    if (order == 4)
+      return launch_step<float, 4, 12, 2>(uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
+                                          border, cx, cy, cz, dt, st);
+    if (order == 2)
+      return launch_step<float, 2, 12, 2>(uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
+                                          border, cx, cy, cz, dt, st);
+  }
+  return hipErrorInvalidValue;
+}

@@ -65,6 +65,7 @@ class Model:
     flops_per_cell = 8.0     # reference's FLOPS constant (metric only)
     bytes_per_cell_step = 64.0  # HBM traffic estimate of the fused path (metric only)
     needs_umax = False
+    supports_fused = False   # one launch per full RK3 step (ghost width 3R)
 
     def bind(self, grid: Grid) -> None:
         self.grid = grid

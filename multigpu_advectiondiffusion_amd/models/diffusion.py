@@ -22,7 +22,8 @@ from .base import Model
 class Diffusion(Model):
     name = "diffusion"
 
-    def __init__(self, K: float = 1.0, order: int = 4, safety: float = 0.9, border=None):
+    def __init__(self, K: float = 1.0, order: int = 4, safety: float = 0.9, border=None,
+                 fused: bool = True):
         if order not in (2, 4):
             raise ValueError("order must be 2 (7-pt) or 4 (13-pt)")
         self.K = float(K)
@@ -32,6 +33,7 @@ class Diffusion(Model):
         self.border = self.radius if border is None else int(border)
         if self.border < self.radius:
             raise ValueError("frozen border must be >= stencil radius")
+        self.fused = bool(fused)
 
     def bind(self, grid):
         super().bind(grid)
@@ -41,8 +43,20 @@ class Diffusion(Model):
         self.title = f"Diffusion-{grid.dims}D MI355X-FD{self.order}"
 
     @property
+    def supports_fused(self) -> bool:
+        """3-D: one temporally blocked launch per RK3 step (diffusion_fused.hip)."""
+        return self.fused and getattr(self, "dims", 3) == 3
+
+    @property
     def bytes_per_cell_step(self):
-        return 64.0  # stage 1: 16 B, stages 2/3: 24 B (read in, read u0, write out)
+        # fused step: read u^n + write u^{n+1}; per-stage: 16 + 24 + 24 B
+        return 16.0 if self.supports_fused else 64.0
+
+    def step(self, uin, uout, lo, hi, zlo, zhi, dt, stream=None):
+        g = self.grid
+        stencil.diffusion3d_step(uin, uout, nx=g.nx, ny=g.ny, k0=lo, k1=hi, zlo=zlo, zhi=zhi,
+                                 border=self.border, order=self.order, cx=self.coef[0],
+                                 cy=self.coef[1], cz=self.coef[2], dt=dt, stream=stream)
 
     def stable_dt(self, umax=None) -> float:
         return self.safety / (2.0 * sum(self.coef))
@@ -61,5 +75,6 @@ class Diffusion(Model):
 
     def describe(self):
         d = super().describe()
-        d.update({"K": self.K, "order": self.order, "safety": self.safety})
+        d.update({"K": self.K, "order": self.order, "safety": self.safety,
+                  "fused_step": self.supports_fused})
         return d

@@ -134,6 +134,22 @@ def diffusion3d_stage(inp, u0, out, nx, ny, k0, k1, border, order, cx, cy, cz, d
              c, lap, dt, a, b)
 
 
+def diffusion3d_step(uin, uout, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy, cz, dt):
+    """One full SSP-RK3 step (semantics of advdiff_diffusion3d_step): intermediate stages
+    on the active planes [zlo, zhi) that the outputs [k0, k1) depend on, frozen cells
+    carry A = B = u."""
+    R = order // 2
+    nz = uin.shape[0]
+    A = uin.clone()
+    B = uin.clone()
+    lo1, hi1 = max(zlo, k0 - 2 * R, R), min(zhi, k1 + 2 * R, nz - R)
+    lo2, hi2 = max(zlo, k0 - R, R), min(zhi, k1 + R, nz - R)
+    diffusion3d_stage(uin, None, A, nx, ny, lo1, hi1, border, order, cx, cy, cz, dt, 0.0, 1.0)
+    diffusion3d_stage(A, uin, B, nx, ny, lo2, hi2, border, order, cx, cy, cz, dt, 0.75, 0.25)
+    diffusion3d_stage(B, uin, uout, nx, ny, k0, k1, border, order, cx, cy, cz, dt, 1.0 / 3.0,
+                      2.0 / 3.0)
+
+
 def diffusion2d_stage(inp, u0, out, nx, j0, j1, border, order, cx, cy, dt, a, b):
     if j1 <= j0 or nx - 2 * border <= 0:
         return

@@ -59,6 +59,23 @@ def diffusion3d_stage(inp, u0, out, *, nx, ny, k0, k1, border, order, cx, cy, cz
         ref.diffusion3d_stage(inp, u0, out, nx, ny, k0, k1, border, order, cx, cy, cz, dt, a, b)
 
 
+def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy, cz, dt,
+                     stream=None):
+    """A FULL SSP-RK3 step in one launch (temporal blocking): uout[k0:k1] = RK3(uin)."""
+    _check_layout(uin, uout)
+    if uin.data_ptr() == uout.data_ptr():
+        raise ValueError("the fused step needs distinct input/output buffers")
+    if uin.is_cuda:
+        lib = _lib.require()
+        assert 0 <= k0 and k1 <= uin.shape[0] and 0 <= zlo and zhi <= uin.shape[0]
+        code = lib.advdiff_diffusion3d_step(
+            _dtype_code(uin), _ptr(uin), _ptr(uout), nx, ny, uin.stride(1), uin.stride(0),
+            uin.shape[0], k0, k1, zlo, zhi, border, order, cx, cy, cz, dt, _stream_ptr(stream))
+        _lib.check(code, "diffusion3d_step")
+    else:
+        ref.diffusion3d_step(uin, uout, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy, cz, dt)
+
+
 def diffusion2d_stage(inp, u0, out, *, nx, j0, j1, border, order, cx, cy, dt, a, b,
                       stream=None):
     _check_layout(inp, u0, out)

@@ -45,7 +45,7 @@ class Solver:
     def __init__(self, model: Model, grid: Grid, comm: Comm | None = None, *,
                  dtype=torch.float64, device=None, ic: str = "sine", ic_params=None,
                  overlap: bool = True, pad_rows: bool = True, t0: float = 0.0,
-                 check_every: int = 0):
+                 check_every: int = 0, fused: bool | None = None):
         if comm is None:
             comm = Comm(device=device or ("cuda" if torch.cuda.is_available() else "cpu"))
             if comm.device.type == "cuda" and comm.device.index is None:
@@ -58,14 +58,24 @@ class Solver:
         self.overlap = overlap
         self.check_every = int(check_every)
         model.bind(grid)
-        G = model.radius
+        # fused: one temporally blocked launch per step -> ghost width 3R, ONE halo
+        # exchange per step; otherwise one fused launch + one exchange per RK stage.
+        self.fused = model.supports_fused if fused is None else (fused and model.supports_fused)
+        if self.fused and grid.n_decomposed // comm.size < 3 * model.radius:
+            self.fused = False  # slabs thinner than the wide halo: per-stage path
+        G = 3 * model.radius if self.fused else model.radius
+        self.ghost = G
         self.d = SlabDecomposition(grid.n_decomposed, comm.size, comm.rank, G)
         elem = torch.empty((), dtype=dtype).element_size()
         self.sx = _row_pitch(grid.nx, elem) if pad_rows else grid.nx
         self.ic_name, self.ic_params = ic, ic_params
         self.u = self._initial_field(ic, ic_params)
-        self.A = self.u.clone()
-        self.B = self.u.clone()
+        if self.fused:
+            self.un = self.u.clone()  # ping-pong partner; frozen cells keep the IC
+            self.A = self.B = None
+        else:
+            self.A = self.u.clone()
+            self.B = self.u.clone()
         self.t = float(t0)
         self.it = 0
         self.comm_stream = None
@@ -74,7 +84,10 @@ class Solver:
             self.comm_stream = torch.cuda.Stream(device=self.device, priority=hi)
         self.halo = SlabHalo(comm, self.d, self.comm_stream)
         self.full = self.d.compute_range(model.border)
-        self.interior, self.blo, self.bhi = self.d.split_ranges(model.border, model.radius)
+        self.interior, self.blo, self.bhi = self.d.split_ranges(model.border, G)
+        # planes (local, ghosts included) whose intermediate stages are updated
+        off = self.d.start - G
+        self.zact = (max(0, model.border - off), min(self.d.alloc, grid.n_decomposed - model.border - off))
         self._pending = {}
         self._reducer = None
 
@@ -82,7 +95,7 @@ class Solver:
         """IC of the local slab incl. ghosts (ghosts = the neighbours' planes at t0).
         On the GPU the native init kernel fills it in place (no host array, no torch
         temporaries); on the CPU the torch formulas of utils/ics.py."""
-        g, G = self.grid, self.model.radius
+        g, G = self.grid, self.ghost
         if self.device.type == "cuda":
             p = params if params is not None else ics.IC_DEFAULT_PARAMS.get(ic, (0.0, 0.0))
             if g.dims == 3:
@@ -110,7 +123,7 @@ class Solver:
         return self.u[o0:o1, ..., :self.grid.nx]
 
     def fields(self):
-        return self.u, self.A, self.B
+        return (self.u, self.un) if self.fused else (self.u, self.A, self.B)
 
     # ------------------------------------------------------------------------------
     # stepping
@@ -142,7 +155,40 @@ class Solver:
         with trace.range_("halo_start"):
             self._pending[id(out)] = self.halo.start(out)
 
+    def _launch_fused(self, rng, dt):
+        lo, hi = rng
+        if hi > lo:
+            self.model.step(self.u, self.un, lo, hi, self.zact[0], self.zact[1], dt)
+            trace.sync_check(f"{self.model.name} fused step [{lo},{hi})", self.device)
+
+    def _step_fused(self, dt: float) -> None:
+        pend = self._pending.pop(id(self.u), None)
+        if self.comm.size == 1:
+            self._launch_fused(self.full, dt)
+        elif self.overlap:
+            with trace.range_("interior"):
+                self._launch_fused(self.interior, dt)
+            with trace.range_("halo_wait"):
+                if pend is not None:
+                    pend.wait()
+            with trace.range_("boundary"):
+                self._launch_fused(self.blo, dt)
+                self._launch_fused(self.bhi, dt)
+        else:
+            if pend is not None:
+                pend.wait()
+            self._launch_fused(self.full, dt)
+        self.u, self.un = self.un, self.u
+        if self.comm.size > 1:
+            with trace.range_("halo_start"):
+                self._pending[id(self.u)] = self.halo.start(self.u)
+        self.t += dt
+        self.it += 1
+
     def step(self, dt: float) -> None:
+        if self.fused:
+            self._step_fused(dt)
+            return
         u, A, B = self.u, self.A, self.B
         (a1, b1), (a2, b2), (a3, b3) = RK3
         self._stage(u, None, A, a1, b1, dt)
@@ -285,13 +331,12 @@ class Solver:
         o0, o1 = self.d.owned
         src = torch.from_numpy(arr).to(self.device, self.dtype)
         self.u[o0:o1, ..., :self.grid.nx].copy_(src)
-        self.A.copy_(self.u)
-        self.B.copy_(self.u)
         self.t = float(meta["t"])
         self.it = int(meta["it"])
+        self._pending.clear()
         self.halo.exchange(self.u)
-        self.A.copy_(self.u)
-        self.B.copy_(self.u)
+        for f in self.fields()[1:]:
+            f.copy_(self.u)
         return meta
 
     # ------------------------------------------------------------------------------

@@ -81,3 +81,22 @@ def test_checkpoint_restart_across_decompositions(tmp_path):
     ref = _serial("burg3", 5)
     assert it == 5
     assert np.array_equal(g, ref)
+
+
+def _run_fused(comm, fused, steps):
+    model = Diffusion(K=1.0, order=4)
+    grid = Grid((20, 18, 40), (1.0, 1.0, 1.0))
+    s = Solver(model, grid, comm, dtype=torch.float64, ic="sine", fused=fused)
+    assert s.fused == fused
+    s.run(iters=steps)
+    g = s.gather()
+    return None if g is None else g.copy()
+
+
+def test_fused_step_wide_halo_matches_per_stage():
+    """Temporally blocked step (ghost width 3R, one exchange per step) == per-stage path
+    (ghost width R, three exchanges), on 1 and 3 ranks, bitwise."""
+    ref = spawn_local(1, _run_fused, False, 4)[0]
+    for world in (1, 3):
+        out = spawn_local(world, _run_fused, True, 4)[0]
+        assert np.array_equal(out, ref), (world, np.abs(out - ref).max())
