@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Run ONE stencil kernel repeatedly (for rocprofv3 --pmc / --kernel-trace).
+
+    python bench/profile_target.py {fused,stage,burgers} [--n 512] [--reps 5]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from multigpu_advectiondiffusion_amd.ops import stencil  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("which", choices=["fused", "stage", "burgers", "burgers_js"])
+ap.add_argument("--n", type=int, default=512)
+ap.add_argument("--reps", type=int, default=5)
+a = ap.parse_args()
+n = a.n if a.which in ("fused", "stage") else min(a.n, 256)
+u = torch.rand((n, n, n), dtype=torch.float64, device="cuda") * 0.5 + 0.1
+o = torch.rand_like(u)
+for _ in range(a.reps):
+    if a.which == "fused":
+        stencil.diffusion3d_step(u, o, nx=n, ny=n, k0=2, k1=n - 2, zlo=2, zhi=n - 2, border=2,
+                                 order=4, cx=1.0, cy=1.0, cz=1.0, dt=0.01)
+    elif a.which == "stage":
+        stencil.diffusion3d_stage(u, u, o, nx=n, ny=n, k0=2, k1=n - 2, border=2, order=4, cx=1.0,
+                                  cy=1.0, cz=1.0, dt=0.01, a=0.75, b=0.25)
+    else:
+        stencil.burgers3d_stage(u, u, o, nx=n, ny=n, k0=3, k1=n - 3, border=3,
+                                weno_z=a.which == "burgers", rdx=n / 2.0, rdy=n / 2.0,
+                                rdz=n / 2.0, vx=1e-5 * n * n / 4, vy=1e-5 * n * n / 4,
+                                vz=1e-5 * n * n / 4, dt=1e-4, a=0.75, b=0.25)
+torch.cuda.synchronize()
+print("done", a.which)

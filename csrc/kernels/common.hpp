@@ -31,6 +31,30 @@ __device__ __forceinline__ T clampi(T v, T lo, T hi) {
   return v < lo ? lo : (v > hi ? hi : v);
 }
 
+// XCD-aware workgroup placement (cdna_hip_programming.md §5.5 T1): the dispatcher deals
+// workgroups round-robin over the 8 XCDs (blocks b, b+8, ... share one L2), so
+// consecutive logical tiles — which overlap in their halos — would land on 8 different
+// L2s.  This bijective remap gives each XCD a CONTIGUOUS range of logical tiles (x
+// fastest, then y, then z), so the tiles running together on one XCD are neighbours and
+// their halo re-reads hit that XCD's L2.  Placement only affects speed, never results.
+struct Tile3 {
+  int x, y, z;
+};
+__device__ __forceinline__ Tile3 xcd_tile() {
+  const int nbx = gridDim.x, nby = gridDim.y;
+  const int total = nbx * nby * (int)gridDim.z;
+  const int b = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
+  const int q = total >> 3, r = total & 7;
+  const int xcd = b & 7, slot = b >> 3;
+  const int t = xcd * q + min(xcd, r) + slot;
+  Tile3 o;
+  o.x = t % nbx;
+  const int yz = t / nbx;
+  o.y = yz % nby;
+  o.z = yz / nby;
+  return o;
+}
+
 // Second-derivative stencils. `d2` returns the UNSCALED combination; the caller folds
 // 1/(12 dx²) (FD4) or 1/dx² (FD2) into a per-axis coefficient.  Written with explicit
 // fma() and contraction off, so every kernel that evaluates a Laplacian (per-stage,

@@ -48,9 +48,10 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_kernel(
   __shared__ T sB[2][S1R * W];
 
   const int lane = threadIdx.x, w = threadIdx.y, tid = w * 64 + lane;
-  const int i0 = blockIdx.x * TX, j0 = blockIdx.y * TY;
+  const Tile3 tile = xcd_tile();
+  const int i0 = tile.x * TX, j0 = tile.y * TY;
   const int x = i0 - 2 * R + lane;
-  const int kc0 = k0 + (int)blockIdx.z * zchunk;
+  const int kc0 = k0 + tile.z * zchunk;
   const int kc1 = min(kc0 + zchunk, k1);
   const bool xin = x >= border && x < nx - border;
   const bool s2c = lane >= R && lane < W - R;
@@ -245,9 +246,10 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
   __shared__ T sB[2][S1R * W];
 
   const int lane = threadIdx.x, w = threadIdx.y, tid = w * 64 + lane;
-  const int i0 = blockIdx.x * TX, j0 = blockIdx.y * TY;
+  const Tile3 tile = xcd_tile();
+  const int i0 = tile.x * TX, j0 = tile.y * TY;
   const int x = i0 - 2 * R + lane;
-  const int kc0 = k0 + (int)blockIdx.z * zchunk;
+  const int kc0 = k0 + tile.z * zchunk;
   const int kc1 = min(kc0 + zchunk, k1);
   const bool xin = x >= border && x < nx - border;
   const bool s2c = lane >= R && lane < W - R;
@@ -420,7 +422,7 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
   }
 }
 
-template <typename T, int ORDER, int NW, int RPW>
+template <typename T, int ORDER, int NW, int RPW, bool RING>
 static hipError_t launch_step(const void* uin, void* uout, int nx, int ny, int64_t sy,
                               int64_t sz, int nz_alloc, int k0, int k1, int zlo, int zhi,
                               int border, double cx, double cy, double cz, double dt,
@@ -434,8 +436,7 @@ static hipError_t launch_step(const void* uin, void* uout, int nx, int ny, int64
   zc = std::max(zc, knob("STEP_MIN_CHUNK", 32));
   const int gz = div_up(k1 - k0, zc);
   const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
-  static const int ring = knob("STEP_RING", 1);
-  if (ring)
+  if constexpr (RING)
     hipLaunchKernelGGL((diffusion3d_step_ring_kernel<T, ORDER, NW, RPW>), dim3(gx, gy, gz),
                        dim3(64, NW, 1), 0, st, (const T*)uin, (T*)uout, nx, ny, sy, sz, nz_alloc,
                        k0, k1, zlo, zhi, zc, border, T(cx * s), T(cy * s), T(cz * s), T(dt));
@@ -444,6 +445,25 @@ static hipError_t launch_step(const void* uin, void* uout, int nx, int ny, int64
                        dim3(64, NW, 1), 0, st, (const T*)uin, (T*)uout, nx, ny, sy, sz, nz_alloc,
                        k0, k1, zlo, zhi, zc, border, T(cx * s), T(cy * s), T(cz * s), T(dt));
   return hipGetLastError();
+}
+
+// Tile/schedule variants (A/B via ADVDIFF_STEP_CFG; measurements in profiles/).
+template <typename T, int ORDER>
+static hipError_t dispatch_step(int cfg, const void* uin, void* uout, int nx, int ny,
+                                int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int zlo,
+                                int zhi, int border, double cx, double cy, double cz, double dt,
+                                hipStream_t st) {
+#define STEPV(NW, RPW, RING)                                                                 \
+  return launch_step<T, ORDER, NW, RPW, RING>(uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, \
+                                              zhi, border, cx, cy, cz, dt, st)
+  switch (cfg) {
+    case 1: STEPV(12, 2, false);
+    case 2: STEPV(6, 4, false);
+    case 3: STEPV(8, 3, false);
+    case 4: STEPV(4, 6, false);
+    default: STEPV(12, 2, true);
+  }
+#undef STEPV
 }
 
 }  // namespace advdiff
@@ -457,23 +477,21 @@ extern "C" int advdiff_diffusion3d_step(int dtype, const void* uin, void* uout, 
   if (nx <= 0 || ny <= 0 || uin == uout || k0 < 0 || k1 > nz_alloc) return hipErrorInvalidValue;
   if (sy * (int64_t)ny >= (int64_t(1) << 31)) return hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  static const int rpw = knob("STEP_RPW", 2);
+  static const int cfg = knob("STEP_CFG", 0);
   if (dtype == ADVDIFF_F64) {
     if (order == 4)
-      return rpw == 3 ? launch_step<double, 4, 8, 3>(uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1,
-                                                     zlo, zhi, border, cx, cy, cz, dt, st)
-                      : launch_step<double, 4, 12, 2>(uin, uout, nx, ny, sy, sz, nz_alloc, k0,
-                                                      k1, zlo, zhi, border, cx, cy, cz, dt, st);
+      return dispatch_step<double, 4>(cfg, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
+                                      border, cx, cy, cz, dt, st);
     if (order == 2)
-      return launch_step<double, 2, 12, 2>(uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
-                                           border, cx, cy, cz, dt, st);
+      return dispatch_step<double, 2>(cfg, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
+                                      border, cx, cy, cz, dt, st);
   } else if (dtype == ADVDIFF_F32) {
     if (order == 4)
-      return launch_step<float, 4, 12, 2>(uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
-                                          border, cx, cy, cz, dt, st);
+      return dispatch_step<float, 4>(cfg, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
+                                     border, cx, cy, cz, dt, st);
     if (order == 2)
-      return launch_step<float, 2, 12, 2>(uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
-                                          border, cx, cy, cz, dt, st);
+      return dispatch_step<float, 2>(cfg, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
+                                     border, cx, cy, cz, dt, st);
   }
   return hipErrorInvalidValue;
 }
