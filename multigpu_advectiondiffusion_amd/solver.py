@@ -228,18 +228,75 @@ class Solver:
         umax = self.global_max_abs() if self.model.needs_umax else None
         return self.model.stable_dt(umax)
 
+    # ------------------------------------------------------------------------------
+    # hipGraph replay (single process): one graph = GRAPH_STEPS steps at a fixed dt.
+    # Small grids are launch-bound (a 1001² heat stage is ~5 µs of HBM time); replaying
+    # a captured graph removes the per-launch host cost (ctypes + hipLaunchKernel).
+    # ------------------------------------------------------------------------------
+    GRAPH_STEPS = 8  # even: the fused path ping-pongs u/un, so buffers line up on replay
+
+    def graph_capable(self) -> bool:
+        return (self.device.type == "cuda" and self.comm.size == 1 and not trace.SYNC_DEBUG
+                and not trace.TRACE)
+
+    def _graph_for(self, dt: float):
+        key = (float(dt), self.GRAPH_STEPS)
+        g = getattr(self, "_graphs", {}).get(key)
+        if g is not None:
+            return g
+        if not hasattr(self, "_graphs"):
+            self._graphs = {}
+        # state snapshot: capture executes nothing, but keep t/it bookkeeping exact
+        t, it = self.t, self.it
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream())
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(graph, stream=side):
+                for _ in range(self.GRAPH_STEPS):
+                    self.step(dt)
+        torch.cuda.current_stream().wait_stream(side)
+        self.t, self.it = t, it
+        self._graphs[key] = graph
+        return graph
+
+    def _advance(self, n: int, dt: float, use_graph: bool):
+        if use_graph and n >= self.GRAPH_STEPS:
+            g = self._graph_for(dt)
+            for _ in range(n // self.GRAPH_STEPS):
+                g.replay()
+                for _ in range(self.GRAPH_STEPS):  # same rounding as eager stepping
+                    self.t += dt
+                self.it += self.GRAPH_STEPS
+            n %= self.GRAPH_STEPS
+        for _ in range(n):
+            self.step(dt)
+
     def run(self, iters: int | None = None, t_end: float | None = None, dt: float | None = None,
-            callback=None) -> RunStats:
+            callback=None, graph: bool | None = None) -> RunStats:
         """Advance `iters` steps (fixed dt) or until `t_end`. Times the loop with a
         barrier + device sync on both sides (reference: MPI_Barrier-fenced MPI_Wtime,
-        `main.c:184-186,305-307`)."""
+        `main.c:184-186,305-307`).  graph=None: replay hipGraphs when possible (single
+        process, fixed dt, no per-step callback/watchdog)."""
         if iters is None and t_end is None:
             raise ValueError("give iters or t_end")
         fixed_dt = dt if dt is not None else (None if self.model.needs_umax else self.dt())
+        use_graph = (self.graph_capable() and fixed_dt is not None and callback is None
+                     and not self.check_every) if graph is None else graph
+        if use_graph:
+            self._graph_for(fixed_dt)  # capture outside the timed region (like a warm-up)
         self._sync()
         self.comm.barrier()
         t_start = time.perf_counter()
         steps0 = self.it
+        if use_graph:
+            if iters is not None:
+                n = iters
+            else:  # full steps that fit before t_end, then a short last step
+                n = max(int((t_end - self.t) / fixed_dt * (1 + 1e-12)), 0)
+                while n > 0 and self.t + n * fixed_dt > t_end:
+                    n -= 1
+            self._advance(n, fixed_dt, True)
         while True:
             if iters is not None and self.it - steps0 >= iters:
                 break
