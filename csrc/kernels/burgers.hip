@@ -279,20 +279,33 @@ __global__ __launch_bounds__(TX) void burgers2d_stage_kernel(
 constexpr int kBTX3 = 64, kBTY3 = 8;
 constexpr int kBTX2 = 256;
 
+template <typename T, bool WZ, bool VISC, bool U0, int TY>
+static hipError_t launch_b3_ty(const void* in, const void* u0, void* out, int nx, int ny,
+                               int64_t sy, int64_t sz, int k0, int k1, int border, double rdx,
+                               double rdy, double rdz, double vx, double vy, double vz,
+                               double dt, double a, double b, hipStream_t st) {
+  const int gx = div_up(nx, kBTX3), gy = div_up(ny, TY);
+  const int zc = pick_chunk(k1 - k0, (long long)gx * gy, 8, 256);
+  const int gz = div_up(k1 - k0, zc);
+  const double s = 1.0 / 12.0;
+  hipLaunchKernelGGL((burgers3d_stage_kernel<T, WZ, VISC, U0, kBTX3, TY>), dim3(gx, gy, gz),
+                     dim3(kBTX3, TY, 1), 0, st, (const T*)in, (const T*)u0, (T*)out, nx, ny, sy,
+                     sz, k0, k1, zc, border, T(rdx), T(rdy), T(rdz), T(vx * s), T(vy * s),
+                     T(vz * s), T(dt), T(a), T(b));
+  return hipGetLastError();
+}
+
 template <typename T, bool WZ, bool VISC, bool U0>
 static hipError_t launch_b3(const void* in, const void* u0, void* out, int nx, int ny,
                             int64_t sy, int64_t sz, int k0, int k1, int border, double rdx,
                             double rdy, double rdz, double vx, double vy, double vz, double dt,
                             double a, double b, hipStream_t st) {
-  const int gx = div_up(nx, kBTX3), gy = div_up(ny, kBTY3);
-  const int zc = pick_chunk(k1 - k0, (long long)gx * gy, 8, 256);
-  const int gz = div_up(k1 - k0, zc);
-  const double s = 1.0 / 12.0;
-  hipLaunchKernelGGL((burgers3d_stage_kernel<T, WZ, VISC, U0, kBTX3, kBTY3>), dim3(gx, gy, gz),
-                     dim3(kBTX3, kBTY3, 1), 0, st, (const T*)in, (const T*)u0, (T*)out, nx, ny,
-                     sy, sz, k0, k1, zc, border, T(rdx), T(rdy), T(rdz), T(vx * s), T(vy * s),
-                     T(vz * s), T(dt), T(a), T(b));
-  return hipGetLastError();
+  static const int ty = knob("B3_TY", kBTY3);
+  if (ty == 16)
+    return launch_b3_ty<T, WZ, VISC, U0, 16>(in, u0, out, nx, ny, sy, sz, k0, k1, border, rdx,
+                                             rdy, rdz, vx, vy, vz, dt, a, b, st);
+  return launch_b3_ty<T, WZ, VISC, U0, 8>(in, u0, out, nx, ny, sy, sz, k0, k1, border, rdx, rdy,
+                                          rdz, vx, vy, vz, dt, a, b, st);
 }
 
 template <typename T, bool WZ, bool VISC, bool U0>
