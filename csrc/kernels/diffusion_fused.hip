@@ -225,7 +225,7 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_kernel(
 // unrolled 8x: plane p lives in slot (p - kst) & 7, so at unrolled phase PH every
 // window index is a compile-time constant and no register is ever moved (the plain
 // version spends ~55 v_mov_b64 per plane shifting its windows).
-template <typename T, int ORDER, int NW, int RPW>
+template <typename T, int ORDER, int NW, int RPW, int PD>
 __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
     int nz_alloc, int k0, int k1, int zlo, int zhi, int zchunk, int border, T cx, T cy, T cz,
@@ -303,11 +303,17 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
       ra[q][s] = rb[q][s] = T(0);
     }
   }
-  T hv[NH], un[RPW];
+  // PD planes of global loads in flight: buffer PH % PD holds the rim of plane k+2R and
+  // the own values of plane k+3R at phase PH, and is refilled with plane k+PD's.
+  static_assert(8 % PD == 0, "prefetch distance must divide the ring unroll");
+  T hv[PD][NH], un[PD][RPW];
 #pragma unroll
-  for (int h = 0; h < NH; ++h) hv[h] = plane(kst + 2 * R)[ho[h]];
+  for (int d = 0; d < PD; ++d) {
 #pragma unroll
-  for (int q = 0; q < RPW; ++q) un[q] = plane(kst + 3 * R)[off[q]];
+    for (int h = 0; h < NH; ++h) hv[d][h] = plane(kst + d + 2 * R)[ho[h]];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) un[d][q] = plane(kst + d + 3 * R)[off[q]];
+  }
   const T third = T(1.0 / 3.0), two3 = T(2.0 / 3.0);
 
   // one plane of the march at compile-time ring phase PH (k - kst == PH mod 8)
@@ -318,25 +324,26 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
     constexpr int U3R = (PH + 3 * R) & 7; // u(k+3R)
     constexpr int A0 = PH & 7, AR = (PH + R) & 7, A2R = (PH + 2 * R) & 7;  // A(k..)
     constexpr int BM = (PH + 8 - R) & 7, B0 = PH & 7, BR = (PH + R) & 7;   // B(k-R..)
+    constexpr int PB = PH % PD;
     const int set = k & 1;
     T* pU = sU[set];
     T* pA = sA[set];
     T* pB = sB[set];
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
-      ru[q][U3R] = un[q];
+      ru[q][U3R] = un[PB][q];
       pU[(row[q] + R) * UW + lane + R] = ru[q][U2R];
       pA[row[q] * W + lane] = ra[q][AR];
       pB[row[q] * W + lane] = rb[q][B0];
     }
 #pragma unroll
     for (int h = 0; h < NH; ++h)
-      if (hl[h] >= 0) pU[hl[h]] = hv[h];
-    if (k + 1 < kc1) {
+      if (hl[h] >= 0) pU[hl[h]] = hv[PB][h];
+    if (k + PD < kc1) {
 #pragma unroll
-      for (int h = 0; h < NH; ++h) hv[h] = plane(k + 1 + 2 * R)[ho[h]];
+      for (int h = 0; h < NH; ++h) hv[PB][h] = plane(k + PD + 2 * R)[ho[h]];
 #pragma unroll
-      for (int q = 0; q < RPW; ++q) un[q] = plane(k + 1 + 3 * R)[off[q]];
+      for (int q = 0; q < RPW; ++q) un[PB][q] = plane(k + PD + 3 * R)[off[q]];
     }
     __syncthreads();
     // stage 1: A(k+2R)
@@ -422,7 +429,7 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
   }
 }
 
-template <typename T, int ORDER, int NW, int RPW, bool RING>
+template <typename T, int ORDER, int NW, int RPW, bool RING, int PD = 1>
 static hipError_t launch_step(const void* uin, void* uout, int nx, int ny, int64_t sy,
                               int64_t sz, int nz_alloc, int k0, int k1, int zlo, int zhi,
                               int border, double cx, double cy, double cz, double dt,
@@ -437,7 +444,7 @@ static hipError_t launch_step(const void* uin, void* uout, int nx, int ny, int64
   const int gz = div_up(k1 - k0, zc);
   const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
   if constexpr (RING)
-    hipLaunchKernelGGL((diffusion3d_step_ring_kernel<T, ORDER, NW, RPW>), dim3(gx, gy, gz),
+    hipLaunchKernelGGL((diffusion3d_step_ring_kernel<T, ORDER, NW, RPW, PD>), dim3(gx, gy, gz),
                        dim3(64, NW, 1), 0, st, (const T*)uin, (T*)uout, nx, ny, sy, sz, nz_alloc,
                        k0, k1, zlo, zhi, zc, border, T(cx * s), T(cy * s), T(cz * s), T(dt));
   else
@@ -453,14 +460,20 @@ static hipError_t dispatch_step(int cfg, const void* uin, void* uout, int nx, in
                                 int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int zlo,
                                 int zhi, int border, double cx, double cy, double cz, double dt,
                                 hipStream_t st) {
-#define STEPV(NW, RPW, RING)                                                                 \
-  return launch_step<T, ORDER, NW, RPW, RING>(uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, \
-                                              zhi, border, cx, cy, cz, dt, st)
+#define STEPV(NW, RPW, RING, ...)                                                          \
+  return launch_step<T, ORDER, NW, RPW, RING, ##__VA_ARGS__>(uin, uout, nx, ny, sy, sz, nz_alloc, \
+                                                             k0, k1, zlo, zhi, border, cx, cy, cz, \
+                                                             dt, st)
   switch (cfg) {
     case 1: STEPV(12, 2, false);
     case 2: STEPV(6, 4, false);
     case 3: STEPV(8, 3, false);
     case 4: STEPV(4, 6, false);
+    case 5: STEPV(8, 2, false);
+    case 6: STEPV(8, 2, true);
+    case 7: STEPV(16, 2, false);
+    case 8: STEPV(12, 2, true, 2);
+    case 9: STEPV(12, 2, true, 4);
     default: STEPV(12, 2, true);
   }
 #undef STEPV
