@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--burgers-steps", type=int, default=None)
     ap.add_argument("--no-burgers", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--decomp", default=None, help="process grid (default: z-slabs)")
     ap.add_argument("--device", default=None)
     args = ap.parse_args()
 
@@ -63,12 +64,13 @@ def main():
     grid = Grid(shape, (1.0, 1.0, 1.0))
     model = Diffusion(K=1.0, order=4)
     solver = Solver(model, grid, comm, dtype=torch.float64, ic="sine",
-                    overlap=not args.no_overlap)
+                    overlap=not args.no_overlap, decomp=args.decomp)
     dt = model.stable_dt()
     secs = timed(solver, args.steps, args.warmup, dt)
     mlups = grid.cells * args.steps / secs / 1e6
     # sanity: the solution must stay finite and decay (sine mode)
     finite = solver.check_finite()
+    pg = solver.pgrid
     del solver
     if dev.type == "cuda":
         torch.cuda.empty_cache()
@@ -88,7 +90,9 @@ def main():
         "data": "synthetic (sinusoidal IC sin(pi x)sin(pi y)sin(pi z), random-free analytic init)",
         "config": {"model": "diffusion3d FD4 13-point + SSP-RK3", "global_batch": 1,
                    "seq_len": grid.cells, "grid": list(shape),
-                   "parallelism": f"z-slab{n} (RCCL halo, overlapped)" if n > 1 else "single GPU",
+                   "parallelism": ("single GPU" if n == 1 else
+                                   f"z-slab{n} (RCCL halo, overlapped)" if pg[1:] == (1, 1) else
+                                   f"cartesian {'x'.join(map(str, pg))} (z,y,x; RCCL halo)"),
                    "cells_per_gpu": grid.cells // n},
         "max_abs_u": finite,
     }
@@ -99,7 +103,7 @@ def main():
         bgrid = Grid(bshape, (2.0, 2.0, 2.0))
         bmodel = Burgers(viscosity=1e-5, weno="z", cfl=0.3)
         bsolver = Solver(bmodel, bgrid, comm, dtype=torch.float64, ic="gaussian",
-                         overlap=not args.no_overlap)
+                         overlap=not args.no_overlap, decomp=args.decomp)
         bsteps = args.burgers_steps or args.steps
         bsecs = timed(bsolver, bsteps, args.warmup, bmodel.stable_dt())
         bml = bgrid.cells * bsteps / bsecs / 1e6

@@ -90,6 +90,11 @@ int advdiff_init_ic(int dtype, int ic, void* u, int nx, int ny, int nzl, int64_t
                     int64_t sz, int kg0, int NX, int NY, int NZ, double dx, double dy,
                     double dz, double p0, double p1, void* stream);
 
+// Same for an arbitrary local box of a Cartesian decomposition: local (i, j, k) is global
+// (ig0+i, jg0+j, kg0+k) (2-D: (ig0+i, jg0+j), nzl = 1); cells outside the domain are 0.
+int advdiff_init_ic_box(int dtype, int ic, void* u, int nx, int ny, int nzl, int64_t sy,
+                        int64_t sz, int ig0, int jg0, int kg0, int NX, int NY, int NZ,
+                        double dx, double dy, double dz, double p0, double p1, void* stream);
 // Copy planes (contiguous z-slabs) — a strided 3-D copy for halo staging and
 // x/y-face pack/unpack of a Cartesian decomposition:
 //   dst[(k)*dsz + j*dsy + i] = src[(k)*ssz + j*ssy + i], (i,j,k) in [0,ni)x[0,nj)x[0,nk)

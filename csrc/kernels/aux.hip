@@ -90,21 +90,21 @@ __global__ __launch_bounds__(kRedThreads) void norms_final(const Norm3* __restri
 // ------------------------------------------------------------------------------
 template <typename T>
 __global__ void init_ic_kernel(int ic, T* u, int nx, int ny, int nzl, int64_t sy, int64_t sz,
-                               int kg0, int NX, int NY, int NZ, double dx, double dy, double dz,
-                               double p0, double p1, int twod) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int j = blockIdx.y * blockDim.y + threadIdx.y;
+                               int ig0, int jg0, int kg0, int NX, int NY, int NZ, double dx,
+                               double dy, double dz, double p0, double p1, int twod) {
+  const int il = blockIdx.x * blockDim.x + threadIdx.x;
+  const int jl = blockIdx.y * blockDim.y + threadIdx.y;
   const int kl = blockIdx.z;
-  if (i >= nx || j >= ny || kl >= nzl) return;
-  // global indices: 3-D slabs are offset along z, 2-D slabs along y (rows)
+  if (il >= nx || jl >= ny || kl >= nzl) return;
+  // global indices of the local box (ghost cells beyond the domain are zero)
+  const int i = ig0 + il;
+  const int jg = jg0 + jl;
   const int k = twod ? 0 : kg0 + kl;
-  const int jl = j;
-  const int jg = twod ? kg0 + jl : jl;
   const double x = i * dx, y = jg * dy, z = k * dz;
   const double cx = 0.5 * (NX - 1) * dx, cy = 0.5 * (NY - 1) * dy, cz = 0.5 * (NZ - 1) * dz;
   const bool face = i == 0 || i == NX - 1 || jg == 0 || jg == NY - 1 ||
                     (!twod && (k == 0 || k == NZ - 1));
-  const bool outside = twod ? (jg < 0 || jg >= NY) : (k < 0 || k >= NZ);  // beyond the domain
+  const bool outside = jg < 0 || jg >= NY || i < 0 || i >= NX || (!twod && (k < 0 || k >= NZ));
   double v = 0.0;
   switch (ic) {
     case 1: {  // square jump: 1 inside the middle half of every axis
@@ -145,7 +145,7 @@ __global__ void init_ic_kernel(int ic, T* u, int nx, int ny, int nzl, int64_t sy
       v = 0.0;
   }
   if (outside) v = 0.0;
-  u[(int64_t)kl * sz + (int64_t)jl * sy + i] = (T)v;
+  u[(int64_t)kl * sz + (int64_t)jl * sy + il] = (T)v;
 }
 
 template <typename T>
@@ -210,22 +210,34 @@ extern "C" int advdiff_reduce_norms(int dtype, const void* x, const void* y, int
   return hipGetLastError();
 }
 
-extern "C" int advdiff_init_ic(int dtype, int ic, void* u, int nx, int ny, int nzl, int64_t sy,
-                               int64_t sz, int kg0, int NX, int NY, int NZ, double dx, double dy,
-                               double dz, double p0, double p1, void* stream) {
+extern "C" int advdiff_init_ic_box(int dtype, int ic, void* u, int nx, int ny, int nzl,
+                                   int64_t sy, int64_t sz, int ig0, int jg0, int kg0, int NX,
+                                   int NY, int NZ, double dx, double dy, double dz, double p0,
+                                   double p1, void* stream) {
   using namespace advdiff;
   hipStream_t st = (hipStream_t)stream;
   const int twod = NZ <= 1 ? 1 : 0;
   dim3 block(64, 4, 1), grid(div_up(nx, 64), div_up(ny, 4), std::max(nzl, 1));
   if (dtype == ADVDIFF_F64)
     hipLaunchKernelGGL(init_ic_kernel<double>, grid, block, 0, st, ic, (double*)u, nx, ny,
-                       std::max(nzl, 1), sy, sz, kg0, NX, NY, NZ, dx, dy, dz, p0, p1, twod);
+                       std::max(nzl, 1), sy, sz, ig0, jg0, kg0, NX, NY, NZ, dx, dy, dz, p0, p1,
+                       twod);
   else if (dtype == ADVDIFF_F32)
     hipLaunchKernelGGL(init_ic_kernel<float>, grid, block, 0, st, ic, (float*)u, nx, ny,
-                       std::max(nzl, 1), sy, sz, kg0, NX, NY, NZ, dx, dy, dz, p0, p1, twod);
+                       std::max(nzl, 1), sy, sz, ig0, jg0, kg0, NX, NY, NZ, dx, dy, dz, p0, p1,
+                       twod);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+extern "C" int advdiff_init_ic(int dtype, int ic, void* u, int nx, int ny, int nzl, int64_t sy,
+                               int64_t sz, int kg0, int NX, int NY, int NZ, double dx, double dy,
+                               double dz, double p0, double p1, void* stream) {
+  // slabs: 3-D offset along z, 2-D offset along y (rows)
+  const bool twod = NZ <= 1;
+  return advdiff_init_ic_box(dtype, ic, u, nx, ny, nzl, sy, sz, 0, twod ? kg0 : 0,
+                             twod ? 0 : kg0, NX, NY, NZ, dx, dy, dz, p0, p1, stream);
 }
 
 extern "C" int advdiff_copy_box(int dtype, void* dst, int64_t dsy, int64_t dsz, const void* src,

@@ -70,7 +70,8 @@ class Model:
     def bind(self, grid: Grid) -> None:
         self.grid = grid
 
-    def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None):  # pragma: no cover
+    def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None, nx=None, ny=None,
+              border=None):  # pragma: no cover
         raise NotImplementedError
 
     def stable_dt(self, umax: float | None = None) -> float:  # pragma: no cover

@@ -63,17 +63,21 @@ class Burgers(Model):
             dt = min(dt, 0.9 / (2.0 * sum(self.visc)))
         return dt
 
-    def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None):
+    def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None, nx=None, ny=None,
+              border=None):
         g = self.grid
+        nx = g.nx if nx is None else nx
+        ny = g.ny if ny is None else ny
+        border = self.border if border is None else border
         z = self.weno == "z"
         if self.dims == 3:
-            stencil.burgers3d_stage(inp, u0, out, nx=g.nx, ny=g.ny, k0=lo, k1=hi,
-                                    border=self.border, weno_z=z, rdx=self.rd[0],
+            stencil.burgers3d_stage(inp, u0, out, nx=nx, ny=ny, k0=lo, k1=hi,
+                                    border=border, weno_z=z, rdx=self.rd[0],
                                     rdy=self.rd[1], rdz=self.rd[2], vx=self.visc[0],
                                     vy=self.visc[1], vz=self.visc[2], dt=dt, a=a, b=b,
                                     stream=stream)
         else:
-            stencil.burgers2d_stage(inp, u0, out, nx=g.nx, j0=lo, j1=hi, border=self.border,
+            stencil.burgers2d_stage(inp, u0, out, nx=nx, j0=lo, j1=hi, border=border,
                                     weno_z=z, rdx=self.rd[0], rdy=self.rd[1], vx=self.visc[0],
                                     vy=self.visc[1], dt=dt, a=a, b=b, stream=stream)
 

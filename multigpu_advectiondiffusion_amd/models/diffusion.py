@@ -61,15 +61,20 @@ class Diffusion(Model):
     def stable_dt(self, umax=None) -> float:
         return self.safety / (2.0 * sum(self.coef))
 
-    def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None):
+    def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None, nx=None, ny=None,
+              border=None):
+        """nx/ny/border override the grid's for launches on a sub-box view (Cartesian)."""
         g = self.grid
+        nx = g.nx if nx is None else nx
+        ny = g.ny if ny is None else ny
+        border = self.border if border is None else border
         if self.dims == 3:
-            stencil.diffusion3d_stage(inp, u0, out, nx=g.nx, ny=g.ny, k0=lo, k1=hi,
-                                      border=self.border, order=self.order, cx=self.coef[0],
+            stencil.diffusion3d_stage(inp, u0, out, nx=nx, ny=ny, k0=lo, k1=hi,
+                                      border=border, order=self.order, cx=self.coef[0],
                                       cy=self.coef[1], cz=self.coef[2], dt=dt, a=a, b=b,
                                       stream=stream)
         else:
-            stencil.diffusion2d_stage(inp, u0, out, nx=g.nx, j0=lo, j1=hi, border=self.border,
+            stencil.diffusion2d_stage(inp, u0, out, nx=nx, j0=lo, j1=hi, border=border,
                                       order=self.order, cx=self.coef[0], cy=self.coef[1],
                                       dt=dt, a=a, b=b, stream=stream)
 

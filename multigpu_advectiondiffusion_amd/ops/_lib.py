@@ -41,6 +41,9 @@ _SIGS = {
                              c_int, c_int, c_vp, c_vp, c_vp],
     "advdiff_init_ic": [c_int, c_int, c_vp, c_int, c_int, c_int, c_i64, c_i64, c_int, c_int,
                         c_int, c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_vp],
+    "advdiff_init_ic_box": [c_int, c_int, c_vp, c_int, c_int, c_int, c_i64, c_i64, c_int,
+                            c_int, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_dbl, c_dbl,
+                            c_dbl, c_vp],
     "advdiff_copy_box": [c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int,
                          c_vp],
 }

@@ -194,3 +194,15 @@ def init_ic_device(u, ic_code, *, nx, ny, nzl, kg0, NX, NY, NZ, dx, dy, dz, p0=0
                                u3.stride(1), u3.stride(0), kg0, NX, NY, NZ, dx, dy, dz, p0,
                                p1, _stream_ptr(stream))
     _lib.check(code, "init_ic")
+
+
+def init_ic_box_device(u, ic_code, *, nx, ny, nzl, ig0, jg0, kg0, NX, NY, NZ, dx, dy, dz,
+                       p0=0.0, p1=0.0, stream=None):
+    """Fill a local box of a Cartesian decomposition: local (i, j, k) is global
+    (ig0+i, jg0+j, kg0+k); 2-D arrays use (i, j) with nzl = 1 and NZ = 1."""
+    lib = _lib.require()
+    u3 = u if u.dim() == 3 else u.unsqueeze(0)
+    code = lib.advdiff_init_ic_box(_dtype_code(u), ic_code, u3.data_ptr(), nx, ny, nzl,
+                                   u3.stride(1), u3.stride(0), ig0, jg0, kg0, NX, NY, NZ, dx,
+                                   dy, dz, p0, p1, _stream_ptr(stream))
+    _lib.check(code, "init_ic_box")

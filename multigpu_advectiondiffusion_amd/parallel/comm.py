@@ -128,6 +128,27 @@ class Comm:
         dist.send(local.detach().contiguous().to(dev), dst=0)
         return None
 
+    def gather_boxes(self, local: torch.Tensor, boxes, global_shape) -> torch.Tensor | None:
+        """Assemble per-rank blocks of a Cartesian decomposition on rank 0 (CPU tensor;
+        None elsewhere).  boxes[r] = ((start, count) per array axis) of rank r."""
+        if self.size == 1:
+            return local.detach().cpu()
+        dev = self._coll_device()
+        if self.rank != 0:
+            dist.send(local.detach().contiguous().to(dev), dst=0)
+            return None
+        out = torch.empty(tuple(global_shape), dtype=local.dtype)
+        for r in range(self.size):
+            box = boxes[r]
+            if r == 0:
+                part = local.detach().cpu()
+            else:
+                buf = torch.empty(tuple(c for _, c in box), dtype=local.dtype, device=dev)
+                dist.recv(buf, src=r)
+                part = buf.cpu()
+            out[tuple(slice(s, s + c) for s, c in box)] = part
+        return out
+
     def broadcast_object(self, obj):
         if self.size == 1:
             return obj

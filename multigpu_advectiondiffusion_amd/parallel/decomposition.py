@@ -139,3 +139,167 @@ def weak_scaling_grid(base: int, nranks: int, dims: int = 3) -> tuple:
         n //= 2
         ax = (ax - 1) % dims
     return tuple(base * x for x in f)
+
+
+# ---------------------------------------------------------------------------------------
+# Cartesian (2-D / 3-D) process grids
+# ---------------------------------------------------------------------------------------
+def _prod(xs):
+    p = 1
+    for x in xs:
+        p *= x
+    return p
+
+
+def parse_proc_grid(spec, world: int, shape_array: tuple, ghost: int) -> tuple:
+    """Process grid in ARRAY axis order (3-D: (pz, py, px); 2-D: (py, px)).
+
+    spec: None / "slab" -> (world, 1, 1) (the reference's layout);
+          "auto"        -> the factorisation of `world` with the smallest halo surface
+                            (ties: more ranks on the slower axes, which keeps the
+                            contiguous z faces);
+          "PZxPYxPX" / "PYxPX" string or a tuple -> explicit.
+    """
+    dims = len(shape_array)
+    if spec is None or spec == "slab":
+        return (world,) + (1,) * (dims - 1)
+    if isinstance(spec, str) and spec != "auto":
+        spec = tuple(int(v) for v in spec.lower().split("x"))
+    if spec == "auto":
+        best = None
+        for p in _factorisations(world, dims):
+            if any(n < q * max(ghost, 1) for n, q in zip(shape_array, p)):
+                continue
+            local = [n / q for n, q in zip(shape_array, p)]
+            # halo cells moved per rank: 2 faces per decomposed axis
+            surf = sum(2 * _prod(local) / local[a] for a in range(dims) if p[a] > 1)
+            key = (surf, tuple(-q for q in p))
+            if best is None or key < best[0]:
+                best = (key, p)
+        if best is None:
+            raise ValueError(f"no process grid of {world} ranks fits {shape_array}")
+        return best[1]
+    p = tuple(int(v) for v in spec)
+    if len(p) != dims or _prod(p) != world:
+        raise ValueError(f"process grid {p} does not match {dims}-D and world size {world}")
+    return p
+
+
+def _factorisations(n: int, dims: int):
+    if dims == 1:
+        yield (n,)
+        return
+    for a in range(1, n + 1):
+        if n % a == 0:
+            for rest in _factorisations(n // a, dims - 1):
+                yield (a,) + rest
+
+
+@dataclass(frozen=True)
+class CartesianDecomposition:
+    """Block decomposition over a process grid (row-major ranks, axis 0 slowest).
+
+    Every array axis is a 1-D :class:`SlabDecomposition`; axis 0 (the marched z / y axis)
+    always carries G ghost layers (as the slab layout does), the other axes carry G
+    ghosts only when they are split.  With ``pgrid = (P, 1, 1)`` this is exactly the slab
+    layout.  Star stencils (FD Laplacians, dimension-split WENO) need face ghosts only, so
+    edges/corners of the ghost shell are never exchanged.
+    """
+    shape: tuple   # global extents in array order
+    pgrid: tuple   # processes per array axis
+    rank: int
+    ghost: int
+
+    def __post_init__(self):
+        if len(self.shape) != len(self.pgrid):
+            raise ValueError("shape / process grid rank mismatch")
+        if not 0 <= self.rank < self.size:
+            raise ValueError(f"bad rank {self.rank}/{self.size}")
+        for a in range(self.dims):
+            self.axis(a)  # validates extents
+
+    @property
+    def dims(self) -> int:
+        return len(self.shape)
+
+    @property
+    def size(self) -> int:
+        return _prod(self.pgrid)
+
+    def coords_of(self, r: int) -> tuple:
+        c = []
+        for p in reversed(self.pgrid):
+            c.append(r % p)
+            r //= p
+        return tuple(reversed(c))
+
+    def rank_of(self, coords) -> int:
+        r = 0
+        for c, p in zip(coords, self.pgrid):
+            r = r * p + c
+        return r
+
+    @property
+    def coords(self) -> tuple:
+        return self.coords_of(self.rank)
+
+    @property
+    def is_slab(self) -> bool:
+        return all(p == 1 for p in self.pgrid[1:])
+
+    def ghost_of_axis(self, a: int) -> int:
+        return self.ghost if (a == 0 or self.pgrid[a] > 1) else 0
+
+    def axis(self, a: int, rank: int | None = None) -> SlabDecomposition:
+        c = self.coords_of(self.rank if rank is None else rank)
+        return SlabDecomposition(self.shape[a], self.pgrid[a], c[a], self.ghost_of_axis(a))
+
+    def neighbor(self, a: int, side: int):
+        """Rank of the neighbour along axis a on side -1 / +1 (None at the domain edge)."""
+        c = list(self.coords)
+        c[a] += side
+        if not 0 <= c[a] < self.pgrid[a]:
+            return None
+        return self.rank_of(c)
+
+    @property
+    def alloc(self) -> tuple:
+        return tuple(self.axis(a).alloc for a in range(self.dims))
+
+    def owned_box(self) -> tuple:
+        """Local (lo, hi) per axis of the owned cells."""
+        return tuple(self.axis(a).owned for a in range(self.dims))
+
+    def global_box(self, rank: int | None = None) -> tuple:
+        """Global (start, count) per axis of the cells owned by `rank`."""
+        out = []
+        for a in range(self.dims):
+            ax = self.axis(a, rank)
+            out.append((ax.start, ax.count))
+        return tuple(out)
+
+    def compute_box(self, border: int) -> tuple:
+        return tuple(self.axis(a).compute_range(border) for a in range(self.dims))
+
+    def split_boxes(self, border: int, width: int):
+        """Partition the compute box into (interior, [boundary boxes]).
+
+        Interior = cells >= `width` away from every face that has a neighbour (computable
+        while the halo is in flight).  The boundary shell is cut into at most 2*dims
+        disjoint boxes: axis-0 slabs over the full extent of the other axes, then axis-1
+        bands inside the axis-0 interior, and so on.  Empty boxes are dropped."""
+        full, inner, sides = [], [], []
+        for a in range(self.dims):
+            inter, blo, bhi = self.axis(a).split_ranges(border, width)
+            full.append(self.axis(a).compute_range(border))
+            inner.append(inter)
+            sides.append((blo, bhi))
+        boundary = []
+        for a in range(self.dims):
+            for rng in sides[a]:
+                box = tuple(inner[b] if b < a else (rng if b == a else full[b])
+                            for b in range(self.dims))
+                if all(hi > lo for lo, hi in box):
+                    boundary.append(box)
+        interior = tuple(inner)
+        return interior, boundary

@@ -26,8 +26,8 @@ import torch
 from .models.base import Grid, Model, RunStats
 from .ops import stencil
 from .parallel.comm import Comm
-from .parallel.decomposition import SlabDecomposition
-from .parallel.halo import SlabHalo
+from .parallel.decomposition import CartesianDecomposition, parse_proc_grid
+from .parallel.halo import CartesianHalo, SlabHalo
 from .utils import ics
 from .utils import io as aio
 from .utils import metrics, trace
@@ -45,7 +45,10 @@ class Solver:
     def __init__(self, model: Model, grid: Grid, comm: Comm | None = None, *,
                  dtype=torch.float64, device=None, ic: str = "sine", ic_params=None,
                  overlap: bool = True, pad_rows: bool = True, t0: float = 0.0,
-                 check_every: int = 0, fused: bool | None = None):
+                 check_every: int = 0, fused: bool | None = None, decomp=None):
+        """decomp: process grid — None/"slab" (split the slowest axis only, the
+        reference's layout), "auto" (smallest halo surface) or "PZxPYxPX" / a tuple in
+        array axis order ((pz, py, px) in 3-D, (py, px) in 2-D)."""
         if comm is None:
             comm = Comm(device=device or ("cuda" if torch.cuda.is_available() else "cpu"))
             if comm.device.type == "cuda" and comm.device.index is None:
@@ -60,14 +63,19 @@ class Solver:
         model.bind(grid)
         # fused: one temporally blocked launch per step -> ghost width 3R, ONE halo
         # exchange per step; otherwise one fused launch + one exchange per RK stage.
+        ashape = tuple(reversed(grid.shape))  # array axis order: (z, y, x) / (y, x)
+        self.pgrid = parse_proc_grid(decomp, comm.size, ashape, model.radius)
+        self.cart = any(p > 1 for p in self.pgrid[1:])
         self.fused = model.supports_fused if fused is None else (fused and model.supports_fused)
-        if self.fused and grid.n_decomposed // comm.size < 3 * model.radius:
-            self.fused = False  # slabs thinner than the wide halo: per-stage path
+        if self.fused and (self.cart or grid.n_decomposed // comm.size < 3 * model.radius):
+            self.fused = False  # x/y split, or slabs thinner than the wide halo: per stage
         G = 3 * model.radius if self.fused else model.radius
         self.ghost = G
-        self.d = SlabDecomposition(grid.n_decomposed, comm.size, comm.rank, G)
+        self.cd = CartesianDecomposition(ashape, self.pgrid, comm.rank, G)
+        self.d = self.cd.axis(0)
         elem = torch.empty((), dtype=dtype).element_size()
-        self.sx = _row_pitch(grid.nx, elem) if pad_rows else grid.nx
+        ax = self.cd.alloc[-1]
+        self.sx = _row_pitch(ax, elem) if pad_rows else ax
         self.ic_name, self.ic_params = ic, ic_params
         self.u = self._initial_field(ic, ic_params)
         if self.fused:
@@ -82,9 +90,15 @@ class Solver:
         if self.device.type == "cuda" and comm.size > 1:
             lo, hi = torch.cuda.Stream.priority_range()
             self.comm_stream = torch.cuda.Stream(device=self.device, priority=hi)
-        self.halo = SlabHalo(comm, self.d, self.comm_stream)
-        self.full = self.d.compute_range(model.border)
-        self.interior, self.blo, self.bhi = self.d.split_ranges(model.border, G)
+        if self.cart:
+            self.halo = CartesianHalo(comm, self.cd, self.comm_stream)
+            self.full = self.cd.compute_box(model.border)
+            self.interior, self.boundary = self.cd.split_boxes(model.border, G)
+        else:
+            self.halo = SlabHalo(comm, self.d, self.comm_stream)
+            self.full = self.d.compute_range(model.border)
+            self.interior, blo, bhi = self.d.split_ranges(model.border, G)
+            self.boundary = [blo, bhi]
         # planes (local, ghosts included) whose intermediate stages are updated
         off = self.d.start - G
         self.zact = (max(0, model.border - off), min(self.d.alloc, grid.n_decomposed - model.border - off))
@@ -96,6 +110,8 @@ class Solver:
         On the GPU the native init kernel fills it in place (no host array, no torch
         temporaries); on the CPU the torch formulas of utils/ics.py."""
         g, G = self.grid, self.ghost
+        if self.cart:
+            return self._initial_box(ic, params)
         if self.device.type == "cuda":
             p = params if params is not None else ics.IC_DEFAULT_PARAMS.get(ic, (0.0, 0.0))
             if g.dims == 3:
@@ -113,14 +129,39 @@ class Solver:
         return ics.evaluate(ic, g.shape, g.spacing, self.d.start - G, self.d.alloc, self.sx,
                             self.dtype, self.device, params)
 
+    def _initial_box(self, ic, params):
+        """Cartesian block (ghost shell included) of the IC."""
+        g, cd = self.grid, self.cd
+        offs = [cd.axis(a).start - cd.ghost_of_axis(a) for a in range(cd.dims)]
+        ext = list(cd.alloc)
+        if self.device.type == "cuda":
+            p = params if params is not None else ics.IC_DEFAULT_PARAMS.get(ic, (0.0, 0.0))
+            u = torch.zeros(tuple(ext[:-1]) + (self.sx,), dtype=self.dtype, device=self.device)
+            if g.dims == 3:
+                stencil.init_ic_box_device(u, ics.ic_code(ic), nx=ext[2], ny=ext[1], nzl=ext[0],
+                                           ig0=offs[2], jg0=offs[1], kg0=offs[0], NX=g.nx,
+                                           NY=g.ny, NZ=g.nz, dx=g.spacing[0], dy=g.spacing[1],
+                                           dz=g.spacing[2], p0=p[0], p1=p[1])
+            else:
+                stencil.init_ic_box_device(u, ics.ic_code(ic), nx=ext[1], ny=ext[0], nzl=1,
+                                           ig0=offs[1], jg0=offs[0], kg0=0, NX=g.nx, NY=g.ny,
+                                           NZ=1, dx=g.spacing[0], dy=g.spacing[1], dz=0.0,
+                                           p0=p[0], p1=p[1])
+            return u
+        return ics.evaluate_box(ic, g.shape, g.spacing, offs, ext, self.sx, self.dtype,
+                                self.device, params)
+
     # ------------------------------------------------------------------------------
     # geometry helpers
     # ------------------------------------------------------------------------------
     @property
     def owned(self) -> torch.Tensor:
-        """View of the owned planes (no ghosts, row padding cropped)."""
-        o0, o1 = self.d.owned
-        return self.u[o0:o1, ..., :self.grid.nx]
+        """View of the owned cells (no ghosts, row padding cropped)."""
+        return self.u[tuple(slice(lo, hi) for lo, hi in self.cd.owned_box())]
+
+    def _owned_xyz_box(self):
+        """Owned box in the reducer's (x, y, z) order of local indices."""
+        return tuple(reversed(self.cd.owned_box()))
 
     def fields(self):
         return (self.u, self.un) if self.fused else (self.u, self.A, self.B)
@@ -129,10 +170,33 @@ class Solver:
     # stepping
     # ------------------------------------------------------------------------------
     def _launch(self, inp, u0, out, rng, dt, a, b):
+        if self.cart:
+            self._launch_box(inp, u0, out, rng, dt, a, b)
+            return
         lo, hi = rng
         if hi > lo:
             self.model.stage(inp, u0, out, lo, hi, dt, a, b)
             trace.sync_check(f"{self.model.name} stage [{lo},{hi})", self.device)
+
+    def _launch_box(self, inp, u0, out, box, dt, a, b):
+        """Stage on a local box (array order).  The kernels update [border, n-border) of
+        the x/y extent they are given, so a box is launched on a VIEW widened by R on
+        each side with border R (the views never leave the allocation: every box lies
+        >= R inside it, see CartesianDecomposition)."""
+        if any(hi <= lo for lo, hi in box):
+            return
+        R = self.model.radius
+        if self.grid.dims == 3:
+            (z0, z1), (y0, y1), (x0, x1) = box
+            sl = (slice(None), slice(y0 - R, y1 + R), slice(x0 - R, x1 + R))
+            kw = dict(nx=x1 - x0 + 2 * R, ny=y1 - y0 + 2 * R, border=R)
+        else:
+            (z0, z1), (x0, x1) = box
+            sl = (slice(None), slice(x0 - R, x1 + R))
+            kw = dict(nx=x1 - x0 + 2 * R, border=R)
+        v = (lambda t: None if t is None else t[sl])
+        self.model.stage(v(inp), v(u0), v(out), z0, z1, dt, a, b, **kw)
+        trace.sync_check(f"{self.model.name} stage box {box}", self.device)
 
     def _stage(self, inp, u0, out, a, b, dt):
         pend = self._pending.pop(id(inp), None)
@@ -146,8 +210,8 @@ class Solver:
                 if pend is not None:
                     pend.wait()
             with trace.range_("boundary"):
-                self._launch(inp, u0, out, self.blo, dt, a, b)
-                self._launch(inp, u0, out, self.bhi, dt, a, b)
+                for rng in self.boundary:
+                    self._launch(inp, u0, out, rng, dt, a, b)
         else:
             if pend is not None:
                 pend.wait()
@@ -172,8 +236,8 @@ class Solver:
                 if pend is not None:
                     pend.wait()
             with trace.range_("boundary"):
-                self._launch_fused(self.blo, dt)
-                self._launch_fused(self.bhi, dt)
+                for rng in self.boundary:
+                    self._launch_fused(rng, dt)
         else:
             if pend is not None:
                 pend.wait()
@@ -215,13 +279,8 @@ class Solver:
         return self._reducer
 
     def global_max_abs(self) -> float:
-        o0, o1 = self.d.owned
         r = self.reducer()
-        if self.grid.dims == 3:
-            box = ((0, self.grid.nx), (0, self.grid.ny), (o0, o1))
-        else:
-            box = ((0, self.grid.nx), (o0, o1))
-        _, _, mx = r(self.u, None, box)
+        _, _, mx = r(self.u, None, self._owned_xyz_box())
         return self.comm.allreduce_max(mx)
 
     def dt(self) -> float:
@@ -333,20 +392,19 @@ class Solver:
                     t_exact: float | None = None):
         """Global (L1, L2, Linf) of u - exact, with the reference's cell-volume weights
         (`Matlab_Prototipes/DiffusionNd/heat3d.m`, fixed `CalcError` indexing)."""
-        o0, o1 = self.d.owned
+        cd = self.cd
         if exact is None:
             K = K if K is not None else getattr(self.model, "K", 1.0)
             tt = self.t if t_exact is None else t_exact
-            exact = ics.exact_solution(self.ic_name, self.grid.shape, self.grid.spacing, tt, K,
-                                       self.ic_params, self.d.start, self.d.count, self.sx,
-                                       self.dtype, self.device)
+            # same (ghost-inclusive, padded) layout as u, so both share the strides
+            offs = [cd.axis(a).start - cd.ghost_of_axis(a) for a in range(cd.dims)]
+            exact = ics.exact_solution_box(self.ic_name, self.grid.shape, self.grid.spacing,
+                                           tt, K, self.ic_params, offs, list(cd.alloc),
+                                           self.sx, self.dtype, self.device)
+        elif tuple(exact.shape) != tuple(self.u.shape):
+            raise ValueError(f"exact must have the local layout {tuple(self.u.shape)}")
         r = self.reducer()
-        own = self.u[o0:o1]
-        if self.grid.dims == 3:
-            box = ((0, self.grid.nx), (0, self.grid.ny), (0, o1 - o0))
-        else:
-            box = ((0, self.grid.nx), (0, o1 - o0))
-        s1, s2, mx = r(own, exact, box)
+        s1, s2, mx = r(self.u, exact, self._owned_xyz_box())
         s1 = self.comm.allreduce_sum(s1)
         s2 = self.comm.allreduce_sum(s2)
         mx = self.comm.allreduce_max(mx)
@@ -360,8 +418,12 @@ class Solver:
         """Global solution (no ghosts) on rank 0 as numpy [z][y][x] ([y][x] in 2-D)."""
         self.sync_halos()
         self._sync()
-        counts = [self.d.count_of(r) for r in range(self.comm.size)]
-        g = self.comm.gather_planes(self.owned.contiguous(), counts)
+        if self.cart:
+            boxes = [self.cd.global_box(r) for r in range(self.comm.size)]
+            g = self.comm.gather_boxes(self.owned.contiguous(), boxes, self.cd.shape)
+        else:
+            counts = [self.d.count_of(r) for r in range(self.comm.size)]
+            g = self.comm.gather_planes(self.owned.contiguous(), counts)
         return None if g is None else g.numpy()
 
     def save_result(self, path) -> None:
@@ -372,22 +434,24 @@ class Solver:
     def meta(self) -> dict:
         return {"grid": list(self.grid.shape), "lengths": list(self.grid.lengths),
                 "t": self.t, "it": self.it, "model": self.model.describe(),
-                "ic": self.ic_name, "world": self.comm.size}
+                "ic": self.ic_name, "world": self.comm.size, "pgrid": list(self.pgrid)}
 
     def save_checkpoint(self, prefix):
         self.sync_halos()
         self._sync()
         local = self.owned.detach().to(torch.float64).cpu().numpy()
-        return aio.save_checkpoint(prefix, self.comm.rank, local, self.d.start, self.meta())
+        box0 = [s for s, _ in self.cd.global_box()]
+        return aio.save_checkpoint(prefix, self.comm.rank, local, self.d.start, self.meta(),
+                                   box0=box0)
 
     def load_checkpoint(self, prefix):
         """Restart from shards written by ANY decomposition of the same grid."""
-        arr, meta = aio.load_checkpoint(prefix, self.d.start, self.d.count)
+        gb = self.cd.global_box()
+        arr, meta = aio.load_checkpoint_box(prefix, [s for s, _ in gb], [c for _, c in gb])
         if list(meta["grid"]) != list(self.grid.shape):
             raise ValueError(f"checkpoint grid {meta['grid']} != {list(self.grid.shape)}")
-        o0, o1 = self.d.owned
         src = torch.from_numpy(arr).to(self.device, self.dtype)
-        self.u[o0:o1, ..., :self.grid.nx].copy_(src)
+        self.owned.copy_(src)
         self.t = float(meta["t"])
         self.it = int(meta["it"])
         self._pending.clear()

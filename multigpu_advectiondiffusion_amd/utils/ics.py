@@ -122,6 +122,43 @@ def evaluate(name: str, shape_global, spacing, axis0_offset: int, n_local: int, 
     return v.to(dtype).contiguous()
 
 
+def _window(full: torch.Tensor, offsets, extents, pad_last: int) -> torch.Tensor:
+    """Cut the box [offsets, offsets+extents) (array axis order) out of a global-extent
+    tensor; cells outside the global array are zero; the last axis is padded to
+    `pad_last` columns."""
+    shape = tuple(extents[:-1]) + (pad_last,)
+    out = torch.zeros(shape, dtype=full.dtype, device=full.device)
+    src, dst = [], []
+    for a, (o, n) in enumerate(zip(offsets, extents)):
+        lo, hi = max(o, 0), min(o + n, full.shape[a])
+        if hi <= lo:
+            return out
+        src.append(slice(lo, hi))
+        dst.append(slice(lo - o, hi - o))
+    out[tuple(dst)] = full[tuple(src)]
+    return out
+
+
+def evaluate_box(name: str, shape_global, spacing, offsets, extents, sx: int,
+                 dtype=torch.float64, device="cpu", params=None) -> torch.Tensor:
+    """IC on a local box of a Cartesian decomposition (array axis order: 3-D (z, y, x),
+    2-D (y, x)); offsets are global indices of local index 0 (may be negative: ghost
+    cells beyond the domain are zero).  Evaluated as a global slab, then cut."""
+    NX = shape_global[0]
+    full = evaluate(name, shape_global, spacing, offsets[0], extents[0], NX, dtype, device,
+                    params)
+    offs = (0,) + tuple(offsets[1:])
+    return _window(full, offs, extents, sx)
+
+
+def exact_solution_box(name: str, shape_global, spacing, t: float, K, params, offsets,
+                       extents, sx: int, dtype=torch.float64, device="cpu"):
+    NX = shape_global[0]
+    full = exact_solution(name, shape_global, spacing, t, K, params, offsets[0], extents[0],
+                          NX, dtype, device)
+    return _window(full, (0,) + tuple(offsets[1:]), extents, sx)
+
+
 def exact_solution(name: str, shape_global, spacing, t: float, K: float = 1.0,
                    params=None, axis0_offset=0, n_local=None, sx=None, dtype=torch.float64,
                    device="cpu"):

@@ -38,15 +38,19 @@ def _shard_name(prefix: Path, rank: int) -> Path:
     return prefix.parent / f"{prefix.name}.rank{rank:05d}.ckpt"
 
 
-def save_checkpoint(prefix, rank: int, local: np.ndarray, plane0: int, meta: dict) -> Path:
+def save_checkpoint(prefix, rank: int, local: np.ndarray, plane0: int, meta: dict,
+                    box0=None) -> Path:
     """Write this rank's shard. `local` holds global planes plane0 .. plane0+len-1 along
-    axis 0 (no ghosts). `meta` must contain JSON-serialisable run metadata."""
+    axis 0 (no ghosts); for a Cartesian block ``box0`` gives its global offset on every
+    axis.  `meta` must contain JSON-serialisable run metadata."""
     prefix = Path(prefix)
     prefix.parent.mkdir(parents=True, exist_ok=True)
     local = np.ascontiguousarray(local)
     header = dict(meta)
     header.update({"plane0": int(plane0), "nplanes": int(local.shape[0]),
-                   "shape": list(local.shape), "dtype": str(local.dtype), "rank": rank})
+                   "shape": list(local.shape), "dtype": str(local.dtype), "rank": rank,
+                   "box0": [int(v) for v in (box0 if box0 is not None
+                                              else [plane0] + [0] * (local.ndim - 1))]})
     hb = json.dumps(header, sort_keys=True).encode()
     path = _shard_name(prefix, rank)
     tmp = path.with_suffix(".tmp")
@@ -80,9 +84,9 @@ def list_shards(prefix):
     return shards
 
 
-def load_checkpoint(prefix, plane0: int, nplanes: int):
-    """Assemble global planes [plane0, plane0+nplanes) from whatever shards exist.
-    Returns (array, meta of the first shard)."""
+def load_checkpoint_box(prefix, box0, extents):
+    """Assemble the global box [box0, box0+extents) (array axis order) from whatever
+    shards exist (slab or Cartesian, any process count).  Returns (array, meta)."""
     out = None
     meta = None
     covered = 0
@@ -92,16 +96,34 @@ def load_checkpoint(prefix, plane0: int, nplanes: int):
             meta = h
         dt = np.dtype(h["dtype"]).newbyteorder("<")
         shape = tuple(h["shape"])
-        mm = np.memmap(path, dtype=dt, mode="r", offset=off, shape=shape)
-        s0, s1 = h["plane0"], h["plane0"] + h["nplanes"]
-        a, b = max(s0, plane0), min(s1, plane0 + nplanes)
-        if a >= b:
+        sb = h.get("box0", [h["plane0"]] + [0] * (len(shape) - 1))
+        lo = [max(s, b) for s, b in zip(sb, box0)]
+        hi = [min(s + n, b + e) for s, n, b, e in zip(sb, shape, box0, extents)]
+        if any(b <= a for a, b in zip(lo, hi)):
             continue
+        mm = np.memmap(path, dtype=dt, mode="r", offset=off, shape=shape)
         if out is None:
-            out = np.empty((nplanes,) + shape[1:], dtype=np.dtype(h["dtype"]))
-        out[a - plane0:b - plane0] = mm[a - s0:b - s0]
-        covered += b - a
+            out = np.empty(tuple(extents), dtype=np.dtype(h["dtype"]))
+        dst = tuple(slice(a - b, c - b) for a, c, b in zip(lo, hi, box0))
+        src = tuple(slice(a - s, c - s) for a, c, s in zip(lo, hi, sb))
+        out[dst] = mm[src]
+        n = 1
+        for a, b in zip(lo, hi):
+            n *= b - a
+        covered += n
         del mm
-    if out is None or covered != nplanes:
-        raise ValueError(f"checkpoint {prefix} does not cover planes [{plane0},{plane0 + nplanes})")
+    total = 1
+    for e in extents:
+        total *= e
+    if out is None or covered != total:
+        raise ValueError(f"checkpoint {prefix} does not cover box {box0} + {extents}")
     return out, meta
+
+
+def load_checkpoint(prefix, plane0: int, nplanes: int):
+    """Assemble global planes [plane0, plane0+nplanes) (full extent of the other axes)
+    from whatever shards exist.  Returns (array, meta of the first shard)."""
+    h, _ = read_header(list_shards(prefix)[0])
+    grid = list(h["grid"])[::-1]  # array order
+    return load_checkpoint_box(prefix, [plane0] + [0] * (len(grid) - 1),
+                               [nplanes] + grid[1:])

@@ -100,3 +100,91 @@ def test_fused_step_wide_halo_matches_per_stage():
     for world in (1, 3):
         out = spawn_local(world, _run_fused, True, 4)[0]
         assert np.array_equal(out, ref), (world, np.abs(out - ref).max())
+
+
+# ---- Cartesian (2-D / 3-D) process grids ----------------------------------------------
+def _run_cart(comm, kind, steps, overlap, decomp):
+    model, grid, ic = _make(kind)
+    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, overlap=overlap, decomp=decomp)
+    assert s.cart and not s.fused
+    s.run(iters=steps)
+    g = s.gather()
+    en = s.error_norms() if ic in ("sine", "heat") else None
+    return None if g is None else (g.copy(), en)
+
+
+@pytest.mark.parametrize("kind,world,decomp", [
+    ("diff3", 4, (1, 2, 2)), ("diff3", 4, (2, 1, 2)), ("diff3", 2, (1, 1, 2)),
+    ("diff3o2", 3, (1, 3, 1)), ("diff2", 4, (2, 2)), ("diff2", 2, (1, 2)),
+    ("burg3", 4, (2, 2, 1)), ("burg3js", 2, (1, 1, 2)), ("burg2", 3, (1, 3)),
+])
+def test_cartesian_decomposition_bitwise(kind, world, decomp):
+    ref = _serial(kind, 3)
+    for overlap in (True, False):
+        out, _ = spawn_local(world, _run_cart, kind, 3, overlap, decomp)[0]
+        assert out.shape == ref.shape
+        assert np.array_equal(out, ref), (kind, decomp, overlap, np.abs(out - ref).max())
+
+
+def test_cartesian_eight_ranks_and_norms():
+    model, grid, ic = _make("diff3")
+    s = Solver(model, grid, dtype=torch.float64, device="cpu", ic=ic)
+    s.run(iters=3)
+    ref, en_ref = s.gather(), s.error_norms()
+    out, en = spawn_local(8, _run_cart, "diff3", 3, True, (2, 2, 2))[0]
+    assert np.array_equal(out, ref)
+    assert np.allclose(en, en_ref, rtol=1e-12, atol=0)
+
+
+def _ckpt_write_cart(comm, prefix, steps, decomp):
+    model, grid, ic = _make("burg3")
+    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, decomp=decomp)
+    s.run(iters=steps)
+    s.save_checkpoint(prefix)
+
+
+def test_checkpoint_cartesian_to_slab(tmp_path):
+    prefix = str(tmp_path / "ckc")
+    spawn_local(4, _ckpt_write_cart, prefix, 2, (1, 2, 2))    # written by a 1x2x2 grid
+    g, t, it = spawn_local(3, _ckpt_resume, prefix, 3)[0]     # resumed on 3 z-slabs
+    model, grid, ic = _make("burg3")
+    s = Solver(model, grid, dtype=torch.float64, device="cpu", ic=ic)
+    s.run(iters=5)
+    assert it == 5 and np.array_equal(g, s.gather())
+
+
+def test_proc_grid_and_box_partition():
+    from multigpu_advectiondiffusion_amd.parallel.decomposition import (
+        CartesianDecomposition, parse_proc_grid)
+    assert parse_proc_grid(None, 4, (64, 64, 64), 2) == (4, 1, 1)
+    assert parse_proc_grid("2x1x2", 4, (64, 64, 64), 2) == (2, 1, 2)
+    assert parse_proc_grid("auto", 8, (512, 64, 64), 2) == (8, 1, 1)   # long z: slabs
+    assert parse_proc_grid("auto", 4, (16, 256, 256), 2) == (1, 4, 1)  # flat z: y split
+    with pytest.raises(ValueError):
+        parse_proc_grid((3, 1, 1), 4, (64, 64, 64), 2)
+    shape = (23, 18, 20)
+    for pg in ((2, 2, 2), (1, 3, 2), (4, 1, 1)):
+        seen = np.zeros(shape, dtype=int)
+        for r in range(int(np.prod(pg))):
+            cd = CartesianDecomposition(shape, pg, r, 2)
+            inner, bnd = cd.split_boxes(2, 2)
+            mark = np.zeros(cd.alloc, dtype=int)
+            for box in [inner] + bnd:
+                mark[tuple(slice(lo, hi) for lo, hi in box)] += 1
+            own = mark[tuple(slice(lo, hi) for lo, hi in cd.owned_box())]
+            gb = cd.global_box()
+            seen[tuple(slice(s, s + c) for s, c in gb)] += own
+            assert mark.sum() == own.sum()  # never updates a ghost cell
+        # every non-frozen cell updated exactly once, frozen border never
+        exp = np.zeros(shape, dtype=int)
+        exp[2:-2, 2:-2, 2:-2] = 1
+        assert np.array_equal(seen, exp), pg
+
+
+def test_evaluate_box_matches_slab():
+    from multigpu_advectiondiffusion_amd.utils import ics
+    shape, sp = (20, 18, 23), (0.1, 0.2, 0.3)
+    full = ics.evaluate("heat", shape, sp, -2, 27, 20)
+    box = ics.evaluate_box("heat", shape, sp, (3, -2, 4), (7, 22, 9), 12)
+    assert torch.equal(box[:, 2:20, :9], full[5:12, 0:18, 4:13])
+    assert float(box[:, :2].abs().max()) == 0.0 and float(box[..., 9:].abs().max()) == 0.0
