@@ -74,15 +74,21 @@ def main():
     u = torch.rand((nb, nb, nb), dtype=dt, device="cuda") * 0.5 + 0.1
     A = torch.rand_like(u)
     B = torch.rand_like(u)
-    for wz in (True, False):
+    for wz in ("z", "js", "js7"):
         for visc in (1e-5, 0.0):
-            kw = dict(nx=nb, ny=nb, k0=3, k1=nb - 3, border=3, weno_z=wz, rdx=nb / 2.0,
+            R = 4 if wz == "js7" else 3
+            kw = dict(nx=nb, ny=nb, k0=R, k1=nb - R, border=R, weno_z=wz, rdx=nb / 2.0,
                       rdy=nb / 2.0, rdz=nb / 2.0, vx=visc * (nb / 2.0) ** 2,
                       vy=visc * (nb / 2.0) ** 2, vz=visc * (nb / 2.0) ** 2, dt=1e-4)
             t2, _ = timeit(lambda: stencil.burgers3d_stage(A, u, B, a=0.75, b=0.25, **kw), args.reps)
-            tag = f"burgers3d_{'z' if wz else 'js'}_{'visc' if visc else 'inv'}"
+            tag = f"burgers3d_{wz}_{'visc' if visc else 'inv'}"
             res[tag + "_stage_us"] = round(t2 * 1e6, 1)
             res[tag + "_step_mlups"] = round(nb ** 3 / (3 * t2) / 1e6, 1)
+            if wz == "js7":  # low-storage RK4(5) stage (5 per step)
+                tl, _ = timeit(lambda: stencil.burgers3d_stage(A, u, B, a=-0.4, b=0.3, ls=True,
+                                                               **kw), args.reps)
+                res[tag + "_ls_stage_us"] = round(tl * 1e6, 1)
+                res[tag + "_lsrk45_step_mlups"] = round(nb ** 3 / (5 * tl) / 1e6, 1)
     print(json.dumps(res, indent=1))
 
 

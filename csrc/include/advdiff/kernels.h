@@ -45,28 +45,49 @@ int advdiff_diffusion3d_step(int dtype, const void* uin, void* uout, int nx, int
                              int zhi, int border, int order, double cx, double cy, double cz,
                              double dt, void* stream);
 
+// Low-storage RK stage (Carpenter–Kennedy 2N, e.g. LSRK4(5)) of the same operator:
+//     d = A*du + dt*L(in);  du = d;  out = in + B*d      (A == 0: du is not read)
+// `du` is read and written in place (pointwise); `out` must differ from `in`.
+int advdiff_diffusion3d_stage_ls(int dtype, const void* in, void* du, void* out, int nx,
+                                 int ny, int64_t sy, int64_t sz, int k0, int k1, int border,
+                                 int order, double cx, double cy, double cz, double dt,
+                                 double A, double B, void* stream);
 // 2-D heat stage, rows j in [j0, j1), columns i in [border, nx-border).
 int advdiff_diffusion2d_stage(int dtype, const void* in, const void* u0, void* out,
                               int nx, int64_t sy, int j0, int j1, int border, int order,
                               double cx, double cy, double dt, double a, double b,
                               void* stream);
+int advdiff_diffusion2d_stage_ls(int dtype, const void* in, void* du, void* out, int nx,
+                                 int64_t sy, int j0, int j1, int border, int order, double cx,
+                                 double cy, double dt, double A, double B, void* stream);
 
 // ---------------------------------------------------------------------------------
 // Burgers u_t + Σ_d ∂_d(u²/2) = C ∇²u : ONE fused SSP-RK3 stage
 //     L(u) = -Σ_d (F_{+½} - F_{-½}) * rd_d  +  C ∇²u (FD4)
-// WENO5 (JS when weno_z == 0, Z otherwise) with local Lax-Friedrichs splitting.
+// Reconstruction `weno`: 0 = WENO5-JS, 1 = WENO5-Z (Borges), 2 = WENO7-JS (the MATLAB
+// prototype's LFWENO7), with local Lax-Friedrichs splitting.  Stencil radius R = 3
+// (WENO5) / 4 (WENO7): reads planes k0-R .. k1+R-1 and needs border >= R.
 // rdx = 1/dx ...; vx = C/dx² ... (all zero = inviscid, the viscous path is not
-// compiled in).  Reads planes k0-3 .. k1+2.
+// compiled in).
 int advdiff_burgers3d_stage(int dtype, const void* in, const void* u0, void* out,
                             int nx, int ny, int64_t sy, int64_t sz, int k0, int k1,
-                            int border, int weno_z, double rdx, double rdy, double rdz,
+                            int border, int weno, double rdx, double rdy, double rdz,
                             double vx, double vy, double vz, double dt, double a,
                             double b, void* stream);
+// Low-storage RK stage of the Burgers operator (see advdiff_diffusion3d_stage_ls).
+int advdiff_burgers3d_stage_ls(int dtype, const void* in, void* du, void* out, int nx, int ny,
+                               int64_t sy, int64_t sz, int k0, int k1, int border, int weno,
+                               double rdx, double rdy, double rdz, double vx, double vy,
+                               double vz, double dt, double A, double B, void* stream);
 
 int advdiff_burgers2d_stage(int dtype, const void* in, const void* u0, void* out,
-                            int nx, int64_t sy, int j0, int j1, int border, int weno_z,
+                            int nx, int64_t sy, int j0, int j1, int border, int weno,
                             double rdx, double rdy, double vx, double vy, double dt,
                             double a, double b, void* stream);
+int advdiff_burgers2d_stage_ls(int dtype, const void* in, void* du, void* out, int nx,
+                               int64_t sy, int j0, int j1, int border, int weno, double rdx,
+                               double rdy, double vx, double vy, double dt, double A, double B,
+                               void* stream);
 
 // ---------------------------------------------------------------------------------
 // Reductions over the box [i0,i1)x[j0,j1)x[k0,k1):

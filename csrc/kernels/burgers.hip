@@ -30,12 +30,14 @@
 
 namespace advdiff {
 
-template <typename T, bool WZ, bool VISC, bool USE_U0, int TX, int TY>
+// Scheme-generic fused stage.  Rc = Recon<T, W, WZ>: R = 3 (WENO5) or 4 (WENO7),
+// NP = 2R-1 values per side of a face.  MODE: stage epilogue (common.hpp).
+template <typename T, int W, bool WZ, bool VISC, int MODE, int TX, int TY>
 __global__ __launch_bounds__(TX* TY) void burgers3d_stage_kernel(
-    const T* __restrict__ in, const T* u0, T* out, int nx, int ny, int64_t sy, int64_t sz,
-    int k0, int k1, int zchunk, int border, T rdx, T rdy, T rdz, T vx, T vy, T vz, T dt, T a,
-    T b) {
-  constexpr int R = 3;
+    const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
+    int k1, int zchunk, int border, T rdx, T rdy, T rdz, T vx, T vy, T vz, T dt, T a, T b) {
+  using Rc = Recon<T, W, WZ>;
+  constexpr int R = Rc::R, NP = 2 * R - 1;
   constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NT = TX * TY;
   constexpr int NPT = (LX * LY + NT - 1) / NT;
   constexpr int FXW = TX + 1;  // x-face row width
@@ -70,30 +72,38 @@ __global__ __launch_bounds__(TX* TY) void burgers3d_stage_kernel(
 #pragma unroll
     for (int r = 0; r < NPT; ++r) pre[r] = src[toff[r]];
   };
+  // flux at the face to the right of LDS cell c along stride st
+  auto lds_face = [&](int c, int st) {
+    T pv[NP], mv[NP];
+#pragma unroll
+    for (int d = 0; d < NP; ++d) {
+      pv[d] = s_p[c + (d - R + 1) * st];
+      mv[d] = s_m[c + (d - R + 2) * st];
+    }
+    return Rc::face(pv, mv);
+  };
 
   // ---- prologue: column window and the face below the first plane ----
-  T P[5], M[5], U[5];  // f+(k-2..k+2), f-(k-1..k+3), u(k-2..k+2)
+  T P[NP], M[NP], U[NP];  // f+(k-R+1..k+R-1), f-(k-R+2..k+R), u(k-R+1..k+R-1)
   T fz_lo;
   {
-    T uz[6], fp[6], fm[6];
+    T uz[2 * R], fp[2 * R], fm[2 * R];
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      uz[q] = in[(int64_t)(kc0 - 3 + q) * sz + own];
+    for (int q = 0; q < 2 * R; ++q) {
+      uz[q] = in[(int64_t)(kc0 - R + q) * sz + own];
       lf_split(uz[q], fp[q], fm[q]);
     }
-    // face kc0-½ : f+(kc0-3..kc0+1), f-(kc0-2..kc0+2)
-    fz_lo = weno5_face<T, WZ>(fp[0], fp[1], fp[2], fp[3], fp[4], fm[1], fm[2], fm[3], fm[4],
-                              fm[5]);
+    fz_lo = Rc::face(fp, fm + 1);  // face kc0-½
 #pragma unroll
-    for (int q = 0; q < 5; ++q) {
+    for (int q = 0; q < NP; ++q) {
       P[q] = fp[q + 1];
       U[q] = uz[q + 1];
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) M[q] = fm[q + 2];
+    for (int q = 0; q < NP - 1; ++q) M[q] = fm[q + 2];
   }
   fetch_tile(kc0);
-  T unext = in[(int64_t)(kc0 + 3) * sz + own];
+  T unext = in[(int64_t)(kc0 + R) * sz + own];
 
   for (int k = kc0; k < kc1; ++k) {
     __syncthreads();  // previous plane's LDS readers are done
@@ -108,37 +118,25 @@ __global__ __launch_bounds__(TX* TY) void burgers3d_stage_kernel(
         s_m[idx] = m;
       }
     }
-    // own column: u(k+3) -> f-(k+3) now, f+(k+3)/u(k+3) after the shift
+    // own column: u(k+R) -> f-(k+R) now, f+(k+R)/u(k+R) after the shift
     T pn, mn;
     lf_split(unext, pn, mn);
-    M[4] = mn;
+    M[NP - 1] = mn;
     const T un = unext;
     if (k + 1 < kc1) {
       fetch_tile(k + 1);
-      unext = in[(int64_t)(k + 4) * sz + own];
+      unext = in[(int64_t)(k + 1 + R) * sz + own];
     }
     __syncthreads();
 
     // x face at i+½ and y face at j+½ of this lane's cell
-    s_fx[ty * FXW + tx + 1] =
-        weno5_face<T, WZ>(s_p[lc - 2], s_p[lc - 1], s_p[lc], s_p[lc + 1], s_p[lc + 2],
-                          s_m[lc - 1], s_m[lc], s_m[lc + 1], s_m[lc + 2], s_m[lc + 3]);
-    s_fy[(ty + 1) * TX + tx] = weno5_face<T, WZ>(
-        s_p[lc - 2 * LX], s_p[lc - LX], s_p[lc], s_p[lc + LX], s_p[lc + 2 * LX],
-        s_m[lc - LX], s_m[lc], s_m[lc + LX], s_m[lc + 2 * LX], s_m[lc + 3 * LX]);
-    if (ty == 0) {  // bottom faces j0-½ of every column (wave-uniform)
-      const int c = 3 * LX + tx + R;  // row j0
-      s_fy[tx] = weno5_face<T, WZ>(s_p[c - 3 * LX], s_p[c - 2 * LX], s_p[c - LX], s_p[c],
-                                   s_p[c + LX], s_m[c - 2 * LX], s_m[c - LX], s_m[c],
-                                   s_m[c + LX], s_m[c + 2 * LX]);
-    }
-    if (ty == TY - 1 && tx < TY) {  // left faces i0-½ of every row
-      const int c = (tx + R) * LX + R;  // (row tx, column i0)
-      s_fx[tx * FXW] = weno5_face<T, WZ>(s_p[c - 3], s_p[c - 2], s_p[c - 1], s_p[c],
-                                         s_p[c + 1], s_m[c - 2], s_m[c - 1], s_m[c],
-                                         s_m[c + 1], s_m[c + 2]);
-    }
-    const T fz_hi = weno5_face<T, WZ>(P[0], P[1], P[2], P[3], P[4], M[0], M[1], M[2], M[3], M[4]);
+    s_fx[ty * FXW + tx + 1] = lds_face(lc, 1);
+    s_fy[(ty + 1) * TX + tx] = lds_face(lc, LX);
+    if (ty == 0)  // bottom faces j0-½ of every column (wave-uniform)
+      s_fy[tx] = lds_face((R - 1) * LX + tx + R, LX);
+    if (ty == TY - 1 && tx < TY)  // left faces i0-½ of every row
+      s_fx[tx * FXW] = lds_face((tx + R) * LX + R - 1, 1);
+    const T fz_hi = Rc::face(P, M);
     __syncthreads();
 
     const T ctr = s_u[lc];
@@ -147,31 +145,32 @@ __global__ __launch_bounds__(TX* TY) void burgers3d_stage_kernel(
     if constexpr (VISC) {
       L += vx * FD<4>::d2(s_u[lc - 2], s_u[lc - 1], ctr, s_u[lc + 1], s_u[lc + 2]) +
            vy * FD<4>::d2(s_u[lc - 2 * LX], s_u[lc - LX], ctr, s_u[lc + LX], s_u[lc + 2 * LX]) +
-           vz * FD<4>::d2(U[0], U[1], ctr, U[3], U[4]);
+           vz * FD<4>::d2(U[R - 3], U[R - 2], ctr, U[R], U[R + 1]);
     }
     if (active) {
       const int64_t o = (int64_t)k * sz + own;
-      T uo = T(0);
-      if constexpr (USE_U0) uo = u0[o];
-      out[o] = rk_stage<T, USE_U0>(uo, ctr, L, dt, a, b);
+      T ax = T(0);
+      if constexpr (reads_aux<MODE>()) ax = aux[o];
+      stage_store<T, MODE>(out, aux, o, ax, ctr, L, dt, a, b);
     }
     fz_lo = fz_hi;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NP - 1; ++q) {
       P[q] = P[q + 1];
       M[q] = M[q + 1];
       U[q] = U[q + 1];
     }
-    P[4] = pn;
-    U[4] = un;
+    P[NP - 1] = pn;
+    U[NP - 1] = un;
   }
 }
 
-template <typename T, bool WZ, bool VISC, bool USE_U0, int TX>
+template <typename T, int W, bool WZ, bool VISC, int MODE, int TX>
 __global__ __launch_bounds__(TX) void burgers2d_stage_kernel(
-    const T* __restrict__ in, const T* u0, T* out, int nx, int64_t sy, int j0, int j1,
-    int ychunk, int border, T rdx, T rdy, T vx, T vy, T dt, T a, T b) {
-  constexpr int R = 3, LX = TX + 2 * R;
+    const T* __restrict__ in, T* aux, T* out, int nx, int64_t sy, int j0, int j1, int ychunk,
+    int border, T rdx, T rdy, T vx, T vy, T dt, T a, T b) {
+  using Rc = Recon<T, W, WZ>;
+  constexpr int R = Rc::R, NP = 2 * R - 1, LX = TX + 2 * R;
   __shared__ T s_u[LX];
   __shared__ T s_p[LX];
   __shared__ T s_m[LX];
@@ -193,28 +192,36 @@ __global__ __launch_bounds__(TX) void burgers2d_stage_kernel(
     pre0 = src[g0];
     if (tx < 2 * R) pre1 = src[g1];
   };
+  auto lds_face = [&](int c) {
+    T pv[NP], mv[NP];
+#pragma unroll
+    for (int d = 0; d < NP; ++d) {
+      pv[d] = s_p[c + d - R + 1];
+      mv[d] = s_m[c + d - R + 2];
+    }
+    return Rc::face(pv, mv);
+  };
 
-  T P[5], M[5], U[5];
+  T P[NP], M[NP], U[NP];
   T fy_lo;
   {
-    T uy[6], fp[6], fm[6];
+    T uy[2 * R], fp[2 * R], fm[2 * R];
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      uy[q] = in[(int64_t)(jc0 - 3 + q) * sy + ic];
+    for (int q = 0; q < 2 * R; ++q) {
+      uy[q] = in[(int64_t)(jc0 - R + q) * sy + ic];
       lf_split(uy[q], fp[q], fm[q]);
     }
-    fy_lo = weno5_face<T, WZ>(fp[0], fp[1], fp[2], fp[3], fp[4], fm[1], fm[2], fm[3], fm[4],
-                              fm[5]);
+    fy_lo = Rc::face(fp, fm + 1);
 #pragma unroll
-    for (int q = 0; q < 5; ++q) {
+    for (int q = 0; q < NP; ++q) {
       P[q] = fp[q + 1];
       U[q] = uy[q + 1];
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) M[q] = fm[q + 2];
+    for (int q = 0; q < NP - 1; ++q) M[q] = fm[q + 2];
   }
   fetch_row(jc0);
-  T unext = in[(int64_t)(jc0 + 3) * sy + ic];
+  T unext = in[(int64_t)(jc0 + R) * sy + ic];
 
   for (int jj = jc0; jj < jc1; ++jj) {
     __syncthreads();
@@ -233,43 +240,38 @@ __global__ __launch_bounds__(TX) void burgers2d_stage_kernel(
     }
     T pn, mn;
     lf_split(unext, pn, mn);
-    M[4] = mn;
+    M[NP - 1] = mn;
     const T un = unext;
     if (jj + 1 < jc1) {
       fetch_row(jj + 1);
-      unext = in[(int64_t)(jj + 4) * sy + ic];
+      unext = in[(int64_t)(jj + 1 + R) * sy + ic];
     }
     __syncthreads();
-    s_fx[tx + 1] = weno5_face<T, WZ>(s_p[lc - 2], s_p[lc - 1], s_p[lc], s_p[lc + 1],
-                                     s_p[lc + 2], s_m[lc - 1], s_m[lc], s_m[lc + 1],
-                                     s_m[lc + 2], s_m[lc + 3]);
-    if (tx == TX - 1) {  // left face i0-½ (last wave, single lane)
-      s_fx[0] = weno5_face<T, WZ>(s_p[0], s_p[1], s_p[2], s_p[3], s_p[4], s_m[1], s_m[2],
-                                  s_m[3], s_m[4], s_m[5]);
-    }
-    const T fy_hi = weno5_face<T, WZ>(P[0], P[1], P[2], P[3], P[4], M[0], M[1], M[2], M[3], M[4]);
+    s_fx[tx + 1] = lds_face(lc);
+    if (tx == TX - 1) s_fx[0] = lds_face(R - 1);  // left face i0-½ (last wave, one lane)
+    const T fy_hi = Rc::face(P, M);
     __syncthreads();
     const T ctr = s_u[lc];
     T L = -((s_fx[tx + 1] - s_fx[tx]) * rdx + (fy_hi - fy_lo) * rdy);
     if constexpr (VISC) {
       L += vx * FD<4>::d2(s_u[lc - 2], s_u[lc - 1], ctr, s_u[lc + 1], s_u[lc + 2]) +
-           vy * FD<4>::d2(U[0], U[1], ctr, U[3], U[4]);
+           vy * FD<4>::d2(U[R - 3], U[R - 2], ctr, U[R], U[R + 1]);
     }
     if (active) {
       const int64_t o = (int64_t)jj * sy + i;
-      T uo = T(0);
-      if constexpr (USE_U0) uo = u0[o];
-      out[o] = rk_stage<T, USE_U0>(uo, ctr, L, dt, a, b);
+      T ax = T(0);
+      if constexpr (reads_aux<MODE>()) ax = aux[o];
+      stage_store<T, MODE>(out, aux, o, ax, ctr, L, dt, a, b);
     }
     fy_lo = fy_hi;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NP - 1; ++q) {
       P[q] = P[q + 1];
       M[q] = M[q + 1];
       U[q] = U[q + 1];
     }
-    P[4] = pn;
-    U[4] = un;
+    P[NP - 1] = pn;
+    U[NP - 1] = un;
   }
 }
 
@@ -279,129 +281,140 @@ __global__ __launch_bounds__(TX) void burgers2d_stage_kernel(
 constexpr int kBTX3 = 64, kBTY3 = 8;
 constexpr int kBTX2 = 256;
 
-template <typename T, bool WZ, bool VISC, bool U0, int TY>
-static hipError_t launch_b3_ty(const void* in, const void* u0, void* out, int nx, int ny,
-                               int64_t sy, int64_t sz, int k0, int k1, int border, double rdx,
-                               double rdy, double rdz, double vx, double vy, double vz,
-                               double dt, double a, double b, hipStream_t st) {
-  const int gx = div_up(nx, kBTX3), gy = div_up(ny, TY);
-  const int zc = pick_chunk(k1 - k0, (long long)gx * gy, 8, 256);
-  const int gz = div_up(k1 - k0, zc);
+struct BArgs {
+  const void* in;
+  void* aux;
+  void* out;
+  int nx, ny;
+  int64_t sy, sz;
+  int lo, hi, border;  // marched-axis range [lo, hi)
+  double rdx, rdy, rdz, vx, vy, vz, dt, a, b;
+  hipStream_t st;
+};
+
+template <typename T, int W, bool WZ, bool VISC, int MODE, int TY>
+static hipError_t launch_b3_ty(const BArgs& p) {
+  const int gx = div_up(p.nx, kBTX3), gy = div_up(p.ny, TY);
+  const int zc = pick_chunk(p.hi - p.lo, (long long)gx * gy, 8, 256);
+  const int gz = div_up(p.hi - p.lo, zc);
   const double s = 1.0 / 12.0;
-  hipLaunchKernelGGL((burgers3d_stage_kernel<T, WZ, VISC, U0, kBTX3, TY>), dim3(gx, gy, gz),
-                     dim3(kBTX3, TY, 1), 0, st, (const T*)in, (const T*)u0, (T*)out, nx, ny, sy,
-                     sz, k0, k1, zc, border, T(rdx), T(rdy), T(rdz), T(vx * s), T(vy * s),
-                     T(vz * s), T(dt), T(a), T(b));
+  hipLaunchKernelGGL((burgers3d_stage_kernel<T, W, WZ, VISC, MODE, kBTX3, TY>),
+                     dim3(gx, gy, gz), dim3(kBTX3, TY, 1), 0, p.st, (const T*)p.in, (T*)p.aux,
+                     (T*)p.out, p.nx, p.ny, p.sy, p.sz, p.lo, p.hi, zc, p.border, T(p.rdx),
+                     T(p.rdy), T(p.rdz), T(p.vx * s), T(p.vy * s), T(p.vz * s), T(p.dt), T(p.a),
+                     T(p.b));
   return hipGetLastError();
 }
 
-template <typename T, bool WZ, bool VISC, bool U0>
-static hipError_t launch_b3(const void* in, const void* u0, void* out, int nx, int ny,
-                            int64_t sy, int64_t sz, int k0, int k1, int border, double rdx,
-                            double rdy, double rdz, double vx, double vy, double vz, double dt,
-                            double a, double b, hipStream_t st) {
+template <typename T, int W, bool WZ, bool VISC, int MODE>
+static hipError_t launch_b3(const BArgs& p) {
   static const int ty = knob("B3_TY", kBTY3);
-  if (ty == 16)
-    return launch_b3_ty<T, WZ, VISC, U0, 16>(in, u0, out, nx, ny, sy, sz, k0, k1, border, rdx,
-                                             rdy, rdz, vx, vy, vz, dt, a, b, st);
-  return launch_b3_ty<T, WZ, VISC, U0, 8>(in, u0, out, nx, ny, sy, sz, k0, k1, border, rdx, rdy,
-                                          rdz, vx, vy, vz, dt, a, b, st);
+  if (W == 5 && ty == 16) return launch_b3_ty<T, W, WZ, VISC, MODE, 16>(p);
+  return launch_b3_ty<T, W, WZ, VISC, MODE, 8>(p);
 }
 
-template <typename T, bool WZ, bool VISC, bool U0>
-static hipError_t launch_b2(const void* in, const void* u0, void* out, int nx, int64_t sy,
-                            int j0, int j1, int border, double rdx, double rdy, double vx,
-                            double vy, double dt, double a, double b, hipStream_t st) {
-  const int gx = div_up(nx, kBTX2);
-  const int yc = pick_chunk(j1 - j0, gx, 4, 256);
-  const int gy = div_up(j1 - j0, yc);
+template <typename T, int W, bool WZ, bool VISC, int MODE>
+static hipError_t launch_b2(const BArgs& p) {
+  const int gx = div_up(p.nx, kBTX2);
+  const int yc = pick_chunk(p.hi - p.lo, gx, 4, 256);
+  const int gy = div_up(p.hi - p.lo, yc);
   const double s = 1.0 / 12.0;
-  hipLaunchKernelGGL((burgers2d_stage_kernel<T, WZ, VISC, U0, kBTX2>), dim3(gx, gy, 1),
-                     dim3(kBTX2, 1, 1), 0, st, (const T*)in, (const T*)u0, (T*)out, nx, sy, j0,
-                     j1, yc, border, T(rdx), T(rdy), T(vx * s), T(vy * s), T(dt), T(a), T(b));
+  hipLaunchKernelGGL((burgers2d_stage_kernel<T, W, WZ, VISC, MODE, kBTX2>), dim3(gx, gy, 1),
+                     dim3(kBTX2, 1, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx,
+                     p.sy, p.lo, p.hi, yc, p.border, T(p.rdx), T(p.rdy), T(p.vx * s),
+                     T(p.vy * s), T(p.dt), T(p.a), T(p.b));
   return hipGetLastError();
 }
 
-template <typename T>
-static hipError_t dispatch_b3(const void* in, const void* u0, void* out, int nx, int ny,
-                              int64_t sy, int64_t sz, int k0, int k1, int border, int wz,
-                              double rdx, double rdy, double rdz, double vx, double vy,
-                              double vz, double dt, double a, double b, hipStream_t st) {
-  const bool visc = vx != 0.0 || vy != 0.0 || vz != 0.0;
-  const bool u0f = a != 0.0;
-  const int key = (wz ? 4 : 0) | (visc ? 2 : 0) | (u0f ? 1 : 0);
-#define B3(W, V, U)                                                                        \
-  return launch_b3<T, W, V, U>(in, u0, out, nx, ny, sy, sz, k0, k1, border, rdx, rdy, rdz, \
-                               vx, vy, vz, dt, a, b, st)
-  switch (key) {
-    case 0: B3(false, false, false);
-    case 1: B3(false, false, true);
-    case 2: B3(false, true, false);
-    case 3: B3(false, true, true);
-    case 4: B3(true, false, false);
-    case 5: B3(true, false, true);
-    case 6: B3(true, true, false);
-    default: B3(true, true, true);
+// runtime (scheme, viscous, mode) -> template instance
+template <typename T, bool THREE_D, int W, bool WZ, bool VISC>
+static hipError_t by_mode(int mode, const BArgs& p) {
+#define BM(M) return THREE_D ? launch_b3<T, W, WZ, VISC, M>(p) : launch_b2<T, W, WZ, VISC, M>(p)
+  switch (mode) {
+    case kSsp1: BM(kSsp1);
+    case kSsp: BM(kSsp);
+    case kLs1: BM(kLs1);
+    default: BM(kLs);
   }
-#undef B3
+#undef BM
 }
 
-template <typename T>
-static hipError_t dispatch_b2(const void* in, const void* u0, void* out, int nx, int64_t sy,
-                              int j0, int j1, int border, int wz, double rdx, double rdy,
-                              double vx, double vy, double dt, double a, double b,
-                              hipStream_t st) {
-  const bool visc = vx != 0.0 || vy != 0.0;
-  const bool u0f = a != 0.0;
-  const int key = (wz ? 4 : 0) | (visc ? 2 : 0) | (u0f ? 1 : 0);
-#define B2(W, V, U) \
-  return launch_b2<T, W, V, U>(in, u0, out, nx, sy, j0, j1, border, rdx, rdy, vx, vy, dt, a, b, st)
-  switch (key) {
-    case 0: B2(false, false, false);
-    case 1: B2(false, false, true);
-    case 2: B2(false, true, false);
-    case 3: B2(false, true, true);
-    case 4: B2(true, false, false);
-    case 5: B2(true, false, true);
-    case 6: B2(true, true, false);
-    default: B2(true, true, true);
+template <typename T, bool THREE_D, int W, bool WZ>
+static hipError_t by_visc(bool visc, int mode, const BArgs& p) {
+  return visc ? by_mode<T, THREE_D, W, WZ, true>(mode, p)
+              : by_mode<T, THREE_D, W, WZ, false>(mode, p);
+}
+
+template <typename T, bool THREE_D>
+static hipError_t dispatch_b(int scheme, bool visc, int mode, const BArgs& p) {
+  switch (scheme) {
+    case 0: return by_visc<T, THREE_D, 5, false>(visc, mode, p);
+    case 1: return by_visc<T, THREE_D, 5, true>(visc, mode, p);
+    case 2: return by_visc<T, THREE_D, 7, false>(visc, mode, p);
+    default: return hipErrorInvalidValue;
   }
-#undef B2
+}
+
+static int scheme_radius(int scheme) { return scheme == 2 ? 4 : 3; }
+
+static hipError_t run_b(int dtype, bool three_d, int scheme, bool ls, const BArgs& p) {
+  if (p.hi <= p.lo) return hipSuccess;
+  const int R = scheme_radius(scheme);
+  if (scheme < 0 || scheme > 2 || p.lo < R || p.nx <= 0 || (three_d && p.ny <= 0) ||
+      p.border < R || p.in == p.out || p.in == p.aux)
+    return hipErrorInvalidValue;
+  const bool visc = p.vx != 0.0 || p.vy != 0.0 || (three_d && p.vz != 0.0);
+  const int mode = ls ? (p.a != 0.0 ? kLs : kLs1) : (p.a != 0.0 ? kSsp : kSsp1);
+  if (dtype == ADVDIFF_F64)
+    return three_d ? dispatch_b<double, true>(scheme, visc, mode, p)
+                   : dispatch_b<double, false>(scheme, visc, mode, p);
+  if (dtype == ADVDIFF_F32)
+    return three_d ? dispatch_b<float, true>(scheme, visc, mode, p)
+                   : dispatch_b<float, false>(scheme, visc, mode, p);
+  return hipErrorInvalidValue;
 }
 
 }  // namespace advdiff
 
 extern "C" int advdiff_burgers3d_stage(int dtype, const void* in, const void* u0, void* out,
                                        int nx, int ny, int64_t sy, int64_t sz, int k0, int k1,
-                                       int border, int weno_z, double rdx, double rdy,
+                                       int border, int weno, double rdx, double rdy,
                                        double rdz, double vx, double vy, double vz, double dt,
                                        double a, double b, void* stream) {
   using namespace advdiff;
-  if (k1 <= k0) return hipSuccess;
-  if (k0 < 3 || nx <= 0 || ny <= 0 || in == out) return hipErrorInvalidValue;
-  hipStream_t st = (hipStream_t)stream;
-  if (dtype == ADVDIFF_F64)
-    return dispatch_b3<double>(in, u0, out, nx, ny, sy, sz, k0, k1, border, weno_z, rdx, rdy,
-                               rdz, vx, vy, vz, dt, a, b, st);
-  if (dtype == ADVDIFF_F32)
-    return dispatch_b3<float>(in, u0, out, nx, ny, sy, sz, k0, k1, border, weno_z, rdx, rdy,
-                              rdz, vx, vy, vz, dt, a, b, st);
-  return hipErrorInvalidValue;
+  const BArgs p{in, const_cast<void*>(u0), out, nx, ny, sy, sz, k0, k1, border, rdx, rdy, rdz,
+                vx, vy, vz, dt, a, b, (hipStream_t)stream};
+  return run_b(dtype, true, weno, false, p);
+}
+
+extern "C" int advdiff_burgers3d_stage_ls(int dtype, const void* in, void* du, void* out,
+                                          int nx, int ny, int64_t sy, int64_t sz, int k0,
+                                          int k1, int border, int weno, double rdx, double rdy,
+                                          double rdz, double vx, double vy, double vz,
+                                          double dt, double A, double B, void* stream) {
+  using namespace advdiff;
+  const BArgs p{in, du, out, nx, ny, sy, sz, k0, k1, border, rdx, rdy, rdz,
+                vx, vy, vz, dt, A, B, (hipStream_t)stream};
+  return run_b(dtype, true, weno, true, p);
 }
 
 extern "C" int advdiff_burgers2d_stage(int dtype, const void* in, const void* u0, void* out,
                                        int nx, int64_t sy, int j0, int j1, int border,
-                                       int weno_z, double rdx, double rdy, double vx, double vy,
+                                       int weno, double rdx, double rdy, double vx, double vy,
                                        double dt, double a, double b, void* stream) {
   using namespace advdiff;
-  if (j1 <= j0) return hipSuccess;
-  if (j0 < 3 || nx <= 0 || in == out) return hipErrorInvalidValue;
-  hipStream_t st = (hipStream_t)stream;
-  if (dtype == ADVDIFF_F64)
-    return dispatch_b2<double>(in, u0, out, nx, sy, j0, j1, border, weno_z, rdx, rdy, vx, vy,
-                               dt, a, b, st);
-  if (dtype == ADVDIFF_F32)
-    return dispatch_b2<float>(in, u0, out, nx, sy, j0, j1, border, weno_z, rdx, rdy, vx, vy,
-                              dt, a, b, st);
-  return hipErrorInvalidValue;
+  const BArgs p{in, const_cast<void*>(u0), out, nx, 0, sy, 0, j0, j1, border, rdx, rdy, 0.0,
+                vx, vy, 0.0, dt, a, b, (hipStream_t)stream};
+  return run_b(dtype, false, weno, false, p);
+}
+
+extern "C" int advdiff_burgers2d_stage_ls(int dtype, const void* in, void* du, void* out,
+                                          int nx, int64_t sy, int j0, int j1, int border,
+                                          int weno, double rdx, double rdy, double vx,
+                                          double vy, double dt, double A, double B,
+                                          void* stream) {
+  using namespace advdiff;
+  const BArgs p{in, du, out, nx, 0, sy, 0, j0, j1, border, rdx, rdy, 0.0,
+                vx, vy, 0.0, dt, A, B, (hipStream_t)stream};
+  return run_b(dtype, false, weno, true, p);
 }

@@ -205,4 +205,109 @@ __device__ __forceinline__ T weno5_face(T p0, T p1, T p2, T p3, T p4,   // fp i-
   }
 }
 
+// Left-biased WENO7 (Jiang–Shu weights) at the right face of v3 from v0..v6 (= f at
+// i-3..i+3), as numerator/denominator.  Smoothness indicators and candidate stencils
+// exactly as the MATLAB prototype (Matlab_Prototipes/InviscidBurgersNd/WENO7resAdv1d.m;
+// CPU port: models/prototypes.py::weno7_res), linear weights (1, 12, 18, 4)/35 and
+// eps = 1e-6; alpha_k = g_k/(eps+beta_k)² over the common denominator Π_k (eps+beta_k)²
+// (the /35 cancels).  The beta_k are symmetric under stencil reversal, so the f⁻ side
+// is this function on the mirrored stencil.
+template <typename T>
+__device__ __forceinline__ void weno7_nd(T m3, T m2, T m1, T o, T p1, T p2, T p3, T& num,
+                                         T& den) {
+#pragma clang fp contract(off)
+  constexpr T eps = T(1e-6);
+  const T b0 = fma(m1, fma(T(134241), m1, T(-114894) * o),
+               fma(m3, fma(T(56694), m1, fma(T(-47214), m2, fma(T(6649), m3, T(-22778) * o))),
+               fma(T(25729) * o, o, m2 * fma(T(-210282), m1, fma(T(85641), m2, T(86214) * o)))));
+  const T b1 = fma(o, fma(T(41001), o, T(-30414) * p1),
+               fma(m2, fma(T(-19374), m1, fma(T(3169), m2, fma(T(19014), o, T(-5978) * p1))),
+               fma(T(6649) * p1, p1, m1 * fma(T(33441), m1, fma(T(-70602), o, T(23094) * p1)))));
+  const T b2 = fma(p1, fma(T(33441), p1, T(-19374) * p2),
+               fma(m1, fma(T(6649), m1, fma(T(-30414), o, fma(T(23094), p1, T(-5978) * p2))),
+               fma(T(3169) * p2, p2, o * fma(T(41001), o, fma(T(-70602), p1, T(19014) * p2)))));
+  const T b3 = fma(p2, fma(T(85641), p2, T(-47214) * p3),
+               fma(o, fma(T(25729), o, fma(T(-114894), p1, fma(T(86214), p2, T(-22778) * p3))),
+               fma(T(6649) * p3, p3, p1 * fma(T(134241), p1, fma(T(-210282), p2, T(56694) * p3)))));
+  // candidate polynomials (times 12)
+  const T q0 = fma(T(25), o, fma(T(-23), m1, fma(T(13), m2, T(-3) * m3)));
+  const T q1 = fma(T(3), p1, fma(T(13), o, fma(T(-5), m1, m2)));
+  const T q2 = fma(T(7), p1, fma(T(7), o, -(m1 + p2)));
+  const T q3 = fma(T(13), p1, fma(T(-5), p2, fma(T(3), o, p3)));
+  const T e0 = eps + b0, e1 = eps + b1, e2 = eps + b2, e3 = eps + b3;
+  const T s0 = e0 * e0, s1 = e1 * e1, s2 = e2 * e2, s3 = e3 * e3;
+  const T s01 = s0 * s1, s23 = s2 * s3;
+  // alpha_k ∝ g_k Π_{j≠k} s_j
+  const T w0 = s23 * s1, w1 = T(12) * (s23 * s0), w2 = T(18) * (s01 * s3), w3 = T(4) * (s01 * s2);
+  num = fma(w0, q0, fma(w1, q1, fma(w2, q2, w3 * q3)));
+  den = T(12) * (((w0 + w1) + w2) + w3);
+}
+
+// WENO7 numerical flux at face i+½ from fp(i-3..i+3) and fm(i-2..i+4).
+template <typename T>
+__device__ __forceinline__ T weno7_face(const T* p, const T* m) {
+#pragma clang fp contract(off)
+  T n1, d1, n2, d2;
+  weno7_nd<T>(p[0], p[1], p[2], p[3], p[4], p[5], p[6], n1, d1);
+  weno7_nd<T>(m[6], m[5], m[4], m[3], m[2], m[1], m[0], n2, d2);
+  if constexpr (sizeof(T) == 8) {
+    return fast_div(fma(n1, d2, n2 * d1), d1 * d2);
+  } else {
+    return fast_div(n1, d1) + fast_div(n2, d2);
+  }
+}
+
+// Face-flux reconstruction by scheme: W = 5 (WZ: Jiang–Shu / Borges-Z) or 7 (Jiang–Shu).
+// face(p, m): flux at c+½ from p = f⁺(c-R+1 .. c+R-1), m = f⁻(c-R+2 .. c+R).
+template <typename T, int W, bool WZ>
+struct Recon;
+
+template <typename T, bool WZ>
+struct Recon<T, 5, WZ> {
+  static constexpr int R = 3;
+  __device__ __forceinline__ static T face(const T* p, const T* m) {
+    return weno5_face<T, WZ>(p[0], p[1], p[2], p[3], p[4], m[0], m[1], m[2], m[3], m[4]);
+  }
+};
+
+template <typename T>
+struct Recon<T, 7, false> {
+  static constexpr int R = 4;
+  __device__ __forceinline__ static T face(const T* p, const T* m) { return weno7_face<T>(p, m); }
+};
+
+// ---------------------------------------------------------------------------------
+// Stage epilogues.  MODE selects the time integrator's per-stage update:
+//   kSsp1 : out = b (c + dt L)                      (SSP-RK3 stage 1)
+//   kSsp  : out = a aux + b (c + dt L)              (SSP-RK3, aux = u^n)
+//   kLs1  : d = dt L;          aux = d; out = c + b d   (low-storage RK, first stage)
+//   kLs   : d = a aux + dt L;  aux = d; out = c + b d   (Carpenter–Kennedy 2N storage)
+// ---------------------------------------------------------------------------------
+enum : int { kSsp1 = 0, kSsp = 1, kLs1 = 2, kLs = 3 };
+
+template <int MODE>
+constexpr bool reads_aux() { return MODE == kSsp || MODE == kLs; }
+
+template <typename T, int MODE>
+__device__ __forceinline__ T stage_value(T ax, T c, T L, T dt, T a, T b, T& dnew) {
+#pragma clang fp contract(off)
+  if constexpr (MODE == kSsp1 || MODE == kSsp) {
+    return rk_stage<T, MODE == kSsp>(ax, c, L, dt, a, b);
+  } else {
+    T d = dt * L;
+    if constexpr (MODE == kLs) d = fma(a, ax, d);
+    dnew = d;
+    return fma(b, d, c);
+  }
+}
+
+// out[o] (and aux[o] for low-storage modes) of an active cell
+template <typename T, int MODE>
+__device__ __forceinline__ void stage_store(T* out, T* aux, int64_t o, T ax, T c, T L, T dt,
+                                            T a, T b) {
+  T d = T(0);
+  out[o] = stage_value<T, MODE>(ax, c, L, dt, a, b, d);
+  if constexpr (MODE == kLs1 || MODE == kLs) aux[o] = d;
+}
+
 }  // namespace advdiff

@@ -26,9 +26,9 @@
 
 namespace advdiff {
 
-template <typename T, int ORDER, int TX, int TY, bool USE_U0>
+template <typename T, int ORDER, int TX, int TY, int MODE>
 __global__ __launch_bounds__(TX* TY) void diffusion3d_stage_kernel(
-    const T* __restrict__ in, const T* u0, T* out, int nx, int ny, int64_t sy, int64_t sz,
+    const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz,
     int k0, int k1, int zchunk, int border, T cx, T cy, T cz, T dt, T a, T b) {
   constexpr int R = FD<ORDER>::R;
   constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NS = R + 2, NT = TX * TY, NE = LX * LY;
@@ -79,8 +79,8 @@ __global__ __launch_bounds__(TX* TY) void diffusion3d_stage_kernel(
   for (int k = kc0; k < kc1; ++k) {
     stash(k + R);                       // plane k+R: loaded one iteration ago
     if (k + 1 < kc1) fetch(k + R + 1);  // keep the next plane's loads in flight
-    T uo = T(0);
-    if constexpr (USE_U0) uo = u0[(int64_t)k * sz + own];
+    T ax = T(0);
+    if constexpr (reads_aux<MODE>()) ax = aux[(int64_t)k * sz + own];
     __syncthreads();
     zw[2 * R] = ring[(k + R) % NS][lc];
     const T* c = ring[k % NS];
@@ -94,15 +94,15 @@ __global__ __launch_bounds__(TX* TY) void diffusion3d_stage_kernel(
       lap = lap3(cx, FD<2>::d2(c[lc - 1], ctr, c[lc + 1]), cy,
                  FD<2>::d2(c[lc - LX], ctr, c[lc + LX]), cz, FD<2>::d2(zw[0], ctr, zw[2]));
     }
-    if (active) out[(int64_t)k * sz + own] = rk_stage<T, USE_U0>(uo, ctr, lap, dt, a, b);
+    if (active) stage_store<T, MODE>(out, aux, (int64_t)k * sz + own, ax, ctr, lap, dt, a, b);
 #pragma unroll
     for (int q = 0; q < 2 * R; ++q) zw[q] = zw[q + 1];
   }
 }
 
-template <typename T, int ORDER, int TX, bool USE_U0>
+template <typename T, int ORDER, int TX, int MODE>
 __global__ __launch_bounds__(TX) void diffusion2d_stage_kernel(
-    const T* __restrict__ in, const T* u0, T* out, int nx, int64_t sy, int j0, int j1,
+    const T* __restrict__ in, T* aux, T* out, int nx, int64_t sy, int j0, int j1,
     int ychunk, int border, T cx, T cy, T dt, T a, T b) {
   constexpr int R = FD<ORDER>::R;
   constexpr int LX = TX + 2 * R, NS = R + 2;
@@ -143,8 +143,8 @@ __global__ __launch_bounds__(TX) void diffusion2d_stage_kernel(
   for (int jj = jc0; jj < jc1; ++jj) {
     stash(jj + R);
     if (jj + 1 < jc1) fetch(jj + R + 1);
-    T uo = T(0);
-    if constexpr (USE_U0) uo = u0[(int64_t)jj * sy + ic];
+    T ax = T(0);
+    if constexpr (reads_aux<MODE>()) ax = aux[(int64_t)jj * sy + ic];
     __syncthreads();
     yw[2 * R] = ring[(jj + R) % NS][lc];
     const T* c = ring[jj % NS];
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(TX) void diffusion2d_stage_kernel(
     } else {
       lap = lap2(cx, FD<2>::d2(c[lc - 1], ctr, c[lc + 1]), cy, FD<2>::d2(yw[0], ctr, yw[2]));
     }
-    if (active) out[(int64_t)jj * sy + i] = rk_stage<T, USE_U0>(uo, ctr, lap, dt, a, b);
+    if (active) stage_store<T, MODE>(out, aux, (int64_t)jj * sy + i, ax, ctr, lap, dt, a, b);
 #pragma unroll
     for (int q = 0; q < 2 * R; ++q) yw[q] = yw[q + 1];
   }
@@ -168,80 +168,85 @@ __global__ __launch_bounds__(TX) void diffusion2d_stage_kernel(
 constexpr int kTX3 = 64, kTY3 = 16;  // 1024-thread groups: one wave per tile row (A/B: profiles/)
 constexpr int kTX2 = 256;
 
-template <typename T, int ORDER, int TY, bool USE_U0>
-static hipError_t launch_d3_ty(const void* in, const void* u0, void* out, int nx, int ny,
-                               int64_t sy, int64_t sz, int k0, int k1, int border, double cx,
-                               double cy, double cz, double dt, double a, double b,
-                               hipStream_t st) {
-  const int gx = div_up(nx, kTX3), gy = div_up(ny, TY);
-  const int zc = pick_chunk(k1 - k0, (long long)gx * gy, 8, 256);
-  const int gz = div_up(k1 - k0, zc);
+struct DArgs {
+  const void* in;
+  void* aux;
+  void* out;
+  int nx, ny;
+  int64_t sy, sz;
+  int lo, hi, border;  // marched-axis range [lo, hi)
+  double cx, cy, cz, dt, a, b;
+  hipStream_t st;
+};
+
+template <typename T, int ORDER, int TY, int MODE>
+static hipError_t launch_d3_ty(const DArgs& p) {
+  const int gx = div_up(p.nx, kTX3), gy = div_up(p.ny, TY);
+  const int zc = pick_chunk(p.hi - p.lo, (long long)gx * gy, 8, 256);
+  const int gz = div_up(p.hi - p.lo, zc);
   const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
-  hipLaunchKernelGGL((diffusion3d_stage_kernel<T, ORDER, kTX3, TY, USE_U0>), dim3(gx, gy, gz),
-                     dim3(kTX3, TY, 1), 0, st, (const T*)in, (const T*)u0, (T*)out, nx, ny, sy,
-                     sz, k0, k1, zc, border, T(cx * s), T(cy * s), T(cz * s), T(dt), T(a), T(b));
+  hipLaunchKernelGGL((diffusion3d_stage_kernel<T, ORDER, kTX3, TY, MODE>), dim3(gx, gy, gz),
+                     dim3(kTX3, TY, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx,
+                     p.ny, p.sy, p.sz, p.lo, p.hi, zc, p.border, T(p.cx * s), T(p.cy * s),
+                     T(p.cz * s), T(p.dt), T(p.a), T(p.b));
   return hipGetLastError();
 }
 
-template <typename T, int ORDER, bool USE_U0>
-static hipError_t launch_d3(const void* in, const void* u0, void* out, int nx, int ny,
-                            int64_t sy, int64_t sz, int k0, int k1, int border, double cx,
-                            double cy, double cz, double dt, double a, double b,
-                            hipStream_t st) {
+template <typename T, int ORDER, int MODE>
+static hipError_t launch_d3(const DArgs& p) {
   static const int ty = knob("D3_TY", kTY3);
-#define TYL(TY) \
-  return launch_d3_ty<T, ORDER, TY, USE_U0>(in, u0, out, nx, ny, sy, sz, k0, k1, border, cx, cy, cz, dt, a, b, st)
   switch (ty) {
-    case 4: TYL(4);
-    case 16: TYL(16);
-    default: TYL(8);
+    case 4: return launch_d3_ty<T, ORDER, 4, MODE>(p);
+    case 16: return launch_d3_ty<T, ORDER, 16, MODE>(p);
+    default: return launch_d3_ty<T, ORDER, 8, MODE>(p);
   }
-#undef TYL
 }
 
-template <typename T, int ORDER, bool USE_U0>
-static hipError_t launch_d2(const void* in, const void* u0, void* out, int nx, int64_t sy,
-                            int j0, int j1, int border, double cx, double cy, double dt,
-                            double a, double b, hipStream_t st) {
-  const int gx = div_up(nx, kTX2);
-  const int yc = pick_chunk(j1 - j0, gx, 8, 256);
-  const int gy = div_up(j1 - j0, yc);
+template <typename T, int ORDER, int MODE>
+static hipError_t launch_d2(const DArgs& p) {
+  const int gx = div_up(p.nx, kTX2);
+  const int yc = pick_chunk(p.hi - p.lo, gx, 8, 256);
+  const int gy = div_up(p.hi - p.lo, yc);
   const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
-  hipLaunchKernelGGL((diffusion2d_stage_kernel<T, ORDER, kTX2, USE_U0>), dim3(gx, gy, 1),
-                     dim3(kTX2, 1, 1), 0, st, (const T*)in, (const T*)u0, (T*)out, nx, sy,
-                     j0, j1, yc, border, T(cx * s), T(cy * s), T(dt), T(a), T(b));
+  hipLaunchKernelGGL((diffusion2d_stage_kernel<T, ORDER, kTX2, MODE>), dim3(gx, gy, 1),
+                     dim3(kTX2, 1, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx,
+                     p.sy, p.lo, p.hi, yc, p.border, T(p.cx * s), T(p.cy * s), T(p.dt),
+                     T(p.a), T(p.b));
   return hipGetLastError();
 }
 
-template <typename T>
-static hipError_t dispatch_d3(const void* in, const void* u0, void* out, int nx, int ny,
-                              int64_t sy, int64_t sz, int k0, int k1, int border, int order,
-                              double cx, double cy, double cz, double dt, double a, double b,
-                              hipStream_t st) {
-  const bool use_u0 = a != 0.0;
-#define D3(ORD, U) \
-  return launch_d3<T, ORD, U>(in, u0, out, nx, ny, sy, sz, k0, k1, border, cx, cy, cz, dt, a, b, st)
-  if (order == 4) {
-    if (use_u0) D3(4, true); else D3(4, false);
-  } else if (order == 2) {
-    if (use_u0) D3(2, true); else D3(2, false);
+template <typename T, bool THREE_D, int ORDER>
+static hipError_t d_by_mode(int mode, const DArgs& p) {
+#define DM(M) return THREE_D ? launch_d3<T, ORDER, M>(p) : launch_d2<T, ORDER, M>(p)
+  switch (mode) {
+    case kSsp1: DM(kSsp1);
+    case kSsp: DM(kSsp);
+    case kLs1: DM(kLs1);
+    default: DM(kLs);
   }
-#undef D3
-  return hipErrorInvalidValue;
+#undef DM
 }
 
-template <typename T>
-static hipError_t dispatch_d2(const void* in, const void* u0, void* out, int nx, int64_t sy,
-                              int j0, int j1, int border, int order, double cx, double cy,
-                              double dt, double a, double b, hipStream_t st) {
-  const bool use_u0 = a != 0.0;
-#define D2(ORD, U) return launch_d2<T, ORD, U>(in, u0, out, nx, sy, j0, j1, border, cx, cy, dt, a, b, st)
-  if (order == 4) {
-    if (use_u0) D2(4, true); else D2(4, false);
-  } else if (order == 2) {
-    if (use_u0) D2(2, true); else D2(2, false);
+static hipError_t run_d(int dtype, bool three_d, int order, bool ls, const DArgs& p) {
+  if (p.hi <= p.lo) return hipSuccess;
+  const int R = order / 2;
+  if ((order != 2 && order != 4) || p.lo < R || p.nx <= 0 || (three_d && p.ny <= 0) ||
+      p.in == p.out || p.in == p.aux)
+    return hipErrorInvalidValue;
+  if (three_d && p.sy * (int64_t)p.ny >= (int64_t(1) << 31))
+    return hipErrorInvalidValue;  // 32-bit plane offsets
+  const int mode = ls ? (p.a != 0.0 ? kLs : kLs1) : (p.a != 0.0 ? kSsp : kSsp1);
+#define DD(T, O) \
+  return three_d ? d_by_mode<T, true, O>(mode, p) : d_by_mode<T, false, O>(mode, p)
+  if (dtype == ADVDIFF_F64) {
+    if (order == 4) DD(double, 4);
+    DD(double, 2);
   }
-#undef D2
+  if (dtype == ADVDIFF_F32) {
+    if (order == 4) DD(float, 4);
+    DD(float, 2);
+  }
+#undef DD
   return hipErrorInvalidValue;
 }
 
@@ -253,18 +258,20 @@ extern "C" int advdiff_diffusion3d_stage(int dtype, const void* in, const void* 
                                          double cz, double dt, double a, double b,
                                          void* stream) {
   using namespace advdiff;
-  if (k1 <= k0) return hipSuccess;
-  const int R = order / 2;
-  if (k0 < R || nx <= 0 || ny <= 0 || in == out) return hipErrorInvalidValue;
-  if (sy * (int64_t)ny >= (int64_t(1) << 31)) return hipErrorInvalidValue;  // 32-bit plane offsets
-  hipStream_t st = (hipStream_t)stream;
-  if (dtype == ADVDIFF_F64)
-    return dispatch_d3<double>(in, u0, out, nx, ny, sy, sz, k0, k1, border, order, cx, cy,
-                               cz, dt, a, b, st);
-  if (dtype == ADVDIFF_F32)
-    return dispatch_d3<float>(in, u0, out, nx, ny, sy, sz, k0, k1, border, order, cx, cy,
-                              cz, dt, a, b, st);
-  return hipErrorInvalidValue;
+  const DArgs p{in, const_cast<void*>(u0), out, nx, ny, sy, sz, k0, k1, border,
+                cx, cy, cz, dt, a, b, (hipStream_t)stream};
+  return run_d(dtype, true, order, false, p);
+}
+
+extern "C" int advdiff_diffusion3d_stage_ls(int dtype, const void* in, void* du, void* out,
+                                            int nx, int ny, int64_t sy, int64_t sz, int k0,
+                                            int k1, int border, int order, double cx,
+                                            double cy, double cz, double dt, double A,
+                                            double B, void* stream) {
+  using namespace advdiff;
+  const DArgs p{in, du, out, nx, ny, sy, sz, k0, k1, border, cx, cy, cz, dt, A, B,
+                (hipStream_t)stream};
+  return run_d(dtype, true, order, true, p);
 }
 
 extern "C" int advdiff_diffusion2d_stage(int dtype, const void* in, const void* u0, void* out,
@@ -272,15 +279,17 @@ extern "C" int advdiff_diffusion2d_stage(int dtype, const void* in, const void* 
                                          int order, double cx, double cy, double dt, double a,
                                          double b, void* stream) {
   using namespace advdiff;
-  if (j1 <= j0) return hipSuccess;
-  const int R = order / 2;
-  if (j0 < R || nx <= 0 || in == out) return hipErrorInvalidValue;
-  hipStream_t st = (hipStream_t)stream;
-  if (dtype == ADVDIFF_F64)
-    return dispatch_d2<double>(in, u0, out, nx, sy, j0, j1, border, order, cx, cy, dt, a, b,
-                               st);
-  if (dtype == ADVDIFF_F32)
-    return dispatch_d2<float>(in, u0, out, nx, sy, j0, j1, border, order, cx, cy, dt, a, b,
-                              st);
-  return hipErrorInvalidValue;
+  const DArgs p{in, const_cast<void*>(u0), out, nx, 0, sy, 0, j0, j1, border,
+                cx, cy, 0.0, dt, a, b, (hipStream_t)stream};
+  return run_d(dtype, false, order, false, p);
+}
+
+extern "C" int advdiff_diffusion2d_stage_ls(int dtype, const void* in, void* du, void* out,
+                                            int nx, int64_t sy, int j0, int j1, int border,
+                                            int order, double cx, double cy, double dt,
+                                            double A, double B, void* stream) {
+  using namespace advdiff;
+  const DArgs p{in, du, out, nx, 0, sy, 0, j0, j1, border, cx, cy, 0.0, dt, A, B,
+                (hipStream_t)stream};
+  return run_d(dtype, false, order, true, p);
 }

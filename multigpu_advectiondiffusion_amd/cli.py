@@ -60,7 +60,10 @@ def build_parser():
     ap.add_argument("--ic", help="initial condition: zero|square|sine|heat|gaussian|plates|disc")
     ap.add_argument("--order", type=int, default=4, help="diffusion FD order: 4 (13-pt) or 2 (7-pt)")
     ap.add_argument("--safety", type=float, default=0.9, help="diffusion dt safety factor (MG used 0.8)")
-    ap.add_argument("--weno", choices=["js", "z"], default="z")
+    ap.add_argument("--weno", choices=["js", "z", "js7"], default="z",
+                    help="WENO5-JS, WENO5-Z (default) or WENO7-JS")
+    ap.add_argument("--integrator", choices=["ssprk3", "lsrk45"], default="ssprk3",
+                    help="SSP-RK3 (reference apps) or low-storage RK4(5) (MATLAB WENO7)")
     ap.add_argument("--viscosity", type=float, default=1e-5, help="Burgers C (0 = inviscid)")
     ap.add_argument("--cfl-mode", choices=["fixed", "adaptive"], default="fixed")
     ap.add_argument("--dtype", choices=["fp64", "fp32"], default="fp64")
@@ -143,7 +146,7 @@ def main(argv=None) -> int:
     dtype = torch.float64 if ns.dtype == "fp64" else torch.float32
     t0 = 0.1 if (ic == "heat") else 0.0  # heat kernel IC is the exact solution at t0
     solver = Solver(model, grid, comm, dtype=dtype, ic=ic, overlap=not ns.no_overlap, t0=t0,
-                    check_every=ns.check_every, decomp=ns.decomp)
+                    check_every=ns.check_every, decomp=ns.decomp, integrator=ns.integrator)
     if ns.restart:
         solver.load_checkpoint(ns.restart)
     if ns.initial:

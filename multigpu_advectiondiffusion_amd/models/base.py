@@ -71,7 +71,7 @@ class Model:
         self.grid = grid
 
     def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None, nx=None, ny=None,
-              border=None):  # pragma: no cover
+              border=None, ls=False):  # pragma: no cover
         raise NotImplementedError
 
     def stable_dt(self, umax: float | None = None) -> float:  # pragma: no cover

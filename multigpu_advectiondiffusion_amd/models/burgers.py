@@ -27,9 +27,10 @@ class Burgers(Model):
     name = "burgers"
 
     def __init__(self, viscosity: float = 0.0, weno: str = "z", cfl: float = 0.3,
-                 cfl_mode: str = "fixed", umax: float = 1.0, border: int = 3):
-        if weno not in ("js", "z"):
-            raise ValueError("weno must be 'js' (Jiang-Shu) or 'z' (Borges)")
+                 cfl_mode: str = "fixed", umax: float = 1.0, border: int | None = None):
+        if weno not in ("js", "z", "js7"):
+            raise ValueError("weno must be 'js' (WENO5 Jiang-Shu), 'z' (WENO5 Borges-Z) or "
+                             "'js7' (WENO7 Jiang-Shu, the MATLAB LFWENO7 prototype)")
         if cfl_mode not in ("fixed", "adaptive"):
             raise ValueError("cfl_mode must be 'fixed' or 'adaptive'")
         self.C = float(viscosity)
@@ -37,10 +38,10 @@ class Burgers(Model):
         self.cfl = float(cfl)
         self.cfl_mode = cfl_mode
         self.umax = float(umax)
-        self.radius = 3
-        self.border = int(border)
-        if self.border < 3:
-            raise ValueError("WENO5 needs a frozen border >= 3")
+        self.radius = 4 if weno == "js7" else 3
+        self.border = self.radius if border is None else int(border)
+        if self.border < self.radius:
+            raise ValueError(f"WENO needs a frozen border >= {self.radius}")
         self.needs_umax = cfl_mode == "adaptive"
 
     def bind(self, grid):
@@ -49,7 +50,7 @@ class Burgers(Model):
         self.dims = grid.dims
         self.rd = tuple(1.0 / h for h in d)
         self.visc = tuple(self.C / (h * h) for h in d)
-        kind = "WENO5-Z" if self.weno == "z" else "WENO5-JS"
+        kind = {"z": "WENO5-Z", "js": "WENO5-JS", "js7": "WENO7-JS"}[self.weno]
         self.title = f"Burgers-{grid.dims}D MI355X-{kind}"
 
     @property
@@ -64,22 +65,22 @@ class Burgers(Model):
         return dt
 
     def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None, nx=None, ny=None,
-              border=None):
+              border=None, ls=False):
         g = self.grid
         nx = g.nx if nx is None else nx
         ny = g.ny if ny is None else ny
         border = self.border if border is None else border
-        z = self.weno == "z"
+        z = self.weno
         if self.dims == 3:
             stencil.burgers3d_stage(inp, u0, out, nx=nx, ny=ny, k0=lo, k1=hi,
                                     border=border, weno_z=z, rdx=self.rd[0],
                                     rdy=self.rd[1], rdz=self.rd[2], vx=self.visc[0],
                                     vy=self.visc[1], vz=self.visc[2], dt=dt, a=a, b=b,
-                                    stream=stream)
+                                    stream=stream, ls=ls)
         else:
             stencil.burgers2d_stage(inp, u0, out, nx=nx, j0=lo, j1=hi, border=border,
                                     weno_z=z, rdx=self.rd[0], rdy=self.rd[1], vx=self.visc[0],
-                                    vy=self.visc[1], dt=dt, a=a, b=b, stream=stream)
+                                    vy=self.visc[1], dt=dt, a=a, b=b, stream=stream, ls=ls)
 
     def describe(self):
         d = super().describe()

@@ -62,7 +62,7 @@ class Diffusion(Model):
         return self.safety / (2.0 * sum(self.coef))
 
     def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None, nx=None, ny=None,
-              border=None):
+              border=None, ls=False):
         """nx/ny/border override the grid's for launches on a sub-box view (Cartesian)."""
         g = self.grid
         nx = g.nx if nx is None else nx
@@ -72,11 +72,11 @@ class Diffusion(Model):
             stencil.diffusion3d_stage(inp, u0, out, nx=nx, ny=ny, k0=lo, k1=hi,
                                       border=border, order=self.order, cx=self.coef[0],
                                       cy=self.coef[1], cz=self.coef[2], dt=dt, a=a, b=b,
-                                      stream=stream)
+                                      stream=stream, ls=ls)
         else:
             stencil.diffusion2d_stage(inp, u0, out, nx=nx, j0=lo, j1=hi, border=border,
                                       order=self.order, cx=self.coef[0], cy=self.coef[1],
-                                      dt=dt, a=a, b=b, stream=stream)
+                                      dt=dt, a=a, b=b, stream=stream, ls=ls)
 
     def describe(self):
         d = super().describe()

@@ -48,6 +48,11 @@ _SIGS = {
                          c_vp],
 }
 
+# low-storage RK variants share the signature of the SSP stage entries
+for _k in ("advdiff_diffusion3d_stage", "advdiff_diffusion2d_stage", "advdiff_burgers3d_stage",
+           "advdiff_burgers2d_stage"):
+    _SIGS[_k + "_ls"] = _SIGS[_k]
+
 
 def _load():
     global _lib, _err

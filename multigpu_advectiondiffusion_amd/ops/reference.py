@@ -100,7 +100,57 @@ def weno5_face(fp, fm, sl, z: bool):
         weno5(sl(fm, 3), sl(fm, 2), sl(fm, 1), sl(fm, 0), sl(fm, -1), z)
 
 
-def _combine(out_view, u0_view, c, L, dt, a, b):
+def weno7(m3, m2, m1, o, p1, p2, p3):
+    """Left-biased WENO7-JS value at the right face of `o`, written as the MATLAB prototype
+    (`Matlab_Prototipes/InviscidBurgersNd/WENO7resAdv1d.m`): alpha_k = g_k/(eps+beta_k)²,
+    w_k = alpha_k/Σalpha — the textbook form the HIP kernel's common-denominator rewrite
+    (csrc/kernels/common.hpp::weno7_nd) is checked against."""
+    B0 = (m1 * (134241 * m1 - 114894 * o) + m3 * (56694 * m1 - 47214 * m2 + 6649 * m3 - 22778 * o)
+          + 25729 * o * o + m2 * (-210282 * m1 + 85641 * m2 + 86214 * o))
+    B1 = (o * (41001 * o - 30414 * p1) + m2 * (-19374 * m1 + 3169 * m2 + 19014 * o - 5978 * p1)
+          + 6649 * p1 * p1 + m1 * (33441 * m1 - 70602 * o + 23094 * p1))
+    B2 = (p1 * (33441 * p1 - 19374 * p2) + m1 * (6649 * m1 - 30414 * o + 23094 * p1 - 5978 * p2)
+          + 3169 * p2 * p2 + o * (41001 * o - 70602 * p1 + 19014 * p2))
+    B3 = (p2 * (85641 * p2 - 47214 * p3) + o * (25729 * o - 114894 * p1 + 86214 * p2 - 22778 * p3)
+          + 6649 * p3 * p3 + p1 * (134241 * p1 - 210282 * p2 + 56694 * p3))
+    g = (1 / 35, 12 / 35, 18 / 35, 4 / 35)
+    al = [gk / (EPS + Bk) ** 2 for gk, Bk in zip(g, (B0, B1, B2, B3))]
+    sm = al[0] + al[1] + al[2] + al[3]
+    q0 = -3 * m3 + 13 * m2 - 23 * m1 + 25 * o
+    q1 = m2 - 5 * m1 + 13 * o + 3 * p1
+    q2 = -m1 + 7 * o + 7 * p1 - p2
+    q3 = 3 * o + 13 * p1 - 5 * p2 + p3
+    return (al[0] * q0 + al[1] * q1 + al[2] * q2 + al[3] * q3) / (12.0 * sm)
+
+
+def weno7_face(fp, fm, sl):
+    """WENO7 face fluxes along the last axis: f⁺ from i-3..i+3, f⁻ mirrored from i+4..i-2."""
+    return (weno7(*(sl(fp, o) for o in range(-3, 4)))
+            + weno7(*(sl(fm, o) for o in range(4, -3, -1))))
+
+
+SCHEMES = {"js": 0, "z": 1, "js7": 2}
+
+
+def scheme_code(weno) -> int:
+    """bool (legacy weno_z flag) | "js" | "z" | "js7" | int code -> kernel scheme code."""
+    if isinstance(weno, bool):
+        return int(weno)
+    if isinstance(weno, str):
+        return SCHEMES[weno]
+    return int(weno)
+
+
+def scheme_radius(weno) -> int:
+    return 4 if scheme_code(weno) == 2 else 3
+
+
+def _combine(out_view, u0_view, c, L, dt, a, b, ls=False):
+    if ls:  # low-storage RK: u0_view is du (read/written)
+        d = dt * L if a == 0.0 else a * u0_view + dt * L
+        u0_view.copy_(d)
+        out_view.copy_(c + b * d)
+        return
     v = b * (c + dt * L)
     if a != 0.0:
         v = a * u0_view + v
@@ -110,7 +160,8 @@ def _combine(out_view, u0_view, c, L, dt, a, b):
 # ---------------------------------------------------------------------------------
 # heat equation stages
 # ---------------------------------------------------------------------------------
-def diffusion3d_stage(inp, u0, out, nx, ny, k0, k1, border, order, cx, cy, cz, dt, a, b):
+def diffusion3d_stage(inp, u0, out, nx, ny, k0, k1, border, order, cx, cy, cz, dt, a, b,
+                      ls=False):
     if k1 <= k0 or nx - 2 * border <= 0 or ny - 2 * border <= 0:
         return
     B = border
@@ -130,8 +181,8 @@ def diffusion3d_stage(inp, u0, out, nx, ny, k0, k1, border, order, cx, cy, cz, d
                + cz * d2_fd2(sh(-1, 0, 0), c, sh(1, 0, 0)))
     else:
         raise ValueError(f"order {order}")
-    _combine(out[k0:k1, B:ny - B, B:nx - B], u0[k0:k1, B:ny - B, B:nx - B] if a != 0 else None,
-             c, lap, dt, a, b)
+    _combine(out[k0:k1, B:ny - B, B:nx - B],
+             u0[k0:k1, B:ny - B, B:nx - B] if (a != 0 or ls) else None, c, lap, dt, a, b, ls)
 
 
 def diffusion3d_step(uin, uout, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy, cz, dt):
@@ -150,7 +201,7 @@ def diffusion3d_step(uin, uout, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy,
                       2.0 / 3.0)
 
 
-def diffusion2d_stage(inp, u0, out, nx, j0, j1, border, order, cx, cy, dt, a, b):
+def diffusion2d_stage(inp, u0, out, nx, j0, j1, border, order, cx, cy, dt, a, b, ls=False):
     if j1 <= j0 or nx - 2 * border <= 0:
         return
     B = border
@@ -166,21 +217,25 @@ def diffusion2d_stage(inp, u0, out, nx, j0, j1, border, order, cx, cy, dt, a, b)
                + cy * d2_fd4(sh(-2, 0), sh(-1, 0), c, sh(1, 0), sh(2, 0)))
     else:
         lap = cx * d2_fd2(sh(0, -1), c, sh(0, 1)) + cy * d2_fd2(sh(-1, 0), c, sh(1, 0))
-    _combine(out[j0:j1, B:nx - B], u0[j0:j1, B:nx - B] if a != 0 else None, c, lap, dt, a, b)
+    _combine(out[j0:j1, B:nx - B], u0[j0:j1, B:nx - B] if (a != 0 or ls) else None, c, lap, dt,
+             a, b, ls)
 
 
 # ---------------------------------------------------------------------------------
 # Burgers stages
 # ---------------------------------------------------------------------------------
 def _faces_last_axis(fp, fm, lo, hi, z):
-    """F_{i+½} for i in [lo, hi) along the last axis."""
+    """F_{i+½} for i in [lo, hi) along the last axis (z: scheme, see scheme_code)."""
     def sl(t, o):
         return t[..., lo + o:hi + o]
-    return weno5_face(fp, fm, sl, z)
+    code = scheme_code(z)
+    if code == 2:
+        return weno7_face(fp, fm, sl)
+    return weno5_face(fp, fm, sl, bool(code))
 
 
 def burgers_rhs_3d(inp, nx, ny, k0, k1, border, weno_z, rdx, rdy, rdz, vx, vy, vz):
-    """L(u) on the box k in [k0,k1), j,i in [border, n-border). Requires border >= 3."""
+    """L(u) on the box k in [k0,k1), j,i in [border, n-border). Requires border >= R."""
     B = border
     fp, fm = lf_split(inp)
     # x faces i+½ for i in [B-1, nx-B): rows restricted to the box
@@ -212,16 +267,16 @@ def burgers_rhs_3d(inp, nx, ny, k0, k1, border, weno_z, rdx, rdy, rdz, vx, vy, v
 
 
 def burgers3d_stage(inp, u0, out, nx, ny, k0, k1, border, weno_z, rdx, rdy, rdz, vx, vy, vz,
-                    dt, a, b):
+                    dt, a, b, ls=False):
     if k1 <= k0 or nx - 2 * border <= 0 or ny - 2 * border <= 0:
         return
-    if border < 3:
-        raise ValueError("WENO5 needs a frozen border of at least 3 cells")
+    if border < scheme_radius(weno_z):
+        raise ValueError("WENO needs a frozen border of at least R cells")
     B = border
     L = burgers_rhs_3d(inp, nx, ny, k0, k1, B, weno_z, rdx, rdy, rdz, vx, vy, vz)
     c = inp[k0:k1, B:ny - B, B:nx - B]
-    _combine(out[k0:k1, B:ny - B, B:nx - B], u0[k0:k1, B:ny - B, B:nx - B] if a != 0 else None,
-             c, L, dt, a, b)
+    _combine(out[k0:k1, B:ny - B, B:nx - B],
+             u0[k0:k1, B:ny - B, B:nx - B] if (a != 0 or ls) else None, c, L, dt, a, b, ls)
 
 
 def burgers_rhs_2d(inp, nx, j0, j1, border, weno_z, rdx, rdy, vx, vy):
@@ -245,15 +300,17 @@ def burgers_rhs_2d(inp, nx, j0, j1, border, weno_z, rdx, rdy, vx, vy):
     return L
 
 
-def burgers2d_stage(inp, u0, out, nx, j0, j1, border, weno_z, rdx, rdy, vx, vy, dt, a, b):
+def burgers2d_stage(inp, u0, out, nx, j0, j1, border, weno_z, rdx, rdy, vx, vy, dt, a, b,
+                    ls=False):
     if j1 <= j0 or nx - 2 * border <= 0:
         return
-    if border < 3:
-        raise ValueError("WENO5 needs a frozen border of at least 3 cells")
+    if border < scheme_radius(weno_z):
+        raise ValueError("WENO needs a frozen border of at least R cells")
     B = border
     L = burgers_rhs_2d(inp, nx, j0, j1, B, weno_z, rdx, rdy, vx, vy)
     c = inp[j0:j1, B:nx - B]
-    _combine(out[j0:j1, B:nx - B], u0[j0:j1, B:nx - B] if a != 0 else None, c, L, dt, a, b)
+    _combine(out[j0:j1, B:nx - B], u0[j0:j1, B:nx - B] if (a != 0 or ls) else None, c, L, dt,
+             a, b, ls)
 
 
 def norms(x, y=None):

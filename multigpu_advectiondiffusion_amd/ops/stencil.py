@@ -41,22 +41,32 @@ def _ptr(t):
     return None if t is None else t.data_ptr()
 
 
+def _aux_ptr(u0, a, ls):
+    if ls:
+        if u0 is None:
+            raise ValueError("low-storage RK stage needs the du buffer")
+        return u0.data_ptr()
+    return _ptr(u0) if a != 0 else None
+
+
 def diffusion3d_stage(inp, u0, out, *, nx, ny, k0, k1, border, order, cx, cy, cz, dt, a, b,
-                      stream=None):
-    """out[k0:k1] = a*u0 + b*(inp + dt*K∇²inp) on the interior box (see kernels.h)."""
+                      stream=None, ls=False):
+    """out[k0:k1] = a*u0 + b*(inp + dt*K∇²inp) on the interior box (see kernels.h).
+    ls=True: low-storage RK stage, u0 is du: du = a*du + dt*L; out = inp + b*du."""
     _check_layout(inp, u0, out)
     if inp.is_cuda:
         lib = _lib.require()
         R = order // 2
         assert k0 >= R and k1 + R <= inp.shape[0], "stencil planes out of bounds"
         assert nx <= inp.shape[2] and ny <= inp.shape[1]
-        code = lib.advdiff_diffusion3d_stage(
-            _dtype_code(inp), _ptr(inp), _ptr(u0) if a != 0 else None, _ptr(out), nx, ny,
-            inp.stride(1), inp.stride(0), k0, k1, border, order, cx, cy, cz, dt, a, b,
-            _stream_ptr(stream))
+        fn = lib.advdiff_diffusion3d_stage_ls if ls else lib.advdiff_diffusion3d_stage
+        code = fn(_dtype_code(inp), _ptr(inp), _aux_ptr(u0, a, ls), _ptr(out), nx, ny,
+                  inp.stride(1), inp.stride(0), k0, k1, border, order, cx, cy, cz, dt, a, b,
+                  _stream_ptr(stream))
         _lib.check(code, "diffusion3d_stage")
     else:
-        ref.diffusion3d_stage(inp, u0, out, nx, ny, k0, k1, border, order, cx, cy, cz, dt, a, b)
+        ref.diffusion3d_stage(inp, u0, out, nx, ny, k0, k1, border, order, cx, cy, cz, dt, a, b,
+                              ls)
 
 
 def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy, cz, dt,
@@ -77,54 +87,57 @@ def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, 
 
 
 def diffusion2d_stage(inp, u0, out, *, nx, j0, j1, border, order, cx, cy, dt, a, b,
-                      stream=None):
+                      stream=None, ls=False):
     _check_layout(inp, u0, out)
     if inp.is_cuda:
         lib = _lib.require()
         R = order // 2
         assert j0 >= R and j1 + R <= inp.shape[0], "stencil rows out of bounds"
-        code = lib.advdiff_diffusion2d_stage(
-            _dtype_code(inp), _ptr(inp), _ptr(u0) if a != 0 else None, _ptr(out), nx,
-            inp.stride(0), j0, j1, border, order, cx, cy, dt, a, b, _stream_ptr(stream))
+        fn = lib.advdiff_diffusion2d_stage_ls if ls else lib.advdiff_diffusion2d_stage
+        code = fn(_dtype_code(inp), _ptr(inp), _aux_ptr(u0, a, ls), _ptr(out), nx,
+                  inp.stride(0), j0, j1, border, order, cx, cy, dt, a, b, _stream_ptr(stream))
         _lib.check(code, "diffusion2d_stage")
     else:
-        ref.diffusion2d_stage(inp, u0, out, nx, j0, j1, border, order, cx, cy, dt, a, b)
+        ref.diffusion2d_stage(inp, u0, out, nx, j0, j1, border, order, cx, cy, dt, a, b, ls)
 
 
 def burgers3d_stage(inp, u0, out, *, nx, ny, k0, k1, border, weno_z, rdx, rdy, rdz,
-                    vx=0.0, vy=0.0, vz=0.0, dt, a, b, stream=None):
+                    vx=0.0, vy=0.0, vz=0.0, dt, a, b, stream=None, ls=False):
+    """weno_z: scheme — bool (WENO5 Z / JS) or "js" | "z" | "js7" (WENO7)."""
     _check_layout(inp, u0, out)
-    if border < 3:
-        raise ValueError("WENO5 needs a frozen border of at least 3 cells")
+    code_s, R = ref.scheme_code(weno_z), ref.scheme_radius(weno_z)
+    if border < R:
+        raise ValueError(f"WENO needs a frozen border of at least {R} cells")
     if inp.is_cuda:
         lib = _lib.require()
-        assert k0 >= 3 and k1 + 3 <= inp.shape[0], "stencil planes out of bounds"
-        code = lib.advdiff_burgers3d_stage(
-            _dtype_code(inp), _ptr(inp), _ptr(u0) if a != 0 else None, _ptr(out), nx, ny,
-            inp.stride(1), inp.stride(0), k0, k1, border, int(bool(weno_z)), rdx, rdy, rdz,
-            vx, vy, vz, dt, a, b, _stream_ptr(stream))
+        assert k0 >= R and k1 + R <= inp.shape[0], "stencil planes out of bounds"
+        fn = lib.advdiff_burgers3d_stage_ls if ls else lib.advdiff_burgers3d_stage
+        code = fn(_dtype_code(inp), _ptr(inp), _aux_ptr(u0, a, ls), _ptr(out), nx, ny,
+                  inp.stride(1), inp.stride(0), k0, k1, border, code_s, rdx, rdy, rdz,
+                  vx, vy, vz, dt, a, b, _stream_ptr(stream))
         _lib.check(code, "burgers3d_stage")
     else:
-        ref.burgers3d_stage(inp, u0, out, nx, ny, k0, k1, border, bool(weno_z), rdx, rdy, rdz,
-                            vx, vy, vz, dt, a, b)
+        ref.burgers3d_stage(inp, u0, out, nx, ny, k0, k1, border, code_s, rdx, rdy, rdz,
+                            vx, vy, vz, dt, a, b, ls)
 
 
 def burgers2d_stage(inp, u0, out, *, nx, j0, j1, border, weno_z, rdx, rdy, vx=0.0, vy=0.0,
-                    dt, a, b, stream=None):
+                    dt, a, b, stream=None, ls=False):
     _check_layout(inp, u0, out)
-    if border < 3:
-        raise ValueError("WENO5 needs a frozen border of at least 3 cells")
+    code_s, R = ref.scheme_code(weno_z), ref.scheme_radius(weno_z)
+    if border < R:
+        raise ValueError(f"WENO needs a frozen border of at least {R} cells")
     if inp.is_cuda:
         lib = _lib.require()
-        assert j0 >= 3 and j1 + 3 <= inp.shape[0], "stencil rows out of bounds"
-        code = lib.advdiff_burgers2d_stage(
-            _dtype_code(inp), _ptr(inp), _ptr(u0) if a != 0 else None, _ptr(out), nx,
-            inp.stride(0), j0, j1, border, int(bool(weno_z)), rdx, rdy, vx, vy, dt, a, b,
-            _stream_ptr(stream))
+        assert j0 >= R and j1 + R <= inp.shape[0], "stencil rows out of bounds"
+        fn = lib.advdiff_burgers2d_stage_ls if ls else lib.advdiff_burgers2d_stage
+        code = fn(_dtype_code(inp), _ptr(inp), _aux_ptr(u0, a, ls), _ptr(out), nx,
+                  inp.stride(0), j0, j1, border, code_s, rdx, rdy, vx, vy, dt, a, b,
+                  _stream_ptr(stream))
         _lib.check(code, "burgers2d_stage")
     else:
-        ref.burgers2d_stage(inp, u0, out, nx, j0, j1, border, bool(weno_z), rdx, rdy, vx, vy,
-                            dt, a, b)
+        ref.burgers2d_stage(inp, u0, out, nx, j0, j1, border, code_s, rdx, rdy, vx, vy,
+                            dt, a, b, ls)
 
 
 class NormReducer:

@@ -24,6 +24,7 @@ import numpy as np
 import torch
 
 from .models.base import Grid, Model, RunStats
+from .models.prototypes import LSRK45_A, LSRK45_B
 from .ops import stencil
 from .parallel.comm import Comm
 from .parallel.decomposition import CartesianDecomposition, parse_proc_grid
@@ -34,6 +35,9 @@ from .utils import metrics, trace
 
 # Shu–Osher SSP-RK3: out = a*u^n + b*(in + dt*L(in))
 RK3 = ((0.0, 1.0), (0.75, 0.25), (1.0 / 3.0, 2.0 / 3.0))
+# Carpenter–Kennedy low-storage RK4(5) (2N storage): du = A*du + dt*L(u); u += B*du
+# (`Matlab_Prototipes/InviscidBurgersNd/LFWENO7FDM1d.m`, models/prototypes.py LSRK45_*)
+INTEGRATORS = ("ssprk3", "lsrk45")
 
 
 def _row_pitch(nx: int, elem: int, align_bytes: int = 256) -> int:
@@ -45,10 +49,16 @@ class Solver:
     def __init__(self, model: Model, grid: Grid, comm: Comm | None = None, *,
                  dtype=torch.float64, device=None, ic: str = "sine", ic_params=None,
                  overlap: bool = True, pad_rows: bool = True, t0: float = 0.0,
-                 check_every: int = 0, fused: bool | None = None, decomp=None):
+                 check_every: int = 0, fused: bool | None = None, decomp=None,
+                 integrator: str = "ssprk3"):
         """decomp: process grid — None/"slab" (split the slowest axis only, the
         reference's layout), "auto" (smallest halo surface) or "PZxPYxPX" / a tuple in
-        array axis order ((pz, py, px) in 3-D, (py, px) in 2-D)."""
+        array axis order ((pz, py, px) in 3-D, (py, px) in 2-D).
+        integrator: "ssprk3" (3 stages, the C++/CUDA apps) or "lsrk45" (low-storage
+        RK4(5), 5 stages, the MATLAB WENO7 prototypes)."""
+        if integrator not in INTEGRATORS:
+            raise ValueError(f"integrator must be one of {INTEGRATORS}")
+        self.integrator = integrator
         if comm is None:
             comm = Comm(device=device or ("cuda" if torch.cuda.is_available() else "cpu"))
             if comm.device.type == "cuda" and comm.device.index is None:
@@ -67,8 +77,9 @@ class Solver:
         self.pgrid = parse_proc_grid(decomp, comm.size, ashape, model.radius)
         self.cart = any(p > 1 for p in self.pgrid[1:])
         self.fused = model.supports_fused if fused is None else (fused and model.supports_fused)
-        if self.fused and (self.cart or grid.n_decomposed // comm.size < 3 * model.radius):
-            self.fused = False  # x/y split, or slabs thinner than the wide halo: per stage
+        if self.fused and (self.cart or integrator != "ssprk3"
+                           or grid.n_decomposed // comm.size < 3 * model.radius):
+            self.fused = False  # x/y split, LSRK, or slabs thinner than the wide halo
         G = 3 * model.radius if self.fused else model.radius
         self.ghost = G
         self.cd = CartesianDecomposition(ashape, self.pgrid, comm.rank, G)
@@ -78,8 +89,13 @@ class Solver:
         self.sx = _row_pitch(ax, elem) if pad_rows else ax
         self.ic_name, self.ic_params = ic, ic_params
         self.u = self._initial_field(ic, ic_params)
+        self.du = None
         if self.fused:
             self.un = self.u.clone()  # ping-pong partner; frozen cells keep the IC
+            self.A = self.B = None
+        elif integrator == "lsrk45":
+            self.un = self.u.clone()  # stage ping-pong partner
+            self.du = torch.zeros_like(self.u)
             self.A = self.B = None
         else:
             self.A = self.u.clone()
@@ -164,21 +180,25 @@ class Solver:
         return tuple(reversed(self.cd.owned_box()))
 
     def fields(self):
-        return (self.u, self.un) if self.fused else (self.u, self.A, self.B)
+        if self.fused:
+            return (self.u, self.un)
+        if self.du is not None:
+            return (self.u, self.un)  # du is scratch (never read at stage 1)
+        return (self.u, self.A, self.B)
 
     # ------------------------------------------------------------------------------
     # stepping
     # ------------------------------------------------------------------------------
-    def _launch(self, inp, u0, out, rng, dt, a, b):
+    def _launch(self, inp, u0, out, rng, dt, a, b, ls=False):
         if self.cart:
-            self._launch_box(inp, u0, out, rng, dt, a, b)
+            self._launch_box(inp, u0, out, rng, dt, a, b, ls)
             return
         lo, hi = rng
         if hi > lo:
-            self.model.stage(inp, u0, out, lo, hi, dt, a, b)
+            self.model.stage(inp, u0, out, lo, hi, dt, a, b, ls=ls)
             trace.sync_check(f"{self.model.name} stage [{lo},{hi})", self.device)
 
-    def _launch_box(self, inp, u0, out, box, dt, a, b):
+    def _launch_box(self, inp, u0, out, box, dt, a, b, ls=False):
         """Stage on a local box (array order).  The kernels update [border, n-border) of
         the x/y extent they are given, so a box is launched on a VIEW widened by R on
         each side with border R (the views never leave the allocation: every box lies
@@ -195,27 +215,27 @@ class Solver:
             sl = (slice(None), slice(x0 - R, x1 + R))
             kw = dict(nx=x1 - x0 + 2 * R, border=R)
         v = (lambda t: None if t is None else t[sl])
-        self.model.stage(v(inp), v(u0), v(out), z0, z1, dt, a, b, **kw)
+        self.model.stage(v(inp), v(u0), v(out), z0, z1, dt, a, b, ls=ls, **kw)
         trace.sync_check(f"{self.model.name} stage box {box}", self.device)
 
-    def _stage(self, inp, u0, out, a, b, dt):
+    def _stage(self, inp, u0, out, a, b, dt, ls=False):
         pend = self._pending.pop(id(inp), None)
         if self.comm.size == 1:
-            self._launch(inp, u0, out, self.full, dt, a, b)
+            self._launch(inp, u0, out, self.full, dt, a, b, ls)
             return
         if self.overlap:
             with trace.range_("interior"):
-                self._launch(inp, u0, out, self.interior, dt, a, b)
+                self._launch(inp, u0, out, self.interior, dt, a, b, ls)
             with trace.range_("halo_wait"):
                 if pend is not None:
                     pend.wait()
             with trace.range_("boundary"):
                 for rng in self.boundary:
-                    self._launch(inp, u0, out, rng, dt, a, b)
+                    self._launch(inp, u0, out, rng, dt, a, b, ls)
         else:
             if pend is not None:
                 pend.wait()
-            self._launch(inp, u0, out, self.full, dt, a, b)
+            self._launch(inp, u0, out, self.full, dt, a, b, ls)
         with trace.range_("halo_start"):
             self._pending[id(out)] = self.halo.start(out)
 
@@ -252,6 +272,13 @@ class Solver:
     def step(self, dt: float) -> None:
         if self.fused:
             self._step_fused(dt)
+            return
+        if self.du is not None:
+            for A, Bc in zip(LSRK45_A, LSRK45_B):
+                self._stage(self.u, self.du, self.un, A, Bc, dt, ls=True)
+                self.u, self.un = self.un, self.u
+            self.t += dt
+            self.it += 1
             return
         u, A, B = self.u, self.A, self.B
         (a1, b1), (a2, b2), (a3, b3) = RK3
@@ -292,7 +319,7 @@ class Solver:
     # Small grids are launch-bound (a 1001² heat stage is ~5 µs of HBM time); replaying
     # a captured graph removes the per-launch host cost (ctypes + hipLaunchKernel).
     # ------------------------------------------------------------------------------
-    GRAPH_STEPS = 8  # even: the fused path ping-pongs u/un, so buffers line up on replay
+    GRAPH_STEPS = 8  # even: fused / LSRK paths ping-pong u/un, so buffers line up on replay
 
     def graph_capable(self) -> bool:
         return (self.device.type == "cuda" and self.comm.size == 1 and not trace.SYNC_DEBUG
@@ -434,7 +461,8 @@ class Solver:
     def meta(self) -> dict:
         return {"grid": list(self.grid.shape), "lengths": list(self.grid.lengths),
                 "t": self.t, "it": self.it, "model": self.model.describe(),
-                "ic": self.ic_name, "world": self.comm.size, "pgrid": list(self.pgrid)}
+                "ic": self.ic_name, "world": self.comm.size, "pgrid": list(self.pgrid),
+                "integrator": self.integrator}
 
     def save_checkpoint(self, prefix):
         self.sync_halos()
@@ -467,9 +495,11 @@ class Solver:
         gf = metrics.gflops_reference(stats.compute_s, stats.steps, cells,
                                       times3=(style == "multigpu" or self.model.name == "burgers"))
         ml = metrics.mlups(stats.compute_s, stats.steps, cells)
-        bw = self.model.bytes_per_cell_step * cells * stats.steps / max(stats.compute_s, 1e-30)
+        # LSRK stage: read u, du; write du, u (stage 1 skips the du read)
+        bpc = 5 * 32.0 - 8.0 if self.du is not None else self.model.bytes_per_cell_step
+        bw = bpc * cells * stats.steps / max(stats.compute_s, 1e-30)
         ex = {"MLUPS (cells x RK3 steps / s)": f"{ml:.1f}",
-              "Stage-MLUPS": f"{3 * ml:.1f}",
+              "Stage-MLUPS": f"{(5 if self.du is not None else 3) * ml:.1f}",
               "Effective HBM bandwidth (GB/s, est.)": f"{bw / 1e9:.1f}",
               "Processes / devices": f"{self.comm.size} x {self.device.type}"}
         if extra:
