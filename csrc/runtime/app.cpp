@@ -7,8 +7,9 @@
 //   burgers3d    tEnd CFL L W H Nx Ny Nz [bx by bz]  (MultiGPU/Burgers3d_Baseline/main.c:36-54)
 //
 // plus named options (runtime replacements of the reference's #defines, §2.7):
-//   --ic NAME  --order 2|4  --safety S  --weno js|z  --visc C  --fp32  --no-overlap
-//   --transport rccl|socket  --write FILE  --error-norms
+//   --ic NAME  --order 2|4  --safety S  --weno js|z|js7  --visc C  --fp32  --no-overlap
+//   --integrator ssprk3|lsrk45  --no-fused  --transport rccl|socket  --write FILE
+//   --error-norms
 // Launch one process per GPU with torchrun-style env vars (RANK/WORLD_SIZE/LOCAL_RANK/
 // MASTER_ADDR/MASTER_PORT), e.g. via `python -m multigpu_advectiondiffusion_amd.launch`.
 #include <chrono>
@@ -36,7 +37,8 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   for (int q = 1; q < argc; ++q) {
     std::string a = argv[q];
     if (a.rfind("--", 0) == 0) {
-      const bool flag = a == "--fp32" || a == "--no-overlap" || a == "--error-norms";
+      const bool flag = a == "--fp32" || a == "--no-overlap" || a == "--error-norms" ||
+                        a == "--no-fused";
       if (flag || q + 1 >= argc) {
         opt[a] = "1";
       } else {
@@ -52,7 +54,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
     std::cerr << "usage: " << argv[0]
               << (diff ? (dims == 3 ? " K L W H Nx Ny Nz iters [bx by bz]" : " K L W Nx Ny iters [bx by]")
                        : (dims == 3 ? " tEnd CFL L W H Nx Ny Nz [bx by bz]" : " tEnd CFL L W Nx Ny [bx by]"))
-              << " [--ic NAME] [--order 2|4] [--weno js|z] [--visc C] [--fp32] [--no-overlap]"
+              << " [--ic NAME] [--order 2|4] [--weno js|z|js7] [--integrator ssprk3|lsrk45] [--no-fused] [--visc C] [--fp32] [--no-overlap]"
                  " [--transport rccl|socket] [--write FILE] [--error-norms]\n";
     return 1;
   }
@@ -77,7 +79,17 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   if (diff) iters = std::stoi(pos[k++]);
   if (opt.count("--order")) p.order = std::stoi(opt["--order"]);
   if (opt.count("--safety")) p.safety = std::stod(opt["--safety"]);
-  if (opt.count("--weno")) p.weno_z = opt["--weno"] == "z";
+  if (opt.count("--weno")) {
+    const std::string w = opt["--weno"];
+    if (w != "js" && w != "z" && w != "js7") throw std::runtime_error("--weno js|z|js7");
+    p.weno = w == "js" ? 0 : (w == "z" ? 1 : 2);
+  }
+  if (opt.count("--integrator")) {
+    const std::string g = opt["--integrator"];
+    if (g != "ssprk3" && g != "lsrk45") throw std::runtime_error("--integrator ssprk3|lsrk45");
+    p.integrator = g == "lsrk45" ? 1 : 0;
+  }
+  if (opt.count("--no-fused")) p.fused = false;
   if (opt.count("--visc")) p.C = std::stod(opt["--visc"]);
   if (opt.count("--fp32")) p.dtype = ADVDIFF_F32;
   if (opt.count("--no-overlap")) p.overlap = false;
@@ -106,7 +118,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   Stats st = diff ? eng.run_iters(iters) : eng.run_until(tEnd + p.t0);
   std::string title =
       std::string(diff ? "Diffusion-" : "Burgers-") + (dims == 3 ? "3D" : "2D") +
-      (diff ? (p.order == 4 ? " MI355X-FD4" : " MI355X-FD2") : (p.weno_z ? " MI355X-WENO5Z" : " MI355X-WENO5JS"));
+      (diff ? (p.order == 4 ? " MI355X-FD4" : " MI355X-FD2") : (p.weno == 1 ? " MI355X-WENO5Z" : p.weno == 0 ? " MI355X-WENO5JS" : " MI355X-WENO7JS"));
   std::string optname = std::string("Fused LDS z-march + RK3 (gfx950), transport=") + tr->name();
   double l1 = 0, l2 = 0, li = 0;
   const bool norms = opt.count("--error-norms") && (p.ic == 2 || p.ic == 3);

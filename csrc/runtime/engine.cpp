@@ -1,9 +1,11 @@
-// SSP-RK3 engine of the native runtime (mirror of multigpu_advectiondiffusion_amd/solver.py).
+// Time-stepping engine of the native runtime (mirror of multigpu_advectiondiffusion_amd/solver.py).
 //
 // Per stage, on the compute stream:  interior(in->out)  -> wait(halo of in) ->
 // boundary(in->out) -> event -> [comm stream] exchange of out's ghost planes, which
-// overlaps the next stage's interior.  Buffers u -> A -> B -> u (stage 3 in place), no
-// Lu array, no uo copy.  Reference: MultiGPU/Diffusion3d_Baseline/main.c:189-303.
+// overlaps the next stage's interior.  SSP-RK3 buffers u -> A -> B -> u (stage 3 in
+// place), no Lu array, no uo copy.  Reference: MultiGPU/Diffusion3d_Baseline/main.c:189-303.
+// 3-D heat: one temporally blocked launch per step (ghost width 3R, one exchange per
+// step).  Low-storage RK4(5): u <-> A ping-pong, du in B.
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -50,7 +52,10 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   slab_.n = p.n_decomposed();
   slab_.size = env.size;
   slab_.rank = env.rank;
-  slab_.ghost = p.radius();
+  const int R = p.radius();
+  fused_ = p.fused && p.physics == Physics::Diffusion && p.dims == 3 && p.integrator == 0 &&
+           slab_.n / slab_.size >= 3 * R;
+  slab_.ghost = fused_ ? 3 * R : R;
   if (slab_.n < slab_.size * slab_.ghost)
     throw std::runtime_error("slab thinner than the ghost width: use fewer ranks");
   elem_ = p.dtype == ADVDIFF_F64 ? 8 : 4;
@@ -85,10 +90,15 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
     KERNEL_CHECK(advdiff_init_ic(p.dtype, p.ic, u_, p.nx, slab_.alloc(), 1, sy_, sz_, kg0, p.nx,
                                  p.ny, 1, p.dx(), p.dy(), 0.0, p.ic_p0, p.ic_p1, compute_));
   HIP_CHECK(hipMemcpyAsync(A_, u_, field_bytes_, hipMemcpyDeviceToDevice, compute_));
-  HIP_CHECK(hipMemcpyAsync(B_, u_, field_bytes_, hipMemcpyDeviceToDevice, compute_));
+  if (p.integrator == 1)
+    HIP_CHECK(hipMemsetAsync(B_, 0, field_bytes_, compute_));  // du
+  else
+    HIP_CHECK(hipMemcpyAsync(B_, u_, field_bytes_, hipMemcpyDeviceToDevice, compute_));
   HIP_CHECK(hipStreamSynchronize(compute_));
   full_ = slab_.compute_range(p.border());
-  slab_.split(p.border(), p.radius(), interior_, blo_, bhi_);
+  slab_.split(p.border(), slab_.ghost, interior_, blo_, bhi_);
+  const int off = slab_.start() - slab_.ghost;
+  zact_ = {std::max(0, p.border() - off), std::min(slab_.alloc(), slab_.n - p.border() - off)};
   t_ = p.t0;
 }
 
@@ -120,31 +130,78 @@ double Engine::stable_dt() const {
   return dt;
 }
 
-void Engine::launch(const void* in, const void* u0, void* out, Range r, double dt, double a,
-                    double b) {
+void Engine::launch(const void* in, void* aux, void* out, Range r, double dt, double a,
+                    double b, bool ls) {
   if (r.empty()) return;
   const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
   const int B = p_.border();
   if (p_.physics == Physics::Diffusion) {
-    const double cx = p_.K / (dx * dx), cy = p_.K / (dy * dy);
-    if (p_.dims == 3)
-      KERNEL_CHECK(advdiff_diffusion3d_stage(p_.dtype, in, u0, out, p_.nx, p_.ny, sy_, sz_, r.lo,
-                                             r.hi, B, p_.order, cx, cy, p_.K / (dz * dz), dt, a,
-                                             b, compute_));
-    else
-      KERNEL_CHECK(advdiff_diffusion2d_stage(p_.dtype, in, u0, out, p_.nx, sy_, r.lo, r.hi, B,
-                                             p_.order, cx, cy, dt, a, b, compute_));
+    const double cx = p_.K / (dx * dx), cy = p_.K / (dy * dy), cz = p_.K / (dz * dz);
+    if (p_.dims == 3) {
+      if (ls)
+        KERNEL_CHECK(advdiff_diffusion3d_stage_ls(p_.dtype, in, aux, out, p_.nx, p_.ny, sy_, sz_,
+                                                  r.lo, r.hi, B, p_.order, cx, cy, cz, dt, a, b,
+                                                  compute_));
+      else
+        KERNEL_CHECK(advdiff_diffusion3d_stage(p_.dtype, in, aux, out, p_.nx, p_.ny, sy_, sz_,
+                                               r.lo, r.hi, B, p_.order, cx, cy, cz, dt, a, b,
+                                               compute_));
+    } else {
+      if (ls)
+        KERNEL_CHECK(advdiff_diffusion2d_stage_ls(p_.dtype, in, aux, out, p_.nx, sy_, r.lo, r.hi,
+                                                  B, p_.order, cx, cy, dt, a, b, compute_));
+      else
+        KERNEL_CHECK(advdiff_diffusion2d_stage(p_.dtype, in, aux, out, p_.nx, sy_, r.lo, r.hi, B,
+                                               p_.order, cx, cy, dt, a, b, compute_));
+    }
   } else {
-    if (p_.dims == 3)
-      KERNEL_CHECK(advdiff_burgers3d_stage(
-          p_.dtype, in, u0, out, p_.nx, p_.ny, sy_, sz_, r.lo, r.hi, B, p_.weno_z, 1.0 / dx,
-          1.0 / dy, 1.0 / dz, p_.C / (dx * dx), p_.C / (dy * dy), p_.C / (dz * dz), dt, a, b,
-          compute_));
-    else
-      KERNEL_CHECK(advdiff_burgers2d_stage(p_.dtype, in, u0, out, p_.nx, sy_, r.lo, r.hi, B,
-                                           p_.weno_z, 1.0 / dx, 1.0 / dy, p_.C / (dx * dx),
-                                           p_.C / (dy * dy), dt, a, b, compute_));
+    const double vx = p_.C / (dx * dx), vy = p_.C / (dy * dy), vz = p_.C / (dz * dz);
+    if (p_.dims == 3) {
+      if (ls)
+        KERNEL_CHECK(advdiff_burgers3d_stage_ls(p_.dtype, in, aux, out, p_.nx, p_.ny, sy_, sz_,
+                                                r.lo, r.hi, B, p_.weno, 1.0 / dx, 1.0 / dy,
+                                                1.0 / dz, vx, vy, vz, dt, a, b, compute_));
+      else
+        KERNEL_CHECK(advdiff_burgers3d_stage(p_.dtype, in, aux, out, p_.nx, p_.ny, sy_, sz_, r.lo,
+                                             r.hi, B, p_.weno, 1.0 / dx, 1.0 / dy, 1.0 / dz, vx,
+                                             vy, vz, dt, a, b, compute_));
+    } else {
+      if (ls)
+        KERNEL_CHECK(advdiff_burgers2d_stage_ls(p_.dtype, in, aux, out, p_.nx, sy_, r.lo, r.hi, B,
+                                                p_.weno, 1.0 / dx, 1.0 / dy, vx, vy, dt, a, b,
+                                                compute_));
+      else
+        KERNEL_CHECK(advdiff_burgers2d_stage(p_.dtype, in, aux, out, p_.nx, sy_, r.lo, r.hi, B,
+                                             p_.weno, 1.0 / dx, 1.0 / dy, vx, vy, dt, a, b,
+                                             compute_));
+    }
   }
+}
+
+void Engine::launch_fused(Range r, double dt) {
+  if (r.empty()) return;
+  const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
+  KERNEL_CHECK(advdiff_diffusion3d_step(p_.dtype, u_, A_, p_.nx, p_.ny, sy_, sz_, slab_.alloc(),
+                                        r.lo, r.hi, zact_.lo, zact_.hi, p_.border(), p_.order,
+                                        p_.K / (dx * dx), p_.K / (dy * dy), p_.K / (dz * dz), dt,
+                                        compute_));
+}
+
+void Engine::step_fused(double dt) {
+  if (env_.size == 1) {
+    launch_fused(full_, dt);
+  } else if (p_.overlap) {
+    launch_fused(interior_, dt);
+    if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
+    launch_fused(blo_, dt);
+    launch_fused(bhi_, dt);
+  } else {
+    if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
+    launch_fused(full_, dt);
+  }
+  halo_pending_ = false;
+  std::swap(u_, A_);
+  start_halo(u_);
 }
 
 void Engine::start_halo(void* field) {
@@ -158,28 +215,48 @@ void Engine::start_halo(void* field) {
   halo_pending_ = true;
 }
 
-void Engine::stage(void* in, void* u0, void* out, double a, double b, double dt) {
+void Engine::stage(void* in, void* aux, void* out, double a, double b, double dt, bool ls) {
   if (env_.size == 1) {
-    launch(in, u0, out, full_, dt, a, b);
+    launch(in, aux, out, full_, dt, a, b, ls);
     return;
   }
   if (p_.overlap) {
-    launch(in, u0, out, interior_, dt, a, b);
+    launch(in, aux, out, interior_, dt, a, b, ls);
     if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
-    launch(in, u0, out, blo_, dt, a, b);
-    launch(in, u0, out, bhi_, dt, a, b);
+    launch(in, aux, out, blo_, dt, a, b, ls);
+    launch(in, aux, out, bhi_, dt, a, b, ls);
   } else {
     if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
-    launch(in, u0, out, full_, dt, a, b);
+    launch(in, aux, out, full_, dt, a, b, ls);
   }
   halo_pending_ = false;
   start_halo(out);
 }
 
+// Carpenter–Kennedy LSRK4(5) (Matlab_Prototipes/InviscidBurgersNd/LFWENO7FDM1d.m)
+static const double kLsA[5] = {0.0, -567301805773.0 / 1357537059087.0,
+                               -2404267990393.0 / 2016746695238.0,
+                               -3550918686646.0 / 2091501179385.0,
+                               -1275806237668.0 / 842570457699.0};
+static const double kLsB[5] = {1432997174477.0 / 9575080441755.0,
+                               5161836677717.0 / 13612068292357.0,
+                               1720146321549.0 / 2090206949498.0,
+                               3134564353537.0 / 4481467310338.0,
+                               2277821191437.0 / 14882151754819.0};
+
 void Engine::step(double dt) {
-  stage(u_, nullptr, A_, 0.0, 1.0, dt);
-  stage(A_, u_, B_, 0.75, 0.25, dt);
-  stage(B_, u_, u_, 1.0 / 3.0, 2.0 / 3.0, dt);
+  if (fused_) {
+    step_fused(dt);
+  } else if (p_.integrator == 1) {
+    for (int s = 0; s < 5; ++s) {
+      stage(u_, B_, A_, kLsA[s], kLsB[s], dt, true);
+      std::swap(u_, A_);
+    }
+  } else {
+    stage(u_, nullptr, A_, 0.0, 1.0, dt);
+    stage(A_, u_, B_, 0.75, 0.25, dt);
+    stage(B_, u_, u_, 1.0 / 3.0, 2.0 / 3.0, dt);
+  }
   t_ += dt;
   ++it_;
 }

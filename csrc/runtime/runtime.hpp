@@ -113,14 +113,18 @@ struct Problem {
   double safety = 0.9;
   // burgers
   double C = 1e-5;
-  int weno_z = 1;
+  int weno = 1;                    // 0 WENO5-JS, 1 WENO5-Z, 2 WENO7-JS (kernels.h codes)
   double cfl = 0.3;
   // common
   int ic = 3;                      // kernels.h IC codes
   double ic_p0 = 1.0, ic_p1 = 0.1;
   double t0 = 0.0;
   bool overlap = true;
-  int radius() const { return physics == Physics::Diffusion ? order / 2 : 3; }
+  int integrator = 0;              // 0 SSP-RK3, 1 low-storage RK4(5)
+  bool fused = true;               // 3-D heat + SSP-RK3: one launch per step (3R ghosts)
+  int radius() const {
+    return physics == Physics::Diffusion ? order / 2 : (weno == 2 ? 4 : 3);
+  }
   int border() const { return radius(); }
   double dx() const { return L / (nx - 1); }
   double dy() const { return W / (ny - 1); }
@@ -148,11 +152,14 @@ class Engine {
   double time() const { return t_; }
   int iteration() const { return it_; }
   const Slab& slab() const { return slab_; }
+  bool fused() const { return fused_; }
 
  private:
-  void launch(const void* in, const void* u0, void* out, Range r, double dt, double a,
-              double b);
-  void stage(void* in, void* u0, void* out, double a, double b, double dt);
+  void launch(const void* in, void* aux, void* out, Range r, double dt, double a, double b,
+              bool ls);
+  void stage(void* in, void* aux, void* out, double a, double b, double dt, bool ls = false);
+  void launch_fused(Range r, double dt);
+  void step_fused(double dt);
   void start_halo(void* field);
   void* plane(void* base, int l) const { return (char*)base + (size_t)l * plane_bytes_; }
 
@@ -162,7 +169,10 @@ class Engine {
   Slab slab_;
   int64_t sy_ = 0, sz_ = 0;  // element pitches (2-D: sz_ = row pitch of the decomposed axis)
   size_t elem_ = 8, plane_bytes_ = 0, field_bytes_ = 0;
+  // SSP-RK3: u -> A -> B -> u.  Fused step / LSRK: u <-> A ping-pong (B = du for LSRK).
   void *u_ = nullptr, *A_ = nullptr, *B_ = nullptr;
+  bool fused_ = false;
+  Range zact_;  // fused: local planes whose intermediate stages are updated
   hipStream_t compute_ = nullptr, comm_ = nullptr;
   hipEvent_t ready_ = nullptr, halo_done_ = nullptr;
   bool halo_pending_ = false;

@@ -38,8 +38,8 @@ def _run(app, args, out, world=1, extra=()):
     return outs[0]
 
 
-def _py(model, grid, ic, **run):
-    s = Solver(model, grid, dtype=torch.float64, device="cuda", ic=ic)
+def _py(model, grid, ic, integrator="ssprk3", **run):
+    s = Solver(model, grid, dtype=torch.float64, device="cuda", ic=ic, integrator=integrator)
     s.run(**run)
     return s.gather().astype(np.float32)
 
@@ -97,3 +97,30 @@ def test_native_error_norms_heat(tmp_path):
                extra=["--error-norms"])
     line = [l for l in txt.splitlines() if l.startswith("Linf norm")][0]
     assert float(line.split(":")[1]) < 5e-2
+
+
+def test_native_weno7_lsrk45_matches_python(tmp_path):
+    out = tmp_path / "b7.bin"
+    _run("burgers3d", [0.04, 0.3, 2.0, 2.0, 2.0, 46, 40, 38], out,
+         extra=["--weno", "js7", "--integrator", "lsrk45"])
+    got = np.fromfile(out, dtype=np.float32).reshape(38, 40, 46)
+    exp = _py(Burgers(viscosity=1e-5, weno="js7", cfl=0.3), Grid((46, 40, 38), (2.0, 2.0, 2.0)),
+              "gaussian", integrator="lsrk45", t_end=0.04)
+    assert np.array_equal(got, exp), np.abs(got - exp).max()
+    out = tmp_path / "d2ls.bin"
+    _run("diffusion2d", [1.0, 1.0, 1.0, 130, 90, 25], out, extra=["--ic", "disc",
+                                                                  "--integrator", "lsrk45"])
+    got = np.fromfile(out, dtype=np.float32).reshape(90, 130)
+    exp = _py(Diffusion(K=1.0, order=4), Grid((130, 90), (1.0, 1.0)), "disc",
+              integrator="lsrk45", iters=25)
+    assert np.array_equal(got, exp)
+
+
+def test_native_fused_equals_per_stage_and_multirank(tmp_path):
+    args = [1.0, 1.0, 1.0, 1.0, 66, 40, 45, 12]
+    a, b, c = tmp_path / "f.bin", tmp_path / "s.bin", tmp_path / "f2.bin"
+    _run("diffusion3d", args, a, extra=["--ic", "sine"])
+    _run("diffusion3d", args, b, extra=["--ic", "sine", "--no-fused"])
+    _run("diffusion3d", args, c, world=3, extra=["--ic", "sine", "--transport", "socket"])
+    fa, fb, fc = (np.fromfile(p, dtype=np.float32) for p in (a, b, c))
+    assert np.array_equal(fa, fb) and np.array_equal(fa, fc)
