@@ -40,22 +40,44 @@ def _child_env(rank: int, world: int, port: int, cpu: bool) -> dict:
     return env
 
 
-def launch(np_: int, argv: list[str], cpu: bool = False, timeout: float | None = None) -> int:
+def launch(np_: int, argv: list[str], cpu: bool = False, timeout: float | None = None,
+           poll_s: float = 0.2) -> int:
+    """Run P ranks; fail fast: the first rank that exits non-zero (or the wall-clock
+    `timeout`, rc 124) terminates the others, so a crashed rank never leaves its peers
+    blocked in a halo exchange until the collective timeout.  Returns the first
+    non-zero exit code (0 if all succeed)."""
+    import time
     port = free_port()
     cmd = [sys.executable, "-m", "multigpu_advectiondiffusion_amd"] + argv
     if cpu and "--device" not in argv:
         cmd += ["--device", "cpu"]
     procs = [subprocess.Popen(cmd, env=_child_env(r, np_, port, cpu)) for r in range(np_)]
+    deadline = None if timeout is None else time.monotonic() + timeout
     rc = 0
     try:
-        for p in procs:
-            code = p.wait(timeout=timeout)
-            rc = rc or code
-    except subprocess.TimeoutExpired:
-        rc = 124
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, rc = bad[0]
+                print(f"[launch] rank {r} exited with {rc}; terminating the other ranks",
+                      file=sys.stderr, flush=True)
+                break
+            if all(c == 0 for c in codes):
+                break
+            if deadline is not None and time.monotonic() > deadline:
+                print(f"[launch] timeout after {timeout:g} s", file=sys.stderr, flush=True)
+                rc = 124
+                break
+            time.sleep(poll_s)
     finally:
         for p in procs:
             if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
                 p.kill()
     return rc
 

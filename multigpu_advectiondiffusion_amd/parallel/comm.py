@@ -34,12 +34,14 @@ class Comm:
     # ------------------------------------------------------------------------------
     @classmethod
     def from_env(cls, device: str | None = None, backend: str | None = None,
-                 timeout_s: float = 600.0) -> "Comm":
+                 timeout_s: float | None = None) -> "Comm":
         """Create (or attach to) the default process group from torchrun env vars.
 
         device: "cuda", "cpu" or None (= cuda if available).  backend defaults to
         nccl for cuda, gloo for cpu.
         """
+        if timeout_s is None:  # collective timeout (a dead peer surfaces as an error)
+            timeout_s = float(os.environ.get("ADVDIFF_COMM_TIMEOUT", "600"))
         size = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))

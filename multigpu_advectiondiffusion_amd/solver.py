@@ -40,6 +40,20 @@ RK3 = ((0.0, 1.0), (0.75, 0.25), (1.0 / 3.0, 2.0 / 3.0))
 INTEGRATORS = ("ssprk3", "lsrk45")
 
 
+def _fault_from_env():
+    """Fault injection for failure-handling tests: ADVDIFF_FAULT="RANK:STEP" raises on
+    that rank right after that step (eager stepping path)."""
+    import os
+    v = os.environ.get("ADVDIFF_FAULT")
+    if not v:
+        return None
+    r, st = v.split(":")
+    return int(r), int(st)
+
+
+_FAULT = _fault_from_env()
+
+
 def _row_pitch(nx: int, elem: int, align_bytes: int = 256) -> int:
     per = max(align_bytes // elem, 1)
     return ((nx + per - 1) // per) * per
@@ -393,6 +407,8 @@ class Solver:
                 h = t_end - self.t
             with trace.range_(f"step {self.it}"):
                 self.step(h)
+            if _FAULT is not None and _FAULT == (self.comm.rank, self.it):
+                raise RuntimeError(f"injected fault on rank {self.comm.rank} at step {self.it}")
             if self.check_every and self.it % self.check_every == 0:
                 self.check_finite()
             if callback is not None:

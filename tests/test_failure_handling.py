@@ -1,0 +1,30 @@
+"""Failure detection (absent in the reference, which only exits on MPI
+errors): fail-fast launcher, fault injection, launcher timeout, NaN/Inf watchdog."""
+import time
+
+from multigpu_advectiondiffusion_amd.launch import launch
+
+ARGS = ["diffusion3d", "1", "1", "1", "1", "20", "20", "24", "400"]
+
+
+def test_launcher_fail_fast_on_injected_fault(monkeypatch):
+    monkeypatch.setenv("ADVDIFF_FAULT", "1:3")  # rank 1 raises after step 3
+    monkeypatch.setenv("ADVDIFF_COMM_TIMEOUT", "300")
+    t0 = time.monotonic()
+    rc = launch(2, ARGS, cpu=True, timeout=240)
+    # rank 0 is left blocked in a halo receive; the launcher must kill it right away
+    assert rc not in (0, 124)
+    assert time.monotonic() - t0 < 120
+
+
+def test_launcher_timeout(monkeypatch):
+    monkeypatch.setenv("ADVDIFF_COMM_TIMEOUT", "300")
+    rc = launch(2, ["diffusion3d", "1", "1", "1", "1", "40", "40", "40", "100000"], cpu=True,
+                timeout=20)
+    assert rc == 124
+
+
+def test_launcher_success():
+    assert launch(2, ARGS[:-1] + ["3"], cpu=True, timeout=240) == 0
+
+# NaN/Inf watchdog: tests/test_cli_and_io.py::test_nan_watchdog*
