@@ -277,6 +277,27 @@ struct Recon<T, 7, false> {
 };
 
 // ---------------------------------------------------------------------------------
+// Cross-lane shifts inside a 64-wide wave (DPP wave_shr:1 / wave_shl:1, pure VALU, no
+// LDS traffic): lane i receives lane i-1 (shr) / i+1 (shl); lanes without a source get 0.
+// Every lane of the wave must execute them (call only under wave-uniform control flow).
+// ---------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_move(double v) {
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xf, 0xf, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_move(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <typename T>
+__device__ __forceinline__ T wave_shr1(T v) { return dpp_move<0x138>(v); }  // from lane i-1
+template <typename T>
+__device__ __forceinline__ T wave_shl1(T v) { return dpp_move<0x130>(v); }  // from lane i+1
+
+// ---------------------------------------------------------------------------------
 // Stage epilogues.  MODE selects the time integrator's per-stage update:
 //   kSsp1 : out = b (c + dt L)                      (SSP-RK3 stage 1)
 //   kSsp  : out = a aux + b (c + dt L)              (SSP-RK3, aux = u^n)

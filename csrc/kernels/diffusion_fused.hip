@@ -225,7 +225,7 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_kernel(
 // unrolled 8x: plane p lives in slot (p - kst) & 7, so at unrolled phase PH every
 // window index is a compile-time constant and no register is ever moved (the plain
 // version spends ~55 v_mov_b64 per plane shifting its windows).
-template <typename T, int ORDER, int NW, int RPW, int PD>
+template <typename T, int ORDER, int NW, int RPW, int PD, int XDPP>
 __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
     int nz_alloc, int k0, int k1, int zlo, int zhi, int zchunk, int border, T cx, T cy, T cz,
@@ -354,7 +354,22 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
     for (int q = 0; q < RPW; ++q) {
       const T c = ru[q][U2R];
       const int l = (row[q] + R) * UW + lane + R;
-      if constexpr (R == 2)
+      if constexpr (XDPP >= 2 && R == 2) {
+        // x neighbours by DPP; the 2R edge lanes take theirs from the LDS halo columns
+        T m1 = wave_shr1(c), p1 = wave_shl1(c);
+        T m2 = wave_shr1(m1), p2 = wave_shl1(p1);
+        if (lane < R) {
+          m1 = pU[l - 1];
+          m2 = pU[l - 2];
+        } else if (lane >= W - R) {
+          p1 = pU[l + 1];
+          p2 = pU[l + 2];
+        }
+        lapA[q] = lap3(cx, FD<4>::d2(m2, m1, c, p1, p2), cy,
+                       FD<4>::d2(pU[l - 2 * UW], pU[l - UW], c, pU[l + UW], pU[l + 2 * UW]), cz,
+                       FD<4>::d2(ru[q][(PH + 2) & 7], ru[q][(PH + 3) & 7], c, ru[q][(PH + 5) & 7],
+                                 ru[q][(PH + 6) & 7]));
+      } else if constexpr (R == 2)
         lapA[q] = lap3(cx, FD<4>::d2(pU[l - 2], pU[l - 1], c, pU[l + 1], pU[l + 2]), cy,
                        FD<4>::d2(pU[l - 2 * UW], pU[l - UW], c, pU[l + UW], pU[l + 2 * UW]), cz,
                        FD<4>::d2(ru[q][(PH + 2) & 7], ru[q][(PH + 3) & 7], c, ru[q][(PH + 5) & 7],
@@ -384,10 +399,18 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
         const int l = row[q] * W + lane;
         const T c = ra[q][AR];
         T lap;
-        if constexpr (R == 2)
+        if constexpr (XDPP >= 1 && R == 2) {  // x neighbours from the wave's own lanes
+          const T m1 = wave_shr1(c), p1 = wave_shl1(c);
+          lap = lap3(cx, FD<4>::d2(wave_shr1(m1), m1, c, p1, wave_shl1(p1)), cy,
+                     FD<4>::d2(pA[l - 2 * W], pA[l - W], c, pA[l + W], pA[l + 2 * W]), cz,
+                     FD<4>::d2(ra[q][A0], ra[q][(PH + 1) & 7], c, ra[q][(PH + 3) & 7], ra[q][A2R]));
+        } else if constexpr (R == 2)
           lap = lap3(cx, FD<4>::d2(pA[l - 2], pA[l - 1], c, pA[l + 1], pA[l + 2]), cy,
                      FD<4>::d2(pA[l - 2 * W], pA[l - W], c, pA[l + W], pA[l + 2 * W]), cz,
                      FD<4>::d2(ra[q][A0], ra[q][(PH + 1) & 7], c, ra[q][(PH + 3) & 7], ra[q][A2R]));
+        else if constexpr (XDPP >= 1)
+          lap = lap3(cx, FD<2>::d2(wave_shr1(c), c, wave_shl1(c)), cy,
+                     FD<2>::d2(pA[l - W], c, pA[l + W]), cz, FD<2>::d2(ra[q][A0], c, ra[q][A2R]));
         else
           lap = lap3(cx, FD<2>::d2(pA[l - 1], c, pA[l + 1]), cy,
                      FD<2>::d2(pA[l - W], c, pA[l + W]), cz, FD<2>::d2(ra[q][A0], c, ra[q][A2R]));
@@ -404,10 +427,18 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
         const T c = rb[q][B0];
         const T uo = ru[q][U0];
         T lap;
-        if constexpr (R == 2)
+        if constexpr (XDPP >= 1 && R == 2) {
+          const T m1 = wave_shr1(c), p1 = wave_shl1(c);
+          lap = lap3(cx, FD<4>::d2(wave_shr1(m1), m1, c, p1, wave_shl1(p1)), cy,
+                     FD<4>::d2(pB[l - 2 * W], pB[l - W], c, pB[l + W], pB[l + 2 * W]), cz,
+                     FD<4>::d2(rb[q][BM], rb[q][(PH + 7) & 7], c, rb[q][(PH + 1) & 7], rb[q][BR]));
+        } else if constexpr (R == 2)
           lap = lap3(cx, FD<4>::d2(pB[l - 2], pB[l - 1], c, pB[l + 1], pB[l + 2]), cy,
                      FD<4>::d2(pB[l - 2 * W], pB[l - W], c, pB[l + W], pB[l + 2 * W]), cz,
                      FD<4>::d2(rb[q][BM], rb[q][(PH + 7) & 7], c, rb[q][(PH + 1) & 7], rb[q][BR]));
+        else if constexpr (XDPP >= 1)
+          lap = lap3(cx, FD<2>::d2(wave_shr1(c), c, wave_shl1(c)), cy,
+                     FD<2>::d2(pB[l - W], c, pB[l + W]), cz, FD<2>::d2(rb[q][BM], c, rb[q][BR]));
         else
           lap = lap3(cx, FD<2>::d2(pB[l - 1], c, pB[l + 1]), cy,
                      FD<2>::d2(pB[l - W], c, pB[l + W]), cz, FD<2>::d2(rb[q][BM], c, rb[q][BR]));
@@ -429,7 +460,7 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
   }
 }
 
-template <typename T, int ORDER, int NW, int RPW, bool RING, int PD = 1>
+template <typename T, int ORDER, int NW, int RPW, bool RING, int PD = 1, int XDPP = 0>
 static hipError_t launch_step(const void* uin, void* uout, int nx, int ny, int64_t sy,
                               int64_t sz, int nz_alloc, int k0, int k1, int zlo, int zhi,
                               int border, double cx, double cy, double cz, double dt,
@@ -444,7 +475,7 @@ static hipError_t launch_step(const void* uin, void* uout, int nx, int ny, int64
   const int gz = div_up(k1 - k0, zc);
   const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
   if constexpr (RING)
-    hipLaunchKernelGGL((diffusion3d_step_ring_kernel<T, ORDER, NW, RPW, PD>), dim3(gx, gy, gz),
+    hipLaunchKernelGGL((diffusion3d_step_ring_kernel<T, ORDER, NW, RPW, PD, XDPP>), dim3(gx, gy, gz),
                        dim3(64, NW, 1), 0, st, (const T*)uin, (T*)uout, nx, ny, sy, sz, nz_alloc,
                        k0, k1, zlo, zhi, zc, border, T(cx * s), T(cy * s), T(cz * s), T(dt));
   else
@@ -474,7 +505,11 @@ static hipError_t dispatch_step(int cfg, const void* uin, void* uout, int nx, in
     case 7: STEPV(16, 2, false);
     case 8: STEPV(12, 2, true, 2);
     case 9: STEPV(12, 2, true, 4);
-    default: STEPV(12, 2, true);
+    case 10: STEPV(12, 2, true);  // ring, all x neighbours from LDS
+    case 11: STEPV(8, 3, true, 1, 1);
+    case 12: STEPV(16, 2, true, 1, 1);
+    case 13: STEPV(12, 2, true, 1, 2);
+    default: STEPV(12, 2, true, 1, 1);  // ring + DPP x neighbours in stages 2/3
   }
 #undef STEPV
 }
