@@ -361,7 +361,7 @@ static hipError_t run_b(int dtype, bool three_d, int scheme, bool ls, const BArg
   if (p.hi <= p.lo) return hipSuccess;
   const int R = scheme_radius(scheme);
   if (scheme < 0 || scheme > 2 || p.lo < R || p.nx <= 0 || (three_d && p.ny <= 0) ||
-      p.border < R || p.in == p.out || p.in == p.aux)
+      p.border < R || p.in == p.out || (ls && (p.in == p.aux || p.out == p.aux)))
     return hipErrorInvalidValue;
   const bool visc = p.vx != 0.0 || p.vy != 0.0 || (three_d && p.vz != 0.0);
   const int mode = ls ? (p.a != 0.0 ? kLs : kLs1) : (p.a != 0.0 ? kSsp : kSsp1);

@@ -231,7 +231,7 @@ static hipError_t run_d(int dtype, bool three_d, int order, bool ls, const DArgs
   if (p.hi <= p.lo) return hipSuccess;
   const int R = order / 2;
   if ((order != 2 && order != 4) || p.lo < R || p.nx <= 0 || (three_d && p.ny <= 0) ||
-      p.in == p.out || p.in == p.aux)
+      p.in == p.out || (ls && (p.in == p.aux || p.out == p.aux)))
     return hipErrorInvalidValue;
   if (three_d && p.sy * (int64_t)p.ny >= (int64_t(1) << 31))
     return hipErrorInvalidValue;  // 32-bit plane offsets

@@ -460,7 +460,271 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
   }
 }
 
-template <typename T, int ORDER, int NW, int RPW, bool RING, int PD = 1, int XDPP = 0>
+// Compact rings: every z-window is a ring of exactly NR = 2R+1 registers (u(k+R..k+3R),
+// A(k..k+2R), B(k-R..k+R)) and the march is unrolled NR times; u(k..k+R-1), still needed
+// as the u^n term of stage 3, move to a short delay line when their ring slot is reused.
+// 17 instead of 24 window values per row (R = 2) leave room for the stage-1 DPP path.
+template <typename T, int ORDER, int NW, int RPW, int XDPP, int PD>
+__global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
+    const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
+    int nz_alloc, int k0, int k1, int zlo, int zhi, int zchunk, int border, T cx, T cy, T cz,
+    T dt) {
+  constexpr int R = FD<ORDER>::R;
+  constexpr int NR = 2 * R + 1;
+  constexpr int W = 64;
+  constexpr int TX = W - 4 * R;
+  constexpr int S1R = NW * RPW;
+  constexpr int TY = S1R - 4 * R;
+  constexpr int UW = W + 2 * R, UH = S1R + 2 * R;
+  constexpr int NT = 64 * NW;
+  constexpr int NHALO = UW * UH - W * S1R;
+  constexpr int NH = (NHALO + NT - 1) / NT;
+  static_assert(TY > 0, "tile too small");
+
+  __shared__ T sU[2][UH * UW];
+  __shared__ T sA[2][S1R * W];
+  __shared__ T sB[2][S1R * W];
+
+  const int lane = threadIdx.x, w = threadIdx.y, tid = w * 64 + lane;
+  const Tile3 tile = xcd_tile();
+  const int i0 = tile.x * TX, j0 = tile.y * TY;
+  const int x = i0 - 2 * R + lane;
+  const int kc0 = k0 + tile.z * zchunk;
+  const int kc1 = min(kc0 + zchunk, k1);
+  const bool xin = x >= border && x < nx - border;
+  const bool s2c = lane >= R && lane < W - R;
+  const bool s3c = lane >= 2 * R && lane < W - 2 * R;
+  const int xc = clampi(x, 0, nx - 1);
+
+  int row[RPW], off[RPW];
+  bool inxy[RPW], s2r[RPW], s3r[RPW];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    row[q] = w + q * NW;  // interleaved: every wave has <= 1 masked halo row per stage
+    const int y = j0 - 2 * R + row[q];
+    inxy[q] = xin && y >= border && y < ny - border;
+    s2r[q] = row[q] >= R && row[q] < S1R - R;
+    s3r[q] = row[q] >= 2 * R && row[q] < S1R - 2 * R;
+    off[q] = clampi(y, 0, ny - 1) * (int)sy + xc;
+  }
+  int hl[NH], ho[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    int idx = tid + h * NT;
+    hl[h] = -1;
+    ho[h] = 0;
+    if (idx < NHALO) {
+      int ur, uc;
+      if (idx < R * UW) {
+        ur = idx / UW;
+        uc = idx - ur * UW;
+      } else if ((idx -= R * UW) < R * UW) {
+        ur = S1R + R + idx / UW;
+        uc = idx % UW;
+      } else {
+        idx -= R * UW;
+        ur = R + idx / (2 * R);
+        const int cc = idx % (2 * R);
+        uc = cc < R ? cc : W + cc;
+      }
+      hl[h] = ur * UW + uc;
+      ho[h] = clampi(j0 - 3 * R + ur, 0, ny - 1) * (int)sy + clampi(i0 - 3 * R + uc, 0, nx - 1);
+    }
+  }
+  auto plane = [&](int k) { return uin + (int64_t)clampi(k, 0, nz_alloc - 1) * sz; };
+
+  // plane p lives in ring slot (p - kst) % NR.  At the start of iteration k the u ring
+  // holds u(k+R-1 .. k+3R-1) and the delay line dl[0..R-2] holds u(k .. k+R-2).
+  T ru[RPW][NR], ra[RPW][NR], rb[RPW][NR], dl[RPW][R];
+  const int kst = kc0 - 4 * R;
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+#pragma unroll
+    for (int d = 0; d < R - 1; ++d) dl[q][d] = plane(kst + d)[off[q]];
+#pragma unroll
+    for (int s = 0; s < NR; ++s) {
+      const int pl = kst + R - 1 + s;  // planes kst+R-1 .. kst+3R-1
+      ru[q][pl - kst < NR ? pl - kst : pl - kst - NR] = plane(pl)[off[q]];
+      ra[q][s] = rb[q][s] = T(0);
+    }
+  }
+  // PD planes of global loads in flight (buffer 0 = the plane consumed next)
+  static_assert(PD == 1 || PD == 2, "prefetch distance 1 or 2");
+  T hv[PD][NH], un[PD][RPW];
+#pragma unroll
+  for (int d = 0; d < PD; ++d) {
+#pragma unroll
+    for (int h = 0; h < NH; ++h) hv[d][h] = plane(kst + d + 2 * R)[ho[h]];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) un[d][q] = plane(kst + d + 3 * R)[off[q]];
+  }
+  const T third = T(1.0 / 3.0), two3 = T(2.0 / 3.0);
+
+  auto body = [&]<int PH>(int k) {
+    auto sl = [](int d) { return (PH + d + 4 * NR) % NR; };  // slot of plane k+d
+    constexpr int UIN = (PH + 3 * R) % NR;                    // u(k+3R) replaces u(k+R-1)
+    const int set = k & 1;
+    T* pU = sU[set];
+    T* pA = sA[set];
+    T* pB = sB[set];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      dl[q][R - 1] = ru[q][UIN];  // u(k+R-1) -> delay line
+      ru[q][UIN] = un[0][q];
+      pU[(row[q] + R) * UW + lane + R] = ru[q][sl(2 * R)];
+      pA[row[q] * W + lane] = ra[q][sl(R)];
+      pB[row[q] * W + lane] = rb[q][sl(0)];
+    }
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+      if (hl[h] >= 0) pU[hl[h]] = hv[0][h];
+    if constexpr (PD == 2) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h) hv[0][h] = hv[1][h];
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) un[0][q] = un[1][q];
+    }
+    if (k + PD < kc1) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h) hv[PD - 1][h] = plane(k + PD + 2 * R)[ho[h]];
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) un[PD - 1][q] = plane(k + PD + 3 * R)[off[q]];
+    }
+    __syncthreads();
+    // stage 1: A(k+2R)
+    const int p1 = k + 2 * R;
+    const bool z1 = p1 >= zlo && p1 < zhi;
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const T c = ru[q][sl(2 * R)];
+      const int l = (row[q] + R) * UW + lane + R;
+      T lap;
+      if constexpr (R == 2) {
+        T m1, m2, p1v, p2v;
+        if constexpr (XDPP >= 2) {
+          m1 = wave_shr1(c);
+          p1v = wave_shl1(c);
+          m2 = wave_shr1(m1);
+          p2v = wave_shl1(p1v);
+          if (lane < R) {
+            m1 = pU[l - 1];
+            m2 = pU[l - 2];
+          } else if (lane >= W - R) {
+            p1v = pU[l + 1];
+            p2v = pU[l + 2];
+          }
+        } else {
+          m2 = pU[l - 2];
+          m1 = pU[l - 1];
+          p1v = pU[l + 1];
+          p2v = pU[l + 2];
+        }
+        lap = lap3(cx, FD<4>::d2(m2, m1, c, p1v, p2v), cy,
+                   FD<4>::d2(pU[l - 2 * UW], pU[l - UW], c, pU[l + UW], pU[l + 2 * UW]), cz,
+                   FD<4>::d2(ru[q][sl(R)], ru[q][sl(R + 1)], c, ru[q][sl(3 * R - 1)],
+                             ru[q][sl(3 * R)]));
+      } else {
+        lap = lap3(cx, FD<2>::d2(pU[l - 1], c, pU[l + 1]), cy,
+                   FD<2>::d2(pU[l - UW], c, pU[l + UW]), cz,
+                   FD<2>::d2(ru[q][sl(R)], c, ru[q][sl(3 * R)]));
+      }
+      const T v = rk_stage<T, false>(T(0), c, lap, dt, T(0), T(1));
+      ra[q][sl(2 * R)] = (z1 && inxy[q]) ? v : c;
+    }
+    // stage 2: B(k+R)
+    if (k >= kc0 - 2 * R) {
+      const int p2 = k + R;
+      const bool z2 = p2 >= zlo && p2 < zhi;
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const T uo = ru[q][sl(R)];
+        if (!s2r[q]) {
+          rb[q][sl(R)] = uo;
+          continue;
+        }
+        const int l = row[q] * W + lane;
+        const T c = ra[q][sl(R)];
+        T lap;
+        if constexpr (R == 2) {
+          T m1, m2, p1v, p2v;
+          if constexpr (XDPP >= 1) {
+            m1 = wave_shr1(c);
+            p1v = wave_shl1(c);
+            m2 = wave_shr1(m1);
+            p2v = wave_shl1(p1v);
+          } else {
+            m2 = pA[l - 2];
+            m1 = pA[l - 1];
+            p1v = pA[l + 1];
+            p2v = pA[l + 2];
+          }
+          lap = lap3(cx, FD<4>::d2(m2, m1, c, p1v, p2v), cy,
+                     FD<4>::d2(pA[l - 2 * W], pA[l - W], c, pA[l + W], pA[l + 2 * W]), cz,
+                     FD<4>::d2(ra[q][sl(0)], ra[q][sl(1)], c, ra[q][sl(3)], ra[q][sl(4)]));
+        } else {
+          const T m1 = XDPP >= 1 ? wave_shr1(c) : pA[l - 1];
+          const T p1v = XDPP >= 1 ? wave_shl1(c) : pA[l + 1];
+          lap = lap3(cx, FD<2>::d2(m1, c, p1v), cy, FD<2>::d2(pA[l - W], c, pA[l + W]), cz,
+                     FD<2>::d2(ra[q][sl(0)], c, ra[q][sl(2)]));
+        }
+        const T v = rk_stage<T, true>(uo, c, lap, dt, T(0.75), T(0.25));
+        rb[q][sl(R)] = (z2 && inxy[q] && s2c) ? v : uo;
+      }
+    }
+    // stage 3: u^{n+1}(k)
+    if (k >= kc0) {
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        if (!s3r[q]) continue;
+        const int l = row[q] * W + lane;
+        const T c = rb[q][sl(0)];
+        const T uo = dl[q][0];
+        T lap;
+        if constexpr (R == 2) {
+          T m1, m2, p1v, p2v;
+          if constexpr (XDPP >= 1) {
+            m1 = wave_shr1(c);
+            p1v = wave_shl1(c);
+            m2 = wave_shr1(m1);
+            p2v = wave_shl1(p1v);
+          } else {
+            m2 = pB[l - 2];
+            m1 = pB[l - 1];
+            p1v = pB[l + 1];
+            p2v = pB[l + 2];
+          }
+          lap = lap3(cx, FD<4>::d2(m2, m1, c, p1v, p2v), cy,
+                     FD<4>::d2(pB[l - 2 * W], pB[l - W], c, pB[l + W], pB[l + 2 * W]), cz,
+                     FD<4>::d2(rb[q][sl(-2)], rb[q][sl(-1)], c, rb[q][sl(1)], rb[q][sl(2)]));
+        } else {
+          const T m1 = XDPP >= 1 ? wave_shr1(c) : pB[l - 1];
+          const T p1v = XDPP >= 1 ? wave_shl1(c) : pB[l + 1];
+          lap = lap3(cx, FD<2>::d2(m1, c, p1v), cy, FD<2>::d2(pB[l - W], c, pB[l + W]), cz,
+                     FD<2>::d2(rb[q][sl(-1)], c, rb[q][sl(1)]));
+        }
+        const T v = rk_stage<T, true>(uo, c, lap, dt, third, two3);
+        if (inxy[q] && s3c) uout[(int64_t)k * sz + off[q]] = v;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+#pragma unroll
+      for (int d = 0; d < R - 1; ++d) dl[q][d] = dl[q][d + 1];
+    }
+  };
+
+  for (int kb = kst; kb < kc1; kb += NR) {
+    body.template operator()<0>(kb);
+    if (kb + 1 < kc1) body.template operator()<1>(kb + 1);
+    if (kb + 2 < kc1) body.template operator()<2>(kb + 2);
+    if constexpr (NR > 3) {
+      if (kb + 3 < kc1) body.template operator()<3>(kb + 3);
+      if (kb + 4 < kc1) body.template operator()<4>(kb + 4);
+    }
+  }
+}
+
+template <typename T, int ORDER, int NW, int RPW, int RING, int PD = 1, int XDPP = 0>
 static hipError_t launch_step(const void* uin, void* uout, int nx, int ny, int64_t sy,
                               int64_t sz, int nz_alloc, int k0, int k1, int zlo, int zhi,
                               int border, double cx, double cy, double cz, double dt,
@@ -474,7 +738,11 @@ static hipError_t launch_step(const void* uin, void* uout, int nx, int ny, int64
   zc = std::max(zc, knob("STEP_MIN_CHUNK", 32));
   const int gz = div_up(k1 - k0, zc);
   const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
-  if constexpr (RING)
+  if constexpr (RING == 2)
+    hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD>), dim3(gx, gy, gz),
+                       dim3(64, NW, 1), 0, st, (const T*)uin, (T*)uout, nx, ny, sy, sz, nz_alloc,
+                       k0, k1, zlo, zhi, zc, border, T(cx * s), T(cy * s), T(cz * s), T(dt));
+  else if constexpr (RING == 1)
     hipLaunchKernelGGL((diffusion3d_step_ring_kernel<T, ORDER, NW, RPW, PD, XDPP>), dim3(gx, gy, gz),
                        dim3(64, NW, 1), 0, st, (const T*)uin, (T*)uout, nx, ny, sy, sz, nz_alloc,
                        k0, k1, zlo, zhi, zc, border, T(cx * s), T(cy * s), T(cz * s), T(dt));
@@ -509,7 +777,20 @@ static hipError_t dispatch_step(int cfg, const void* uin, void* uout, int nx, in
     case 11: STEPV(8, 3, true, 1, 1);
     case 12: STEPV(16, 2, true, 1, 1);
     case 13: STEPV(12, 2, true, 1, 2);
-    default: STEPV(12, 2, true, 1, 1);  // ring + DPP x neighbours in stages 2/3
+    case 14: STEPV(12, 2, 2, 1, 1);   // compact rings, DPP stages 2/3
+    case 15: STEPV(12, 2, 2, 1, 2);   // compact rings, DPP stages 1-3
+    case 16: STEPV(16, 2, 2, 1, 1);
+    case 17: STEPV(16, 2, 2, 1, 2);
+    case 18: STEPV(12, 2, 2, 1, 0);
+    case 19: STEPV(16, 2, 2, 2, 2);   // compact rings, DPP 1-3, prefetch distance 2
+    case 20: STEPV(16, 2, 2, 2, 1);
+    case 24: STEPV(12, 2, 1, 1, 1);     // 8-slot rings + DPP x neighbours in stages 2/3
+    default:  // compact rings; FD4: 16 waves, DPP in all stages; FD2: 12 waves, stages 2/3
+      if constexpr (ORDER == 4) {
+        STEPV(16, 2, 2, 1, 2);
+      } else {
+        STEPV(12, 2, 2, 1, 1);
+      }
   }
 #undef STEPV
 }

@@ -142,3 +142,18 @@ def test_gpu_lsrk45_multirank_bitwise(kind, world, decomp, monkeypatch):
     ref_g = s.gather()
     out = spawn_local(world, _run, kind, 4, decomp, device="cuda", backend="gloo")[0]
     assert np.array_equal(out, ref_g), np.abs(out - ref_g).max()
+
+
+def test_stage_aliasing_rules():
+    """SSP stages may read u0 from the input buffer; LSRK stages must not alias du."""
+    n = 24
+    u = _smooth((n, n, n), 1, torch.float64).to(DEV)
+    o = torch.zeros_like(u)
+    kw = dict(nx=n, ny=n, k0=3, k1=n - 3, border=3, weno_z="z", rdx=10.0, rdy=10.0, rdz=10.0,
+              dt=1e-3, a=0.75, b=0.25)
+    stencil.burgers3d_stage(u, u, o, **kw)  # u0 == in: fine
+    with pytest.raises(RuntimeError):
+        stencil.burgers3d_stage(u, u, o, ls=True, **kw)  # du == in: rejected
+    with pytest.raises(RuntimeError):
+        stencil.diffusion3d_stage(u, o, o, nx=n, ny=n, k0=2, k1=n - 2, border=2, order=4,
+                                  cx=1.0, cy=1.0, cz=1.0, dt=1e-3, a=0.5, b=0.5, ls=True)
