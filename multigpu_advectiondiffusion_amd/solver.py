@@ -193,6 +193,11 @@ class Solver:
         """Owned box in the reducer's (x, y, z) order of local indices."""
         return tuple(reversed(self.cd.owned_box()))
 
+    def memory_bytes(self) -> int:
+        """Device bytes of the resident fields (see utils/sizing.py)."""
+        n = sum(f.numel() for f in self.fields()) + (self.du.numel() if self.du is not None else 0)
+        return n * self.u.element_size()
+
     def fields(self):
         if self.fused:
             return (self.u, self.un)
