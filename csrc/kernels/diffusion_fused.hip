@@ -732,10 +732,31 @@ static hipError_t launch_step(const void* uin, void* uout, int nx, int ny, int64
   constexpr int R = ORDER / 2;
   constexpr int TX = 64 - 4 * R, TY = NW * RPW - 4 * R;
   const int gx = div_up(nx, TX), gy = div_up(ny, TY);
-  static const int target = knob("STEP_TARGET_BLOCKS", 1280);
-  long long chunks = (target + (long long)gx * gy - 1) / ((long long)gx * gy);
-  int zc = div_up(k1 - k0, std::max<long long>(chunks, 1));
-  zc = std::max(zc, knob("STEP_MIN_CHUNK", 32));
+  // z chunks: minimise (rounds of resident workgroups) x (chunk + 4R warm-up planes);
+  // resident workgroups = CUs x occupancy of this instance (LDS / VGPR bound: 1-2 per CU)
+  static const int target = knob("STEP_TARGET_BLOCKS", 0);  // >0: legacy fixed target
+  static const int per_cu = [] {
+    int nb = 0;
+    const void* fn;
+    if constexpr (RING == 2)
+      fn = (const void*)diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD>;
+    else if constexpr (RING == 1)
+      fn = (const void*)diffusion3d_step_ring_kernel<T, ORDER, NW, RPW, PD, XDPP>;
+    else
+      fn = (const void*)diffusion3d_step_kernel<T, ORDER, NW, RPW>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * NW, 0) != hipSuccess || nb < 1)
+      nb = 1;
+    return nb;
+  }();
+  static const int minc = knob("STEP_MIN_CHUNK", 32);
+  int zc;
+  if (target > 0) {
+    long long chunks = (target + (long long)gx * gy - 1) / ((long long)gx * gy);
+    zc = std::max(div_up(k1 - k0, std::max<long long>(chunks, 1)), minc);
+  } else {
+    zc = pick_chunk_rounds(k1 - k0, (long long)gx * gy, (long long)device_cus() * per_cu, 4 * R,
+                           minc);
+  }
   const int gz = div_up(k1 - k0, zc);
   const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
   if constexpr (RING == 2)

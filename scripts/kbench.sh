@@ -7,7 +7,7 @@ timeout -k 10 300 python -m pytest tests/test_kernels_gpu.py -x -q > gpurun_out/
 case $rc in 0|1) ;; *) exit $rc;; esac
 for cfg in ${KB_CONFIGS:-"ADVDIFF_D3_TY=8"}; do
   echo "== $cfg" | tee -a gpurun_out/kbench.log
-  env $cfg timeout -k 10 120 python bench/kernels.py ${KB_ARGS:-} >> gpurun_out/kbench.log 2>&1
+  env ${cfg//+/ } timeout -k 10 120 python bench/kernels.py ${KB_ARGS:-} >> gpurun_out/kbench.log 2>&1
   rc=$?; [ $rc -eq 0 ] || { echo "exit $rc"; exit $rc; }
 done
 cat gpurun_out/kbench.log
