@@ -52,6 +52,12 @@ int advdiff_diffusion3d_stage_ls(int dtype, const void* in, void* du, void* out,
                                  int ny, int64_t sy, int64_t sz, int k0, int k1, int border,
                                  int order, double cx, double cy, double cz, double dt,
                                  double A, double B, void* stream);
+// The same step on TWO plane ranges [k0,k1) and [k0b,k1b) in one launch (the two
+// boundary slabs of a multi-GPU rank: one grid, better CU utilisation than two launches).
+int advdiff_diffusion3d_step2(int dtype, const void* uin, void* uout, int nx, int ny,
+                              int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int k0b,
+                              int k1b, int zlo, int zhi, int border, int order, double cx,
+                              double cy, double cz, double dt, void* stream);
 // 2-D heat stage, rows j in [j0, j1), columns i in [border, nx-border).
 int advdiff_diffusion2d_stage(int dtype, const void* in, const void* u0, void* out,
                               int nx, int64_t sy, int j0, int j1, int border, int order,

@@ -30,7 +30,8 @@ namespace advdiff {
 template <typename T, int ORDER, int NW, int RPW>
 __global__ __launch_bounds__(64 * NW) void diffusion3d_step_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
-    int nz_alloc, int k0, int k1, int zlo, int zhi, int zchunk, int border, T cx, T cy, T cz,
+    int nz_alloc, int k0, int k1, int k0b, int k1b, int gza, int zlo, int zhi, int zchunk,
+    int border, T cx, T cy, T cz,
     T dt) {
   constexpr int R = FD<ORDER>::R;
   constexpr int W = 64;             // stage-1 columns (one wave)
@@ -51,8 +52,10 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_kernel(
   const Tile3 tile = xcd_tile();
   const int i0 = tile.x * TX, j0 = tile.y * TY;
   const int x = i0 - 2 * R + lane;
-  const int kc0 = k0 + tile.z * zchunk;
-  const int kc1 = min(kc0 + zchunk, k1);
+  // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
+  const bool second = (int)tile.z >= gza;
+  const int kc0 = second ? k0b + ((int)tile.z - gza) * zchunk : k0 + tile.z * zchunk;
+  const int kc1 = min(kc0 + zchunk, second ? k1b : k1);
   const bool xin = x >= border && x < nx - border;
   const bool s2c = lane >= R && lane < W - R;
   const bool s3c = lane >= 2 * R && lane < W - 2 * R;
@@ -228,7 +231,8 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_kernel(
 template <typename T, int ORDER, int NW, int RPW, int PD, int XDPP>
 __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
-    int nz_alloc, int k0, int k1, int zlo, int zhi, int zchunk, int border, T cx, T cy, T cz,
+    int nz_alloc, int k0, int k1, int k0b, int k1b, int gza, int zlo, int zhi, int zchunk,
+    int border, T cx, T cy, T cz,
     T dt) {
   constexpr int R = FD<ORDER>::R;
   constexpr int W = 64;
@@ -249,8 +253,10 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
   const Tile3 tile = xcd_tile();
   const int i0 = tile.x * TX, j0 = tile.y * TY;
   const int x = i0 - 2 * R + lane;
-  const int kc0 = k0 + tile.z * zchunk;
-  const int kc1 = min(kc0 + zchunk, k1);
+  // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
+  const bool second = (int)tile.z >= gza;
+  const int kc0 = second ? k0b + ((int)tile.z - gza) * zchunk : k0 + tile.z * zchunk;
+  const int kc1 = min(kc0 + zchunk, second ? k1b : k1);
   const bool xin = x >= border && x < nx - border;
   const bool s2c = lane >= R && lane < W - R;
   const bool s3c = lane >= 2 * R && lane < W - 2 * R;
@@ -467,7 +473,8 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
 template <typename T, int ORDER, int NW, int RPW, int XDPP, int PD>
 __global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
-    int nz_alloc, int k0, int k1, int zlo, int zhi, int zchunk, int border, T cx, T cy, T cz,
+    int nz_alloc, int k0, int k1, int k0b, int k1b, int gza, int zlo, int zhi, int zchunk,
+    int border, T cx, T cy, T cz,
     T dt) {
   constexpr int R = FD<ORDER>::R;
   constexpr int NR = 2 * R + 1;
@@ -489,8 +496,10 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
   const Tile3 tile = xcd_tile();
   const int i0 = tile.x * TX, j0 = tile.y * TY;
   const int x = i0 - 2 * R + lane;
-  const int kc0 = k0 + tile.z * zchunk;
-  const int kc1 = min(kc0 + zchunk, k1);
+  // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
+  const bool second = (int)tile.z >= gza;
+  const int kc0 = second ? k0b + ((int)tile.z - gza) * zchunk : k0 + tile.z * zchunk;
+  const int kc1 = min(kc0 + zchunk, second ? k1b : k1);
   const bool xin = x >= border && x < nx - border;
   const bool s2c = lane >= R && lane < W - R;
   const bool s3c = lane >= 2 * R && lane < W - 2 * R;
@@ -724,14 +733,23 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
   }
 }
 
+struct SArgs {
+  const void* uin;
+  void* uout;
+  int nx, ny;
+  int64_t sy, sz;
+  int nz_alloc;
+  int k0, k1, k0b, k1b;  // one or two output plane ranges (second may be empty)
+  int zlo, zhi, border;
+  double cx, cy, cz, dt;
+  hipStream_t st;
+};
+
 template <typename T, int ORDER, int NW, int RPW, int RING, int PD = 1, int XDPP = 0>
-static hipError_t launch_step(const void* uin, void* uout, int nx, int ny, int64_t sy,
-                              int64_t sz, int nz_alloc, int k0, int k1, int zlo, int zhi,
-                              int border, double cx, double cy, double cz, double dt,
-                              hipStream_t st) {
+static hipError_t launch_step(const SArgs& a) {
   constexpr int R = ORDER / 2;
   constexpr int TX = 64 - 4 * R, TY = NW * RPW - 4 * R;
-  const int gx = div_up(nx, TX), gy = div_up(ny, TY);
+  const int gx = div_up(a.nx, TX), gy = div_up(a.ny, TY);
   // z chunks: minimise (rounds of resident workgroups) x (chunk + 4R warm-up planes);
   // resident workgroups = CUs x occupancy of this instance (LDS / VGPR bound: 1-2 per CU)
   static const int target = knob("STEP_TARGET_BLOCKS", 0);  // >0: legacy fixed target
@@ -749,41 +767,36 @@ static hipError_t launch_step(const void* uin, void* uout, int nx, int ny, int64
     return nb;
   }();
   static const int minc = knob("STEP_MIN_CHUNK", 32);
+  const int na = std::max(a.k1 - a.k0, 0), nb = std::max(a.k1b - a.k0b, 0);
   int zc;
   if (target > 0) {
     long long chunks = (target + (long long)gx * gy - 1) / ((long long)gx * gy);
-    zc = std::max(div_up(k1 - k0, std::max<long long>(chunks, 1)), minc);
+    zc = std::max(div_up(na + nb, std::max<long long>(chunks, 1)), minc);
   } else {
-    zc = pick_chunk_rounds(k1 - k0, (long long)gx * gy, (long long)device_cus() * per_cu, 4 * R,
+    zc = pick_chunk_rounds(na + nb, (long long)gx * gy, (long long)device_cus() * per_cu, 4 * R,
                            minc);
   }
-  const int gz = div_up(k1 - k0, zc);
+  const int gza = na > 0 ? div_up(na, zc) : 0;
+  const int gz = gza + (nb > 0 ? div_up(nb, zc) : 0);
   const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
+#define STEP_ARGS                                                                              \
+  dim3(gx, gy, gz), dim3(64, NW, 1), 0, a.st, (const T*)a.uin, (T*)a.uout, a.nx, a.ny, a.sy,    \
+      a.sz, a.nz_alloc, a.k0, a.k1, a.k0b, a.k1b, gza, a.zlo, a.zhi, zc, a.border, T(a.cx * s), \
+      T(a.cy * s), T(a.cz * s), T(a.dt)
   if constexpr (RING == 2)
-    hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD>), dim3(gx, gy, gz),
-                       dim3(64, NW, 1), 0, st, (const T*)uin, (T*)uout, nx, ny, sy, sz, nz_alloc,
-                       k0, k1, zlo, zhi, zc, border, T(cx * s), T(cy * s), T(cz * s), T(dt));
+    hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD>), STEP_ARGS);
   else if constexpr (RING == 1)
-    hipLaunchKernelGGL((diffusion3d_step_ring_kernel<T, ORDER, NW, RPW, PD, XDPP>), dim3(gx, gy, gz),
-                       dim3(64, NW, 1), 0, st, (const T*)uin, (T*)uout, nx, ny, sy, sz, nz_alloc,
-                       k0, k1, zlo, zhi, zc, border, T(cx * s), T(cy * s), T(cz * s), T(dt));
+    hipLaunchKernelGGL((diffusion3d_step_ring_kernel<T, ORDER, NW, RPW, PD, XDPP>), STEP_ARGS);
   else
-    hipLaunchKernelGGL((diffusion3d_step_kernel<T, ORDER, NW, RPW>), dim3(gx, gy, gz),
-                       dim3(64, NW, 1), 0, st, (const T*)uin, (T*)uout, nx, ny, sy, sz, nz_alloc,
-                       k0, k1, zlo, zhi, zc, border, T(cx * s), T(cy * s), T(cz * s), T(dt));
+    hipLaunchKernelGGL((diffusion3d_step_kernel<T, ORDER, NW, RPW>), STEP_ARGS);
+#undef STEP_ARGS
   return hipGetLastError();
 }
 
 // Tile/schedule variants (A/B via ADVDIFF_STEP_CFG; measurements in profiles/).
 template <typename T, int ORDER>
-static hipError_t dispatch_step(int cfg, const void* uin, void* uout, int nx, int ny,
-                                int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int zlo,
-                                int zhi, int border, double cx, double cy, double cz, double dt,
-                                hipStream_t st) {
-#define STEPV(NW, RPW, RING, ...)                                                          \
-  return launch_step<T, ORDER, NW, RPW, RING, ##__VA_ARGS__>(uin, uout, nx, ny, sy, sz, nz_alloc, \
-                                                             k0, k1, zlo, zhi, border, cx, cy, cz, \
-                                                             dt, st)
+static hipError_t dispatch_step(int cfg, const SArgs& a) {
+#define STEPV(NW, RPW, RING, ...) return launch_step<T, ORDER, NW, RPW, RING, ##__VA_ARGS__>(a)
   switch (cfg) {
     case 1: STEPV(12, 2, false);
     case 2: STEPV(6, 4, false);
@@ -818,30 +831,40 @@ static hipError_t dispatch_step(int cfg, const void* uin, void* uout, int nx, in
 
 }  // namespace advdiff
 
+extern "C" int advdiff_diffusion3d_step2(int dtype, const void* uin, void* uout, int nx, int ny,
+                                         int64_t sy, int64_t sz, int nz_alloc, int k0, int k1,
+                                         int k0b, int k1b, int zlo, int zhi, int border,
+                                         int order, double cx, double cy, double cz, double dt,
+                                         void* stream) {
+  using namespace advdiff;
+  if (k1 <= k0) {  // only the second range (or nothing)
+    k0 = k0b;
+    k1 = k1b;
+    k0b = k1b = 0;
+  }
+  if (k1 <= k0) return hipSuccess;
+  if (k1b <= k0b) k0b = k1b = 0;
+  if (nx <= 0 || ny <= 0 || uin == uout || k0 < 0 || k1 > nz_alloc || k0b < 0 ||
+      k1b > nz_alloc)
+    return hipErrorInvalidValue;
+  if (sy * (int64_t)ny >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+  const SArgs a{uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, k0b, k1b, zlo, zhi, border,
+                cx, cy, cz, dt, (hipStream_t)stream};
+  static const int cfg = knob("STEP_CFG", 0);
+  if (dtype == ADVDIFF_F64) {
+    if (order == 4) return dispatch_step<double, 4>(cfg, a);
+    if (order == 2) return dispatch_step<double, 2>(cfg, a);
+  } else if (dtype == ADVDIFF_F32) {
+    if (order == 4) return dispatch_step<float, 4>(cfg, a);
+    if (order == 2) return dispatch_step<float, 2>(cfg, a);
+  }
+  return hipErrorInvalidValue;
+}
+
 extern "C" int advdiff_diffusion3d_step(int dtype, const void* uin, void* uout, int nx, int ny,
                                         int64_t sy, int64_t sz, int nz_alloc, int k0, int k1,
                                         int zlo, int zhi, int border, int order, double cx,
                                         double cy, double cz, double dt, void* stream) {
-  using namespace advdiff;
-  if (k1 <= k0) return hipSuccess;
-  if (nx <= 0 || ny <= 0 || uin == uout || k0 < 0 || k1 > nz_alloc) return hipErrorInvalidValue;
-  if (sy * (int64_t)ny >= (int64_t(1) << 31)) return hipErrorInvalidValue;
-  hipStream_t st = (hipStream_t)stream;
-  static const int cfg = knob("STEP_CFG", 0);
-  if (dtype == ADVDIFF_F64) {
-    if (order == 4)
-      return dispatch_step<double, 4>(cfg, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
-                                      border, cx, cy, cz, dt, st);
-    if (order == 2)
-      return dispatch_step<double, 2>(cfg, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
-                                      border, cx, cy, cz, dt, st);
-  } else if (dtype == ADVDIFF_F32) {
-    if (order == 4)
-      return dispatch_step<float, 4>(cfg, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
-                                     border, cx, cy, cz, dt, st);
-    if (order == 2)
-      return dispatch_step<float, 2>(cfg, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
-                                     border, cx, cy, cz, dt, st);
-  }
-  return hipErrorInvalidValue;
+  return advdiff_diffusion3d_step2(dtype, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, 0, 0, zlo,
+                                   zhi, border, order, cx, cy, cz, dt, stream);
 }

@@ -178,13 +178,13 @@ void Engine::launch(const void* in, void* aux, void* out, Range r, double dt, do
   }
 }
 
-void Engine::launch_fused(Range r, double dt) {
-  if (r.empty()) return;
+void Engine::launch_fused(Range r, double dt, Range r2) {
+  if (r.empty() && r2.empty()) return;
   const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
-  KERNEL_CHECK(advdiff_diffusion3d_step(p_.dtype, u_, A_, p_.nx, p_.ny, sy_, sz_, slab_.alloc(),
-                                        r.lo, r.hi, zact_.lo, zact_.hi, p_.border(), p_.order,
-                                        p_.K / (dx * dx), p_.K / (dy * dy), p_.K / (dz * dz), dt,
-                                        compute_));
+  KERNEL_CHECK(advdiff_diffusion3d_step2(p_.dtype, u_, A_, p_.nx, p_.ny, sy_, sz_, slab_.alloc(),
+                                         r.lo, r.hi, r2.lo, r2.hi, zact_.lo, zact_.hi,
+                                         p_.border(), p_.order, p_.K / (dx * dx),
+                                         p_.K / (dy * dy), p_.K / (dz * dz), dt, compute_));
 }
 
 void Engine::step_fused(double dt) {
@@ -193,8 +193,7 @@ void Engine::step_fused(double dt) {
   } else if (p_.overlap) {
     launch_fused(interior_, dt);
     if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
-    launch_fused(blo_, dt);
-    launch_fused(bhi_, dt);
+    launch_fused(blo_, dt, bhi_);  // both boundary slabs in one launch
   } else {
     if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
     launch_fused(full_, dt);

@@ -158,7 +158,7 @@ class Engine {
   void launch(const void* in, void* aux, void* out, Range r, double dt, double a, double b,
               bool ls);
   void stage(void* in, void* aux, void* out, double a, double b, double dt, bool ls = false);
-  void launch_fused(Range r, double dt);
+  void launch_fused(Range r, double dt, Range r2 = Range{});
   void step_fused(double dt);
   void start_halo(void* field);
   void* plane(void* base, int l) const { return (char*)base + (size_t)l * plane_bytes_; }

@@ -52,11 +52,13 @@ class Diffusion(Model):
         # fused step: read u^n + write u^{n+1}; per-stage: 16 + 24 + 24 B
         return 16.0 if self.supports_fused else 64.0
 
-    def step(self, uin, uout, lo, hi, zlo, zhi, dt, stream=None):
+    def step(self, uin, uout, lo, hi, zlo, zhi, dt, stream=None, lo2=0, hi2=0):
+        """Fused RK3 step on planes [lo, hi) (and [lo2, hi2) in the same launch)."""
         g = self.grid
         stencil.diffusion3d_step(uin, uout, nx=g.nx, ny=g.ny, k0=lo, k1=hi, zlo=zlo, zhi=zhi,
                                  border=self.border, order=self.order, cx=self.coef[0],
-                                 cy=self.coef[1], cz=self.coef[2], dt=dt, stream=stream)
+                                 cy=self.coef[1], cz=self.coef[2], dt=dt, stream=stream,
+                                 k0b=lo2, k1b=hi2)
 
     def stable_dt(self, umax=None) -> float:
         return self.safety / (2.0 * sum(self.coef))

@@ -70,20 +70,25 @@ def diffusion3d_stage(inp, u0, out, *, nx, ny, k0, k1, border, order, cx, cy, cz
 
 
 def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy, cz, dt,
-                     stream=None):
-    """A FULL SSP-RK3 step in one launch (temporal blocking): uout[k0:k1] = RK3(uin)."""
+                     stream=None, k0b=0, k1b=0):
+    """A FULL SSP-RK3 step in one launch (temporal blocking): uout[k0:k1] = RK3(uin), and
+    uout[k0b:k1b] too when a second range is given (one launch for both)."""
     _check_layout(uin, uout)
     if uin.data_ptr() == uout.data_ptr():
         raise ValueError("the fused step needs distinct input/output buffers")
     if uin.is_cuda:
         lib = _lib.require()
-        assert 0 <= k0 and k1 <= uin.shape[0] and 0 <= zlo and zhi <= uin.shape[0]
-        code = lib.advdiff_diffusion3d_step(
-            _dtype_code(uin), _ptr(uin), _ptr(uout), nx, ny, uin.stride(1), uin.stride(0),
-            uin.shape[0], k0, k1, zlo, zhi, border, order, cx, cy, cz, dt, _stream_ptr(stream))
+        nz = uin.shape[0]
+        assert 0 <= k0 and k1 <= nz and 0 <= zlo and zhi <= nz and 0 <= k0b and k1b <= nz
+        code = lib.advdiff_diffusion3d_step2(
+            _dtype_code(uin), _ptr(uin), _ptr(uout), nx, ny, uin.stride(1), uin.stride(0), nz,
+            k0, k1, k0b, k1b, zlo, zhi, border, order, cx, cy, cz, dt, _stream_ptr(stream))
         _lib.check(code, "diffusion3d_step")
     else:
-        ref.diffusion3d_step(uin, uout, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy, cz, dt)
+        for a, b in ((k0, k1), (k0b, k1b)):
+            if b > a:
+                ref.diffusion3d_step(uin, uout, nx, ny, a, b, zlo, zhi, border, order, cx, cy,
+                                     cz, dt)
 
 
 def diffusion2d_stage(inp, u0, out, *, nx, j0, j1, border, order, cx, cy, dt, a, b,

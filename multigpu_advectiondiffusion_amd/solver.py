@@ -258,11 +258,13 @@ class Solver:
         with trace.range_("halo_start"):
             self._pending[id(out)] = self.halo.start(out)
 
-    def _launch_fused(self, rng, dt):
-        lo, hi = rng
-        if hi > lo:
-            self.model.step(self.u, self.un, lo, hi, self.zact[0], self.zact[1], dt)
-            trace.sync_check(f"{self.model.name} fused step [{lo},{hi})", self.device)
+    def _launch_fused(self, rng, dt, rng2=(0, 0)):
+        (lo, hi), (lo2, hi2) = rng, rng2
+        if hi > lo or hi2 > lo2:
+            self.model.step(self.u, self.un, lo, hi, self.zact[0], self.zact[1], dt, lo2=lo2,
+                            hi2=hi2)
+            trace.sync_check(f"{self.model.name} fused step [{lo},{hi}) [{lo2},{hi2})",
+                             self.device)
 
     def _step_fused(self, dt: float) -> None:
         pend = self._pending.pop(id(self.u), None)
@@ -274,9 +276,8 @@ class Solver:
             with trace.range_("halo_wait"):
                 if pend is not None:
                     pend.wait()
-            with trace.range_("boundary"):
-                for rng in self.boundary:
-                    self._launch_fused(rng, dt)
+            with trace.range_("boundary"):  # both boundary slabs in ONE launch
+                self._launch_fused(self.boundary[0], dt, self.boundary[1])
         else:
             if pend is not None:
                 pend.wait()
