@@ -131,6 +131,11 @@ int advdiff_copy_box(int dtype, void* dst, int64_t dsy, int64_t dsz, const void*
 // x[0:n] *= s (contiguous), e.g. to scale a device-generated IC into an exact solution.
 int advdiff_scale(int dtype, void* x, int64_t n, double s, void* stream);
 
+// Device scan: out[0..n) = CU count, ECC enabled, L2 bytes, LDS per workgroup, clock kHz,
+// memory clock kHz, memory bus bits, wavefront size.
+int advdiff_device_info(int dev, int64_t* out, int n);
+// Peer topology: can_access (hipDeviceCanAccessPeer), HSA link type (4 = xGMI), hop count.
+int advdiff_peer_info(int a, int b, int* can_access, int* link_type, int* hops);
 // Library identification (build flags, arch) for diagnostics.
 const char* advdiff_build_info(void);
 

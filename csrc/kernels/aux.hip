@@ -257,6 +257,36 @@ extern "C" int advdiff_copy_box(int dtype, void* dst, int64_t dsy, int64_t dsz, 
   return hipGetLastError();
 }
 
+extern "C" int advdiff_device_info(int dev, int64_t* out, int n) {
+  // [cu_count, ecc_enabled, l2_bytes, lds_per_block, clock_khz, mem_clock_khz,
+  //  mem_bus_bits, warp_size]  (the reference's DeviceScan / ECCCheck, Util.cu:32-93)
+  const hipDeviceAttribute_t attrs[] = {
+      hipDeviceAttributeMultiprocessorCount, hipDeviceAttributeEccEnabled,
+      hipDeviceAttributeL2CacheSize,         hipDeviceAttributeMaxSharedMemoryPerBlock,
+      hipDeviceAttributeClockRate,           hipDeviceAttributeMemoryClockRate,
+      hipDeviceAttributeMemoryBusWidth,      hipDeviceAttributeWarpSize};
+  const int na = (int)(sizeof(attrs) / sizeof(attrs[0]));
+  for (int i = 0; i < n && i < na; ++i) {
+    int v = -1;
+    const hipError_t e = hipDeviceGetAttribute(&v, attrs[i], dev);
+    if (e != hipSuccess) return e;
+    out[i] = v;
+  }
+  return hipSuccess;
+}
+
+extern "C" int advdiff_peer_info(int a, int b, int* can_access, int* link_type, int* hops) {
+  // xGMI topology between two devices: peer access, HSA link type (4 = xGMI), hop count
+  hipError_t e = hipDeviceCanAccessPeer(can_access, a, b);
+  if (e != hipSuccess) return e;
+  uint32_t lt = 0, hc = 0;
+  e = hipExtGetLinkTypeAndHopCount(a, b, &lt, &hc);
+  if (e != hipSuccess) return e;
+  *link_type = (int)lt;
+  *hops = (int)hc;
+  return hipSuccess;
+}
+
 extern "C" const char* advdiff_build_info(void) {
   return "libadvdiff gfx950 (CDNA4) HIP kernels: diffusion{2,3}d FD2/FD4 fused SSP-RK3, "
          "burgers{2,3}d WENO5-JS/Z fused SSP-RK3, norms, init, copy_box";

@@ -73,6 +73,9 @@ def build_parser():
                     help="process grid: slab (default), auto, or PZxPYxPX / PYxPX")
     ap.add_argument("--write", default=None, help="write float32 result.bin to this path")
     ap.add_argument("--initial", default=None, help="write float32 initial.bin to this path")
+    ap.add_argument("--ascii", default=None, help="write the result as ASCII (one %%g per line)")
+    ap.add_argument("--print", dest="print_field", action="store_true",
+                    help="print the final field (small grids; the reference's Print3D)")
     ap.add_argument("--checkpoint", default=None, help="write fp64 checkpoint shards to PREFIX")
     ap.add_argument("--restart", default=None, help="restart from checkpoint PREFIX")
     ap.add_argument("--style", choices=["multigpu", "singlegpu"], default="multigpu",
@@ -168,6 +171,14 @@ def main(argv=None) -> int:
     text = solver.summary(stats, style=ns.style, extra=extra)
     if ns.write:
         solver.save_result(ns.write)
+    if ns.ascii or ns.print_field:
+        from .utils import io as aio
+        g = solver.gather()
+        if comm.rank == 0:
+            if ns.ascii:
+                aio.save_ascii(ns.ascii, g)
+            if ns.print_field:
+                print(aio.format_field(g))
     if ns.checkpoint:
         solver.save_checkpoint(ns.checkpoint)
     if comm.rank == 0:

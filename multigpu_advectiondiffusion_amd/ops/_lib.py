@@ -77,6 +77,10 @@ def _load():
         lib.advdiff_reduce_workspace_bytes.restype = c_sz
         lib.advdiff_reduce_workspace_bytes.argtypes = []
         lib.advdiff_build_info.restype = ctypes.c_char_p
+        lib.advdiff_device_info.argtypes = [c_int, ctypes.POINTER(c_i64), c_int]
+        lib.advdiff_device_info.restype = c_int
+        lib.advdiff_peer_info.argtypes = [c_int, c_int] + [ctypes.POINTER(c_int)] * 3
+        lib.advdiff_peer_info.restype = c_int
         _lib = lib
         return _lib
 

@@ -34,6 +34,25 @@ def load_binary(path, shape) -> np.ndarray:
     return np.fromfile(path, dtype=np.float32).reshape(shape)
 
 
+def save_ascii(path, arr: np.ndarray) -> None:
+    """One value per line ("%g"), x fastest — the reference's ASCII `Save3D`/`Save2D`
+    dump (`MultiGPU/Diffusion3d_Baseline/Tools.c:66-86`)."""
+    np.savetxt(path, np.ascontiguousarray(arr).reshape(-1), fmt="%g")
+
+
+def format_field(arr: np.ndarray, fmt: str = "%8.2f") -> str:
+    """Text block of a 2-D/3-D field, rows of x, blank line between planes — the
+    reference's `Print3D`/`Print2D` debug printers (`Tools.c:32-61`)."""
+    a = np.asarray(arr)
+    planes = a.reshape((-1,) + a.shape[-2:]) if a.ndim >= 2 else a.reshape(1, 1, -1)
+    out = []
+    for p in planes:
+        for row in p:
+            out.append("".join(fmt % v for v in row))
+        out.append("")
+    return "\n".join(out) + "\n"
+
+
 def _shard_name(prefix: Path, rank: int) -> Path:
     return prefix.parent / f"{prefix.name}.rank{rank:05d}.ckpt"
 

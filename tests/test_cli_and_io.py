@@ -121,3 +121,17 @@ def test_runall_quick_subset(capsys):
     rc = runall.main(["--quick", "--only", "MG Diffusion2d", "--device", "cpu"])
     assert rc == 0
     assert "2D Grid Size" in capsys.readouterr().out
+
+
+def test_ascii_dump_and_print(tmp_path, capsys):
+    from multigpu_advectiondiffusion_amd.cli import main
+    from multigpu_advectiondiffusion_amd.utils import io as aio
+    out = tmp_path / "r.txt"
+    assert main(["diffusion2d", "1", "1", "1", "9", "7", "3", "--device", "cpu", "--ascii",
+                 str(out), "--print"]) == 0
+    vals = np.loadtxt(out)
+    assert vals.shape == (63,)
+    txt = capsys.readouterr().out
+    assert txt.count("\n") > 7
+    block = aio.format_field(np.arange(6.0).reshape(2, 3))
+    assert block.splitlines()[0] == "    0.00    1.00    2.00"
