@@ -85,6 +85,7 @@ __global__ __launch_bounds__(TX* TY) void burgers3d_stage_kernel(
 
   // ---- prologue: column window and the face below the first plane ----
   T P[NP], M[NP], U[NP];  // f+(k-R+1..k+R-1), f-(k-R+2..k+R), u(k-R+1..k+R-1)
+  T KP[3], KM[3];         // WENO5: curvatures of f+ at k-1..k+1 and f- at k..k+2
   T fz_lo;
   {
     T uz[2 * R], fp[2 * R], fm[2 * R];
@@ -94,6 +95,12 @@ __global__ __launch_bounds__(TX* TY) void burgers3d_stage_kernel(
       lf_split(uz[q], fp[q], fm[q]);
     }
     fz_lo = Rc::face(fp, fm + 1);  // face kc0-½
+    if constexpr (W == 5) {  // curvatures carried along z: f+ at kc0-1, kc0; f- at kc0, kc0+1
+      KP[0] = weno5_curv(fp[1], fp[2], fp[3]);
+      KP[1] = weno5_curv(fp[2], fp[3], fp[4]);
+      KM[0] = weno5_curv(fm[2], fm[3], fm[4]);
+      KM[1] = weno5_curv(fm[3], fm[4], fm[5]);
+    }
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       P[q] = fp[q + 1];
@@ -136,7 +143,18 @@ __global__ __launch_bounds__(TX* TY) void burgers3d_stage_kernel(
       s_fy[tx] = lds_face((R - 1) * LX + tx + R, LX);
     if (ty == TY - 1 && tx < TY)  // left faces i0-½ of every row
       s_fx[tx * FXW] = lds_face((tx + R) * LX + R - 1, 1);
-    const T fz_hi = Rc::face(P, M);
+    T fz_hi;
+    if constexpr (W == 5) {  // two of three curvatures per side come from the last plane
+      KP[2] = weno5_curv(P[2], P[3], P[4]);
+      KM[2] = weno5_curv(M[2], M[3], M[4]);
+      fz_hi = weno5_face_k<T, WZ>(P, M, KP, KM);
+      KP[0] = KP[1];
+      KP[1] = KP[2];
+      KM[0] = KM[1];
+      KM[1] = KM[2];
+    } else {
+      fz_hi = Rc::face(P, M);
+    }
     __syncthreads();
 
     const T ctr = s_u[lc];

@@ -145,17 +145,28 @@ __device__ __forceinline__ T fast_div(T n, T d) {
 //                 tau5 = |beta_0 - beta_2|
 // alpha_k is rewritten over a common denominator (alpha_k ∝ d_k · prod_{j≠k} s_j), so
 // w_k = alpha_k / Σalpha needs no division of its own.
-template <typename T, bool ZVARIANT>
-__device__ __forceinline__ void weno5_nd(T v0, T v1, T v2, T v3, T v4, T& num, T& den) {
+// Curvature part of a WENO5 smoothness indicator, 13/12 (a - 2b + c)²: the same for
+// every sub-stencil centred on b, so a z-marching lane reuses two of three per side.
+template <typename T>
+__device__ __forceinline__ T weno5_curv(T a, T b, T c) {
 #pragma clang fp contract(off)
-  constexpr T c1312 = T(13.0 / 12.0);
+  const T t = fma(T(-2), b, a + c);
+  return (T(13.0 / 12.0) * t) * t;
+}
+
+// weno5_nd with the curvature terms K0 = curv(v0,v1,v2), K1 = curv(v1,v2,v3),
+// K2 = curv(v2,v3,v4) supplied by the caller.
+template <typename T, bool ZVARIANT>
+__device__ __forceinline__ void weno5_nd_k(T v0, T v1, T v2, T v3, T v4, T K0, T K1, T K2,
+                                           T& num, T& den) {
+#pragma clang fp contract(off)
   constexpr T eps = T(1e-6);
-  const T t0a = fma(T(-2), v1, v0 + v2), t0b = fma(T(3), v2, fma(T(-4), v1, v0));
-  const T t1a = fma(T(-2), v2, v1 + v3), t1b = v1 - v3;
-  const T t2a = fma(T(-2), v3, v2 + v4), t2b = fma(T(3), v2, fma(T(-4), v3, v4));
-  const T b0 = fma(c1312 * t0a, t0a, (T(0.25) * t0b) * t0b);
-  const T b1 = fma(c1312 * t1a, t1a, (T(0.25) * t1b) * t1b);
-  const T b2 = fma(c1312 * t2a, t2a, (T(0.25) * t2b) * t2b);
+  const T t0b = fma(T(3), v2, fma(T(-4), v1, v0));
+  const T t1b = v1 - v3;
+  const T t2b = fma(T(3), v2, fma(T(-4), v3, v4));
+  const T b0 = fma(T(0.25) * t0b, t0b, K0);
+  const T b1 = fma(T(0.25) * t1b, t1b, K1);
+  const T b2 = fma(T(0.25) * t2b, t2b, K2);
   // candidate polynomials (times 6)
   const T q0 = fma(T(11), v2, fma(T(-7), v1, T(2) * v0));
   const T q1 = fma(T(5), v2, fma(T(2), v3, -v1));
@@ -181,6 +192,12 @@ __device__ __forceinline__ void weno5_nd(T v0, T v1, T v2, T v3, T v4, T& num, T
 }
 
 template <typename T, bool ZVARIANT>
+__device__ __forceinline__ void weno5_nd(T v0, T v1, T v2, T v3, T v4, T& num, T& den) {
+  weno5_nd_k<T, ZVARIANT>(v0, v1, v2, v3, v4, weno5_curv(v0, v1, v2), weno5_curv(v1, v2, v3),
+                          weno5_curv(v2, v3, v4), num, den);
+}
+
+template <typename T, bool ZVARIANT>
 __device__ __forceinline__ T weno5(T v0, T v1, T v2, T v3, T v4) {
   T n, d;
   weno5_nd<T, ZVARIANT>(v0, v1, v2, v3, v4, n, d);
@@ -198,6 +215,21 @@ __device__ __forceinline__ T weno5_face(T p0, T p1, T p2, T p3, T p4,   // fp i-
   T n1, d1, n2, d2;
   weno5_nd<T, ZVARIANT>(p0, p1, p2, p3, p4, n1, d1);
   weno5_nd<T, ZVARIANT>(m4, m3, m2, m1, m0, n2, d2);
+  if constexpr (sizeof(T) == 8) {
+    return fast_div(fma(n1, d2, n2 * d1), d1 * d2);
+  } else {
+    return fast_div(n1, d1) + fast_div(n2, d2);
+  }
+}
+
+// weno5_face with precomputed curvatures: kp = curv of f+ centred on p1, p2, p3 and
+// km = curv of f- centred on m1, m2, m3 (bit-identical to weno5_face).
+template <typename T, bool ZVARIANT>
+__device__ __forceinline__ T weno5_face_k(const T* p, const T* m, const T* kp, const T* km) {
+#pragma clang fp contract(off)
+  T n1, d1, n2, d2;
+  weno5_nd_k<T, ZVARIANT>(p[0], p[1], p[2], p[3], p[4], kp[0], kp[1], kp[2], n1, d1);
+  weno5_nd_k<T, ZVARIANT>(m[4], m[3], m[2], m[1], m[0], km[2], km[1], km[0], n2, d2);
   if constexpr (sizeof(T) == 8) {
     return fast_div(fma(n1, d2, n2 * d1), d1 * d2);
   } else {
