@@ -69,6 +69,8 @@ def build_parser():
     ap.add_argument("--dtype", choices=["fp64", "fp32"], default="fp64")
     ap.add_argument("--device", choices=["cuda", "cpu"], default=None)
     ap.add_argument("--no-overlap", action="store_true", help="disable halo/compute overlap")
+    ap.add_argument("--kernel", choices=["native", "torch"], default="native",
+                    help="stencil implementation: gfx950 HIP kernels or the PyTorch reference ops")
     ap.add_argument("--decomp", default=None,
                     help="process grid: slab (default), auto, or PZxPYxPX / PYxPX")
     ap.add_argument("--write", default=None, help="write float32 result.bin to this path")
@@ -149,7 +151,8 @@ def main(argv=None) -> int:
     dtype = torch.float64 if ns.dtype == "fp64" else torch.float32
     t0 = 0.1 if (ic == "heat") else 0.0  # heat kernel IC is the exact solution at t0
     solver = Solver(model, grid, comm, dtype=dtype, ic=ic, overlap=not ns.no_overlap, t0=t0,
-                    check_every=ns.check_every, decomp=ns.decomp, integrator=ns.integrator)
+                    check_every=ns.check_every, decomp=ns.decomp, integrator=ns.integrator,
+                    kernel=ns.kernel)
     if ns.restart:
         solver.load_checkpoint(ns.restart)
     if ns.initial:

@@ -16,6 +16,32 @@ from . import reference as ref
 
 _DT = {torch.float32: 0, torch.float64: 1}
 
+# Explicit A/B switch: run the PyTorch reference ops (ops/reference.py) on device tensors
+# instead of the HIP kernels — the "naive kernel" baseline of SURVEY.md §7.1.  Off by
+# default and never a silent fallback: it must be requested (use_torch_reference() or
+# Solver(kernel="torch")).
+_TORCH_REF = False
+
+
+class use_torch_reference:
+    """Context manager (or call .enable()/.disable()) selecting the PyTorch stencil ops."""
+
+    def __init__(self, on: bool = True):
+        self.on = on
+
+    def __enter__(self):
+        global _TORCH_REF
+        self.prev, _TORCH_REF = _TORCH_REF, self.on
+        return self
+
+    def __exit__(self, *exc):
+        global _TORCH_REF
+        _TORCH_REF = self.prev
+
+
+def _native(t) -> bool:
+    return t.is_cuda and not _TORCH_REF
+
 
 def _dtype_code(t: torch.Tensor) -> int:
     try:
@@ -54,7 +80,7 @@ def diffusion3d_stage(inp, u0, out, *, nx, ny, k0, k1, border, order, cx, cy, cz
     """out[k0:k1] = a*u0 + b*(inp + dt*K∇²inp) on the interior box (see kernels.h).
     ls=True: low-storage RK stage, u0 is du: du = a*du + dt*L; out = inp + b*du."""
     _check_layout(inp, u0, out)
-    if inp.is_cuda:
+    if _native(inp):
         lib = _lib.require()
         R = order // 2
         assert k0 >= R and k1 + R <= inp.shape[0], "stencil planes out of bounds"
@@ -76,7 +102,7 @@ def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, 
     _check_layout(uin, uout)
     if uin.data_ptr() == uout.data_ptr():
         raise ValueError("the fused step needs distinct input/output buffers")
-    if uin.is_cuda:
+    if _native(uin):
         lib = _lib.require()
         nz = uin.shape[0]
         assert 0 <= k0 and k1 <= nz and 0 <= zlo and zhi <= nz and 0 <= k0b and k1b <= nz
@@ -94,7 +120,7 @@ def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, 
 def diffusion2d_stage(inp, u0, out, *, nx, j0, j1, border, order, cx, cy, dt, a, b,
                       stream=None, ls=False):
     _check_layout(inp, u0, out)
-    if inp.is_cuda:
+    if _native(inp):
         lib = _lib.require()
         R = order // 2
         assert j0 >= R and j1 + R <= inp.shape[0], "stencil rows out of bounds"
@@ -113,7 +139,7 @@ def burgers3d_stage(inp, u0, out, *, nx, ny, k0, k1, border, weno_z, rdx, rdy, r
     code_s, R = ref.scheme_code(weno_z), ref.scheme_radius(weno_z)
     if border < R:
         raise ValueError(f"WENO needs a frozen border of at least {R} cells")
-    if inp.is_cuda:
+    if _native(inp):
         lib = _lib.require()
         assert k0 >= R and k1 + R <= inp.shape[0], "stencil planes out of bounds"
         fn = lib.advdiff_burgers3d_stage_ls if ls else lib.advdiff_burgers3d_stage
@@ -132,7 +158,7 @@ def burgers2d_stage(inp, u0, out, *, nx, j0, j1, border, weno_z, rdx, rdy, vx=0.
     code_s, R = ref.scheme_code(weno_z), ref.scheme_radius(weno_z)
     if border < R:
         raise ValueError(f"WENO needs a frozen border of at least {R} cells")
-    if inp.is_cuda:
+    if _native(inp):
         lib = _lib.require()
         assert j0 >= R and j1 + R <= inp.shape[0], "stencil rows out of bounds"
         fn = lib.advdiff_burgers2d_stage_ls if ls else lib.advdiff_burgers2d_stage

@@ -64,12 +64,17 @@ class Solver:
                  dtype=torch.float64, device=None, ic: str = "sine", ic_params=None,
                  overlap: bool = True, pad_rows: bool = True, t0: float = 0.0,
                  check_every: int = 0, fused: bool | None = None, decomp=None,
-                 integrator: str = "ssprk3"):
+                 integrator: str = "ssprk3", kernel: str = "native"):
         """decomp: process grid — None/"slab" (split the slowest axis only, the
         reference's layout), "auto" (smallest halo surface) or "PZxPYxPX" / a tuple in
         array axis order ((pz, py, px) in 3-D, (py, px) in 2-D).
         integrator: "ssprk3" (3 stages, the C++/CUDA apps) or "lsrk45" (low-storage
-        RK4(5), 5 stages, the MATLAB WENO7 prototypes)."""
+        RK4(5), 5 stages, the MATLAB WENO7 prototypes).
+        kernel: "native" (the gfx950 HIP kernels) or "torch" (the PyTorch reference ops on
+        the same device — the naive A/B baseline; same launch ranges and schedule)."""
+        if kernel not in ("native", "torch"):
+            raise ValueError("kernel must be 'native' or 'torch'")
+        self.kernel = kernel
         if integrator not in INTEGRATORS:
             raise ValueError(f"integrator must be one of {INTEGRATORS}")
         self.integrator = integrator
@@ -290,6 +295,13 @@ class Solver:
         self.it += 1
 
     def step(self, dt: float) -> None:
+        if self.kernel == "torch":
+            with stencil.use_torch_reference():
+                self._step(dt)
+        else:
+            self._step(dt)
+
+    def _step(self, dt: float) -> None:
         if self.fused:
             self._step_fused(dt)
             return

@@ -135,3 +135,15 @@ def test_ascii_dump_and_print(tmp_path, capsys):
     assert txt.count("\n") > 7
     block = aio.format_field(np.arange(6.0).reshape(2, 3))
     assert block.splitlines()[0] == "    0.00    1.00    2.00"
+
+
+def test_torch_kernel_switch_cpu_equivalence():
+    """kernel="torch" is the explicit A/B path; on the CPU both settings run the reference."""
+    m, g = Diffusion(K=1.0, order=4), Grid((12, 12, 12), (1.0, 1.0, 1.0))
+    a = Solver(m, g, dtype=torch.float64, device="cpu", ic="sine", kernel="torch")
+    b = Solver(Diffusion(K=1.0, order=4), g, dtype=torch.float64, device="cpu", ic="sine")
+    a.run(iters=2)
+    b.run(iters=2)
+    assert np.array_equal(a.gather(), b.gather())
+    with pytest.raises(ValueError):
+        Solver(m, g, dtype=torch.float64, device="cpu", kernel="triton")
