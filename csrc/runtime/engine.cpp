@@ -53,7 +53,7 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   slab_.size = env.size;
   slab_.rank = env.rank;
   const int R = p.radius();
-  fused_ = p.fused && p.physics == Physics::Diffusion && p.dims == 3 && p.integrator == 0 &&
+  fused_ = p.fused && p.physics == Physics::Diffusion && p.integrator == 0 &&
            slab_.n / slab_.size >= 3 * R;
   slab_.ghost = fused_ ? 3 * R : R;
   if (slab_.n < slab_.size * slab_.ghost)
@@ -181,6 +181,15 @@ void Engine::launch(const void* in, void* aux, void* out, Range r, double dt, do
 void Engine::launch_fused(Range r, double dt, Range r2) {
   if (r.empty() && r2.empty()) return;
   const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
+  if (p_.dims == 2) {
+    for (const Range& q : {r, r2})
+      if (!q.empty())
+        KERNEL_CHECK(advdiff_diffusion2d_step(p_.dtype, u_, A_, p_.nx, sy_, slab_.alloc(), q.lo,
+                                              q.hi, zact_.lo, zact_.hi, p_.border(), p_.order,
+                                              p_.K / (dx * dx), p_.K / (dy * dy), dt,
+                                              compute_));
+    return;
+  }
   KERNEL_CHECK(advdiff_diffusion3d_step2(p_.dtype, u_, A_, p_.nx, p_.ny, sy_, sz_, slab_.alloc(),
                                          r.lo, r.hi, r2.lo, r2.hi, zact_.lo, zact_.hi,
                                          p_.border(), p_.order, p_.K / (dx * dx),

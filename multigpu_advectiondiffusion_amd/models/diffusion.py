@@ -44,8 +44,9 @@ class Diffusion(Model):
 
     @property
     def supports_fused(self) -> bool:
-        """3-D: one temporally blocked launch per RK3 step (diffusion_fused.hip)."""
-        return self.fused and getattr(self, "dims", 3) == 3
+        """One temporally blocked launch per RK3 step (diffusion_fused.hip in 3-D,
+        diffusion2d_fused.hip in 2-D)."""
+        return self.fused
 
     @property
     def bytes_per_cell_step(self):
@@ -55,6 +56,14 @@ class Diffusion(Model):
     def step(self, uin, uout, lo, hi, zlo, zhi, dt, stream=None, lo2=0, hi2=0):
         """Fused RK3 step on planes [lo, hi) (and [lo2, hi2) in the same launch)."""
         g = self.grid
+        if self.dims == 2:
+            for a, b in ((lo, hi), (lo2, hi2)):
+                if b > a:
+                    stencil.diffusion2d_step(uin, uout, nx=g.nx, j0=a, j1=b, ylo=zlo, yhi=zhi,
+                                             border=self.border, order=self.order,
+                                             cx=self.coef[0], cy=self.coef[1], dt=dt,
+                                             stream=stream)
+            return
         stencil.diffusion3d_step(uin, uout, nx=g.nx, ny=g.ny, k0=lo, k1=hi, zlo=zlo, zhi=zhi,
                                  border=self.border, order=self.order, cx=self.coef[0],
                                  cy=self.coef[1], cz=self.coef[2], dt=dt, stream=stream,

@@ -33,6 +33,8 @@ _SIGS = {
     "advdiff_diffusion3d_step2": [c_int, c_vp, c_vp, c_int, c_int, c_i64, c_i64, c_int, c_int,
                                   c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_dbl, c_dbl,
                                   c_dbl, c_dbl, c_vp],
+    "advdiff_diffusion2d_step": [c_int, c_vp, c_vp, c_int, c_i64, c_int, c_int, c_int, c_int,
+                                 c_int, c_int, c_int, c_dbl, c_dbl, c_dbl, c_vp],
     "advdiff_diffusion2d_stage": [c_int, c_vp, c_vp, c_vp, c_int, c_i64, c_int, c_int, c_int,
                                   c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_vp],
     "advdiff_burgers3d_stage": [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_i64, c_i64, c_int,

@@ -201,6 +201,19 @@ def diffusion3d_step(uin, uout, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy,
                       2.0 / 3.0)
 
 
+def diffusion2d_step(uin, uout, nx, j0, j1, ylo, yhi, border, order, cx, cy, dt):
+    """2-D counterpart of diffusion3d_step (semantics of advdiff_diffusion2d_step)."""
+    R = order // 2
+    ny = uin.shape[0]
+    A = uin.clone()
+    B = uin.clone()
+    lo1, hi1 = max(ylo, j0 - 2 * R, R), min(yhi, j1 + 2 * R, ny - R)
+    lo2, hi2 = max(ylo, j0 - R, R), min(yhi, j1 + R, ny - R)
+    diffusion2d_stage(uin, None, A, nx, lo1, hi1, border, order, cx, cy, dt, 0.0, 1.0)
+    diffusion2d_stage(A, uin, B, nx, lo2, hi2, border, order, cx, cy, dt, 0.75, 0.25)
+    diffusion2d_stage(B, uin, uout, nx, j0, j1, border, order, cx, cy, dt, 1.0 / 3.0, 2.0 / 3.0)
+
+
 def diffusion2d_stage(inp, u0, out, nx, j0, j1, border, order, cx, cy, dt, a, b, ls=False):
     if j1 <= j0 or nx - 2 * border <= 0:
         return

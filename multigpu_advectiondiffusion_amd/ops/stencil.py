@@ -117,6 +117,24 @@ def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, 
                                      cz, dt)
 
 
+def diffusion2d_step(uin, uout, *, nx, j0, j1, ylo, yhi, border, order, cx, cy, dt,
+                     stream=None):
+    """A FULL 2-D SSP-RK3 step in one launch: uout[j0:j1] = RK3(uin) (rows)."""
+    _check_layout(uin, uout)
+    if uin.data_ptr() == uout.data_ptr():
+        raise ValueError("the fused step needs distinct input/output buffers")
+    if _native(uin):
+        lib = _lib.require()
+        ny = uin.shape[0]
+        assert 0 <= j0 and j1 <= ny and 0 <= ylo and yhi <= ny
+        code = lib.advdiff_diffusion2d_step(
+            _dtype_code(uin), _ptr(uin), _ptr(uout), nx, uin.stride(0), ny, j0, j1, ylo, yhi,
+            border, order, cx, cy, dt, _stream_ptr(stream))
+        _lib.check(code, "diffusion2d_step")
+    else:
+        ref.diffusion2d_step(uin, uout, nx, j0, j1, ylo, yhi, border, order, cx, cy, dt)
+
+
 def diffusion2d_stage(inp, u0, out, *, nx, j0, j1, border, order, cx, cy, dt, a, b,
                       stream=None, ls=False):
     _check_layout(inp, u0, out)

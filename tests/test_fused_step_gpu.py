@@ -53,3 +53,42 @@ def test_fused_step_bitwise_equals_per_stage(dtype, order, case):
     ref.diffusion3d_step(cpu, out, nx, ny, k0, k1, zlo, zhi, border, order, *c, dt)
     tol = 1e-12 if dtype == torch.float64 else 1e-5
     assert (got.cpu().double() - out).abs().max().item() < tol
+
+
+def _per_stage_2d(u, nx, j0, j1, ylo, yhi, border, order, c, dt):
+    R = order // 2
+    ny = u.shape[0]
+    A, B, out = u.clone(), u.clone(), u.clone()
+    lo1, hi1 = max(ylo, j0 - 2 * R, R), min(yhi, j1 + 2 * R, ny - R)
+    lo2, hi2 = max(ylo, j0 - R, R), min(yhi, j1 + R, ny - R)
+    kw = dict(nx=nx, border=border, order=order, cx=c[0], cy=c[1], dt=dt)
+    stencil.diffusion2d_stage(u, None, A, j0=lo1, j1=hi1, a=0.0, b=1.0, **kw)
+    stencil.diffusion2d_stage(A, u, B, j0=lo2, j1=hi2, a=0.75, b=0.25, **kw)
+    stencil.diffusion2d_stage(B, u, out, j0=j0, j1=j1, a=1.0 / 3.0, b=2.0 / 3.0, **kw)
+    return out
+
+
+CASES_2D = [
+    # (ny, nx, sx, j0, j1, ylo, yhi, border)
+    (60, 130, 192, 2, 58, 2, 58, 2),
+    (300, 1001, 1024, 2, 298, 2, 298, 2),     # many tiles, several y chunks
+    (90, 57, 64, 20, 70, 0, 90, 2),           # middle-rank rows, all active
+    (45, 61, 64, 3, 42, 3, 42, 3),            # wider frozen border
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("order", [4, 2])
+@pytest.mark.parametrize("case", CASES_2D)
+def test_fused_step_2d_bitwise_equals_per_stage(dtype, order, case):
+    ny, nx, sx, j0, j1, ylo, yhi, border = case
+    g = torch.Generator().manual_seed(5)
+    u = torch.rand((ny, sx), generator=g, dtype=torch.float64).to(dtype).cuda()
+    c = (0.23, 0.19)
+    dt = 0.9 / (2 * sum(c)) if order == 2 else 0.5 / sum(c)
+    exp = _per_stage_2d(u, nx, j0, j1, ylo, yhi, border, order, c, dt)
+    got = u.clone()
+    stencil.diffusion2d_step(u, got, nx=nx, j0=j0, j1=j1, ylo=ylo, yhi=yhi, border=border,
+                             order=order, cx=c[0], cy=c[1], dt=dt)
+    torch.cuda.synchronize()
+    assert torch.equal(got, exp), (got - exp).abs().max().item()
