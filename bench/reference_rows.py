@@ -43,9 +43,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--md", default=None)
     ap.add_argument("--scale", type=float, default=1.0, help="step-count multiplier")
+    ap.add_argument("--only", default=None, help="substring filter on the case label")
     a = ap.parse_args()
     out = []
     for label, ref, src, mk, shape, lengths, ic, steps in ROWS:
+        if a.only and a.only not in label:
+            continue
         model = mk()
         s = Solver(model, Grid(shape, lengths), dtype=torch.float64, device="cuda", ic=ic)
         n = max(int(steps * a.scale), 8)

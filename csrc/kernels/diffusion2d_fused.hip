@@ -159,11 +159,23 @@ static hipError_t launch_step2d(const void* uin, void* uout, int nx, int64_t sy,
   constexpr int R = ORDER / 2;
   constexpr int TX = 64 - 4 * R;
   const int ntiles = div_up(nx, TX);
-  // waves are independent (no LDS): aim for ~8 resident waves per SIMD
-  static const int waves = knob("STEP2D_WAVES", 8192);
-  static const int minc = knob("STEP2D_MIN_CHUNK", 16);
+  // Waves are independent and latency-bound when few: cost(C chunks) ~ (rows per wave +
+  // 4R warm-up) x max(1, waves / wave slots), wave slots ~ 4 per SIMD (fitted on 400² ..
+  // 16384²: profiles/heat2d_sizes.log).  Small grids get short chunks (more waves), large
+  // grids long ones (less warm-up).
+  static const int slots = knob("STEP2D_SLOTS", 4 * 4 * device_cus());
+  static const int minc = knob("STEP2D_MIN_CHUNK", 2);
   const int n = j1 - j0;
-  int chunks = std::max(1, std::min(div_up(waves, ntiles), std::max(1, n / minc)));
+  int chunks = 1;
+  double best = -1.0;
+  for (int C = 1; C <= std::max(1, n / minc); ++C) {
+    const double len = (double)div_up(n, C);
+    const double cost = (len + 4 * R) * std::max(1.0, (double)ntiles * C / slots);
+    if (best < 0 || cost < best) {
+      best = cost;
+      chunks = C;
+    }
+  }
   const int yc = div_up(n, chunks);
   chunks = div_up(n, yc);
   const int items = ntiles * chunks;
