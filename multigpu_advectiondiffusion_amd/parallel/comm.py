@@ -21,6 +21,26 @@ import torch
 import torch.distributed as dist
 
 
+def pg_kwargs(backend: str, dev: torch.device) -> dict:
+    """Extra init_process_group arguments for RCCL:
+    * device_id: eager communicator creation (no lazy setup inside the first halo);
+    * a HIGH-PRIORITY internal RCCL stream: the fused interior kernel fills every CU
+      (VGPR/LDS), so RCCL's copy workgroups can only start as interior workgroups retire —
+      at high priority they are dispatched first, which keeps the halo transfer inside
+      the interior compute window (ADVDIFF_RCCL_HIGH_PRIORITY=0 disables)."""
+    kw = {}
+    if dev.type == "cuda" and backend == "nccl":
+        kw["device_id"] = dev
+        if os.environ.get("ADVDIFF_RCCL_HIGH_PRIORITY", "1") != "0":
+            try:
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+                kw["pg_options"] = opts
+            except (AttributeError, RuntimeError):  # pragma: no cover - older torch
+                pass
+    return kw
+
+
 class Comm:
     def __init__(self, rank=0, size=1, local_rank=0, device=None, backend=None, group=None):
         self.rank = rank
@@ -67,8 +87,7 @@ class Comm:
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 kw = dict(backend=c.backend, rank=rank, world_size=size,
                           timeout=datetime.timedelta(seconds=timeout_s))
-                if dev.type == "cuda" and c.backend == "nccl":
-                    kw["device_id"] = dev  # eager communicator init: no lazy P2P setup
+                kw.update(pg_kwargs(c.backend, dev))
                 dist.init_process_group(**kw)
                 c._owns_pg = True
             c.group = dist.group.WORLD

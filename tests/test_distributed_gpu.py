@@ -87,3 +87,28 @@ def test_gpu_init_ic_box_matches_torch():
                                    dz=g.spacing[2], p0=p[0], p1=p[1])
         ref = ics.evaluate_box(name, shape, g.spacing, offs, ext, sx)
         torch.testing.assert_close(u.cpu()[..., :ext[2]], ref[..., :ext[2]], rtol=1e-14, atol=1e-15)
+
+
+def _nccl_world1(_comm):
+    """init_process_group with the framework's RCCL options (eager device_id,
+    high-priority stream) on a 1-rank group, then a collective and a barrier."""
+    import datetime
+    import os
+
+    import torch.distributed as dist
+
+    from multigpu_advectiondiffusion_amd.parallel.comm import pg_kwargs
+    os.environ["MASTER_PORT"] = str(int(os.environ["MASTER_PORT"]) + 1)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group(backend="nccl", rank=0, world_size=1,
+                            timeout=datetime.timedelta(seconds=120), **pg_kwargs("nccl", dev))
+    t = torch.ones(4, device=dev)
+    dist.all_reduce(t)
+    dist.barrier(device_ids=[0])
+    ok = float(t.sum()) == 4.0
+    dist.destroy_process_group()
+    return ok
+
+
+def test_rccl_init_options_world1():
+    assert spawn_local(1, _nccl_world1, device="cuda", backend="gloo")[0]
