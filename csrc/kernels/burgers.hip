@@ -33,7 +33,9 @@ namespace advdiff {
 // Scheme-generic fused stage.  Rc = Recon<T, W, WZ>: R = 3 (WENO5) or 4 (WENO7),
 // NP = 2R-1 values per side of a face.  MODE: stage epilogue (common.hpp).
 template <typename T, int W, bool WZ, bool VISC, int MODE, int TX, int TY>
-__global__ __launch_bounds__(TX* TY) void burgers3d_stage_kernel(
+// WENO7 (136 VGPRs unconstrained): capped at 128 for 4 waves/SIMD = two 8-wave groups
+// per CU; a 20-byte spill, -12 % stage time (profiles/kbench_latest.log)
+__global__ __launch_bounds__(TX* TY) __attribute__((amdgpu_waves_per_eu(W == 7 ? 4 : 1))) void burgers3d_stage_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
     int k1, int zchunk, int border, T rdx, T rdy, T rdz, T vx, T vy, T vz, T dt, T a, T b) {
   using Rc = Recon<T, W, WZ>;
