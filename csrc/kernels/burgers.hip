@@ -35,7 +35,8 @@ namespace advdiff {
 template <typename T, int W, bool WZ, bool VISC, int MODE, int TX, int TY>
 // WENO7 (136 VGPRs unconstrained): capped at 128 for 4 waves/SIMD = two 8-wave groups
 // per CU; a 20-byte spill, -12 % stage time (profiles/kbench_latest.log)
-__global__ __launch_bounds__(TX* TY) __attribute__((amdgpu_waves_per_eu(W == 7 ? 4 : 1))) void burgers3d_stage_kernel(
+__global__ __launch_bounds__(TX* TY)
+__attribute__((amdgpu_waves_per_eu(W == 7 ? 4 : 1))) void burgers3d_stage_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
     int k1, int zchunk, int border, T rdx, T rdy, T rdz, T vx, T vy, T vz, T dt, T a, T b) {
   using Rc = Recon<T, W, WZ>;
