@@ -798,27 +798,14 @@ template <typename T, int ORDER>
 static hipError_t dispatch_step(int cfg, const SArgs& a) {
 #define STEPV(NW, RPW, RING, ...) return launch_step<T, ORDER, NW, RPW, RING, ##__VA_ARGS__>(a)
   switch (cfg) {
-    case 1: STEPV(12, 2, false);
-    case 2: STEPV(6, 4, false);
-    case 3: STEPV(8, 3, false);
-    case 4: STEPV(4, 6, false);
-    case 5: STEPV(8, 2, false);
-    case 6: STEPV(8, 2, true);
-    case 7: STEPV(16, 2, false);
-    case 8: STEPV(12, 2, true, 2);
-    case 9: STEPV(12, 2, true, 4);
-    case 10: STEPV(12, 2, true);  // ring, all x neighbours from LDS
-    case 11: STEPV(8, 3, true, 1, 1);
-    case 12: STEPV(16, 2, true, 1, 1);
-    case 13: STEPV(12, 2, true, 1, 2);
-    case 14: STEPV(12, 2, 2, 1, 1);   // compact rings, DPP stages 2/3
-    case 15: STEPV(12, 2, 2, 1, 2);   // compact rings, DPP stages 1-3
-    case 16: STEPV(16, 2, 2, 1, 1);
-    case 17: STEPV(16, 2, 2, 1, 2);
-    case 18: STEPV(12, 2, 2, 1, 0);
-    case 19: STEPV(16, 2, 2, 2, 2);   // compact rings, DPP 1-3, prefetch distance 2
-    case 20: STEPV(16, 2, 2, 2, 1);
-    case 24: STEPV(12, 2, 1, 1, 1);     // 8-slot rings + DPP x neighbours in stages 2/3
+    // measured alternatives (profiles/kbench_fused_*.log); rejected ones were removed
+    case 1: STEPV(12, 2, 0);           // plain: z-windows shifted by register moves
+    case 10: STEPV(12, 2, 1);          // 8-slot rings, all x neighbours from LDS
+    case 24: STEPV(12, 2, 1, 1, 1);    // 8-slot rings + DPP x neighbours in stages 2/3
+    case 14: STEPV(12, 2, 2, 1, 1);    // compact rings, 12 waves, DPP stages 2/3
+    case 15: STEPV(12, 2, 2, 1, 2);    // compact rings, 12 waves, DPP stages 1-3
+    case 16: STEPV(16, 2, 2, 1, 1);    // compact rings, 16 waves, DPP stages 2/3
+    case 19: STEPV(16, 2, 2, 2, 2);    // + prefetch distance 2
     default:  // compact rings; FD4: 16 waves, DPP in all stages; FD2: 12 waves, stages 2/3
       if constexpr (ORDER == 4) {
         STEPV(16, 2, 2, 1, 2);
