@@ -50,6 +50,9 @@ def main():
     ap.add_argument("--no-burgers", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--decomp", default=None, help="process grid (default: z-slabs)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: base^3 cells per GPU (default); strong: the 8-GPU grid "
+                         "(2*base)^3 on any N")
     ap.add_argument("--device", default=None)
     args = ap.parse_args()
 
@@ -60,7 +63,9 @@ def main():
     dev = comm.device
 
     # ---- headline: 3-D heat, FD4, fp64, sine IC -------------------------------------
-    shape = weak_scaling_grid(args.base, n)
+    grid_of = ((lambda b: weak_scaling_grid(b, n)) if args.scaling == "weak"
+               else (lambda b: weak_scaling_grid(b, 8)))
+    shape = grid_of(args.base)
     grid = Grid(shape, (1.0, 1.0, 1.0))
     model = Diffusion(K=1.0, order=4)
     solver = Solver(model, grid, comm, dtype=torch.float64, ic="sine",
@@ -84,7 +89,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(secs / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": round(mlups / BASE_DIFFUSION, 2),
         "dtype": "fp64",
         "data": "synthetic (sinusoidal IC sin(pi x)sin(pi y)sin(pi z), random-free analytic init)",
@@ -99,7 +104,7 @@ def main():
 
     # ---- secondary: 3-D Burgers WENO5-Z + C∇²u, fp64 ----------------------------------
     if not args.no_burgers:
-        bshape = weak_scaling_grid(args.burgers_base, n)
+        bshape = grid_of(args.burgers_base)
         bgrid = Grid(bshape, (2.0, 2.0, 2.0))
         bmodel = Burgers(viscosity=1e-5, weno="z", cfl=0.3)
         bsolver = Solver(bmodel, bgrid, comm, dtype=torch.float64, ic="gaussian",
