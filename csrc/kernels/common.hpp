@@ -313,16 +313,18 @@ struct Recon<T, 7, false> {
 // LDS traffic): lane i receives lane i-1 (shr) / i+1 (shl); lanes without a source get 0.
 // Every lane of the wave must execute them (call only under wave-uniform control flow).
 // ---------------------------------------------------------------------------------
+// bound_ctrl = 1: lanes without a source read 0 and no "old" value has to be
+// materialised (update_dpp with old = 0 costs an extra v_mov per 32-bit half).
 template <int CTRL>
 __device__ __forceinline__ double dpp_move(double v) {
   int lo = __double2loint(v), hi = __double2hiint(v);
-  lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xf, 0xf, false);
-  hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xf, 0xf, false);
+  lo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xf, 0xf, true);
+  hi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xf, 0xf, true);
   return __hiloint2double(hi, lo);
 }
 template <int CTRL>
 __device__ __forceinline__ float dpp_move(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, true));
 }
 template <typename T>
 __device__ __forceinline__ T wave_shr1(T v) { return dpp_move<0x138>(v); }  // from lane i-1
