@@ -137,6 +137,9 @@ int advdiff_copy_box(int dtype, void* dst, int64_t dsy, int64_t dsz, const void*
 // x[0:n] *= s (contiguous), e.g. to scale a device-generated IC into an exact solution.
 int advdiff_scale(int dtype, void* x, int64_t n, double s, void* stream);
 
+// Debug dump (device printf) of the box [i0,i1)x[j0,j1)x[k0,k1) (at most 4096 values).
+int advdiff_debug_print(int dtype, const void* u, int64_t sy, int64_t sz, int i0, int i1,
+                        int j0, int j1, int k0, int k1, void* stream);
 // Device scan: out[0..n) = CU count, ECC enabled, L2 bytes, LDS per workgroup, clock kHz,
 // memory clock kHz, memory bus bits, wavefront size.
 int advdiff_device_info(int dev, int64_t* out, int n);

@@ -257,6 +257,40 @@ extern "C" int advdiff_copy_box(int dtype, void* dst, int64_t dsy, int64_t dsz, 
   return hipGetLastError();
 }
 
+namespace advdiff {
+// Device-side dump of a small box (one thread, printf) — the reference's PrintGPUmemory
+// debug kernels (MultiGPU/Diffusion3d_Baseline/Kernels.cu).
+template <typename T>
+__global__ void debug_print_kernel(const T* u, int64_t sy, int64_t sz, int i0, int i1, int j0,
+                                   int j1, int k0, int k1) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int k = k0; k < k1; ++k) {
+    printf("[k=%d]\n", k);
+    for (int j = j0; j < j1; ++j) {
+      for (int i = i0; i < i1; ++i) printf("%8.4f ", (double)u[(int64_t)k * sz + (int64_t)j * sy + i]);
+      printf("\n");
+    }
+  }
+}
+
+}  // namespace advdiff
+
+extern "C" int advdiff_debug_print(int dtype, const void* u, int64_t sy, int64_t sz, int i0,
+                                   int i1, int j0, int j1, int k0, int k1, void* stream) {
+  using namespace advdiff;
+  hipStream_t st = (hipStream_t)stream;
+  if ((int64_t)(i1 - i0) * (j1 - j0) * (k1 - k0) > 4096) return hipErrorInvalidValue;
+  if (dtype == ADVDIFF_F64)
+    hipLaunchKernelGGL(debug_print_kernel<double>, dim3(1), dim3(64), 0, st, (const double*)u,
+                       sy, sz, i0, i1, j0, j1, k0, k1);
+  else if (dtype == ADVDIFF_F32)
+    hipLaunchKernelGGL(debug_print_kernel<float>, dim3(1), dim3(64), 0, st, (const float*)u, sy,
+                       sz, i0, i1, j0, j1, k0, k1);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 extern "C" int advdiff_device_info(int dev, int64_t* out, int n) {
   // [cu_count, ecc_enabled, l2_bytes, lds_per_block, clock_khz, mem_clock_khz,
   //  mem_bus_bits, warp_size]  (the reference's DeviceScan / ECCCheck, Util.cu:32-93)

@@ -49,6 +49,8 @@ _SIGS = {
     "advdiff_init_ic_box": [c_int, c_int, c_vp, c_int, c_int, c_int, c_i64, c_i64, c_int,
                             c_int, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_dbl, c_dbl,
                             c_dbl, c_vp],
+    "advdiff_debug_print": [c_int, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int, c_int,
+                            c_int, c_vp],
     "advdiff_copy_box": [c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int,
                          c_vp],
 }

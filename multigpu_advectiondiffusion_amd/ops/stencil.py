@@ -268,3 +268,20 @@ def init_ic_box_device(u, ic_code, *, nx, ny, nzl, ig0, jg0, kg0, NX, NY, NZ, dx
                                    u3.stride(1), u3.stride(0), ig0, jg0, kg0, NX, NY, NZ, dx,
                                    dy, dz, p0, p1, _stream_ptr(stream))
     _lib.check(code, "init_ic_box")
+
+
+def debug_print(u, box, stream=None):
+    """Device-side printf of a small box ((i0,i1),(j0,j1),(k0,k1)) of a 3-D (or 2-D) field —
+    the reference's PrintGPUmemory.  CPU tensors are printed from the host."""
+    (i0, i1), (j0, j1), (k0, k1) = box if len(box) == 3 else (box[0], box[1], (0, 1))
+    u3 = u if u.dim() == 3 else u.unsqueeze(0)
+    if not u.is_cuda:
+        for k in range(k0, k1):
+            print(f"[k={k}]")
+            for j in range(j0, j1):
+                print(" ".join(f"{float(v):8.4f}" for v in u3[k, j, i0:i1]))
+        return
+    lib = _lib.require()
+    code = lib.advdiff_debug_print(_dtype_code(u), u3.data_ptr(), u3.stride(1), u3.stride(0),
+                                   i0, i1, j0, j1, k0, k1, _stream_ptr(stream))
+    _lib.check(code, "debug_print")

@@ -177,3 +177,11 @@ def test_copy_box():
     torch.cuda.synchronize()
     assert torch.equal(dst[:5, :9, :33].cpu(), src[:5, :9, :33].cpu())
     assert dst[5].abs().sum().item() == 0.0
+
+
+def test_debug_print_kernel(capfd):
+    u = torch.arange(24, dtype=torch.float64, device=DEV).reshape(2, 3, 4)
+    stencil.debug_print(u, ((1, 3), (0, 2), (1, 2)))
+    torch.cuda.synchronize()
+    out = capfd.readouterr().out
+    assert "[k=1]" in out and "13.0000" in out and "18.0000" in out
