@@ -58,12 +58,24 @@ int advdiff_diffusion3d_step2(int dtype, const void* uin, void* uout, int nx, in
                               int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int k0b,
                               int k1b, int zlo, int zhi, int border, int order, double cx,
                               double cy, double cz, double dt, void* stream);
+// General form for blocks of a Cartesian decomposition, launched on a VIEW: box[8] =
+// {xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1} (view coordinates): cells outside the active
+// box [xa0,xa1) x [ya0,ya1) are frozen, u^{n+1} is written on active cells inside the
+// output box [xo0,xo1) x [yo0,yo1) (which must lie >= 3R inside the view on split axes).
+int advdiff_diffusion3d_step_box(int dtype, const void* uin, void* uout, int nx, int ny,
+                                 int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int k0b,
+                                 int k1b, int zlo, int zhi, const int* box, int order,
+                                 double cx, double cy, double cz, double dt, void* stream);
 // 2-D heat: ONE FULL SSP-RK3 step per launch on rows [j0, j1) (intermediate stages on
 // the active rows [ylo, yhi)); reads rows j0-3R .. j1+3R-1 (clamped to [0, ny_alloc)).
 // Wave-independent y-march, no LDS; bit-identical to three advdiff_diffusion2d_stage.
 int advdiff_diffusion2d_step(int dtype, const void* uin, void* uout, int nx, int64_t sy,
                              int ny_alloc, int j0, int j1, int ylo, int yhi, int border,
                              int order, double cx, double cy, double dt, void* stream);
+// Cartesian-block form: box[4] = {xa0, xa1, xo0, xo1} (active / output columns, view coords).
+int advdiff_diffusion2d_step_box(int dtype, const void* uin, void* uout, int nx, int64_t sy,
+                                 int ny_alloc, int j0, int j1, int ylo, int yhi, const int* box,
+                                 int order, double cx, double cy, double dt, void* stream);
 // 2-D heat stage, rows j in [j0, j1), columns i in [border, nx-border).
 int advdiff_diffusion2d_stage(int dtype, const void* in, const void* u0, void* out,
                               int nx, int64_t sy, int j0, int j1, int border, int order,

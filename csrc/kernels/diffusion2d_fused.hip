@@ -22,8 +22,8 @@ constexpr int kWavesPerBlock2 = 4;
 template <typename T, int ORDER>
 __global__ __launch_bounds__(64 * kWavesPerBlock2) void diffusion2d_step_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int64_t sy, int ny_alloc, int j0,
-    int j1, int ylo, int yhi, int ychunk, int nchunks, int ntiles, int border, T cx, T cy,
-    T dt) {
+    int j1, int ylo, int yhi, int ychunk, int nchunks, int ntiles, int xa0, int xa1, int xo0,
+    int xo1, T cx, T cy, T dt) {
   constexpr int R = FD<ORDER>::R;
   constexpr int NR = 2 * R + 1;
   constexpr int W = 64;
@@ -36,7 +36,8 @@ __global__ __launch_bounds__(64 * kWavesPerBlock2) void diffusion2d_step_kernel(
   const int x = i0 - 2 * R + lane;
   const int jc0 = j0 + chunk * ychunk;
   const int jc1 = min(jc0 + ychunk, j1);
-  const bool xin = x >= border && x < nx - border;
+  const bool xin = x >= xa0 && x < xa1;                 // non-frozen columns
+  const bool xout = xin && x >= xo0 && x < xo1;          // columns this launch writes
   const bool s2c = lane >= R && lane < W - R;
   const bool s3c = lane >= 2 * R && lane < W - 2 * R;
   const int xc = clampi(x, 0, nx - 1);
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock2) void diffusion2d_step_kernel(
                    FD<2>::d2(rb[sl(-1)], c, rb[sl(1)]));
       }
       const T v = rk_stage<T, true>(uo, c, lap, dt, third, two3);
-      if (xin && s3c) uout[(int64_t)j * sy + x] = v;
+      if (xout && s3c) uout[(int64_t)j * sy + x] = v;
     }
 #pragma unroll
     for (int d = 0; d < R - 1; ++d) dl[d] = dl[d + 1];
@@ -154,7 +155,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock2) void diffusion2d_step_kernel(
 
 template <typename T, int ORDER>
 static hipError_t launch_step2d(const void* uin, void* uout, int nx, int64_t sy, int ny_alloc,
-                                int j0, int j1, int ylo, int yhi, int border, double cx,
+                                int j0, int j1, int ylo, int yhi, const int* bx, double cx,
                                 double cy, double dt, hipStream_t st) {
   constexpr int R = ORDER / 2;
   constexpr int TX = 64 - 4 * R;
@@ -182,35 +183,40 @@ static hipError_t launch_step2d(const void* uin, void* uout, int nx, int64_t sy,
   const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
   hipLaunchKernelGGL((diffusion2d_step_kernel<T, ORDER>), dim3(div_up(items, kWavesPerBlock2)),
                      dim3(64, kWavesPerBlock2, 1), 0, st, (const T*)uin, (T*)uout, nx, sy,
-                     ny_alloc, j0, j1, ylo, yhi, yc, chunks, ntiles, border, T(cx * s),
-                     T(cy * s), T(dt));
+                     ny_alloc, j0, j1, ylo, yhi, yc, chunks, ntiles, bx[0], bx[1], bx[2],
+                     bx[3], T(cx * s), T(cy * s), T(dt));
   return hipGetLastError();
 }
 
 }  // namespace advdiff
 
+extern "C" int advdiff_diffusion2d_step_box(int dtype, const void* uin, void* uout, int nx,
+                                            int64_t sy, int ny_alloc, int j0, int j1, int ylo,
+                                            int yhi, const int* box, int order, double cx,
+                                            double cy, double dt, void* stream) {
+  using namespace advdiff;
+  if (j1 <= j0) return hipSuccess;
+  if (nx <= 0 || uin == uout || j0 < 0 || j1 > ny_alloc || box == nullptr)
+    return hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+#define S2D(T, O) \
+  return launch_step2d<T, O>(uin, uout, nx, sy, ny_alloc, j0, j1, ylo, yhi, box, cx, cy, dt, st)
+  if (dtype == ADVDIFF_F64) {
+    if (order == 4) S2D(double, 4);
+    if (order == 2) S2D(double, 2);
+  } else if (dtype == ADVDIFF_F32) {
+    if (order == 4) S2D(float, 4);
+    if (order == 2) S2D(float, 2);
+  }
+#undef S2D
+  return hipErrorInvalidValue;
+}
+
 extern "C" int advdiff_diffusion2d_step(int dtype, const void* uin, void* uout, int nx,
                                         int64_t sy, int ny_alloc, int j0, int j1, int ylo,
                                         int yhi, int border, int order, double cx, double cy,
                                         double dt, void* stream) {
-  using namespace advdiff;
-  if (j1 <= j0) return hipSuccess;
-  if (nx <= 0 || uin == uout || j0 < 0 || j1 > ny_alloc) return hipErrorInvalidValue;
-  hipStream_t st = (hipStream_t)stream;
-  if (dtype == ADVDIFF_F64) {
-    if (order == 4)
-      return launch_step2d<double, 4>(uin, uout, nx, sy, ny_alloc, j0, j1, ylo, yhi, border, cx,
-                                      cy, dt, st);
-    if (order == 2)
-      return launch_step2d<double, 2>(uin, uout, nx, sy, ny_alloc, j0, j1, ylo, yhi, border, cx,
-                                      cy, dt, st);
-  } else if (dtype == ADVDIFF_F32) {
-    if (order == 4)
-      return launch_step2d<float, 4>(uin, uout, nx, sy, ny_alloc, j0, j1, ylo, yhi, border, cx,
-                                     cy, dt, st);
-    if (order == 2)
-      return launch_step2d<float, 2>(uin, uout, nx, sy, ny_alloc, j0, j1, ylo, yhi, border, cx,
-                                     cy, dt, st);
-  }
-  return hipErrorInvalidValue;
+  const int box[4] = {border, nx - border, 0, nx};
+  return advdiff_diffusion2d_step_box(dtype, uin, uout, nx, sy, ny_alloc, j0, j1, ylo, yhi, box,
+                                      order, cx, cy, dt, stream);
 }

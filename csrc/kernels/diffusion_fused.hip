@@ -27,11 +27,20 @@
 
 namespace advdiff {
 
+// x/y bounds of a fused-step launch (view coordinates): cells outside [xa0,xa1) x
+// [ya0,ya1) are frozen (A = B = u there, never written); u^{n+1} is written on the active
+// cells inside [xo0,xo1) x [yo0,yo1).  Slab layout: active = [border, n-border), output =
+// everything; Cartesian blocks: active = the global interior seen through the view,
+// output = the block (3R inside the view on split axes).
+struct Box2 {
+  int xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1;
+};
+
 template <typename T, int ORDER, int NW, int RPW>
 __global__ __launch_bounds__(64 * NW) void diffusion3d_step_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
     int nz_alloc, int k0, int k1, int k0b, int k1b, int gza, int zlo, int zhi, int zchunk,
-    int border, T cx, T cy, T cz,
+    Box2 bx, T cx, T cy, T cz,
     T dt) {
   constexpr int R = FD<ORDER>::R;
   constexpr int W = 64;             // stage-1 columns (one wave)
@@ -56,18 +65,20 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_kernel(
   const bool second = (int)tile.z >= gza;
   const int kc0 = second ? k0b + ((int)tile.z - gza) * zchunk : k0 + tile.z * zchunk;
   const int kc1 = min(kc0 + zchunk, second ? k1b : k1);
-  const bool xin = x >= border && x < nx - border;
+  const bool xin = x >= bx.xa0 && x < bx.xa1;   // non-frozen columns
+  const bool xout = x >= bx.xo0 && x < bx.xo1;  // columns this launch writes
   const bool s2c = lane >= R && lane < W - R;
   const bool s3c = lane >= 2 * R && lane < W - 2 * R;
   const int xc = clampi(x, 0, nx - 1);
 
   int row[RPW], off[RPW];
-  bool inxy[RPW], s2r[RPW], s3r[RPW];
+  bool inxy[RPW], outq[RPW], s2r[RPW], s3r[RPW];
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
     row[q] = w + q * NW;
     const int y = j0 - 2 * R + row[q];
-    inxy[q] = xin && y >= border && y < ny - border;
+    inxy[q] = xin && y >= bx.ya0 && y < bx.ya1;
+    outq[q] = inxy[q] && xout && y >= bx.yo0 && y < bx.yo1;
     s2r[q] = row[q] >= R && row[q] < S1R - R;
     s3r[q] = row[q] >= 2 * R && row[q] < S1R - 2 * R;
     off[q] = clampi(y, 0, ny - 1) * (int)sy + xc;
@@ -207,7 +218,7 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_kernel(
           lap = lap3(cx, FD<2>::d2(pB[l - 1], c, pB[l + 1]), cy,
                      FD<2>::d2(pB[l - W], c, pB[l + W]), cz, FD<2>::d2(bw[q][0], c, bw[q][2]));
         const T v = rk_stage<T, true>(uo, c, lap, dt, third, two3);
-        if (inxy[q] && s3c) uout[(int64_t)k * sz + off[q]] = v;  // k in [kc0,kc1): interior
+        if (outq[q] && s3c) uout[(int64_t)k * sz + off[q]] = v;  // k in [kc0,kc1): interior
       }
     }
     // ---- advance the register windows ----
@@ -232,7 +243,7 @@ template <typename T, int ORDER, int NW, int RPW, int PD, int XDPP>
 __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
     int nz_alloc, int k0, int k1, int k0b, int k1b, int gza, int zlo, int zhi, int zchunk,
-    int border, T cx, T cy, T cz,
+    Box2 bx, T cx, T cy, T cz,
     T dt) {
   constexpr int R = FD<ORDER>::R;
   constexpr int W = 64;
@@ -257,18 +268,20 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
   const bool second = (int)tile.z >= gza;
   const int kc0 = second ? k0b + ((int)tile.z - gza) * zchunk : k0 + tile.z * zchunk;
   const int kc1 = min(kc0 + zchunk, second ? k1b : k1);
-  const bool xin = x >= border && x < nx - border;
+  const bool xin = x >= bx.xa0 && x < bx.xa1;   // non-frozen columns
+  const bool xout = x >= bx.xo0 && x < bx.xo1;  // columns this launch writes
   const bool s2c = lane >= R && lane < W - R;
   const bool s3c = lane >= 2 * R && lane < W - 2 * R;
   const int xc = clampi(x, 0, nx - 1);
 
   int row[RPW], off[RPW];
-  bool inxy[RPW], s2r[RPW], s3r[RPW];
+  bool inxy[RPW], outq[RPW], s2r[RPW], s3r[RPW];
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
     row[q] = w + q * NW;
     const int y = j0 - 2 * R + row[q];
-    inxy[q] = xin && y >= border && y < ny - border;
+    inxy[q] = xin && y >= bx.ya0 && y < bx.ya1;
+    outq[q] = inxy[q] && xout && y >= bx.yo0 && y < bx.yo1;
     s2r[q] = row[q] >= R && row[q] < S1R - R;
     s3r[q] = row[q] >= 2 * R && row[q] < S1R - 2 * R;
     off[q] = clampi(y, 0, ny - 1) * (int)sy + xc;
@@ -449,7 +462,7 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
           lap = lap3(cx, FD<2>::d2(pB[l - 1], c, pB[l + 1]), cy,
                      FD<2>::d2(pB[l - W], c, pB[l + W]), cz, FD<2>::d2(rb[q][BM], c, rb[q][BR]));
         const T v = rk_stage<T, true>(uo, c, lap, dt, third, two3);
-        if (inxy[q] && s3c) uout[(int64_t)k * sz + off[q]] = v;
+        if (outq[q] && s3c) uout[(int64_t)k * sz + off[q]] = v;
       }
     }
   };
@@ -474,7 +487,7 @@ template <typename T, int ORDER, int NW, int RPW, int XDPP, int PD>
 __global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
     int nz_alloc, int k0, int k1, int k0b, int k1b, int gza, int zlo, int zhi, int zchunk,
-    int border, T cx, T cy, T cz,
+    Box2 bx, T cx, T cy, T cz,
     T dt) {
   constexpr int R = FD<ORDER>::R;
   constexpr int NR = 2 * R + 1;
@@ -500,18 +513,20 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
   const bool second = (int)tile.z >= gza;
   const int kc0 = second ? k0b + ((int)tile.z - gza) * zchunk : k0 + tile.z * zchunk;
   const int kc1 = min(kc0 + zchunk, second ? k1b : k1);
-  const bool xin = x >= border && x < nx - border;
+  const bool xin = x >= bx.xa0 && x < bx.xa1;   // non-frozen columns
+  const bool xout = x >= bx.xo0 && x < bx.xo1;  // columns this launch writes
   const bool s2c = lane >= R && lane < W - R;
   const bool s3c = lane >= 2 * R && lane < W - 2 * R;
   const int xc = clampi(x, 0, nx - 1);
 
   int row[RPW], off[RPW];
-  bool inxy[RPW], s2r[RPW], s3r[RPW];
+  bool inxy[RPW], outq[RPW], s2r[RPW], s3r[RPW];
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
     row[q] = w + q * NW;  // interleaved: every wave has <= 1 masked halo row per stage
     const int y = j0 - 2 * R + row[q];
-    inxy[q] = xin && y >= border && y < ny - border;
+    inxy[q] = xin && y >= bx.ya0 && y < bx.ya1;
+    outq[q] = inxy[q] && xout && y >= bx.yo0 && y < bx.yo1;
     s2r[q] = row[q] >= R && row[q] < S1R - R;
     s3r[q] = row[q] >= 2 * R && row[q] < S1R - 2 * R;
     off[q] = clampi(y, 0, ny - 1) * (int)sy + xc;
@@ -712,7 +727,7 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
                      FD<2>::d2(rb[q][sl(-1)], c, rb[q][sl(1)]));
         }
         const T v = rk_stage<T, true>(uo, c, lap, dt, third, two3);
-        if (inxy[q] && s3c) uout[(int64_t)k * sz + off[q]] = v;
+        if (outq[q] && s3c) uout[(int64_t)k * sz + off[q]] = v;
       }
     }
 #pragma unroll
@@ -740,7 +755,8 @@ struct SArgs {
   int64_t sy, sz;
   int nz_alloc;
   int k0, k1, k0b, k1b;  // one or two output plane ranges (second may be empty)
-  int zlo, zhi, border;
+  int zlo, zhi;
+  Box2 bx;
   double cx, cy, cz, dt;
   hipStream_t st;
 };
@@ -781,7 +797,7 @@ static hipError_t launch_step(const SArgs& a) {
   const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
 #define STEP_ARGS                                                                              \
   dim3(gx, gy, gz), dim3(64, NW, 1), 0, a.st, (const T*)a.uin, (T*)a.uout, a.nx, a.ny, a.sy,    \
-      a.sz, a.nz_alloc, a.k0, a.k1, a.k0b, a.k1b, gza, a.zlo, a.zhi, zc, a.border, T(a.cx * s), \
+      a.sz, a.nz_alloc, a.k0, a.k1, a.k0b, a.k1b, gza, a.zlo, a.zhi, zc, a.bx, T(a.cx * s), \
       T(a.cy * s), T(a.cz * s), T(a.dt)
   if constexpr (RING == 2)
     hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD>), STEP_ARGS);
@@ -818,11 +834,11 @@ static hipError_t dispatch_step(int cfg, const SArgs& a) {
 
 }  // namespace advdiff
 
-extern "C" int advdiff_diffusion3d_step2(int dtype, const void* uin, void* uout, int nx, int ny,
-                                         int64_t sy, int64_t sz, int nz_alloc, int k0, int k1,
-                                         int k0b, int k1b, int zlo, int zhi, int border,
-                                         int order, double cx, double cy, double cz, double dt,
-                                         void* stream) {
+extern "C" int advdiff_diffusion3d_step_box(int dtype, const void* uin, void* uout, int nx,
+                                            int ny, int64_t sy, int64_t sz, int nz_alloc, int k0,
+                                            int k1, int k0b, int k1b, int zlo, int zhi,
+                                            const int* box, int order, double cx, double cy,
+                                            double cz, double dt, void* stream) {
   using namespace advdiff;
   if (k1 <= k0) {  // only the second range (or nothing)
     k0 = k0b;
@@ -832,10 +848,11 @@ extern "C" int advdiff_diffusion3d_step2(int dtype, const void* uin, void* uout,
   if (k1 <= k0) return hipSuccess;
   if (k1b <= k0b) k0b = k1b = 0;
   if (nx <= 0 || ny <= 0 || uin == uout || k0 < 0 || k1 > nz_alloc || k0b < 0 ||
-      k1b > nz_alloc)
+      k1b > nz_alloc || box == nullptr)
     return hipErrorInvalidValue;
   if (sy * (int64_t)ny >= (int64_t(1) << 31)) return hipErrorInvalidValue;
-  const SArgs a{uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, k0b, k1b, zlo, zhi, border,
+  const Box2 bx{box[0], box[1], box[2], box[3], box[4], box[5], box[6], box[7]};
+  const SArgs a{uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, k0b, k1b, zlo, zhi, bx,
                 cx, cy, cz, dt, (hipStream_t)stream};
   static const int cfg = knob("STEP_CFG", 0);
   if (dtype == ADVDIFF_F64) {
@@ -846,6 +863,16 @@ extern "C" int advdiff_diffusion3d_step2(int dtype, const void* uin, void* uout,
     if (order == 2) return dispatch_step<float, 2>(cfg, a);
   }
   return hipErrorInvalidValue;
+}
+
+extern "C" int advdiff_diffusion3d_step2(int dtype, const void* uin, void* uout, int nx, int ny,
+                                         int64_t sy, int64_t sz, int nz_alloc, int k0, int k1,
+                                         int k0b, int k1b, int zlo, int zhi, int border,
+                                         int order, double cx, double cy, double cz, double dt,
+                                         void* stream) {
+  const int box[8] = {border, nx - border, border, ny - border, 0, nx, 0, ny};
+  return advdiff_diffusion3d_step_box(dtype, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, k0b,
+                                      k1b, zlo, zhi, box, order, cx, cy, cz, dt, stream);
 }
 
 extern "C" int advdiff_diffusion3d_step(int dtype, const void* uin, void* uout, int nx, int ny,

@@ -53,21 +53,25 @@ class Diffusion(Model):
         # fused step: read u^n + write u^{n+1}; per-stage: 16 + 24 + 24 B
         return 16.0 if self.supports_fused else 64.0
 
-    def step(self, uin, uout, lo, hi, zlo, zhi, dt, stream=None, lo2=0, hi2=0):
-        """Fused RK3 step on planes [lo, hi) (and [lo2, hi2) in the same launch)."""
+    def step(self, uin, uout, lo, hi, zlo, zhi, dt, stream=None, lo2=0, hi2=0, nx=None,
+             ny=None, box=None):
+        """Fused RK3 step on planes [lo, hi) (and [lo2, hi2) in the same launch).
+        nx/ny/box: extents and explicit active/output bounds of a view (Cartesian blocks)."""
         g = self.grid
+        nx = g.nx if nx is None else nx
+        ny = g.ny if ny is None else ny
         if self.dims == 2:
             for a, b in ((lo, hi), (lo2, hi2)):
                 if b > a:
-                    stencil.diffusion2d_step(uin, uout, nx=g.nx, j0=a, j1=b, ylo=zlo, yhi=zhi,
+                    stencil.diffusion2d_step(uin, uout, nx=nx, j0=a, j1=b, ylo=zlo, yhi=zhi,
                                              border=self.border, order=self.order,
                                              cx=self.coef[0], cy=self.coef[1], dt=dt,
-                                             stream=stream)
+                                             stream=stream, box=box)
             return
-        stencil.diffusion3d_step(uin, uout, nx=g.nx, ny=g.ny, k0=lo, k1=hi, zlo=zlo, zhi=zhi,
+        stencil.diffusion3d_step(uin, uout, nx=nx, ny=ny, k0=lo, k1=hi, zlo=zlo, zhi=zhi,
                                  border=self.border, order=self.order, cx=self.coef[0],
                                  cy=self.coef[1], cz=self.coef[2], dt=dt, stream=stream,
-                                 k0b=lo2, k1b=hi2)
+                                 k0b=lo2, k1b=hi2, box=box)
 
     def stable_dt(self, umax=None) -> float:
         return self.safety / (2.0 * sum(self.coef))

@@ -201,6 +201,69 @@ def diffusion3d_step(uin, uout, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy,
                       2.0 / 3.0)
 
 
+def _sub3(t, ys, ye, xs, xe, R):
+    return None if t is None else t[:, ys - R:ye + R, xs - R:xe + R]
+
+
+def diffusion3d_step_box(uin, uout, nx, ny, k0, k1, zlo, zhi, box, order, cx, cy, cz, dt):
+    """Semantics of advdiff_diffusion3d_step_box: box = (xa0, xa1, ya0, ya1, xo0, xo1,
+    yo0, yo1); cells outside the active box are frozen (A = B = u), u^{n+1} is written on
+    active cells inside the output box."""
+    xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1 = box
+    R = order // 2
+    nz = uin.shape[0]
+    A = uin.clone()
+    B = uin.clone()
+    xs, xe = max(xa0, R), min(xa1, nx - R)
+    ys, ye = max(ya0, R), min(ya1, ny - R)
+    if xe <= xs or ye <= ys:
+        return
+    lo1, hi1 = max(zlo, k0 - 2 * R, R), min(zhi, k1 + 2 * R, nz - R)
+    lo2, hi2 = max(zlo, k0 - R, R), min(zhi, k1 + R, nz - R)
+    kw = dict(nx=xe - xs + 2 * R, ny=ye - ys + 2 * R, border=R, order=order, cx=cx, cy=cy,
+              cz=cz, dt=dt)
+    diffusion3d_stage(_sub3(uin, ys, ye, xs, xe, R), None, _sub3(A, ys, ye, xs, xe, R),
+                      k0=lo1, k1=hi1, a=0.0, b=1.0, **kw)
+    diffusion3d_stage(_sub3(A, ys, ye, xs, xe, R), _sub3(uin, ys, ye, xs, xe, R),
+                      _sub3(B, ys, ye, xs, xe, R), k0=lo2, k1=hi2, a=0.75, b=0.25, **kw)
+    oxs, oxe = max(xo0, xs), min(xo1, xe)
+    oys, oye = max(yo0, ys), min(yo1, ye)
+    if oxe <= oxs or oye <= oys:
+        return
+    kw.update(nx=oxe - oxs + 2 * R, ny=oye - oys + 2 * R)
+    diffusion3d_stage(_sub3(B, oys, oye, oxs, oxe, R), _sub3(uin, oys, oye, oxs, oxe, R),
+                      _sub3(uout, oys, oye, oxs, oxe, R), k0=k0, k1=k1, a=1.0 / 3.0,
+                      b=2.0 / 3.0, **kw)
+
+
+def diffusion2d_step_box(uin, uout, nx, j0, j1, ylo, yhi, box, order, cx, cy, dt):
+    """Semantics of advdiff_diffusion2d_step_box: box = (xa0, xa1, xo0, xo1)."""
+    xa0, xa1, xo0, xo1 = box
+    R = order // 2
+    ny = uin.shape[0]
+    A = uin.clone()
+    B = uin.clone()
+    xs, xe = max(xa0, R), min(xa1, nx - R)
+    if xe <= xs:
+        return
+    lo1, hi1 = max(ylo, j0 - 2 * R, R), min(yhi, j1 + 2 * R, ny - R)
+    lo2, hi2 = max(ylo, j0 - R, R), min(yhi, j1 + R, ny - R)
+
+    def sub(t, a, b):
+        return None if t is None else t[:, a - R:b + R]
+    kw = dict(nx=xe - xs + 2 * R, border=R, order=order, cx=cx, cy=cy, dt=dt)
+    diffusion2d_stage(sub(uin, xs, xe), None, sub(A, xs, xe), j0=lo1, j1=hi1, a=0.0, b=1.0,
+                      **kw)
+    diffusion2d_stage(sub(A, xs, xe), sub(uin, xs, xe), sub(B, xs, xe), j0=lo2, j1=hi2,
+                      a=0.75, b=0.25, **kw)
+    oxs, oxe = max(xo0, xs), min(xo1, xe)
+    if oxe <= oxs:
+        return
+    kw.update(nx=oxe - oxs + 2 * R)
+    diffusion2d_stage(sub(B, oxs, oxe), sub(uin, oxs, oxe), sub(uout, oxs, oxe), j0=j0, j1=j1,
+                      a=1.0 / 3.0, b=2.0 / 3.0, **kw)
+
+
 def diffusion2d_step(uin, uout, nx, j0, j1, ylo, yhi, border, order, cx, cy, dt):
     """2-D counterpart of diffusion3d_step (semantics of advdiff_diffusion2d_step)."""
     R = order // 2

@@ -95,44 +95,58 @@ def diffusion3d_stage(inp, u0, out, *, nx, ny, k0, k1, border, order, cx, cy, cz
                               ls)
 
 
+def _int_array(vals):
+    import ctypes
+    return (ctypes.c_int * len(vals))(*[int(v) for v in vals])
+
+
 def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy, cz, dt,
-                     stream=None, k0b=0, k1b=0):
+                     stream=None, k0b=0, k1b=0, box=None):
     """A FULL SSP-RK3 step in one launch (temporal blocking): uout[k0:k1] = RK3(uin), and
-    uout[k0b:k1b] too when a second range is given (one launch for both)."""
+    uout[k0b:k1b] too when a second range is given (one launch for both).
+    box = (xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1): explicit active / output x-y bounds
+    (Cartesian blocks launched on a view); default from `border`."""
     _check_layout(uin, uout)
     if uin.data_ptr() == uout.data_ptr():
         raise ValueError("the fused step needs distinct input/output buffers")
+    if box is None:
+        box = (border, nx - border, border, ny - border, 0, nx, 0, ny)
     if _native(uin):
         lib = _lib.require()
         nz = uin.shape[0]
         assert 0 <= k0 and k1 <= nz and 0 <= zlo and zhi <= nz and 0 <= k0b and k1b <= nz
-        code = lib.advdiff_diffusion3d_step2(
+        assert nx <= uin.shape[2] and ny <= uin.shape[1]
+        code = lib.advdiff_diffusion3d_step_box(
             _dtype_code(uin), _ptr(uin), _ptr(uout), nx, ny, uin.stride(1), uin.stride(0), nz,
-            k0, k1, k0b, k1b, zlo, zhi, border, order, cx, cy, cz, dt, _stream_ptr(stream))
+            k0, k1, k0b, k1b, zlo, zhi, _int_array(box), order, cx, cy, cz, dt,
+            _stream_ptr(stream))
         _lib.check(code, "diffusion3d_step")
     else:
         for a, b in ((k0, k1), (k0b, k1b)):
             if b > a:
-                ref.diffusion3d_step(uin, uout, nx, ny, a, b, zlo, zhi, border, order, cx, cy,
-                                     cz, dt)
+                ref.diffusion3d_step_box(uin, uout, nx, ny, a, b, zlo, zhi, box, order, cx, cy,
+                                         cz, dt)
 
 
 def diffusion2d_step(uin, uout, *, nx, j0, j1, ylo, yhi, border, order, cx, cy, dt,
-                     stream=None):
-    """A FULL 2-D SSP-RK3 step in one launch: uout[j0:j1] = RK3(uin) (rows)."""
+                     stream=None, box=None):
+    """A FULL 2-D SSP-RK3 step in one launch: uout[j0:j1] = RK3(uin) (rows).
+    box = (xa0, xa1, xo0, xo1): explicit active / output columns (Cartesian blocks)."""
     _check_layout(uin, uout)
     if uin.data_ptr() == uout.data_ptr():
         raise ValueError("the fused step needs distinct input/output buffers")
+    if box is None:
+        box = (border, nx - border, 0, nx)
     if _native(uin):
         lib = _lib.require()
         ny = uin.shape[0]
-        assert 0 <= j0 and j1 <= ny and 0 <= ylo and yhi <= ny
-        code = lib.advdiff_diffusion2d_step(
+        assert 0 <= j0 and j1 <= ny and 0 <= ylo and yhi <= ny and nx <= uin.shape[1]
+        code = lib.advdiff_diffusion2d_step_box(
             _dtype_code(uin), _ptr(uin), _ptr(uout), nx, uin.stride(0), ny, j0, j1, ylo, yhi,
-            border, order, cx, cy, dt, _stream_ptr(stream))
+            _int_array(box), order, cx, cy, dt, _stream_ptr(stream))
         _lib.check(code, "diffusion2d_step")
     else:
-        ref.diffusion2d_step(uin, uout, nx, j0, j1, ylo, yhi, border, order, cx, cy, dt)
+        ref.diffusion2d_step_box(uin, uout, nx, j0, j1, ylo, yhi, box, order, cx, cy, dt)
 
 
 def diffusion2d_stage(inp, u0, out, *, nx, j0, j1, border, order, cx, cy, dt, a, b,

@@ -139,42 +139,58 @@ class SlabHalo:
 
 
 class CartesianHalo:
-    """Face-ghost exchange for a 2-D/3-D process grid (``CartesianDecomposition``).
+    """Ghost exchange for a 2-D/3-D process grid (``CartesianDecomposition``).
 
-    Per split axis and side one message of G layers over the owned extent of the other
-    axes (edges/corners are not needed by star stencils).  Axis-0 faces are whole planes
-    (contiguous: RCCL reads/writes the field directly, like the slab path); other faces
-    are strided and go through pack/unpack with the native ``advdiff_copy_box`` kernel on
-    the comm stream.  All messages of a rank form ONE grouped RCCL call.  Reference: none
-    (the reference only splits z).
+    faces (default, star stencils applied once per exchange): per split axis and side one
+    message of G layers over the owned extent of the other axes; all messages of a rank
+    form ONE grouped RCCL call.
+    corners=True (the fused full-step kernel: three stacked star stencils reach diagonal
+    neighbours): axis by axis, fastest first (x, then y, then z); each phase's message
+    spans the FULL allocated extent of the axes already exchanged, so edge and corner
+    ghosts arrive with the faces — three dependent phases, ordered on the comm stream
+    (no host blocking).
+    Axis-0 messages with full x/y extent are whole planes (contiguous, zero-copy); other
+    messages are strided and go through pack/unpack with the native ``advdiff_copy_box``
+    kernel on the comm stream.  Reference: none (the reference only splits z, §2.5).
     """
 
-    def __init__(self, comm, decomp, comm_stream=None):
+    def __init__(self, comm, decomp, comm_stream=None, corners: bool = False):
         self.comm = comm
         self.cd = decomp
         self.comm_stream = comm_stream
+        self.corners = corners
         self._bufs = {}
 
-    def _regions(self, field):
-        """[(peer, send_view, recv_view, key)] in a fixed order."""
+    def _phases(self):
+        """Axis groups exchanged together: all at once (faces) or fastest axis first."""
+        split = [a for a in range(self.cd.dims) if self.cd.pgrid[a] > 1]
+        return [sorted(split, reverse=True)] if not self.corners else \
+            [[a] for a in sorted(split, reverse=True)]
+
+    def _regions(self, field, axes):
+        """[(peer, send_view, recv_view, key)] for the given axes, fixed order."""
         cd = self.cd
         own = cd.owned_box()
         out = []
-        for a in range(cd.dims):
+        for a in axes:
             ax = cd.axis(a)
             for side, peer in ((-1, cd.neighbor(a, -1)), (1, cd.neighbor(a, 1))):
                 if peer is None:
                     continue
                 s = ax.send_lower() if side < 0 else ax.send_upper()
                 r = ax.recv_lower() if side < 0 else ax.recv_upper()
-                if a == 0:
-                    sv, rv = field[s[0]:s[1]], field[r[0]:r[1]]
-                else:
-                    sl_s = [slice(lo, hi) for lo, hi in own]
-                    sl_r = list(sl_s)
-                    sl_s[a] = slice(*s)
-                    sl_r[a] = slice(*r)
-                    sv, rv = field[tuple(sl_s)], field[tuple(sl_r)]
+                sl_s = []
+                for b, (lo, hi) in enumerate(own):
+                    if b == a:
+                        sl_s.append(None)
+                    elif self.corners and b > a:  # already exchanged: carry its ghosts
+                        sl_s.append(slice(0, cd.axis(b).alloc))
+                    else:
+                        sl_s.append(slice(lo, hi))
+                sl_r = list(sl_s)
+                sl_s[a] = slice(*s)
+                sl_r[a] = slice(*r)
+                sv, rv = field[tuple(sl_s)], field[tuple(sl_r)]
                 out.append((peer, sv, rv, (a, side)))
         return out
 
@@ -195,10 +211,10 @@ class CartesianHalo:
         else:
             dst.copy_(src)
 
-    def _plan(self, field):
-        """Contiguous send/recv tensors + the unpack list."""
+    def _plan(self, field, axes):
+        """Contiguous send/recv tensors + the unpack list of one phase."""
         sends, recvs, unpack = [], [], []
-        for peer, sv, rv, key in self._regions(field):
+        for peer, sv, rv, key in self._regions(field, axes):
             if sv.is_contiguous():
                 st = sv
             else:
@@ -213,21 +229,25 @@ class CartesianHalo:
             recvs.append((peer, rt))
         return sends, recvs, unpack
 
+    @staticmethod
+    def _ops(sends, recvs):
+        ops = [dist.P2POp(dist.isend, t, p) for p, t in sends]
+        ops += [dist.P2POp(dist.irecv, t, p) for p, t in recvs]
+        return ops
+
     def start(self, field: torch.Tensor, after_event=None) -> PendingExchange | None:
         if self.comm.size == 1:
             return None
-        if not field.is_cuda:
-            sends, recvs, unpack = self._plan(field)
-            ops = [dist.P2POp(dist.isend, t, p) for p, t in sends]
-            ops += [dist.P2POp(dist.irecv, t, p) for p, t in recvs]
-            if not ops:
-                return None
-            works = dist.batch_isend_irecv(ops)
-
-            def finish_cpu():
+        phases = self._phases()
+        if not field.is_cuda:  # gloo on the CPU: phases run to completion here
+            for axes in phases:
+                sends, recvs, unpack = self._plan(field, axes)
+                ops = self._ops(sends, recvs)
+                for w in (dist.batch_isend_irecv(ops) if ops else []):
+                    w.wait()
                 for dst, src in unpack:
                     dst.copy_(src)
-            return PendingExchange(works, None, finish_cpu)
+            return None
         cur = torch.cuda.current_stream()
         cs = self.comm_stream or cur
         if after_event is None:
@@ -236,32 +256,31 @@ class CartesianHalo:
         cs.wait_event(after_event)
         if self.comm.backend != "nccl":
             # device tensors over gloo (one-GPU multi-process tests): host-staged, blocking
-            with torch.cuda.stream(cs):
-                sends, recvs, unpack = self._plan(field)
-                hs = [(p, t.cpu()) for p, t in sends]
-                hr = [(p, torch.empty(t.shape, dtype=t.dtype)) for p, t in recvs]
-            ops = [dist.P2POp(dist.isend, t, p) for p, t in hs]
-            ops += [dist.P2POp(dist.irecv, t, p) for p, t in hr]
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
-            with torch.cuda.stream(cs):
-                for (_, dev), (_, host) in zip(recvs, hr):
-                    dev.copy_(host)
-                for dst, src in unpack:
-                    self._copy(dst, src)
-                done = torch.cuda.Event()
-                done.record(cs)
-            cs.synchronize()
+            for axes in phases:
+                with torch.cuda.stream(cs):
+                    sends, recvs, unpack = self._plan(field, axes)
+                    hs = [(p, t.cpu()) for p, t in sends]
+                    hr = [(p, torch.empty(t.shape, dtype=t.dtype)) for p, t in recvs]
+                ops = self._ops(hs, hr)
+                for w in (dist.batch_isend_irecv(ops) if ops else []):
+                    w.wait()
+                with torch.cuda.stream(cs):
+                    for (_, dev), (_, host) in zip(recvs, hr):
+                        dev.copy_(host)
+                    for dst, src in unpack:
+                        self._copy(dst, src)
+                cs.synchronize()
+            done = torch.cuda.Event()
+            done.record(cs)
             return PendingExchange([], cs, lambda: torch.cuda.current_stream().wait_event(done))
         with torch.cuda.stream(cs):
-            sends, recvs, unpack = self._plan(field)
-            ops = [dist.P2POp(dist.isend, t, p) for p, t in sends]
-            ops += [dist.P2POp(dist.irecv, t, p) for p, t in recvs]
-            works = dist.batch_isend_irecv(ops) if ops else []
-            for w in works:
-                w.wait()  # comm stream waits for RCCL (no host block)
-            for dst, src in unpack:
-                self._copy(dst, src)
+            for axes in phases:  # stream-ordered phases: pack -> RCCL -> unpack
+                sends, recvs, unpack = self._plan(field, axes)
+                ops = self._ops(sends, recvs)
+                for w in (dist.batch_isend_irecv(ops) if ops else []):
+                    w.wait()  # comm stream waits for RCCL (no host block)
+                for dst, src in unpack:
+                    self._copy(dst, src)
             done = torch.cuda.Event()
             done.record(cs)
         return PendingExchange([], cs, lambda: torch.cuda.current_stream().wait_event(done))

@@ -96,9 +96,9 @@ class Solver:
         self.pgrid = parse_proc_grid(decomp, comm.size, ashape, model.radius)
         self.cart = any(p > 1 for p in self.pgrid[1:])
         self.fused = model.supports_fused if fused is None else (fused and model.supports_fused)
-        if self.fused and (self.cart or integrator != "ssprk3"
-                           or grid.n_decomposed // comm.size < 3 * model.radius):
-            self.fused = False  # x/y split, LSRK, or slabs thinner than the wide halo
+        thin = any(n // p < 3 * model.radius for n, p in zip(ashape, self.pgrid) if p > 1)
+        if self.fused and (integrator != "ssprk3" or thin):
+            self.fused = False  # LSRK, or blocks thinner than the wide (3R) halo
         G = 3 * model.radius if self.fused else model.radius
         self.ghost = G
         self.cd = CartesianDecomposition(ashape, self.pgrid, comm.rank, G)
@@ -126,7 +126,8 @@ class Solver:
             lo, hi = torch.cuda.Stream.priority_range()
             self.comm_stream = torch.cuda.Stream(device=self.device, priority=hi)
         if self.cart:
-            self.halo = CartesianHalo(comm, self.cd, self.comm_stream)
+            # the fused step stacks three star stencils: it needs edge/corner ghosts too
+            self.halo = CartesianHalo(comm, self.cd, self.comm_stream, corners=self.fused)
             self.full = self.cd.compute_box(model.border)
             self.interior, self.boundary = self.cd.split_boxes(model.border, G)
         else:
@@ -264,12 +265,46 @@ class Solver:
             self._pending[id(out)] = self.halo.start(out)
 
     def _launch_fused(self, rng, dt, rng2=(0, 0)):
+        if self.cart:  # boundary boxes are launched one by one by the caller
+            self._launch_fused_box(rng, dt)
+            return
         (lo, hi), (lo2, hi2) = rng, rng2
         if hi > lo or hi2 > lo2:
             self.model.step(self.u, self.un, lo, hi, self.zact[0], self.zact[1], dt, lo2=lo2,
                             hi2=hi2)
             trace.sync_check(f"{self.model.name} fused step [{lo},{hi}) [{lo2},{hi2})",
                              self.device)
+
+    def _fused_view(self, a: int, lo: int, hi: int):
+        """View window, active and output bounds (view coordinates) along array axis a for
+        a fused launch on local cells [lo, hi): the window reaches 3R beyond the box
+        (ghosts on split axes), the active range is the global interior."""
+        cd, R3 = self.cd, 3 * self.model.radius
+        ax = cd.axis(a)
+        v0, v1 = max(0, lo - R3), min(ax.alloc, hi + R3)
+        origin = ax.start - ax.ghost + v0  # global index of view cell 0
+        B, N = self.model.border, cd.shape[a]
+        return (v0, v1), (max(0, B - origin), min(v1 - v0, N - B - origin)), (lo - v0, hi - v0)
+
+    def _launch_fused_box(self, box, dt):
+        """Fused step of a Cartesian block box (array order) on a kernel VIEW."""
+        if any(hi <= lo for lo, hi in box):
+            return
+        if self.grid.dims == 3:
+            (z0, z1), (y0, y1), (x0, x1) = box
+            (vy0, vy1), (ya0, ya1), (yo0, yo1) = self._fused_view(1, y0, y1)
+            (vx0, vx1), (xa0, xa1), (xo0, xo1) = self._fused_view(2, x0, x1)
+            sl = (slice(None), slice(vy0, vy1), slice(vx0, vx1))
+            self.model.step(self.u[sl], self.un[sl], z0, z1, self.zact[0], self.zact[1], dt,
+                            nx=vx1 - vx0, ny=vy1 - vy0,
+                            box=(xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1))
+        else:
+            (y0, y1), (x0, x1) = box
+            (vx0, vx1), (xa0, xa1), (xo0, xo1) = self._fused_view(1, x0, x1)
+            sl = (slice(None), slice(vx0, vx1))
+            self.model.step(self.u[sl], self.un[sl], y0, y1, self.zact[0], self.zact[1], dt,
+                            nx=vx1 - vx0, box=(xa0, xa1, xo0, xo1))
+        trace.sync_check(f"{self.model.name} fused step box {box}", self.device)
 
     def _step_fused(self, dt: float) -> None:
         pend = self._pending.pop(id(self.u), None)
@@ -282,7 +317,11 @@ class Solver:
                 if pend is not None:
                     pend.wait()
             with trace.range_("boundary"):  # both boundary slabs in ONE launch
-                self._launch_fused(self.boundary[0], dt, self.boundary[1])
+                if self.cart:
+                    for box in self.boundary:
+                        self._launch_fused_box(box, dt)
+                else:
+                    self._launch_fused(self.boundary[0], dt, self.boundary[1])
         else:
             if pend is not None:
                 pend.wait()

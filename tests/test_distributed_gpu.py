@@ -112,3 +112,15 @@ def _nccl_world1(_comm):
 
 def test_rccl_init_options_world1():
     assert spawn_local(1, _nccl_world1, device="cuda", backend="gloo")[0]
+
+
+@pytest.mark.parametrize("kind,world,decomp", [("diff3", 4, (1, 2, 2)), ("diff2", 4, (2, 2))])
+def test_gpu_cartesian_fused_bitwise(kind, world, decomp, monkeypatch):
+    """Fused full-step kernel on Cartesian blocks (3R ghosts incl. edges/corners)."""
+    monkeypatch.setenv("ADVDIFF_SHARE_GPU", "1")
+    model, grid, ic = _make(kind)
+    s = Solver(model, grid, dtype=torch.float64, device="cuda", ic=ic)
+    s.run(iters=5)
+    ref_g = s.gather()
+    out = spawn_local(world, _run_cart, kind, 5, decomp, device="cuda", backend="gloo")[0]
+    assert np.array_equal(out, ref_g), np.abs(out - ref_g).max()

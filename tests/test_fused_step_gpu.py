@@ -92,3 +92,23 @@ def test_fused_step_2d_bitwise_equals_per_stage(dtype, order, case):
                              order=order, cx=c[0], cy=c[1], dt=dt)
     torch.cuda.synchronize()
     assert torch.equal(got, exp), (got - exp).abs().max().item()
+
+
+def test_fused_step_box_bounds_match_reference():
+    """Explicit active/output boxes (Cartesian views) vs the CPU reference."""
+    nz, ny, nx = 40, 44, 70
+    g = torch.Generator().manual_seed(3)
+    u = torch.rand((nz, ny, nx), generator=g, dtype=torch.float64).cuda()
+    c = (0.21, 0.17, 0.13)
+    dt = 0.5 / sum(c)
+    for box in ((2, 68, 2, 42, 0, 70, 0, 44),      # slab-like
+                (0, 70, 0, 44, 6, 64, 6, 38),      # interior block: everything active
+                (0, 63, 4, 44, 6, 60, 9, 38)):     # global edge on the high x side
+        got = u.clone()
+        stencil.diffusion3d_step(u, got, nx=nx, ny=ny, k0=6, k1=34, zlo=0, zhi=nz, border=2,
+                                 order=4, cx=c[0], cy=c[1], cz=c[2], dt=dt, box=box)
+        cpu = u.cpu()
+        out = cpu.clone()
+        ref.diffusion3d_step_box(cpu, out, nx, ny, 6, 34, 0, nz, box, 4, *c, dt)
+        torch.cuda.synchronize()
+        assert (got.cpu() - out).abs().max().item() < 1e-12, box
