@@ -75,5 +75,37 @@ def main():
     print(json.dumps(res))
 
 
+
+
+def cartesian(pgrid=(4, 2, 1), n=1024, reps=10, rank=None):
+    """Same measurement for one block of a Cartesian 8-GPU decomposition of n^3 (fused
+    kernel on views, 3R ghosts on split axes): full block launch vs interior + boundary
+    boxes.  No communication (a stand-in Comm with the block's rank)."""
+    from multigpu_advectiondiffusion_amd import Diffusion, Grid, Solver
+    from multigpu_advectiondiffusion_amd.parallel.comm import Comm
+    size = pgrid[0] * pgrid[1] * pgrid[2]
+    rank = size // 2 if rank is None else rank  # an interior-ish block
+    comm = Comm(rank=rank, size=size, device="cuda:0")
+    s = Solver(Diffusion(K=1.0, order=4), Grid((n, n, n), (1.0, 1.0, 1.0)), comm,
+               dtype=torch.float64, ic="sine", decomp=pgrid)
+    assert s.cart and s.fused
+    dt = s.model.stable_dt()
+    res = {"pgrid": list(pgrid), "block": [c for _, c in s.cd.global_box()],
+           "boundary_boxes": len(s.boundary)}
+    res["full_us"] = round(timeit(lambda: s._launch_fused_box(s.full, dt), reps), 1)
+    res["interior_us"] = round(timeit(lambda: s._launch_fused_box(s.interior, dt), reps), 1)
+
+    def bnd():
+        for b in s.boundary:
+            s._launch_fused_box(b, dt)
+    res["boundary_us"] = round(timeit(bnd, reps), 1)
+    res["overhead_pct"] = round(100 * ((res["interior_us"] + res["boundary_us"]) / res["full_us"] - 1), 1)
+    print(json.dumps(res))
+
+
 if __name__ == "__main__":
-    main()
+    if "--cart" in sys.argv:
+        for pg in ((4, 2, 1), (2, 2, 2), (2, 4, 1)):
+            cartesian(pg)
+    else:
+        main()
