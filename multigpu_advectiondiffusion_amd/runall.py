@@ -29,6 +29,11 @@ CANONICAL = [
      ["--weno", "js", "--viscosity", "0"]),
     ("MG Diffusion2d", "diffusion2d", [1.0, 2.0, 2.0, 400, 400, 1000], ["--ic", "disc", "--safety", "0.8"]),
     ("MG Burgers2d", "burgers2d", [0.40, 0.40, 2.0, 2.0, 400, 400], ["--weno", "js", "--viscosity", "0"]),
+    # Matlab_Prototipes/InviscidBurgersNd/LFWENO7FDM{2,3}d.m: WENO7 + LSRK4(5), dt from max|u|
+    ("MP Burgers2d WENO7", "burgers2d", [0.40, 0.40, 2.0, 2.0, 400, 400],
+     ["--weno", "js7", "--integrator", "lsrk45", "--cfl-mode", "adaptive", "--viscosity", "0"]),
+    ("MP Burgers3d WENO7", "burgers3d", [0.20, 0.40, 2.0, 2.0, 2.0, 160, 160, 160],
+     ["--weno", "js7", "--integrator", "lsrk45", "--cfl-mode", "adaptive", "--viscosity", "0"]),
 ]
 
 
