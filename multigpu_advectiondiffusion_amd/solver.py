@@ -571,7 +571,8 @@ class Solver:
         # LSRK stage: read u, du; write du, u (stage 1 skips the du read)
         bpc = 5 * 32.0 - 8.0 if self.du is not None else self.model.bytes_per_cell_step
         bw = bpc * cells * stats.steps / max(stats.compute_s, 1e-30)
-        ex = {"MLUPS (cells x RK3 steps / s)": f"{ml:.1f}",
+        ex = {("MLUPS (cells x RK steps / s)" if self.du is not None
+               else "MLUPS (cells x RK3 steps / s)"): f"{ml:.1f}",
               "Stage-MLUPS": f"{(5 if self.du is not None else 3) * ml:.1f}",
               "Effective HBM bandwidth (GB/s, est.)": f"{bw / 1e9:.1f}",
               "Processes / devices": f"{self.comm.size} x {self.device.type}"}
@@ -580,6 +581,7 @@ class Solver:
         opt = "Fused LDS z-march + RK3 (gfx950)" if self.device.type == "cuda" else "PyTorch CPU"
         if style == "multigpu":
             return metrics.summary_multigpu(self.model.title, opt, stats.compute_s, stats.htod_s,
-                                            stats.dtoh_s, gf, stats.steps, g.shape, ex)
+                                            stats.dtoh_s, gf, stats.steps, g.shape, ex,
+                                            stages=5 if self.du is not None else 3)
         return metrics.summary_singlegpu(self.model.title, opt, stats.compute_s, gf, stats.steps,
                                          g.shape, stats.t, ex)

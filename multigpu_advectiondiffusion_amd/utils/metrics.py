@@ -28,7 +28,8 @@ def mlups(seconds: float, steps: int, cells: int) -> float:
 
 
 def summary_multigpu(title: str, optimization: str, compute_s: float, htod_s: float,
-                     dtoh_s: float, gflops: float, iterations: int, grid, extra=None) -> str:
+                     dtoh_s: float, gflops: float, iterations: int, grid, extra=None,
+                     stages: int = 3) -> str:
     nx, ny = grid[0], grid[1]
     lines = [f"======================={title}=====================",
              f"Optimization                                 :  {optimization}",
@@ -42,7 +43,7 @@ def summary_multigpu(title: str, optimization: str, compute_s: float, htod_s: fl
         lines.append(f"3D Grid Size                                 :  {nx} x {ny} x {grid[2]}")
     else:
         lines.append(f"2D Grid Size                                 :  {nx} x {ny}")
-    lines.append(f"Iterations                                   :  {iterations} x 3 RK steps")
+    lines.append(f"Iterations                                   :  {iterations} x {stages} RK steps")
     lines.append(SEP)
     for k, v in (extra or {}).items():
         lines.append(f"{k:<45}:  {v}")
