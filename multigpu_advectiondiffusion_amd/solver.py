@@ -1,5 +1,6 @@
-"""The time-stepping engine: device-resident slabs, SSP-RK3 with fused stage kernels,
-halo exchange overlapped with interior compute.
+"""The time-stepping engine: device-resident blocks, SSP-RK3 (or low-storage RK4(5)) with
+fused stage kernels — or ONE temporally blocked launch per step for the heat equation —
+and halo exchange overlapped with interior compute.
 
 Reference call stack being replaced (`MultiGPU/Diffusion3d_Baseline/main.c:30-385`):
 host builds the global array on every rank -> host scatter -> HtD -> per step: memcpy
@@ -7,14 +8,17 @@ uo <- u, 3 x {boundary Laplacian on 2 send streams, pack, D2H, host-blocking
 stream sync, MPI_Isend; interior Laplacian; MPI_Irecv/Wait; H2D; unpack; RK kernel;
 cudaDeviceSynchronize} -> DtH -> host gather.
 
-Here, per stage (three per step, buffers u -> A -> B -> u, no Lu array, no uo copy):
+Here, per exchange (per stage: buffers u -> A -> B -> u, no Lu array, no uo copy; or per
+step in the fused path: u <-> u' with 3R ghosts):
 
     compute stream : [interior(in -> out)] --wait(halo of in)--> [boundary(in -> out)] --event-->
     comm stream    :                                   grouped RCCL send/recv of out's ghosts
-                                                       (overlaps the NEXT stage's interior)
+                                                       (overlaps the NEXT interior)
 
-The host never blocks inside a step; the only host/device syncs are the optional
-adaptive-CFL reduction and the timers around ``run``.
+Decompositions: z-slabs (default) or 2-D/3-D Cartesian blocks (boxes launched on kernel
+views).  The host never blocks inside a step; the only host/device syncs are the
+optional adaptive-CFL reduction and the timers around ``run``.  Single-process runs
+replay the step loop as hipGraphs.
 """
 from __future__ import annotations
 
