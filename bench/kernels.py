@@ -66,6 +66,10 @@ def main():
         res[f"diffusion3d_fd{order}_fused_step_us"] = round(tf * 1e6, 1)
         res[f"diffusion3d_fd{order}_fused_step_mlups"] = round(cells / tf / 1e6, 1)
         res[f"diffusion3d_fd{order}_fused_TBps_eff"] = round(2 * es * cells / tf / 1e12, 2)
+        # exclusive launch: one round of persistent groups (single-rank production path)
+        tp, _ = timeit(lambda: stencil.diffusion3d_step(u, A, exclusive=True, **kw), args.reps)
+        res[f"diffusion3d_fd{order}_fused_persist_us"] = round(tp * 1e6, 1)
+        res[f"diffusion3d_fd{order}_fused_persist_mlups"] = round(cells / tp / 1e6, 1)
     # copy roofline for reference: B <- A (16 B/cell)
     tc, _ = timeit(lambda: B.copy_(A), args.reps)
     res["copy_TBps"] = round(2 * es * cells / tc / 1e12, 2)

@@ -66,6 +66,20 @@ int advdiff_diffusion3d_step_box(int dtype, const void* uin, void* uout, int nx,
                                  int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int k0b,
                                  int k1b, int zlo, int zhi, const int* box, int order,
                                  double cx, double cy, double cz, double dt, void* stream);
+// Launch-policy flags of the _ex entry.
+//   ADVDIFF_EXCLUSIVE: the launch has the GPU to itself (single rank, or a full-range
+//   launch after the halo wait): the fused step then runs as ONE round of persistent
+//   workgroups (CUs x occupancy), each marching an equal contiguous share of the
+//   linearised (tile, plane) space — no round quantisation, ~2 z warm-ups per group
+//   instead of one per chunk.  Without it (an interior launch that overlaps RCCL copy
+//   kernels, which may hold CUs for the whole launch) the grid of z chunks keeps the
+//   dispatcher's dynamic load balancing.  Placement only: results are bit-identical.
+#define ADVDIFF_EXCLUSIVE 1
+int advdiff_diffusion3d_step_box_ex(int dtype, const void* uin, void* uout, int nx, int ny,
+                                    int64_t sy, int64_t sz, int nz_alloc, int k0, int k1,
+                                    int k0b, int k1b, int zlo, int zhi, const int* box,
+                                    int order, double cx, double cy, double cz, double dt,
+                                    int flags, void* stream);
 // 2-D heat: ONE FULL SSP-RK3 step per launch on rows [j0, j1) (intermediate stages on
 // the active rows [ylo, yhi)); reads rows j0-3R .. j1+3R-1 (clamped to [0, ny_alloc)).
 // Wave-independent y-march, no LDS; bit-identical to three advdiff_diffusion2d_stage.

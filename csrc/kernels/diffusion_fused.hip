@@ -36,12 +36,30 @@ struct Box2 {
   int xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1;
 };
 
+// Work split of a launch.
+//   Grid mode (persistent = 0): blockIdx -> (x tile, y tile, z chunk of `zchunk` planes;
+//   chunks z >= gza belong to the second plane range), as many rounds of resident groups
+//   as the grid needs — the dispatcher balances the load dynamically.
+//   Persistent mode (compact-ring kernel, PERSIST = true): a 1-D grid of G = CUs x
+//   occupancy groups; the (tile, plane) space is linearised tile-major (tile index
+//   t = ty gx + tx, then the planes of range 1 followed by those of range 2), L = tiles x
+//   planes, and group g marches an equal share of it (per or per + 1 planes) as 1-3 z
+//   segments (a segment ends at a tile or range boundary and pays the 4R-plane warm-up
+//   again).  512³: 220 tiles x 512 planes = 440 planes per group + ~2 warm-ups, against
+//   7 rounds x (64 + 8) planes in grid mode.
+struct StepSched {
+  int gx, gy;       // tiles along x / y
+  int gza, zchunk;  // grid mode
+  int per, rem;     // persistent mode: L = per G + rem
+};
+
 template <typename T, int ORDER, int NW, int RPW>
 __global__ __launch_bounds__(64 * NW) void diffusion3d_step_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
-    int nz_alloc, int k0, int k1, int k0b, int k1b, int gza, int zlo, int zhi, int zchunk,
+    int nz_alloc, int k0, int k1, int k0b, int k1b, StepSched sc, int zlo, int zhi,
     Box2 bx, T cx, T cy, T cz,
     T dt) {
+  const int gza = sc.gza, zchunk = sc.zchunk;
   constexpr int R = FD<ORDER>::R;
   constexpr int W = 64;             // stage-1 columns (one wave)
   constexpr int TX = W - 4 * R;     // output columns
@@ -242,9 +260,10 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_kernel(
 template <typename T, int ORDER, int NW, int RPW, int PD, int XDPP>
 __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
-    int nz_alloc, int k0, int k1, int k0b, int k1b, int gza, int zlo, int zhi, int zchunk,
+    int nz_alloc, int k0, int k1, int k0b, int k1b, StepSched sc, int zlo, int zhi,
     Box2 bx, T cx, T cy, T cz,
     T dt) {
+  const int gza = sc.gza, zchunk = sc.zchunk;
   constexpr int R = FD<ORDER>::R;
   constexpr int W = 64;
   constexpr int TX = W - 4 * R;
@@ -483,12 +502,24 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
 // A(k..k+2R), B(k-R..k+R)) and the march is unrolled NR times; u(k..k+R-1), still needed
 // as the u^n term of stage 3, move to a short delay line when their ring slot is reused.
 // 17 instead of 24 window values per row (R = 2) leave room for the stage-1 DPP path.
+template <int ORDER, int NW, int RPW>
+struct CringGeom {
+  static constexpr int R = FD<ORDER>::R;
+  static constexpr int W = 64;
+  static constexpr int TX = W - 4 * R;
+  static constexpr int S1R = NW * RPW;
+  static constexpr int TY = S1R - 4 * R;
+  static constexpr int UW = W + 2 * R, UH = S1R + 2 * R;
+  static constexpr int LDS_U = UH * UW, LDS_AB = S1R * W;  // per buffer set
+};
+
+// One z segment [kc0, kc1) of output tile (tx, ty): warm-up + march (the whole
+// algorithm; sU/sA/sB are the workgroup's double-buffered LDS planes).
 template <typename T, int ORDER, int NW, int RPW, int XDPP, int PD>
-__global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
-    const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
-    int nz_alloc, int k0, int k1, int k0b, int k1b, int gza, int zlo, int zhi, int zchunk,
-    Box2 bx, T cx, T cy, T cz,
-    T dt) {
+__device__ __forceinline__ void cring_march(
+    T* sU, T* sA, T* sB, int tx, int ty, int kc0, int kc1, const T* __restrict__ uin,
+    T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz, int nz_alloc, int zlo,
+    int zhi, const Box2& bx, T cx, T cy, T cz, T dt) {
   constexpr int R = FD<ORDER>::R;
   constexpr int NR = 2 * R + 1;
   constexpr int W = 64;
@@ -501,18 +532,9 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
   constexpr int NH = (NHALO + NT - 1) / NT;
   static_assert(TY > 0, "tile too small");
 
-  __shared__ T sU[2][UH * UW];
-  __shared__ T sA[2][S1R * W];
-  __shared__ T sB[2][S1R * W];
-
   const int lane = threadIdx.x, w = threadIdx.y, tid = w * 64 + lane;
-  const Tile3 tile = xcd_tile();
-  const int i0 = tile.x * TX, j0 = tile.y * TY;
+  const int i0 = tx * TX, j0 = ty * TY;
   const int x = i0 - 2 * R + lane;
-  // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
-  const bool second = (int)tile.z >= gza;
-  const int kc0 = second ? k0b + ((int)tile.z - gza) * zchunk : k0 + tile.z * zchunk;
-  const int kc1 = min(kc0 + zchunk, second ? k1b : k1);
   const bool xin = x >= bx.xa0 && x < bx.xa1;   // non-frozen columns
   const bool xout = x >= bx.xo0 && x < bx.xo1;  // columns this launch writes
   const bool s2c = lane >= R && lane < W - R;
@@ -588,9 +610,9 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
     auto sl = [](int d) { return (PH + d + 4 * NR) % NR; };  // slot of plane k+d
     constexpr int UIN = (PH + 3 * R) % NR;                    // u(k+3R) replaces u(k+R-1)
     const int set = k & 1;
-    T* pU = sU[set];
-    T* pA = sA[set];
-    T* pB = sB[set];
+    T* pU = sU + set * (UH * UW);
+    T* pA = sA + set * (S1R * W);
+    T* pB = sB + set * (S1R * W);
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
       dl[q][R - 1] = ru[q][UIN];  // u(k+R-1) -> delay line
@@ -748,6 +770,46 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
   }
 }
 
+template <typename T, int ORDER, int NW, int RPW, int XDPP, int PD, bool PERSIST>
+__global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
+    const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
+    int nz_alloc, int k0, int k1, int k0b, int k1b, StepSched sc, int zlo, int zhi,
+    Box2 bx, T cx, T cy, T cz, T dt) {
+  using Gm = CringGeom<ORDER, NW, RPW>;
+  __shared__ T sU[2 * Gm::LDS_U];
+  __shared__ T sA[2 * Gm::LDS_AB];
+  __shared__ T sB[2 * Gm::LDS_AB];
+  const Tile3 tile = xcd_tile();
+  if constexpr (!PERSIST) {
+    // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
+    const bool second = tile.z >= sc.gza;
+    const int kc0 = second ? k0b + (tile.z - sc.gza) * sc.zchunk : k0 + tile.z * sc.zchunk;
+    const int kc1 = min(kc0 + sc.zchunk, second ? k1b : k1);
+    cring_march<T, ORDER, NW, RPW, XDPP, PD>(sU, sA, sB, tile.x, tile.y, kc0, kc1, uin, uout,
+                                             nx, ny, sy, sz, nz_alloc, zlo, zhi, bx, cx, cy,
+                                             cz, dt);
+  } else {
+    // 1-D grid; tile.x = this group's XCD-contiguous logical id, so the groups of one XCD
+    // march neighbouring tiles.  Group g owns the linear planes [s, e), s = g per +
+    // min(g, rem) (32-bit: the host keeps L < 2^31).  Wave-uniform (scalar) loop.
+    const int g = tile.x;
+    const int na = k1 - k0, P = na + (k1b - k0b);
+    int s = g * sc.per + min(g, sc.rem);
+    const int e = s + sc.per + (g < sc.rem ? 1 : 0);
+    while (s < e) {
+      const int t = s / P, p0 = s - t * P;
+      int p1 = min(P, e - t * P);
+      if (p0 < na) p1 = min(p1, na);  // a segment never spans both plane ranges
+      const int kc0 = p0 < na ? k0 + p0 : k0b + (p0 - na);
+      __syncthreads();  // nobody still reads the previous segment's last LDS planes
+      cring_march<T, ORDER, NW, RPW, XDPP, PD>(sU, sA, sB, t % sc.gx, t / sc.gx, kc0,
+                                               kc0 + (p1 - p0), uin, uout, nx, ny, sy, sz,
+                                               nz_alloc, zlo, zhi, bx, cx, cy, cz, dt);
+      s += p1 - p0;
+    }
+  }
+}
+
 struct SArgs {
   const void* uin;
   void* uout;
@@ -759,6 +821,7 @@ struct SArgs {
   Box2 bx;
   double cx, cy, cz, dt;
   hipStream_t st;
+  int flags;  // ADVDIFF_EXCLUSIVE: persistent schedule allowed
 };
 
 template <typename T, int ORDER, int NW, int RPW, int RING, int PD = 1, int XDPP = 0>
@@ -773,7 +836,7 @@ static hipError_t launch_step(const SArgs& a) {
     int nb = 0;
     const void* fn;
     if constexpr (RING == 2)
-      fn = (const void*)diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD>;
+      fn = (const void*)diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD, false>;
     else if constexpr (RING == 1)
       fn = (const void*)diffusion3d_step_ring_kernel<T, ORDER, NW, RPW, PD, XDPP>;
     else
@@ -783,25 +846,46 @@ static hipError_t launch_step(const SArgs& a) {
     return nb;
   }();
   static const int minc = knob("STEP_MIN_CHUNK", 32);
+  static const int persist = knob("STEP_PERSIST", 1);  // 0: grid schedule only (A/B)
+  static const int minseg = std::max(knob("STEP_MIN_SEG", 32), 1);
   const int na = std::max(a.k1 - a.k0, 0), nb = std::max(a.k1b - a.k0b, 0);
-  int zc;
-  if (target > 0) {
-    long long chunks = (target + (long long)gx * gy - 1) / ((long long)gx * gy);
-    zc = std::max(div_up(na + nb, std::max<long long>(chunks, 1)), minc);
+  const long long slots = (long long)device_cus() * per_cu;
+  StepSched sc{gx, gy, 0, 0, 0, 0};
+  dim3 grid;
+  const long long L = (long long)gx * gy * (na + nb);
+  const bool persistent =
+      RING == 2 && persist && (a.flags & ADVDIFF_EXCLUSIVE) && L < (1LL << 31);
+  if (persistent) {
+    // one round of resident groups; small launches keep >= minseg planes per group
+    const long long G = std::max(1LL, std::min(slots, (L + minseg - 1) / minseg));
+    sc.per = (int)(L / G);
+    sc.rem = (int)(L % G);
+    grid = dim3((unsigned)G, 1, 1);
   } else {
-    zc = pick_chunk_rounds(na + nb, (long long)gx * gy, (long long)device_cus() * per_cu, 4 * R,
-                           minc);
+    int zc;
+    if (target > 0) {
+      long long chunks = (target + (long long)gx * gy - 1) / ((long long)gx * gy);
+      zc = std::max(div_up(na + nb, std::max<long long>(chunks, 1)), minc);
+    } else {
+      zc = pick_chunk_rounds(na + nb, (long long)gx * gy, slots, 4 * R, minc);
+    }
+    sc.gza = na > 0 ? div_up(na, zc) : 0;
+    sc.zchunk = zc;
+    grid = dim3(gx, gy, sc.gza + (nb > 0 ? div_up(nb, zc) : 0));
   }
-  const int gza = na > 0 ? div_up(na, zc) : 0;
-  const int gz = gza + (nb > 0 ? div_up(nb, zc) : 0);
   const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
 #define STEP_ARGS                                                                              \
-  dim3(gx, gy, gz), dim3(64, NW, 1), 0, a.st, (const T*)a.uin, (T*)a.uout, a.nx, a.ny, a.sy,    \
-      a.sz, a.nz_alloc, a.k0, a.k1, a.k0b, a.k1b, gza, a.zlo, a.zhi, zc, a.bx, T(a.cx * s), \
-      T(a.cy * s), T(a.cz * s), T(a.dt)
-  if constexpr (RING == 2)
-    hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD>), STEP_ARGS);
-  else if constexpr (RING == 1)
+  grid, dim3(64, NW, 1), 0, a.st, (const T*)a.uin, (T*)a.uout, a.nx, a.ny, a.sy, a.sz,        \
+      a.nz_alloc, a.k0, a.k1, a.k0b, a.k1b, sc, a.zlo, a.zhi, a.bx, T(a.cx * s), T(a.cy * s),  \
+      T(a.cz * s), T(a.dt)
+  if constexpr (RING == 2) {
+    if (persistent)
+      hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD, true>),
+                         STEP_ARGS);
+    else
+      hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD, false>),
+                         STEP_ARGS);
+  } else if constexpr (RING == 1)
     hipLaunchKernelGGL((diffusion3d_step_ring_kernel<T, ORDER, NW, RPW, PD, XDPP>), STEP_ARGS);
   else
     hipLaunchKernelGGL((diffusion3d_step_kernel<T, ORDER, NW, RPW>), STEP_ARGS);
@@ -839,6 +923,15 @@ extern "C" int advdiff_diffusion3d_step_box(int dtype, const void* uin, void* uo
                                             int k1, int k0b, int k1b, int zlo, int zhi,
                                             const int* box, int order, double cx, double cy,
                                             double cz, double dt, void* stream) {
+  return advdiff_diffusion3d_step_box_ex(dtype, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, k0b,
+                                         k1b, zlo, zhi, box, order, cx, cy, cz, dt, 0, stream);
+}
+
+extern "C" int advdiff_diffusion3d_step_box_ex(int dtype, const void* uin, void* uout, int nx,
+                                               int ny, int64_t sy, int64_t sz, int nz_alloc,
+                                               int k0, int k1, int k0b, int k1b, int zlo, int zhi,
+                                               const int* box, int order, double cx, double cy,
+                                               double cz, double dt, int flags, void* stream) {
   using namespace advdiff;
   if (k1 <= k0) {  // only the second range (or nothing)
     k0 = k0b;
@@ -853,7 +946,7 @@ extern "C" int advdiff_diffusion3d_step_box(int dtype, const void* uin, void* uo
   if (sy * (int64_t)ny >= (int64_t(1) << 31)) return hipErrorInvalidValue;
   const Box2 bx{box[0], box[1], box[2], box[3], box[4], box[5], box[6], box[7]};
   const SArgs a{uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, k0b, k1b, zlo, zhi, bx,
-                cx, cy, cz, dt, (hipStream_t)stream};
+                cx, cy, cz, dt, (hipStream_t)stream, flags};
   static const int cfg = knob("STEP_CFG", 0);
   if (dtype == ADVDIFF_F64) {
     if (order == 4) return dispatch_step<double, 4>(cfg, a);

@@ -178,7 +178,7 @@ void Engine::launch(const void* in, void* aux, void* out, Range r, double dt, do
   }
 }
 
-void Engine::launch_fused(Range r, double dt, Range r2) {
+void Engine::launch_fused(Range r, double dt, Range r2, bool exclusive) {
   if (r.empty() && r2.empty()) return;
   const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
   if (p_.dims == 2) {
@@ -190,22 +190,24 @@ void Engine::launch_fused(Range r, double dt, Range r2) {
                                               compute_));
     return;
   }
-  KERNEL_CHECK(advdiff_diffusion3d_step2(p_.dtype, u_, A_, p_.nx, p_.ny, sy_, sz_, slab_.alloc(),
-                                         r.lo, r.hi, r2.lo, r2.hi, zact_.lo, zact_.hi,
-                                         p_.border(), p_.order, p_.K / (dx * dx),
-                                         p_.K / (dy * dy), p_.K / (dz * dz), dt, compute_));
+  const int B = p_.border();
+  const int box[8] = {B, p_.nx - B, B, p_.ny - B, 0, p_.nx, 0, p_.ny};
+  KERNEL_CHECK(advdiff_diffusion3d_step_box_ex(
+      p_.dtype, u_, A_, p_.nx, p_.ny, sy_, sz_, slab_.alloc(), r.lo, r.hi, r2.lo, r2.hi,
+      zact_.lo, zact_.hi, box, p_.order, p_.K / (dx * dx), p_.K / (dy * dy), p_.K / (dz * dz),
+      dt, exclusive ? ADVDIFF_EXCLUSIVE : 0, compute_));
 }
 
 void Engine::step_fused(double dt) {
   if (env_.size == 1) {
-    launch_fused(full_, dt);
+    launch_fused(full_, dt, Range{}, true);
   } else if (p_.overlap) {
-    launch_fused(interior_, dt);
+    launch_fused(interior_, dt);  // overlaps the RCCL exchange: grid schedule
     if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
     launch_fused(blo_, dt, bhi_);  // both boundary slabs in one launch
   } else {
     if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
-    launch_fused(full_, dt);
+    launch_fused(full_, dt, Range{}, true);
   }
   halo_pending_ = false;
   std::swap(u_, A_);

@@ -158,7 +158,9 @@ class Engine {
   void launch(const void* in, void* aux, void* out, Range r, double dt, double a, double b,
               bool ls);
   void stage(void* in, void* aux, void* out, double a, double b, double dt, bool ls = false);
-  void launch_fused(Range r, double dt, Range r2 = Range{});
+  // exclusive: nothing runs beside the launch (single rank / full range after the halo
+  // wait) -> persistent schedule of the 3-D step kernel (ADVDIFF_EXCLUSIVE)
+  void launch_fused(Range r, double dt, Range r2 = Range{}, bool exclusive = false);
   void step_fused(double dt);
   void start_halo(void* field);
   void* plane(void* base, int l) const { return (char*)base + (size_t)l * plane_bytes_; }

@@ -54,9 +54,10 @@ class Diffusion(Model):
         return 16.0 if self.supports_fused else 64.0
 
     def step(self, uin, uout, lo, hi, zlo, zhi, dt, stream=None, lo2=0, hi2=0, nx=None,
-             ny=None, box=None):
+             ny=None, box=None, exclusive=False):
         """Fused RK3 step on planes [lo, hi) (and [lo2, hi2) in the same launch).
-        nx/ny/box: extents and explicit active/output bounds of a view (Cartesian blocks)."""
+        nx/ny/box: extents and explicit active/output bounds of a view (Cartesian blocks).
+        exclusive: the launch has the GPU to itself (3-D: persistent schedule)."""
         g = self.grid
         nx = g.nx if nx is None else nx
         ny = g.ny if ny is None else ny
@@ -71,7 +72,7 @@ class Diffusion(Model):
         stencil.diffusion3d_step(uin, uout, nx=nx, ny=ny, k0=lo, k1=hi, zlo=zlo, zhi=zhi,
                                  border=self.border, order=self.order, cx=self.coef[0],
                                  cy=self.coef[1], cz=self.coef[2], dt=dt, stream=stream,
-                                 k0b=lo2, k1b=hi2, box=box)
+                                 k0b=lo2, k1b=hi2, box=box, exclusive=exclusive)
 
     def stable_dt(self, umax=None) -> float:
         return self.safety / (2.0 * sum(self.coef))

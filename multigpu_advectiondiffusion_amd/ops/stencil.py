@@ -100,12 +100,18 @@ def _int_array(vals):
     return (ctypes.c_int * len(vals))(*[int(v) for v in vals])
 
 
+EXCLUSIVE = 1  # ADVDIFF_EXCLUSIVE (kernels.h)
+
+
 def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy, cz, dt,
-                     stream=None, k0b=0, k1b=0, box=None):
+                     stream=None, k0b=0, k1b=0, box=None, exclusive=False):
     """A FULL SSP-RK3 step in one launch (temporal blocking): uout[k0:k1] = RK3(uin), and
     uout[k0b:k1b] too when a second range is given (one launch for both).
     box = (xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1): explicit active / output x-y bounds
-    (Cartesian blocks launched on a view); default from `border`."""
+    (Cartesian blocks launched on a view); default from `border`.
+    exclusive=True: nothing else runs on the GPU meanwhile (single rank / full-range
+    launch) -> one round of persistent workgroups; False (an interior launch overlapping
+    RCCL) keeps the dynamically balanced grid of z chunks.  Results are bit-identical."""
     _check_layout(uin, uout)
     if uin.data_ptr() == uout.data_ptr():
         raise ValueError("the fused step needs distinct input/output buffers")
@@ -116,10 +122,10 @@ def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, 
         nz = uin.shape[0]
         assert 0 <= k0 and k1 <= nz and 0 <= zlo and zhi <= nz and 0 <= k0b and k1b <= nz
         assert nx <= uin.shape[2] and ny <= uin.shape[1]
-        code = lib.advdiff_diffusion3d_step_box(
+        code = lib.advdiff_diffusion3d_step_box_ex(
             _dtype_code(uin), _ptr(uin), _ptr(uout), nx, ny, uin.stride(1), uin.stride(0), nz,
             k0, k1, k0b, k1b, zlo, zhi, _int_array(box), order, cx, cy, cz, dt,
-            _stream_ptr(stream))
+            EXCLUSIVE if exclusive else 0, _stream_ptr(stream))
         _lib.check(code, "diffusion3d_step")
     else:
         for a, b in ((k0, k1), (k0b, k1b)):

@@ -268,14 +268,17 @@ class Solver:
         with trace.range_("halo_start"):
             self._pending[id(out)] = self.halo.start(out)
 
-    def _launch_fused(self, rng, dt, rng2=(0, 0)):
+    def _launch_fused(self, rng, dt, rng2=(0, 0), exclusive=False):
+        """exclusive: nothing else (RCCL copy kernels) runs beside this launch — a single
+        rank, or a full-range launch after the halo wait — so the 3-D step may run as one
+        round of persistent workgroups (ops/stencil.py::diffusion3d_step)."""
         if self.cart:  # boundary boxes are launched one by one by the caller
-            self._launch_fused_box(rng, dt)
+            self._launch_fused_box(rng, dt, exclusive)
             return
         (lo, hi), (lo2, hi2) = rng, rng2
         if hi > lo or hi2 > lo2:
             self.model.step(self.u, self.un, lo, hi, self.zact[0], self.zact[1], dt, lo2=lo2,
-                            hi2=hi2)
+                            hi2=hi2, exclusive=exclusive)
             trace.sync_check(f"{self.model.name} fused step [{lo},{hi}) [{lo2},{hi2})",
                              self.device)
 
@@ -290,7 +293,7 @@ class Solver:
         B, N = self.model.border, cd.shape[a]
         return (v0, v1), (max(0, B - origin), min(v1 - v0, N - B - origin)), (lo - v0, hi - v0)
 
-    def _launch_fused_box(self, box, dt):
+    def _launch_fused_box(self, box, dt, exclusive=False):
         """Fused step of a Cartesian block box (array order) on a kernel VIEW."""
         if any(hi <= lo for lo, hi in box):
             return
@@ -301,7 +304,7 @@ class Solver:
             sl = (slice(None), slice(vy0, vy1), slice(vx0, vx1))
             self.model.step(self.u[sl], self.un[sl], z0, z1, self.zact[0], self.zact[1], dt,
                             nx=vx1 - vx0, ny=vy1 - vy0,
-                            box=(xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1))
+                            box=(xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1), exclusive=exclusive)
         else:
             (y0, y1), (x0, x1) = box
             (vx0, vx1), (xa0, xa1), (xo0, xo1) = self._fused_view(1, x0, x1)
@@ -313,7 +316,7 @@ class Solver:
     def _step_fused(self, dt: float) -> None:
         pend = self._pending.pop(id(self.u), None)
         if self.comm.size == 1:
-            self._launch_fused(self.full, dt)
+            self._launch_fused(self.full, dt, exclusive=True)
         elif self.overlap:
             with trace.range_("interior"):
                 self._launch_fused(self.interior, dt)
@@ -326,10 +329,10 @@ class Solver:
                         self._launch_fused_box(box, dt)
                 else:
                     self._launch_fused(self.boundary[0], dt, self.boundary[1])
-        else:
+        else:  # the launch starts after the exchange has completed: nothing runs beside it
             if pend is not None:
                 pend.wait()
-            self._launch_fused(self.full, dt)
+            self._launch_fused(self.full, dt, exclusive=True)
         self.u, self.un = self.un, self.u
         if self.comm.size > 1:
             with trace.range_("halo_start"):

@@ -55,6 +55,29 @@ def test_fused_step_bitwise_equals_per_stage(dtype, order, case):
     assert (got.cpu().double() - out).abs().max().item() < tol
 
 
+@pytest.mark.parametrize("order", [4, 2])
+@pytest.mark.parametrize("case", CASES + [
+    (200, 70, 130, 136, 3, 197, 3, 197, 3),   # many (tile, plane) segments per group
+])
+def test_fused_step_persistent_schedule_bitwise(order, case):
+    """exclusive=True (one round of persistent groups marching segments of the linearised
+    (tile, plane) space) == the grid of z chunks, bitwise; also with two plane ranges."""
+    nz, ny, nx, sx, k0, k1, zlo, zhi, border = case
+    g = torch.Generator().manual_seed(7)
+    u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).cuda()
+    c = (0.21, 0.17, 0.13)
+    dt = 0.5 / sum(c)
+    kw = dict(nx=nx, ny=ny, zlo=zlo, zhi=zhi, border=border, order=order, cx=c[0], cy=c[1],
+              cz=c[2], dt=dt)
+    mid = (k0 + k1) // 2
+    for ranges in (dict(k0=k0, k1=k1), dict(k0=k0, k1=k0 + 3, k0b=mid, k1b=k1)):
+        grid, pers = u.clone(), u.clone()
+        stencil.diffusion3d_step(u, grid, exclusive=False, **ranges, **kw)
+        stencil.diffusion3d_step(u, pers, exclusive=True, **ranges, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(grid, pers), (ranges, (grid - pers).abs().max().item())
+
+
 def _per_stage_2d(u, nx, j0, j1, ylo, yhi, border, order, c, dt):
     R = order // 2
     ny = u.shape[0]
