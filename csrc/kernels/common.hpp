@@ -103,6 +103,61 @@ __device__ __forceinline__ T rk_stage(T uo, T c, T L, T dt, T a, T b) {
   return v;
 }
 
+// ---------------------------------------------------------------------------------
+// Folded heat-equation stage update (every diffusion kernel: per-stage, fused step,
+// 2-D and 3-D).  An SSP stage  out = a u0 + b (c + dt Σ_d k_d d2_d(c))  with the FD4
+// d2 = 16 (m1+p1) - (m2+p2) - 30 c is evaluated as
+//     out = a u0 + KC c + Σ_d K_d [16 (m1+p1)_d - (m2+p2)_d]
+//     K_d = b dt k_d,  KC = b (1 - 30 dt Σ_d k_d)
+// (FD2: d2 = (m1+p1) - 2c, KC = b (1 - 2 dt Σ k_d)): per point 13-14 fp64 VALU ops
+// (FD4) instead of 16-18 for d2 -> Laplacian -> RK combination, with 4 coefficients per
+// stage (16 is an inline constant).  A low-storage stage uses the same chain with b = 1
+// and no c term (it yields d = a du + dt L).  The coefficients come from one host helper
+// (fd_coef) and the chain has a fixed evaluation order (centre, z, x, y; 2-D: centre,
+// y, x), so the per-stage and fused kernels stay bit-identical.
+// ---------------------------------------------------------------------------------
+template <typename T>
+struct FdCoef {
+  T kc;    // centre
+  T k[3];  // per axis (x, y, z)
+};
+
+// s: the stage's b (SSP) or 1 (low-storage); with_c: the "+ s c" term (SSP only).
+// kx, ky, kz: K/dx², K/dy², K/dz² (unscaled; kz = 0 in 2-D).
+template <typename T>
+inline FdCoef<T> fd_coef(int order, double kx, double ky, double kz, double dt, double s,
+                         bool with_c) {
+  const double f = order == 4 ? 1.0 / 12.0 : 1.0, ctr = order == 4 ? 30.0 : 2.0;
+  const double k[3] = {kx * f, ky * f, kz * f};
+  FdCoef<T> c;
+  c.kc = T(s * ((with_c ? 1.0 : 0.0) - ctr * dt * ((k[0] + k[1]) + k[2])));
+  for (int d = 0; d < 3; ++d) c.k[d] = T(s * dt * k[d]);
+  return c;
+}
+
+// centre term: base + KC c (base = a u0 / a du) or KC c
+template <typename T>
+__device__ __forceinline__ T fd_ctr(T kc, T c) {
+  return kc * c;
+}
+template <typename T>
+__device__ __forceinline__ T fd_ctr(T kc, T c, T base) {
+#pragma clang fp contract(off)
+  return fma(kc, c, base);
+}
+// one FD4 axis: acc + K (16 (m1+p1) - (m2+p2))
+template <typename T>
+__device__ __forceinline__ T fd4_axis(T acc, T k, T m2, T m1, T p1, T p2) {
+#pragma clang fp contract(off)
+  return fma(k, fma(T(16), m1 + p1, -(m2 + p2)), acc);
+}
+// one FD2 axis: acc + K (m1+p1)
+template <typename T>
+__device__ __forceinline__ T fd2_axis(T acc, T k, T m1, T p1) {
+#pragma clang fp contract(off)
+  return fma(k, m1 + p1, acc);
+}
+
 // Burgers flux f(u) = u²/2, local Lax-Friedrichs split  f± = ½(f(u) ± |u|·u).
 // (reference: MultiGPU/Burgers3d_Baseline/Kernels.cu:256-264)
 //
@@ -363,6 +418,27 @@ __device__ __forceinline__ void stage_store(T* out, T* aux, int64_t o, T ax, T c
   T d = T(0);
   out[o] = stage_value<T, MODE>(ax, c, L, dt, a, b, d);
   if constexpr (MODE == kLs1 || MODE == kLs) aux[o] = d;
+}
+
+// Folded heat stage (see FdCoef): base term of the chain for MODE, and the epilogue.
+// SSP: chain = [a u0 +] KC c + Σ..., out = chain.  Low-storage: chain = [a du +] dt L = d,
+// du = d, out = c + b d.
+template <typename T, int MODE>
+__device__ __forceinline__ T fd_start(T kc, T c, T ax, T a) {
+  if constexpr (reads_aux<MODE>())
+    return fd_ctr(kc, c, a * ax);
+  else
+    return fd_ctr(kc, c);
+}
+template <typename T, int MODE>
+__device__ __forceinline__ void fd_store(T* out, T* aux, int64_t o, T c, T acc, T b) {
+#pragma clang fp contract(off)
+  if constexpr (MODE == kSsp1 || MODE == kSsp) {
+    out[o] = acc;
+  } else {
+    aux[o] = acc;
+    out[o] = fma(b, acc, c);
+  }
 }
 
 }  // namespace advdiff

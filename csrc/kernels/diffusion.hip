@@ -29,7 +29,7 @@ namespace advdiff {
 template <typename T, int ORDER, int TX, int TY, int MODE>
 __global__ __launch_bounds__(TX* TY) void diffusion3d_stage_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz,
-    int k0, int k1, int zchunk, int border, T cx, T cy, T cz, T dt, T a, T b) {
+    int k0, int k1, int zchunk, int border, FdCoef<T> q, T a, T b) {
   constexpr int R = FD<ORDER>::R;
   constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NS = R + 2, NT = TX * TY, NE = LX * LY;
   constexpr int NPT = (NE + NT - 1) / NT;  // tile elements staged per thread and plane
@@ -85,16 +85,18 @@ __global__ __launch_bounds__(TX* TY) void diffusion3d_stage_kernel(
     zw[2 * R] = ring[(k + R) % NS][lc];
     const T* c = ring[k % NS];
     const T ctr = zw[R];
-    T lap;
+    T acc = fd_start<T, MODE>(q.kc, ctr, ax, a);  // fixed order: centre, z, x, y
     if constexpr (ORDER == 4) {
-      lap = lap3(cx, FD<4>::d2(c[lc - 2], c[lc - 1], ctr, c[lc + 1], c[lc + 2]), cy,
-                 FD<4>::d2(c[lc - 2 * LX], c[lc - LX], ctr, c[lc + LX], c[lc + 2 * LX]), cz,
-                 FD<4>::d2(zw[0], zw[1], ctr, zw[3], zw[4]));
+      acc = fd4_axis(acc, q.k[2], zw[0], zw[1], zw[3], zw[4]);
+      acc = fd4_axis(acc, q.k[0], c[lc - 2], c[lc - 1], c[lc + 1], c[lc + 2]);
+      acc = fd4_axis(acc, q.k[1], c[lc - 2 * LX], c[lc - LX], c[lc + LX],
+                     c[lc + 2 * LX]);
     } else {
-      lap = lap3(cx, FD<2>::d2(c[lc - 1], ctr, c[lc + 1]), cy,
-                 FD<2>::d2(c[lc - LX], ctr, c[lc + LX]), cz, FD<2>::d2(zw[0], ctr, zw[2]));
+      acc = fd2_axis(acc, q.k[2], zw[0], zw[2]);
+      acc = fd2_axis(acc, q.k[0], c[lc - 1], c[lc + 1]);
+      acc = fd2_axis(acc, q.k[1], c[lc - LX], c[lc + LX]);
     }
-    if (active) stage_store<T, MODE>(out, aux, (int64_t)k * sz + own, ax, ctr, lap, dt, a, b);
+    if (active) fd_store<T, MODE>(out, aux, (int64_t)k * sz + own, ctr, acc, b);
 #pragma unroll
     for (int q = 0; q < 2 * R; ++q) zw[q] = zw[q + 1];
   }
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(TX* TY) void diffusion3d_stage_kernel(
 template <typename T, int ORDER, int TX, int MODE>
 __global__ __launch_bounds__(TX) void diffusion2d_stage_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int64_t sy, int j0, int j1,
-    int ychunk, int border, T cx, T cy, T dt, T a, T b) {
+    int ychunk, int border, FdCoef<T> q, T a, T b) {
   constexpr int R = FD<ORDER>::R;
   constexpr int LX = TX + 2 * R, NS = R + 2;
   __shared__ T ring[NS][LX];
@@ -149,14 +151,15 @@ __global__ __launch_bounds__(TX) void diffusion2d_stage_kernel(
     yw[2 * R] = ring[(jj + R) % NS][lc];
     const T* c = ring[jj % NS];
     const T ctr = yw[R];
-    T lap;
+    T acc = fd_start<T, MODE>(q.kc, ctr, ax, a);  // fixed order: centre, y, x
     if constexpr (ORDER == 4) {
-      lap = lap2(cx, FD<4>::d2(c[lc - 2], c[lc - 1], ctr, c[lc + 1], c[lc + 2]), cy,
-                 FD<4>::d2(yw[0], yw[1], ctr, yw[3], yw[4]));
+      acc = fd4_axis(acc, q.k[1], yw[0], yw[1], yw[3], yw[4]);
+      acc = fd4_axis(acc, q.k[0], c[lc - 2], c[lc - 1], c[lc + 1], c[lc + 2]);
     } else {
-      lap = lap2(cx, FD<2>::d2(c[lc - 1], ctr, c[lc + 1]), cy, FD<2>::d2(yw[0], ctr, yw[2]));
+      acc = fd2_axis(acc, q.k[1], yw[0], yw[2]);
+      acc = fd2_axis(acc, q.k[0], c[lc - 1], c[lc + 1]);
     }
-    if (active) stage_store<T, MODE>(out, aux, (int64_t)jj * sy + i, ax, ctr, lap, dt, a, b);
+    if (active) fd_store<T, MODE>(out, aux, (int64_t)jj * sy + i, ctr, acc, b);
 #pragma unroll
     for (int q = 0; q < 2 * R; ++q) yw[q] = yw[q + 1];
   }
@@ -179,16 +182,23 @@ struct DArgs {
   hipStream_t st;
 };
 
+// folded stage coefficients (common.hpp FdCoef): SSP stages scale by b and keep the c
+// term; low-storage stages produce d = a du + dt L (b = 1, no c term)
+template <typename T, int MODE>
+static FdCoef<T> stage_coef(int order, const DArgs& p) {
+  const bool ls = MODE == kLs1 || MODE == kLs;
+  return fd_coef<T>(order, p.cx, p.cy, p.cz, p.dt, ls ? 1.0 : p.b, !ls);
+}
+
 template <typename T, int ORDER, int TY, int MODE>
 static hipError_t launch_d3_ty(const DArgs& p) {
   const int gx = div_up(p.nx, kTX3), gy = div_up(p.ny, TY);
   const int zc = pick_chunk(p.hi - p.lo, (long long)gx * gy, 8, 256);
   const int gz = div_up(p.hi - p.lo, zc);
-  const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
   hipLaunchKernelGGL((diffusion3d_stage_kernel<T, ORDER, kTX3, TY, MODE>), dim3(gx, gy, gz),
                      dim3(kTX3, TY, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx,
-                     p.ny, p.sy, p.sz, p.lo, p.hi, zc, p.border, T(p.cx * s), T(p.cy * s),
-                     T(p.cz * s), T(p.dt), T(p.a), T(p.b));
+                     p.ny, p.sy, p.sz, p.lo, p.hi, zc, p.border, stage_coef<T, MODE>(ORDER, p),
+                     T(p.a), T(p.b));
   return hipGetLastError();
 }
 
@@ -207,11 +217,10 @@ static hipError_t launch_d2(const DArgs& p) {
   const int gx = div_up(p.nx, kTX2);
   const int yc = pick_chunk(p.hi - p.lo, gx, 8, 256);
   const int gy = div_up(p.hi - p.lo, yc);
-  const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
   hipLaunchKernelGGL((diffusion2d_stage_kernel<T, ORDER, kTX2, MODE>), dim3(gx, gy, 1),
                      dim3(kTX2, 1, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx,
-                     p.sy, p.lo, p.hi, yc, p.border, T(p.cx * s), T(p.cy * s), T(p.dt),
-                     T(p.a), T(p.b));
+                     p.sy, p.lo, p.hi, yc, p.border, stage_coef<T, MODE>(ORDER, p), T(p.a),
+                     T(p.b));
   return hipGetLastError();
 }
 

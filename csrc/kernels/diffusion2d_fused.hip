@@ -23,7 +23,7 @@ template <typename T, int ORDER>
 __global__ __launch_bounds__(64 * kWavesPerBlock2) void diffusion2d_step_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int64_t sy, int ny_alloc, int j0,
     int j1, int ylo, int yhi, int ychunk, int nchunks, int ntiles, int xa0, int xa1, int xo0,
-    int xo1, T cx, T cy, T dt) {
+    int xo1, FdCoef<T> q1, FdCoef<T> q2, FdCoef<T> q3) {
   constexpr int R = FD<ORDER>::R;
   constexpr int NR = 2 * R + 1;
   constexpr int W = 64;
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock2) void diffusion2d_step_kernel(
     ev1 = row(jst + 2 * R)[e1];
     ev2 = row(jst + 2 * R)[e2];
   }
-  const T third = T(1.0 / 3.0), two3 = T(2.0 / 3.0);
+  const T third = T(1.0 / 3.0);
 
   auto body = [&]<int PH>(int j) {
     auto sl = [](int d) { return (PH + d + 4 * NR) % NR; };
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock2) void diffusion2d_step_kernel(
     // stage 1: A(j+2R) on all lanes
     {
       const T c = ru[sl(2 * R)];
-      T lap;
+      T acc = fd_ctr(q1.kc, c);  // order: centre, y, x (as the per-stage kernel)
       if constexpr (R == 2) {
         T m1 = wave_shr1(c), p1 = wave_shl1(c);
         T m2 = wave_shr1(m1), p2 = wave_shl1(p1);
@@ -93,49 +93,51 @@ __global__ __launch_bounds__(64 * kWavesPerBlock2) void diffusion2d_step_kernel(
           p1 = ee1;
           p2 = ee2;
         }
-        lap = lap2(cx, FD<4>::d2(m2, m1, c, p1, p2), cy,
-                   FD<4>::d2(ru[sl(R)], ru[sl(R + 1)], c, ru[sl(3 * R - 1)], ru[sl(3 * R)]));
+        acc = fd4_axis(acc, q1.k[1], ru[sl(R)], ru[sl(R + 1)], ru[sl(3 * R - 1)],
+                       ru[sl(3 * R)]);
+        acc = fd4_axis(acc, q1.k[0], m2, m1, p1, p2);
       } else {
         T m1 = wave_shr1(c), p1 = wave_shl1(c);
         if (lane == 0) m1 = ee1;
         if (lane == W - 1) p1 = ee1;
-        lap = lap2(cx, FD<2>::d2(m1, c, p1), cy, FD<2>::d2(ru[sl(R)], c, ru[sl(3 * R)]));
+        acc = fd2_axis(acc, q1.k[1], ru[sl(R)], ru[sl(3 * R)]);
+        acc = fd2_axis(acc, q1.k[0], m1, p1);
       }
       const int p = j + 2 * R;
-      const T v = rk_stage<T, false>(T(0), c, lap, dt, T(0), T(1));
+      const T v = acc;
       ra[sl(2 * R)] = (p >= ylo && p < yhi && xin) ? v : c;
     }
     // stage 2: B(j+R)
     if (j >= jc0 - 2 * R) {
       const T c = ra[sl(R)];
       const T uo = ru[sl(R)];
-      T lap;
+      T acc = fd_ctr(q2.kc, c, T(0.75) * uo);
       if constexpr (R == 2) {
         const T m1 = wave_shr1(c), p1 = wave_shl1(c);
-        lap = lap2(cx, FD<4>::d2(wave_shr1(m1), m1, c, p1, wave_shl1(p1)), cy,
-                   FD<4>::d2(ra[sl(0)], ra[sl(1)], c, ra[sl(3)], ra[sl(4)]));
+        acc = fd4_axis(acc, q2.k[1], ra[sl(0)], ra[sl(1)], ra[sl(3)], ra[sl(4)]);
+        acc = fd4_axis(acc, q2.k[0], wave_shr1(m1), m1, p1, wave_shl1(p1));
       } else {
-        lap = lap2(cx, FD<2>::d2(wave_shr1(c), c, wave_shl1(c)), cy,
-                   FD<2>::d2(ra[sl(0)], c, ra[sl(2)]));
+        acc = fd2_axis(acc, q2.k[1], ra[sl(0)], ra[sl(2)]);
+        acc = fd2_axis(acc, q2.k[0], wave_shr1(c), wave_shl1(c));
       }
       const int p = j + R;
-      const T v = rk_stage<T, true>(uo, c, lap, dt, T(0.75), T(0.25));
+      const T v = acc;
       rb[sl(R)] = (p >= ylo && p < yhi && xin && s2c) ? v : uo;
     }
     // stage 3: u^{n+1}(j)
     if (j >= jc0) {
       const T c = rb[sl(0)];
       const T uo = dl[0];
-      T lap;
+      T acc = fd_ctr(q3.kc, c, third * uo);
       if constexpr (R == 2) {
         const T m1 = wave_shr1(c), p1 = wave_shl1(c);
-        lap = lap2(cx, FD<4>::d2(wave_shr1(m1), m1, c, p1, wave_shl1(p1)), cy,
-                   FD<4>::d2(rb[sl(-2)], rb[sl(-1)], c, rb[sl(1)], rb[sl(2)]));
+        acc = fd4_axis(acc, q3.k[1], rb[sl(-2)], rb[sl(-1)], rb[sl(1)], rb[sl(2)]);
+        acc = fd4_axis(acc, q3.k[0], wave_shr1(m1), m1, p1, wave_shl1(p1));
       } else {
-        lap = lap2(cx, FD<2>::d2(wave_shr1(c), c, wave_shl1(c)), cy,
-                   FD<2>::d2(rb[sl(-1)], c, rb[sl(1)]));
+        acc = fd2_axis(acc, q3.k[1], rb[sl(-1)], rb[sl(1)]);
+        acc = fd2_axis(acc, q3.k[0], wave_shr1(c), wave_shl1(c));
       }
-      const T v = rk_stage<T, true>(uo, c, lap, dt, third, two3);
+      const T v = acc;
       if (xout && s3c) uout[(int64_t)j * sy + x] = v;
     }
 #pragma unroll
@@ -180,11 +182,13 @@ static hipError_t launch_step2d(const void* uin, void* uout, int nx, int64_t sy,
   const int yc = div_up(n, chunks);
   chunks = div_up(n, yc);
   const int items = ntiles * chunks;
-  const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
+  // SSP-RK3 stage coefficients b = 1, 1/4, 2/3 (the per-stage path's, common.hpp FdCoef)
   hipLaunchKernelGGL((diffusion2d_step_kernel<T, ORDER>), dim3(div_up(items, kWavesPerBlock2)),
                      dim3(64, kWavesPerBlock2, 1), 0, st, (const T*)uin, (T*)uout, nx, sy,
                      ny_alloc, j0, j1, ylo, yhi, yc, chunks, ntiles, bx[0], bx[1], bx[2],
-                     bx[3], T(cx * s), T(cy * s), T(dt));
+                     bx[3], fd_coef<T>(ORDER, cx, cy, 0.0, dt, 1.0, true),
+                     fd_coef<T>(ORDER, cx, cy, 0.0, dt, 0.25, true),
+                     fd_coef<T>(ORDER, cx, cy, 0.0, dt, 2.0 / 3.0, true));
   return hipGetLastError();
 }
 

@@ -53,451 +53,6 @@ struct StepSched {
   int per, rem;     // persistent mode: L = per G + rem
 };
 
-template <typename T, int ORDER, int NW, int RPW>
-__global__ __launch_bounds__(64 * NW) void diffusion3d_step_kernel(
-    const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
-    int nz_alloc, int k0, int k1, int k0b, int k1b, StepSched sc, int zlo, int zhi,
-    Box2 bx, T cx, T cy, T cz,
-    T dt) {
-  const int gza = sc.gza, zchunk = sc.zchunk;
-  constexpr int R = FD<ORDER>::R;
-  constexpr int W = 64;             // stage-1 columns (one wave)
-  constexpr int TX = W - 4 * R;     // output columns
-  constexpr int S1R = NW * RPW;     // stage-1 rows
-  constexpr int TY = S1R - 4 * R;   // output rows
-  constexpr int UW = W + 2 * R, UH = S1R + 2 * R;
-  constexpr int NT = 64 * NW;
-  constexpr int NHALO = UW * UH - W * S1R;
-  constexpr int NH = (NHALO + NT - 1) / NT;
-  static_assert(TY > 0, "too few rows per workgroup");
-
-  __shared__ T sU[2][UH * UW];
-  __shared__ T sA[2][S1R * W];
-  __shared__ T sB[2][S1R * W];
-
-  const int lane = threadIdx.x, w = threadIdx.y, tid = w * 64 + lane;
-  const Tile3 tile = xcd_tile();
-  const int i0 = tile.x * TX, j0 = tile.y * TY;
-  const int x = i0 - 2 * R + lane;
-  // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
-  const bool second = (int)tile.z >= gza;
-  const int kc0 = second ? k0b + ((int)tile.z - gza) * zchunk : k0 + tile.z * zchunk;
-  const int kc1 = min(kc0 + zchunk, second ? k1b : k1);
-  const bool xin = x >= bx.xa0 && x < bx.xa1;   // non-frozen columns
-  const bool xout = x >= bx.xo0 && x < bx.xo1;  // columns this launch writes
-  const bool s2c = lane >= R && lane < W - R;
-  const bool s3c = lane >= 2 * R && lane < W - 2 * R;
-  const int xc = clampi(x, 0, nx - 1);
-
-  int row[RPW], off[RPW];
-  bool inxy[RPW], outq[RPW], s2r[RPW], s3r[RPW];
-#pragma unroll
-  for (int q = 0; q < RPW; ++q) {
-    row[q] = w + q * NW;
-    const int y = j0 - 2 * R + row[q];
-    inxy[q] = xin && y >= bx.ya0 && y < bx.ya1;
-    outq[q] = inxy[q] && xout && y >= bx.yo0 && y < bx.yo1;
-    s2r[q] = row[q] >= R && row[q] < S1R - R;
-    s3r[q] = row[q] >= 2 * R && row[q] < S1R - 2 * R;
-    off[q] = clampi(y, 0, ny - 1) * (int)sy + xc;
-  }
-  // halo cells of the u plane (the R-wide rim around S1), precomputed per thread
-  int hl[NH], ho[NH];
-#pragma unroll
-  for (int h = 0; h < NH; ++h) {
-    int idx = tid + h * NT;  // enumerate the rim: top R rows, bottom R rows, left/right R cols
-    hl[h] = -1;
-    ho[h] = 0;
-    if (idx < NHALO) {
-      int ur, uc;
-      if (idx < R * UW) {  // top rows
-        ur = idx / UW;
-        uc = idx - ur * UW;
-      } else if ((idx -= R * UW) < R * UW) {  // bottom rows
-        ur = S1R + R + idx / UW;
-        uc = idx % UW;
-      } else {  // side columns of the S1 rows
-        idx -= R * UW;
-        ur = R + idx / (2 * R);
-        const int cc = idx % (2 * R);
-        uc = cc < R ? cc : W + cc;
-      }
-      hl[h] = ur * UW + uc;
-      ho[h] = clampi(j0 - 3 * R + ur, 0, ny - 1) * (int)sy + clampi(i0 - 3 * R + uc, 0, nx - 1);
-    }
-  }
-
-  auto plane = [&](int k) { return uin + (int64_t)clampi(k, 0, nz_alloc - 1) * sz; };
-
-  T uw[RPW][3 * R + 1], aw[RPW][2 * R + 1], bw[RPW][2 * R + 1];
-  const int kst = kc0 - 4 * R;
-#pragma unroll
-  for (int q = 0; q < RPW; ++q) {
-#pragma unroll
-    for (int s = 0; s < 3 * R; ++s) uw[q][s] = plane(kst + s)[off[q]];
-#pragma unroll
-    for (int s = 0; s <= 2 * R; ++s) aw[q][s] = bw[q][s] = T(0);
-  }
-  T hv[NH], un[RPW];
-#pragma unroll
-  for (int h = 0; h < NH; ++h) hv[h] = plane(kst + 2 * R)[ho[h]];
-#pragma unroll
-  for (int q = 0; q < RPW; ++q) un[q] = plane(kst + 3 * R)[off[q]];
-
-  const T third = T(1.0 / 3.0), two3 = T(2.0 / 3.0);
-  for (int k = kst; k < kc1; ++k) {
-    const int set = k & 1;
-    T* pU = sU[set];
-    T* pA = sA[set];
-    T* pB = sB[set];
-    // ---- stage the planes: u(k+2R) (own + rim), A(k+R), B(k) ----
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-      uw[q][3 * R] = un[q];
-      pU[(row[q] + R) * UW + lane + R] = uw[q][2 * R];
-      pA[row[q] * W + lane] = aw[q][R];
-      pB[row[q] * W + lane] = bw[q][R];
-    }
-#pragma unroll
-    for (int h = 0; h < NH; ++h)
-      if (hl[h] >= 0) pU[hl[h]] = hv[h];
-    if (k + 1 < kc1) {  // next plane's loads stay in flight across this plane's compute
-#pragma unroll
-      for (int h = 0; h < NH; ++h) hv[h] = plane(k + 1 + 2 * R)[ho[h]];
-#pragma unroll
-      for (int q = 0; q < RPW; ++q) un[q] = plane(k + 1 + 3 * R)[off[q]];
-    }
-    __syncthreads();
-
-    // Every stage is evaluated UNCONDITIONALLY on all lanes of its (wave-uniform) rows
-    // and the frozen/rim lanes are fixed up with a select: straight-line code lets the
-    // compiler issue the LDS reads of all rows before the first FMA (latency hiding).
-    // ---- stage 1: A(k+2R) on S1 ----
-    const int p1 = k + 2 * R;
-    const bool z1 = p1 >= zlo && p1 < zhi;
-    T lapA[RPW];
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-      const T c = uw[q][2 * R];
-      const int l = (row[q] + R) * UW + lane + R;
-      if constexpr (R == 2)
-        lapA[q] = lap3(cx, FD<4>::d2(pU[l - 2], pU[l - 1], c, pU[l + 1], pU[l + 2]), cy,
-                       FD<4>::d2(pU[l - 2 * UW], pU[l - UW], c, pU[l + UW], pU[l + 2 * UW]), cz,
-                       FD<4>::d2(uw[q][2], uw[q][3], c, uw[q][5], uw[q][6]));
-      else
-        lapA[q] = lap3(cx, FD<2>::d2(pU[l - 1], c, pU[l + 1]), cy,
-                       FD<2>::d2(pU[l - UW], c, pU[l + UW]), cz, FD<2>::d2(uw[q][1], c, uw[q][3]));
-    }
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-      const T c = uw[q][2 * R];
-      const T v = rk_stage<T, false>(T(0), c, lapA[q], dt, T(0), T(1));
-      aw[q][2 * R] = (z1 && inxy[q]) ? v : c;
-    }
-    // ---- stage 2: B(k+R) on S2 ----
-    if (k >= kc0 - 2 * R) {
-      const int p2 = k + R;
-      const bool z2 = p2 >= zlo && p2 < zhi;
-#pragma unroll
-      for (int q = 0; q < RPW; ++q) {
-        const T uo = uw[q][R];
-        if (!s2r[q]) {  // wave-uniform
-          bw[q][2 * R] = uo;
-          continue;
-        }
-        const int l = row[q] * W + lane;
-        const T c = aw[q][R];
-        T lap;
-        if constexpr (R == 2)
-          lap = lap3(cx, FD<4>::d2(pA[l - 2], pA[l - 1], c, pA[l + 1], pA[l + 2]), cy,
-                     FD<4>::d2(pA[l - 2 * W], pA[l - W], c, pA[l + W], pA[l + 2 * W]), cz,
-                     FD<4>::d2(aw[q][0], aw[q][1], c, aw[q][3], aw[q][4]));
-        else
-          lap = lap3(cx, FD<2>::d2(pA[l - 1], c, pA[l + 1]), cy,
-                     FD<2>::d2(pA[l - W], c, pA[l + W]), cz, FD<2>::d2(aw[q][0], c, aw[q][2]));
-        const T v = rk_stage<T, true>(uo, c, lap, dt, T(0.75), T(0.25));
-        bw[q][2 * R] = (z2 && inxy[q] && s2c) ? v : uo;
-      }
-    }
-    // ---- stage 3: u^{n+1}(k) on S3 ----
-    if (k >= kc0) {
-#pragma unroll
-      for (int q = 0; q < RPW; ++q) {
-        if (!s3r[q]) continue;  // wave-uniform
-        const int l = row[q] * W + lane;
-        const T c = bw[q][R];
-        const T uo = uw[q][0];
-        T lap;
-        if constexpr (R == 2)
-          lap = lap3(cx, FD<4>::d2(pB[l - 2], pB[l - 1], c, pB[l + 1], pB[l + 2]), cy,
-                     FD<4>::d2(pB[l - 2 * W], pB[l - W], c, pB[l + W], pB[l + 2 * W]), cz,
-                     FD<4>::d2(bw[q][0], bw[q][1], c, bw[q][3], bw[q][4]));
-        else
-          lap = lap3(cx, FD<2>::d2(pB[l - 1], c, pB[l + 1]), cy,
-                     FD<2>::d2(pB[l - W], c, pB[l + W]), cz, FD<2>::d2(bw[q][0], c, bw[q][2]));
-        const T v = rk_stage<T, true>(uo, c, lap, dt, third, two3);
-        if (outq[q] && s3c) uout[(int64_t)k * sz + off[q]] = v;  // k in [kc0,kc1): interior
-      }
-    }
-    // ---- advance the register windows ----
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-#pragma unroll
-      for (int s = 0; s < 3 * R; ++s) uw[q][s] = uw[q][s + 1];
-#pragma unroll
-      for (int s = 0; s < 2 * R; ++s) {
-        aw[q][s] = aw[q][s + 1];
-        bw[q][s] = bw[q][s + 1];
-      }
-    }
-  }
-}
-
-// Same algorithm with the z-windows kept as 8-slot register rings and the march
-// unrolled 8x: plane p lives in slot (p - kst) & 7, so at unrolled phase PH every
-// window index is a compile-time constant and no register is ever moved (the plain
-// version spends ~55 v_mov_b64 per plane shifting its windows).
-template <typename T, int ORDER, int NW, int RPW, int PD, int XDPP>
-__global__ __launch_bounds__(64 * NW) void diffusion3d_step_ring_kernel(
-    const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
-    int nz_alloc, int k0, int k1, int k0b, int k1b, StepSched sc, int zlo, int zhi,
-    Box2 bx, T cx, T cy, T cz,
-    T dt) {
-  const int gza = sc.gza, zchunk = sc.zchunk;
-  constexpr int R = FD<ORDER>::R;
-  constexpr int W = 64;
-  constexpr int TX = W - 4 * R;
-  constexpr int S1R = NW * RPW;
-  constexpr int TY = S1R - 4 * R;
-  constexpr int UW = W + 2 * R, UH = S1R + 2 * R;
-  constexpr int NT = 64 * NW;
-  constexpr int NHALO = UW * UH - W * S1R;
-  constexpr int NH = (NHALO + NT - 1) / NT;
-  static_assert(TY > 0 && 3 * R + 1 <= 8, "ring too small");
-
-  __shared__ T sU[2][UH * UW];
-  __shared__ T sA[2][S1R * W];
-  __shared__ T sB[2][S1R * W];
-
-  const int lane = threadIdx.x, w = threadIdx.y, tid = w * 64 + lane;
-  const Tile3 tile = xcd_tile();
-  const int i0 = tile.x * TX, j0 = tile.y * TY;
-  const int x = i0 - 2 * R + lane;
-  // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
-  const bool second = (int)tile.z >= gza;
-  const int kc0 = second ? k0b + ((int)tile.z - gza) * zchunk : k0 + tile.z * zchunk;
-  const int kc1 = min(kc0 + zchunk, second ? k1b : k1);
-  const bool xin = x >= bx.xa0 && x < bx.xa1;   // non-frozen columns
-  const bool xout = x >= bx.xo0 && x < bx.xo1;  // columns this launch writes
-  const bool s2c = lane >= R && lane < W - R;
-  const bool s3c = lane >= 2 * R && lane < W - 2 * R;
-  const int xc = clampi(x, 0, nx - 1);
-
-  int row[RPW], off[RPW];
-  bool inxy[RPW], outq[RPW], s2r[RPW], s3r[RPW];
-#pragma unroll
-  for (int q = 0; q < RPW; ++q) {
-    row[q] = w + q * NW;
-    const int y = j0 - 2 * R + row[q];
-    inxy[q] = xin && y >= bx.ya0 && y < bx.ya1;
-    outq[q] = inxy[q] && xout && y >= bx.yo0 && y < bx.yo1;
-    s2r[q] = row[q] >= R && row[q] < S1R - R;
-    s3r[q] = row[q] >= 2 * R && row[q] < S1R - 2 * R;
-    off[q] = clampi(y, 0, ny - 1) * (int)sy + xc;
-  }
-  int hl[NH], ho[NH];
-#pragma unroll
-  for (int h = 0; h < NH; ++h) {
-    int idx = tid + h * NT;
-    hl[h] = -1;
-    ho[h] = 0;
-    if (idx < NHALO) {
-      int ur, uc;
-      if (idx < R * UW) {
-        ur = idx / UW;
-        uc = idx - ur * UW;
-      } else if ((idx -= R * UW) < R * UW) {
-        ur = S1R + R + idx / UW;
-        uc = idx % UW;
-      } else {
-        idx -= R * UW;
-        ur = R + idx / (2 * R);
-        const int cc = idx % (2 * R);
-        uc = cc < R ? cc : W + cc;
-      }
-      hl[h] = ur * UW + uc;
-      ho[h] = clampi(j0 - 3 * R + ur, 0, ny - 1) * (int)sy + clampi(i0 - 3 * R + uc, 0, nx - 1);
-    }
-  }
-  auto plane = [&](int k) { return uin + (int64_t)clampi(k, 0, nz_alloc - 1) * sz; };
-
-  T ru[RPW][8], ra[RPW][8], rb[RPW][8];  // plane p -> slot (p - kst) & 7
-  const int kst = kc0 - 4 * R;
-#pragma unroll
-  for (int q = 0; q < RPW; ++q) {
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      ru[q][s] = s < 3 * R ? plane(kst + s)[off[q]] : T(0);
-      ra[q][s] = rb[q][s] = T(0);
-    }
-  }
-  // PD planes of global loads in flight: buffer PH % PD holds the rim of plane k+2R and
-  // the own values of plane k+3R at phase PH, and is refilled with plane k+PD's.
-  static_assert(8 % PD == 0, "prefetch distance must divide the ring unroll");
-  T hv[PD][NH], un[PD][RPW];
-#pragma unroll
-  for (int d = 0; d < PD; ++d) {
-#pragma unroll
-    for (int h = 0; h < NH; ++h) hv[d][h] = plane(kst + d + 2 * R)[ho[h]];
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) un[d][q] = plane(kst + d + 3 * R)[off[q]];
-  }
-  const T third = T(1.0 / 3.0), two3 = T(2.0 / 3.0);
-
-  // one plane of the march at compile-time ring phase PH (k - kst == PH mod 8)
-  auto body = [&]<int PH>(int k) {
-    constexpr int U0 = PH & 7;            // u(k)
-    constexpr int UR = (PH + R) & 7;      // u(k+R)
-    constexpr int U2R = (PH + 2 * R) & 7; // u(k+2R)
-    constexpr int U3R = (PH + 3 * R) & 7; // u(k+3R)
-    constexpr int A0 = PH & 7, AR = (PH + R) & 7, A2R = (PH + 2 * R) & 7;  // A(k..)
-    constexpr int BM = (PH + 8 - R) & 7, B0 = PH & 7, BR = (PH + R) & 7;   // B(k-R..)
-    constexpr int PB = PH % PD;
-    const int set = k & 1;
-    T* pU = sU[set];
-    T* pA = sA[set];
-    T* pB = sB[set];
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-      ru[q][U3R] = un[PB][q];
-      pU[(row[q] + R) * UW + lane + R] = ru[q][U2R];
-      pA[row[q] * W + lane] = ra[q][AR];
-      pB[row[q] * W + lane] = rb[q][B0];
-    }
-#pragma unroll
-    for (int h = 0; h < NH; ++h)
-      if (hl[h] >= 0) pU[hl[h]] = hv[PB][h];
-    if (k + PD < kc1) {
-#pragma unroll
-      for (int h = 0; h < NH; ++h) hv[PB][h] = plane(k + PD + 2 * R)[ho[h]];
-#pragma unroll
-      for (int q = 0; q < RPW; ++q) un[PB][q] = plane(k + PD + 3 * R)[off[q]];
-    }
-    __syncthreads();
-    // stage 1: A(k+2R)
-    const int p1 = k + 2 * R;
-    const bool z1 = p1 >= zlo && p1 < zhi;
-    T lapA[RPW];
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-      const T c = ru[q][U2R];
-      const int l = (row[q] + R) * UW + lane + R;
-      if constexpr (XDPP >= 2 && R == 2) {
-        // x neighbours by DPP; the 2R edge lanes take theirs from the LDS halo columns
-        T m1 = wave_shr1(c), p1 = wave_shl1(c);
-        T m2 = wave_shr1(m1), p2 = wave_shl1(p1);
-        if (lane < R) {
-          m1 = pU[l - 1];
-          m2 = pU[l - 2];
-        } else if (lane >= W - R) {
-          p1 = pU[l + 1];
-          p2 = pU[l + 2];
-        }
-        lapA[q] = lap3(cx, FD<4>::d2(m2, m1, c, p1, p2), cy,
-                       FD<4>::d2(pU[l - 2 * UW], pU[l - UW], c, pU[l + UW], pU[l + 2 * UW]), cz,
-                       FD<4>::d2(ru[q][(PH + 2) & 7], ru[q][(PH + 3) & 7], c, ru[q][(PH + 5) & 7],
-                                 ru[q][(PH + 6) & 7]));
-      } else if constexpr (R == 2)
-        lapA[q] = lap3(cx, FD<4>::d2(pU[l - 2], pU[l - 1], c, pU[l + 1], pU[l + 2]), cy,
-                       FD<4>::d2(pU[l - 2 * UW], pU[l - UW], c, pU[l + UW], pU[l + 2 * UW]), cz,
-                       FD<4>::d2(ru[q][(PH + 2) & 7], ru[q][(PH + 3) & 7], c, ru[q][(PH + 5) & 7],
-                                 ru[q][(PH + 6) & 7]));
-      else
-        lapA[q] = lap3(cx, FD<2>::d2(pU[l - 1], c, pU[l + 1]), cy,
-                       FD<2>::d2(pU[l - UW], c, pU[l + UW]), cz,
-                       FD<2>::d2(ru[q][(PH + 1) & 7], c, ru[q][(PH + 3) & 7]));
-    }
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-      const T c = ru[q][U2R];
-      const T v = rk_stage<T, false>(T(0), c, lapA[q], dt, T(0), T(1));
-      ra[q][A2R] = (z1 && inxy[q]) ? v : c;
-    }
-    // stage 2: B(k+R)
-    if (k >= kc0 - 2 * R) {
-      const int p2 = k + R;
-      const bool z2 = p2 >= zlo && p2 < zhi;
-#pragma unroll
-      for (int q = 0; q < RPW; ++q) {
-        const T uo = ru[q][UR];
-        if (!s2r[q]) {
-          rb[q][BR] = uo;
-          continue;
-        }
-        const int l = row[q] * W + lane;
-        const T c = ra[q][AR];
-        T lap;
-        if constexpr (XDPP >= 1 && R == 2) {  // x neighbours from the wave's own lanes
-          const T m1 = wave_shr1(c), p1 = wave_shl1(c);
-          lap = lap3(cx, FD<4>::d2(wave_shr1(m1), m1, c, p1, wave_shl1(p1)), cy,
-                     FD<4>::d2(pA[l - 2 * W], pA[l - W], c, pA[l + W], pA[l + 2 * W]), cz,
-                     FD<4>::d2(ra[q][A0], ra[q][(PH + 1) & 7], c, ra[q][(PH + 3) & 7], ra[q][A2R]));
-        } else if constexpr (R == 2)
-          lap = lap3(cx, FD<4>::d2(pA[l - 2], pA[l - 1], c, pA[l + 1], pA[l + 2]), cy,
-                     FD<4>::d2(pA[l - 2 * W], pA[l - W], c, pA[l + W], pA[l + 2 * W]), cz,
-                     FD<4>::d2(ra[q][A0], ra[q][(PH + 1) & 7], c, ra[q][(PH + 3) & 7], ra[q][A2R]));
-        else if constexpr (XDPP >= 1)
-          lap = lap3(cx, FD<2>::d2(wave_shr1(c), c, wave_shl1(c)), cy,
-                     FD<2>::d2(pA[l - W], c, pA[l + W]), cz, FD<2>::d2(ra[q][A0], c, ra[q][A2R]));
-        else
-          lap = lap3(cx, FD<2>::d2(pA[l - 1], c, pA[l + 1]), cy,
-                     FD<2>::d2(pA[l - W], c, pA[l + W]), cz, FD<2>::d2(ra[q][A0], c, ra[q][A2R]));
-        const T v = rk_stage<T, true>(uo, c, lap, dt, T(0.75), T(0.25));
-        rb[q][BR] = (z2 && inxy[q] && s2c) ? v : uo;
-      }
-    }
-    // stage 3: u^{n+1}(k)
-    if (k >= kc0) {
-#pragma unroll
-      for (int q = 0; q < RPW; ++q) {
-        if (!s3r[q]) continue;
-        const int l = row[q] * W + lane;
-        const T c = rb[q][B0];
-        const T uo = ru[q][U0];
-        T lap;
-        if constexpr (XDPP >= 1 && R == 2) {
-          const T m1 = wave_shr1(c), p1 = wave_shl1(c);
-          lap = lap3(cx, FD<4>::d2(wave_shr1(m1), m1, c, p1, wave_shl1(p1)), cy,
-                     FD<4>::d2(pB[l - 2 * W], pB[l - W], c, pB[l + W], pB[l + 2 * W]), cz,
-                     FD<4>::d2(rb[q][BM], rb[q][(PH + 7) & 7], c, rb[q][(PH + 1) & 7], rb[q][BR]));
-        } else if constexpr (R == 2)
-          lap = lap3(cx, FD<4>::d2(pB[l - 2], pB[l - 1], c, pB[l + 1], pB[l + 2]), cy,
-                     FD<4>::d2(pB[l - 2 * W], pB[l - W], c, pB[l + W], pB[l + 2 * W]), cz,
-                     FD<4>::d2(rb[q][BM], rb[q][(PH + 7) & 7], c, rb[q][(PH + 1) & 7], rb[q][BR]));
-        else if constexpr (XDPP >= 1)
-          lap = lap3(cx, FD<2>::d2(wave_shr1(c), c, wave_shl1(c)), cy,
-                     FD<2>::d2(pB[l - W], c, pB[l + W]), cz, FD<2>::d2(rb[q][BM], c, rb[q][BR]));
-        else
-          lap = lap3(cx, FD<2>::d2(pB[l - 1], c, pB[l + 1]), cy,
-                     FD<2>::d2(pB[l - W], c, pB[l + W]), cz, FD<2>::d2(rb[q][BM], c, rb[q][BR]));
-        const T v = rk_stage<T, true>(uo, c, lap, dt, third, two3);
-        if (outq[q] && s3c) uout[(int64_t)k * sz + off[q]] = v;
-      }
-    }
-  };
-
-  for (int kb = kst; kb < kc1; kb += 8) {
-    body.template operator()<0>(kb);
-    if (kb + 1 < kc1) body.template operator()<1>(kb + 1);
-    if (kb + 2 < kc1) body.template operator()<2>(kb + 2);
-    if (kb + 3 < kc1) body.template operator()<3>(kb + 3);
-    if (kb + 4 < kc1) body.template operator()<4>(kb + 4);
-    if (kb + 5 < kc1) body.template operator()<5>(kb + 5);
-    if (kb + 6 < kc1) body.template operator()<6>(kb + 6);
-    if (kb + 7 < kc1) body.template operator()<7>(kb + 7);
-  }
-}
-
 // Compact rings: every z-window is a ring of exactly NR = 2R+1 registers (u(k+R..k+3R),
 // A(k..k+2R), B(k-R..k+R)) and the march is unrolled NR times; u(k..k+R-1), still needed
 // as the u^n term of stage 3, move to a short delay line when their ring slot is reused.
@@ -519,7 +74,7 @@ template <typename T, int ORDER, int NW, int RPW, int XDPP, int PD>
 __device__ __forceinline__ void cring_march(
     T* sU, T* sA, T* sB, int tx, int ty, int kc0, int kc1, const T* __restrict__ uin,
     T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz, int nz_alloc, int zlo,
-    int zhi, const Box2& bx, T cx, T cy, T cz, T dt) {
+    int zhi, const Box2& bx, const FdCoef<T>& q1, const FdCoef<T>& q2, const FdCoef<T>& q3) {
   constexpr int R = FD<ORDER>::R;
   constexpr int NR = 2 * R + 1;
   constexpr int W = 64;
@@ -594,17 +149,31 @@ __device__ __forceinline__ void cring_march(
       ra[q][s] = rb[q][s] = T(0);
     }
   }
-  // PD planes of global loads in flight (buffer 0 = the plane consumed next)
-  static_assert(PD == 1 || PD == 2, "prefetch distance 1 or 2");
-  T hv[PD][NH], un[PD][RPW];
+  // Global prefetch, one plane ahead: un = own column of u(k+3R) (enters the ring at the
+  // top of iteration k), hv = rim of u(k+1+2R).  The LDS u plane of iteration k+1 is
+  // written at the END of iteration k and A/B right after they are computed, so the LDS
+  // stores overlap the VALU work instead of forming a burst in front of the barrier.
+  static_assert(PD == 1, "prefetch distance 1");
+  T hv[NH], un[RPW];
+  {  // LDS u plane of the first iteration: u(kst+2R) (ring slot 2R) and its rim
+    T* pU = sU + (kst & 1) * (UH * UW);
 #pragma unroll
-  for (int d = 0; d < PD; ++d) {
+    for (int h = 0; h < NH; ++h) hv[h] = plane(kst + 2 * R)[ho[h]];
 #pragma unroll
-    for (int h = 0; h < NH; ++h) hv[d][h] = plane(kst + d + 2 * R)[ho[h]];
+    for (int q = 0; q < RPW; ++q) pU[(row[q] + R) * UW + lane + R] = ru[q][2 * R];
 #pragma unroll
-    for (int q = 0; q < RPW; ++q) un[d][q] = plane(kst + d + 3 * R)[off[q]];
+    for (int h = 0; h < NH; ++h)
+      if (hl[h] >= 0) pU[hl[h]] = hv[h];
   }
-  const T third = T(1.0 / 3.0), two3 = T(2.0 / 3.0);
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) un[q] = plane(kst + 3 * R)[off[q]];
+  const T third = T(1.0 / 3.0);
+  // A(p) and B(p) stay in LDS slot (p - kst) % NS from the iteration that computes them
+  // to the one that reads them as a centre plane, R iterations later (NS = R+1 slots).
+  // cs = slot of A(k+2R) (written at iteration k); cs+1: A(k+R) (read) = B(k+R)
+  // (written); cs+2: B(k) (read).
+  constexpr int NS = R + 1;
+  int cs = (2 * R) % NS;
 
   auto body = [&]<int PH>(int k) {
     auto sl = [](int d) { return (PH + d + 4 * NR) % NR; };  // slot of plane k+d
@@ -644,7 +213,7 @@ __device__ __forceinline__ void cring_march(
     for (int q = 0; q < RPW; ++q) {
       const T c = ru[q][sl(2 * R)];
       const int l = (row[q] + R) * UW + lane + R;
-      T lap;
+      T acc = fd_ctr(q1.kc, c);  // order: centre, z, x, y (as the per-stage kernel)
       if constexpr (R == 2) {
         T m1, m2, p1v, p2v;
         if constexpr (XDPP >= 2) {
@@ -665,16 +234,16 @@ __device__ __forceinline__ void cring_march(
           p1v = pU[l + 1];
           p2v = pU[l + 2];
         }
-        lap = lap3(cx, FD<4>::d2(m2, m1, c, p1v, p2v), cy,
-                   FD<4>::d2(pU[l - 2 * UW], pU[l - UW], c, pU[l + UW], pU[l + 2 * UW]), cz,
-                   FD<4>::d2(ru[q][sl(R)], ru[q][sl(R + 1)], c, ru[q][sl(3 * R - 1)],
-                             ru[q][sl(3 * R)]));
+        acc = fd4_axis(acc, q1.k[2], ru[q][sl(R)], ru[q][sl(R + 1)], ru[q][sl(3 * R - 1)],
+                       ru[q][sl(3 * R)]);
+        acc = fd4_axis(acc, q1.k[0], m2, m1, p1v, p2v);
+        acc = fd4_axis(acc, q1.k[1], pU[l - 2 * UW], pU[l - UW], pU[l + UW], pU[l + 2 * UW]);
       } else {
-        lap = lap3(cx, FD<2>::d2(pU[l - 1], c, pU[l + 1]), cy,
-                   FD<2>::d2(pU[l - UW], c, pU[l + UW]), cz,
-                   FD<2>::d2(ru[q][sl(R)], c, ru[q][sl(3 * R)]));
+        acc = fd2_axis(acc, q1.k[2], ru[q][sl(R)], ru[q][sl(3 * R)]);
+        acc = fd2_axis(acc, q1.k[0], pU[l - 1], pU[l + 1]);
+        acc = fd2_axis(acc, q1.k[1], pU[l - UW], pU[l + UW]);
       }
-      const T v = rk_stage<T, false>(T(0), c, lap, dt, T(0), T(1));
+      const T v = acc;
       ra[q][sl(2 * R)] = (z1 && inxy[q]) ? v : c;
     }
     // stage 2: B(k+R)
@@ -690,7 +259,7 @@ __device__ __forceinline__ void cring_march(
         }
         const int l = row[q] * W + lane;
         const T c = ra[q][sl(R)];
-        T lap;
+        T acc = fd_ctr(q2.kc, c, T(0.75) * uo);
         if constexpr (R == 2) {
           T m1, m2, p1v, p2v;
           if constexpr (XDPP >= 1) {
@@ -704,16 +273,17 @@ __device__ __forceinline__ void cring_march(
             p1v = pA[l + 1];
             p2v = pA[l + 2];
           }
-          lap = lap3(cx, FD<4>::d2(m2, m1, c, p1v, p2v), cy,
-                     FD<4>::d2(pA[l - 2 * W], pA[l - W], c, pA[l + W], pA[l + 2 * W]), cz,
-                     FD<4>::d2(ra[q][sl(0)], ra[q][sl(1)], c, ra[q][sl(3)], ra[q][sl(4)]));
+          acc = fd4_axis(acc, q2.k[2], ra[q][sl(0)], ra[q][sl(1)], ra[q][sl(3)], ra[q][sl(4)]);
+          acc = fd4_axis(acc, q2.k[0], m2, m1, p1v, p2v);
+          acc = fd4_axis(acc, q2.k[1], pA[l - 2 * W], pA[l - W], pA[l + W], pA[l + 2 * W]);
         } else {
           const T m1 = XDPP >= 1 ? wave_shr1(c) : pA[l - 1];
           const T p1v = XDPP >= 1 ? wave_shl1(c) : pA[l + 1];
-          lap = lap3(cx, FD<2>::d2(m1, c, p1v), cy, FD<2>::d2(pA[l - W], c, pA[l + W]), cz,
-                     FD<2>::d2(ra[q][sl(0)], c, ra[q][sl(2)]));
+          acc = fd2_axis(acc, q2.k[2], ra[q][sl(0)], ra[q][sl(2)]);
+          acc = fd2_axis(acc, q2.k[0], m1, p1v);
+          acc = fd2_axis(acc, q2.k[1], pA[l - W], pA[l + W]);
         }
-        const T v = rk_stage<T, true>(uo, c, lap, dt, T(0.75), T(0.25));
+        const T v = acc;
         rb[q][sl(R)] = (z2 && inxy[q] && s2c) ? v : uo;
       }
     }
@@ -725,7 +295,7 @@ __device__ __forceinline__ void cring_march(
         const int l = row[q] * W + lane;
         const T c = rb[q][sl(0)];
         const T uo = dl[q][0];
-        T lap;
+        T acc = fd_ctr(q3.kc, c, third * uo);
         if constexpr (R == 2) {
           T m1, m2, p1v, p2v;
           if constexpr (XDPP >= 1) {
@@ -739,16 +309,17 @@ __device__ __forceinline__ void cring_march(
             p1v = pB[l + 1];
             p2v = pB[l + 2];
           }
-          lap = lap3(cx, FD<4>::d2(m2, m1, c, p1v, p2v), cy,
-                     FD<4>::d2(pB[l - 2 * W], pB[l - W], c, pB[l + W], pB[l + 2 * W]), cz,
-                     FD<4>::d2(rb[q][sl(-2)], rb[q][sl(-1)], c, rb[q][sl(1)], rb[q][sl(2)]));
+          acc = fd4_axis(acc, q3.k[2], rb[q][sl(-2)], rb[q][sl(-1)], rb[q][sl(1)], rb[q][sl(2)]);
+          acc = fd4_axis(acc, q3.k[0], m2, m1, p1v, p2v);
+          acc = fd4_axis(acc, q3.k[1], pB[l - 2 * W], pB[l - W], pB[l + W], pB[l + 2 * W]);
         } else {
           const T m1 = XDPP >= 1 ? wave_shr1(c) : pB[l - 1];
           const T p1v = XDPP >= 1 ? wave_shl1(c) : pB[l + 1];
-          lap = lap3(cx, FD<2>::d2(m1, c, p1v), cy, FD<2>::d2(pB[l - W], c, pB[l + W]), cz,
-                     FD<2>::d2(rb[q][sl(-1)], c, rb[q][sl(1)]));
+          acc = fd2_axis(acc, q3.k[2], rb[q][sl(-1)], rb[q][sl(1)]);
+          acc = fd2_axis(acc, q3.k[0], m1, p1v);
+          acc = fd2_axis(acc, q3.k[1], pB[l - W], pB[l + W]);
         }
-        const T v = rk_stage<T, true>(uo, c, lap, dt, third, two3);
+        const T v = acc;
         if (outq[q] && s3c) uout[(int64_t)k * sz + off[q]] = v;
       }
     }
@@ -770,11 +341,24 @@ __device__ __forceinline__ void cring_march(
   }
 }
 
+// Waves per SIMD to budget registers for (fp64): as many workgroups as the LDS admits
+// (FD4 16 waves: 1/CU -> 4; FD2 12 waves: 2/CU -> 6).  Without it the compiler spent 86
+// VGPRs on the FD2 step and lost the second workgroup per CU (-25 %).
+template <typename T, int ORDER, int NW, int RPW>
+constexpr int cring_min_waves() {
+  using Gm = CringGeom<ORDER, NW, RPW>;
+  constexpr int lds = (int)sizeof(T) * 2 * (Gm::LDS_U + 2 * Gm::LDS_AB);
+  constexpr int wgs = 163840 / lds;
+  constexpr int w = wgs * NW / 4;
+  return sizeof(T) == 8 ? (w > 8 ? 8 : (w < 1 ? 1 : w)) : 1;
+}
+
 template <typename T, int ORDER, int NW, int RPW, int XDPP, int PD, bool PERSIST>
-__global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
+__global__ __launch_bounds__(64 * NW) __attribute__((
+    amdgpu_waves_per_eu(cring_min_waves<T, ORDER, NW, RPW>()))) void diffusion3d_step_cring_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
     int nz_alloc, int k0, int k1, int k0b, int k1b, StepSched sc, int zlo, int zhi,
-    Box2 bx, T cx, T cy, T cz, T dt) {
+    Box2 bx, FdCoef<T> q1, FdCoef<T> q2, FdCoef<T> q3) {
   using Gm = CringGeom<ORDER, NW, RPW>;
   __shared__ T sU[2 * Gm::LDS_U];
   __shared__ T sA[2 * Gm::LDS_AB];
@@ -786,8 +370,8 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
     const int kc0 = second ? k0b + (tile.z - sc.gza) * sc.zchunk : k0 + tile.z * sc.zchunk;
     const int kc1 = min(kc0 + sc.zchunk, second ? k1b : k1);
     cring_march<T, ORDER, NW, RPW, XDPP, PD>(sU, sA, sB, tile.x, tile.y, kc0, kc1, uin, uout,
-                                             nx, ny, sy, sz, nz_alloc, zlo, zhi, bx, cx, cy,
-                                             cz, dt);
+                                             nx, ny, sy, sz, nz_alloc, zlo, zhi, bx, q1, q2,
+                                             q3);
   } else {
     // 1-D grid; tile.x = this group's XCD-contiguous logical id, so the groups of one XCD
     // march neighbouring tiles.  Group g owns the linear planes [s, e), s = g per +
@@ -804,7 +388,7 @@ __global__ __launch_bounds__(64 * NW) void diffusion3d_step_cring_kernel(
       __syncthreads();  // nobody still reads the previous segment's last LDS planes
       cring_march<T, ORDER, NW, RPW, XDPP, PD>(sU, sA, sB, t % sc.gx, t / sc.gx, kc0,
                                                kc0 + (p1 - p0), uin, uout, nx, ny, sy, sz,
-                                               nz_alloc, zlo, zhi, bx, cx, cy, cz, dt);
+                                               nz_alloc, zlo, zhi, bx, q1, q2, q3);
       s += p1 - p0;
     }
   }
@@ -824,7 +408,7 @@ struct SArgs {
   int flags;  // ADVDIFF_EXCLUSIVE: persistent schedule allowed
 };
 
-template <typename T, int ORDER, int NW, int RPW, int RING, int PD = 1, int XDPP = 0>
+template <typename T, int ORDER, int NW, int RPW, int PD = 1, int XDPP = 0>
 static hipError_t launch_step(const SArgs& a) {
   constexpr int R = ORDER / 2;
   constexpr int TX = 64 - 4 * R, TY = NW * RPW - 4 * R;
@@ -834,13 +418,7 @@ static hipError_t launch_step(const SArgs& a) {
   static const int target = knob("STEP_TARGET_BLOCKS", 0);  // >0: legacy fixed target
   static const int per_cu = [] {
     int nb = 0;
-    const void* fn;
-    if constexpr (RING == 2)
-      fn = (const void*)diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD, false>;
-    else if constexpr (RING == 1)
-      fn = (const void*)diffusion3d_step_ring_kernel<T, ORDER, NW, RPW, PD, XDPP>;
-    else
-      fn = (const void*)diffusion3d_step_kernel<T, ORDER, NW, RPW>;
+    const void* fn = (const void*)diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD, false>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * NW, 0) != hipSuccess || nb < 1)
       nb = 1;
     return nb;
@@ -853,8 +431,7 @@ static hipError_t launch_step(const SArgs& a) {
   StepSched sc{gx, gy, 0, 0, 0, 0};
   dim3 grid;
   const long long L = (long long)gx * gy * (na + nb);
-  const bool persistent =
-      RING == 2 && persist && (a.flags & ADVDIFF_EXCLUSIVE) && L < (1LL << 31);
+  const bool persistent = persist && (a.flags & ADVDIFF_EXCLUSIVE) && L < (1LL << 31);
   if (persistent) {
     // one round of resident groups; small launches keep >= minseg planes per group
     const long long G = std::max(1LL, std::min(slots, (L + minseg - 1) / minseg));
@@ -873,44 +450,39 @@ static hipError_t launch_step(const SArgs& a) {
     sc.zchunk = zc;
     grid = dim3(gx, gy, sc.gza + (nb > 0 ? div_up(nb, zc) : 0));
   }
-  const double s = ORDER == 4 ? 1.0 / 12.0 : 1.0;
+  // SSP-RK3 stage coefficients b = 1, 1/4, 2/3: exactly the per-stage path's (FdCoef)
+  const FdCoef<T> q1 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 1.0, true);
+  const FdCoef<T> q2 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 0.25, true);
+  const FdCoef<T> q3 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 2.0 / 3.0, true);
 #define STEP_ARGS                                                                              \
   grid, dim3(64, NW, 1), 0, a.st, (const T*)a.uin, (T*)a.uout, a.nx, a.ny, a.sy, a.sz,        \
-      a.nz_alloc, a.k0, a.k1, a.k0b, a.k1b, sc, a.zlo, a.zhi, a.bx, T(a.cx * s), T(a.cy * s),  \
-      T(a.cz * s), T(a.dt)
-  if constexpr (RING == 2) {
-    if (persistent)
-      hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD, true>),
-                         STEP_ARGS);
-    else
-      hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD, false>),
-                         STEP_ARGS);
-  } else if constexpr (RING == 1)
-    hipLaunchKernelGGL((diffusion3d_step_ring_kernel<T, ORDER, NW, RPW, PD, XDPP>), STEP_ARGS);
+      a.nz_alloc, a.k0, a.k1, a.k0b, a.k1b, sc, a.zlo, a.zhi, a.bx, q1, q2, q3
+  if (persistent)
+    hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD, true>),
+                       STEP_ARGS);
   else
-    hipLaunchKernelGGL((diffusion3d_step_kernel<T, ORDER, NW, RPW>), STEP_ARGS);
+    hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD, false>),
+                       STEP_ARGS);
 #undef STEP_ARGS
   return hipGetLastError();
 }
 
-// Tile/schedule variants (A/B via ADVDIFF_STEP_CFG; measurements in profiles/).
+// Tile/schedule variants (A/B via ADVDIFF_STEP_CFG; measurements in profiles/).  The
+// plain register-shifting and 8-slot-ring kernels measured in profiles/kbench_fused_*.log
+// were slower and are gone; the compact-ring variants stay selectable.
 template <typename T, int ORDER>
 static hipError_t dispatch_step(int cfg, const SArgs& a) {
-#define STEPV(NW, RPW, RING, ...) return launch_step<T, ORDER, NW, RPW, RING, ##__VA_ARGS__>(a)
+#define STEPV(NW, RPW, ...) return launch_step<T, ORDER, NW, RPW, ##__VA_ARGS__>(a)
   switch (cfg) {
-    // measured alternatives (profiles/kbench_fused_*.log); rejected ones were removed
-    case 1: STEPV(12, 2, 0);           // plain: z-windows shifted by register moves
-    case 10: STEPV(12, 2, 1);          // 8-slot rings, all x neighbours from LDS
-    case 24: STEPV(12, 2, 1, 1, 1);    // 8-slot rings + DPP x neighbours in stages 2/3
-    case 14: STEPV(12, 2, 2, 1, 1);    // compact rings, 12 waves, DPP stages 2/3
-    case 15: STEPV(12, 2, 2, 1, 2);    // compact rings, 12 waves, DPP stages 1-3
-    case 16: STEPV(16, 2, 2, 1, 1);    // compact rings, 16 waves, DPP stages 2/3
-    case 19: STEPV(16, 2, 2, 2, 2);    // + prefetch distance 2
-    default:  // compact rings; FD4: 16 waves, DPP in all stages; FD2: 12 waves, stages 2/3
+    case 14: STEPV(12, 2, 1, 1);    // 12 waves, DPP stages 2/3
+    case 15: STEPV(12, 2, 1, 2);    // 12 waves, DPP stages 1-3
+    case 16: STEPV(16, 2, 1, 1);    // 16 waves, DPP stages 2/3
+    case 19: STEPV(16, 2, 2, 2);    // + prefetch distance 2
+    default:  // FD4: 16 waves, DPP in all stages; FD2: 12 waves, stages 2/3
       if constexpr (ORDER == 4) {
-        STEPV(16, 2, 2, 1, 2);
+        STEPV(16, 2, 1, 2);
       } else {
-        STEPV(12, 2, 2, 1, 1);
+        STEPV(12, 2, 1, 1);
       }
   }
 #undef STEPV
