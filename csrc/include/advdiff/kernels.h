@@ -173,6 +173,9 @@ int advdiff_device_info(int dev, int64_t* out, int n);
 int advdiff_peer_info(int a, int b, int* can_access, int* link_type, int* hops);
 // Library identification (build flags, arch) for diagnostics.
 const char* advdiff_build_info(void);
+// sha256 (first 16 hex digits) of the kernel sources this library was built from
+// (csrc/Makefile SRC_HASH); the Python loader refuses a library that does not match the tree
+const char* advdiff_source_hash(void);
 
 #ifdef __cplusplus
 }

@@ -70,7 +70,7 @@ struct CringGeom {
 
 // One z segment [kc0, kc1) of output tile (tx, ty): warm-up + march (the whole
 // algorithm; sU/sA/sB are the workgroup's double-buffered LDS planes).
-template <typename T, int ORDER, int NW, int RPW, int XDPP, int PD>
+template <typename T, int ORDER, int NW, int RPW, int XDPP>
 __device__ __forceinline__ void cring_march(
     T* sU, T* sA, T* sB, int tx, int ty, int kc0, int kc1, const T* __restrict__ uin,
     T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz, int nz_alloc, int zlo,
@@ -153,7 +153,6 @@ __device__ __forceinline__ void cring_march(
   // top of iteration k), hv = rim of u(k+1+2R).  The LDS u plane of iteration k+1 is
   // written at the END of iteration k and A/B right after they are computed, so the LDS
   // stores overlap the VALU work instead of forming a burst in front of the barrier.
-  static_assert(PD == 1, "prefetch distance 1");
   T hv[NH], un[RPW];
   {  // LDS u plane of the first iteration: u(kst+2R) (ring slot 2R) and its rim
     T* pU = sU + (kst & 1) * (UH * UW);
@@ -168,12 +167,6 @@ __device__ __forceinline__ void cring_march(
 #pragma unroll
   for (int q = 0; q < RPW; ++q) un[q] = plane(kst + 3 * R)[off[q]];
   const T third = T(1.0 / 3.0);
-  // A(p) and B(p) stay in LDS slot (p - kst) % NS from the iteration that computes them
-  // to the one that reads them as a centre plane, R iterations later (NS = R+1 slots).
-  // cs = slot of A(k+2R) (written at iteration k); cs+1: A(k+R) (read) = B(k+R)
-  // (written); cs+2: B(k) (read).
-  constexpr int NS = R + 1;
-  int cs = (2 * R) % NS;
 
   auto body = [&]<int PH>(int k) {
     auto sl = [](int d) { return (PH + d + 4 * NR) % NR; };  // slot of plane k+d
@@ -185,25 +178,19 @@ __device__ __forceinline__ void cring_march(
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
       dl[q][R - 1] = ru[q][UIN];  // u(k+R-1) -> delay line
-      ru[q][UIN] = un[0][q];
+      ru[q][UIN] = un[q];
       pU[(row[q] + R) * UW + lane + R] = ru[q][sl(2 * R)];
       pA[row[q] * W + lane] = ra[q][sl(R)];
       pB[row[q] * W + lane] = rb[q][sl(0)];
     }
 #pragma unroll
     for (int h = 0; h < NH; ++h)
-      if (hl[h] >= 0) pU[hl[h]] = hv[0][h];
-    if constexpr (PD == 2) {
+      if (hl[h] >= 0) pU[hl[h]] = hv[h];
+    if (k + 1 < kc1) {
 #pragma unroll
-      for (int h = 0; h < NH; ++h) hv[0][h] = hv[1][h];
+      for (int h = 0; h < NH; ++h) hv[h] = plane(k + 1 + 2 * R)[ho[h]];
 #pragma unroll
-      for (int q = 0; q < RPW; ++q) un[0][q] = un[1][q];
-    }
-    if (k + PD < kc1) {
-#pragma unroll
-      for (int h = 0; h < NH; ++h) hv[PD - 1][h] = plane(k + PD + 2 * R)[ho[h]];
-#pragma unroll
-      for (int q = 0; q < RPW; ++q) un[PD - 1][q] = plane(k + PD + 3 * R)[off[q]];
+      for (int q = 0; q < RPW; ++q) un[q] = plane(k + 1 + 3 * R)[off[q]];
     }
     __syncthreads();
     // stage 1: A(k+2R)
@@ -353,7 +340,7 @@ constexpr int cring_min_waves() {
   return sizeof(T) == 8 ? (w > 8 ? 8 : (w < 1 ? 1 : w)) : 1;
 }
 
-template <typename T, int ORDER, int NW, int RPW, int XDPP, int PD, bool PERSIST>
+template <typename T, int ORDER, int NW, int RPW, int XDPP, bool PERSIST>
 __global__ __launch_bounds__(64 * NW) __attribute__((
     amdgpu_waves_per_eu(cring_min_waves<T, ORDER, NW, RPW>()))) void diffusion3d_step_cring_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
@@ -369,7 +356,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((
     const bool second = tile.z >= sc.gza;
     const int kc0 = second ? k0b + (tile.z - sc.gza) * sc.zchunk : k0 + tile.z * sc.zchunk;
     const int kc1 = min(kc0 + sc.zchunk, second ? k1b : k1);
-    cring_march<T, ORDER, NW, RPW, XDPP, PD>(sU, sA, sB, tile.x, tile.y, kc0, kc1, uin, uout,
+    cring_march<T, ORDER, NW, RPW, XDPP>(sU, sA, sB, tile.x, tile.y, kc0, kc1, uin, uout,
                                              nx, ny, sy, sz, nz_alloc, zlo, zhi, bx, q1, q2,
                                              q3);
   } else {
@@ -386,7 +373,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((
       if (p0 < na) p1 = min(p1, na);  // a segment never spans both plane ranges
       const int kc0 = p0 < na ? k0 + p0 : k0b + (p0 - na);
       __syncthreads();  // nobody still reads the previous segment's last LDS planes
-      cring_march<T, ORDER, NW, RPW, XDPP, PD>(sU, sA, sB, t % sc.gx, t / sc.gx, kc0,
+      cring_march<T, ORDER, NW, RPW, XDPP>(sU, sA, sB, t % sc.gx, t / sc.gx, kc0,
                                                kc0 + (p1 - p0), uin, uout, nx, ny, sy, sz,
                                                nz_alloc, zlo, zhi, bx, q1, q2, q3);
       s += p1 - p0;
@@ -408,7 +395,7 @@ struct SArgs {
   int flags;  // ADVDIFF_EXCLUSIVE: persistent schedule allowed
 };
 
-template <typename T, int ORDER, int NW, int RPW, int PD = 1, int XDPP = 0>
+template <typename T, int ORDER, int NW, int RPW, int XDPP = 0>
 static hipError_t launch_step(const SArgs& a) {
   constexpr int R = ORDER / 2;
   constexpr int TX = 64 - 4 * R, TY = NW * RPW - 4 * R;
@@ -418,7 +405,7 @@ static hipError_t launch_step(const SArgs& a) {
   static const int target = knob("STEP_TARGET_BLOCKS", 0);  // >0: legacy fixed target
   static const int per_cu = [] {
     int nb = 0;
-    const void* fn = (const void*)diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD, false>;
+    const void* fn = (const void*)diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, false>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * NW, 0) != hipSuccess || nb < 1)
       nb = 1;
     return nb;
@@ -458,10 +445,10 @@ static hipError_t launch_step(const SArgs& a) {
   grid, dim3(64, NW, 1), 0, a.st, (const T*)a.uin, (T*)a.uout, a.nx, a.ny, a.sy, a.sz,        \
       a.nz_alloc, a.k0, a.k1, a.k0b, a.k1b, sc, a.zlo, a.zhi, a.bx, q1, q2, q3
   if (persistent)
-    hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD, true>),
+    hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, true>),
                        STEP_ARGS);
   else
-    hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, PD, false>),
+    hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, false>),
                        STEP_ARGS);
 #undef STEP_ARGS
   return hipGetLastError();
@@ -474,15 +461,14 @@ template <typename T, int ORDER>
 static hipError_t dispatch_step(int cfg, const SArgs& a) {
 #define STEPV(NW, RPW, ...) return launch_step<T, ORDER, NW, RPW, ##__VA_ARGS__>(a)
   switch (cfg) {
-    case 14: STEPV(12, 2, 1, 1);    // 12 waves, DPP stages 2/3
-    case 15: STEPV(12, 2, 1, 2);    // 12 waves, DPP stages 1-3
-    case 16: STEPV(16, 2, 1, 1);    // 16 waves, DPP stages 2/3
-    case 19: STEPV(16, 2, 2, 2);    // + prefetch distance 2
+    case 14: STEPV(12, 2, 1);    // 12 waves, DPP stages 2/3
+    case 15: STEPV(12, 2, 2);    // 12 waves, DPP stages 1-3
+    case 16: STEPV(16, 2, 1);    // 16 waves, DPP stages 2/3
     default:  // FD4: 16 waves, DPP in all stages; FD2: 12 waves, stages 2/3
       if constexpr (ORDER == 4) {
-        STEPV(16, 2, 1, 2);
+        STEPV(16, 2, 2);
       } else {
-        STEPV(12, 2, 1, 1);
+        STEPV(12, 2, 1);
       }
   }
 #undef STEPV

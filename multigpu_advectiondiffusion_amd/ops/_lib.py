@@ -9,12 +9,14 @@ on a GPU box has provably run the native kernels.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 import threading
 from pathlib import Path
 
 _LIB_DIR = Path(__file__).resolve().parent.parent / "lib"
 LIB_PATH = Path(os.environ.get("ADVDIFF_LIB", _LIB_DIR / "libadvdiff.so"))
+CSRC = Path(__file__).resolve().parents[2] / "csrc"
 
 _lock = threading.Lock()
 _lib = None
@@ -72,6 +74,22 @@ for _k in ("advdiff_diffusion3d_stage", "advdiff_diffusion2d_stage", "advdiff_bu
     _SIGS[_k + "_ls"] = _SIGS[_k]
 
 
+def source_hash() -> str | None:
+    """Hash of the library sources in this tree, exactly as ``csrc/Makefile`` computes
+    SRC_HASH (sha256 of the contents of kernels/*.hip, kernels/*.hpp and
+    include/advdiff/kernels.h concatenated in sorted relative-path order; 16 hex digits).
+    None when the tree carries no csrc/ (an installed copy)."""
+    kdir = CSRC / "kernels"
+    if not kdir.is_dir():
+        return None
+    rel = sorted([f"kernels/{p.name}" for p in kdir.iterdir() if p.suffix in (".hip", ".hpp")]
+                 + ["include/advdiff/kernels.h"])
+    h = hashlib.sha256()
+    for r in rel:
+        h.update((CSRC / r).read_bytes())
+    return h.hexdigest()[:16]
+
+
 def _load():
     global _lib, _err
     with _lock:
@@ -84,6 +102,18 @@ def _load():
             lib = ctypes.CDLL(str(LIB_PATH))
         except OSError as e:  # missing HIP runtime etc.
             _err = f"failed to load {LIB_PATH}: {e}"
+            return None
+        # A library built from other sources than this tree's is refused: every GPU result
+        # must come from code that is in the tree (ADVDIFF_ALLOW_STALE=1 overrides, for A/B).
+        try:
+            lib.advdiff_source_hash.restype = ctypes.c_char_p
+            built = lib.advdiff_source_hash().decode()
+        except AttributeError:  # built before the hash existed
+            built = "unknown"
+        tree = source_hash()
+        if tree is not None and built != tree and os.environ.get("ADVDIFF_ALLOW_STALE") != "1":
+            _err = (f"{LIB_PATH} is stale: built from sources {built}, tree is {tree} "
+                    f"(rebuild with `make -C csrc`)")
             return None
         for name, args in _SIGS.items():
             fn = getattr(lib, name)
@@ -122,4 +152,9 @@ def check(code: int, what: str) -> None:
 
 
 def build_info() -> str:
-    return require().advdiff_build_info().decode()
+    lib = require()
+    return f"{lib.advdiff_build_info().decode()} [src {lib.advdiff_source_hash().decode()}]"
+
+
+def library_hash() -> str:
+    return require().advdiff_source_hash().decode()

@@ -21,3 +21,21 @@ def test_runtime_host_asan():
                        timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "runtime host tests: OK" in r.stdout
+
+
+def test_library_matches_tree():
+    """The in-tree libadvdiff.so must be built from the kernel sources in this tree: its
+    compiled-in source hash (csrc/Makefile SRC_HASH) equals the hash of csrc/ now, and the
+    Makefile and the Python loader compute that hash identically."""
+    from multigpu_advectiondiffusion_amd.ops import _lib
+    r = subprocess.run(["make", "-s", "-C", str(CSRC), "hash"], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == _lib.source_hash()
+    if not _lib.LIB_PATH.exists():
+        pytest.skip("libadvdiff.so not built")
+    if not _lib.available():
+        err = _lib.load_error() or ""
+        assert "stale" not in err, err
+        pytest.skip(f"library not loadable here: {err}")
+    assert _lib.library_hash() == _lib.source_hash()
