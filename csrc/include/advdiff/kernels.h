@@ -171,6 +171,12 @@ int advdiff_debug_print(int dtype, const void* u, int64_t sy, int64_t sz, int i0
 int advdiff_device_info(int dev, int64_t* out, int n);
 // Peer topology: can_access (hipDeviceCanAccessPeer), HSA link type (4 = xGMI), hop count.
 int advdiff_peer_info(int a, int b, int* can_access, int* link_type, int* hops);
+// Select the 3-D fused-step kernel variant (0 = default; A/B and tests); returns the
+// previous value.  Initialised from ADVDIFF_STEP_CFG.
+int advdiff_set_step_cfg(int cfg);
+// Allow (1) the persistent schedule for ADVDIFF_EXCLUSIVE 3-D fused launches (default 0:
+// grid of z chunks); returns the previous value.  Initialised from ADVDIFF_STEP_PERSIST.
+int advdiff_set_step_persist(int on);
 // Library identification (build flags, arch) for diagnostics.
 const char* advdiff_build_info(void);
 // sha256 (first 16 hex digits) of the kernel sources this library was built from

@@ -25,6 +25,8 @@
 #include "launch.hpp"
 #include "advdiff/kernels.h"
 
+#include <utility>
+
 namespace advdiff {
 
 // x/y bounds of a fused-step launch (view coordinates): cells outside [xa0,xa1) x
@@ -328,6 +330,363 @@ __device__ __forceinline__ void cring_march(
   }
 }
 
+// ---------------------------------------------------------------------------------
+// v3 march: the same algorithm (compact rings, trapezoid, one barrier per plane) with
+// the code shaped for the gfx950 issue model:
+//   * the wave index is made scalar (readfirstlane), so every per-row condition is a
+//     scalar branch and never an exec-mask region;
+//   * ONE shared LDS block (U0 U1 | A0 A1 B0 B1) and one base VGPR per row and plane
+//     kind: every neighbour, the buffer set and the A->B distance are immediate
+//     ds_read/ds_write offsets (the march is unrolled 2 NR times, so the set is static);
+//   * stage 1 reads its x and y neighbours from the haloed u plane (no divergent edge
+//     lanes); stages 2/3 take y from LDS and x by DPP (XS = 1) or LDS (XS = 0);
+//   * global traffic uses a scalar plane base + a 32-bit per-lane byte offset (saddr
+//     form: no 64-bit VALU address math in the march);
+//   * PF: prefetch distance in planes (1 or 2).
+// The arithmetic (fd_ctr / fd4_axis / fd2_axis in the fixed order centre, z, x, y) is
+// unchanged, so v3 is bit-identical to the cring march and to the per-stage kernels.
+// ---------------------------------------------------------------------------------
+template <typename T, int ORDER, int NW, int RPW>
+struct V3Geom {
+  static constexpr int R = FD<ORDER>::R;
+  static constexpr int W = 64;
+  static constexpr int S1R = NW * RPW;
+  static constexpr int UW = W + 2 * R, UH = S1R + 2 * R;
+  static constexpr int USET = UH * UW;             // elements per u plane buffer
+  static constexpr int ASET = S1R * W + 2 * R;      // A/B plane buffer (+R pad each side)
+  static constexpr int OFF_A = 2 * USET;            // element offset of A0 in the block
+  static constexpr int OFF_B = OFF_A + 2 * ASET;    // B0
+  static constexpr int TOTAL = OFF_B + 2 * ASET;
+};
+
+template <typename T>
+__device__ __forceinline__ T lds_ld(const char* base, int byte_off) {
+  return *(const T*)(base + byte_off);
+}
+template <typename T>
+__device__ __forceinline__ void lds_st(char* base, int byte_off, T v) {
+  *(T*)(base + byte_off) = v;
+}
+// Plane-relative global access through a raw buffer resource: the plane base lives in
+// the (scalar) descriptor and the per-lane part is a 32-bit byte offset, so a load or
+// store costs no VALU address arithmetic (gfx9 descriptor word 3 = 0x00020000; the range
+// check is disabled by num_records = 2^32 - 1; offsets stay inside one plane < 2^31 B).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
+}
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ __forceinline__ T gld(__amdgpu_buffer_rsrc_t r, uint32_t boff) {
+  if constexpr (sizeof(T) == 8)
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, (int)boff, 0, 0));
+  else
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, (int)boff, 0, 0));
+}
+template <typename T>
+__device__ __forceinline__ void gst(__amdgpu_buffer_rsrc_t r, uint32_t boff, T v) {
+  if constexpr (sizeof(T) == 8)
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)boff, 0, 0);
+  else
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)boff, 0, 0);
+}
+// keep a value computed on every lane (no exec-masked skip of the computation): the
+// frozen-cell choice below it must be a v_cndmask, not a branch around the stencil
+template <typename T>
+__device__ __forceinline__ T pin(T v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+template <typename T, int ORDER, int NW, int RPW, int XS, int PF, bool SEP>
+__device__ __forceinline__ void v3_march(
+    T* lds, int tx, int ty, int kc0, int kc1, const T* __restrict__ uin,
+    T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz, int nz_alloc, int zlo,
+    int zhi, const Box2& bx, const FdCoef<T>& q1, const FdCoef<T>& q2, const FdCoef<T>& q3) {
+  using G = V3Geom<T, ORDER, NW, RPW>;
+  constexpr int R = G::R, NR = 2 * R + 1, W = G::W, S1R = G::S1R, UW = G::UW, UH = G::UH;
+  constexpr int TX = W - 4 * R, TY = S1R - 4 * R;
+  constexpr int NT = 64 * NW;
+  constexpr int NHALO = UW * UH - W * S1R;
+  constexpr int NH = (NHALO + NT - 1) / NT;
+  constexpr int E = (int)sizeof(T);
+  constexpr int USETB = G::USET * E, ASETB = G::ASET * E, ABB = (G::OFF_B - G::OFF_A) * E;
+  static_assert(TY > 0, "tile too small");
+  static_assert(ASETB + ABB + (2 * R * W + 2 * R) * E < 65536, "A/B offsets must fit the 16-bit DS offset");
+  static_assert(USETB + (2 * R * UW + 2 * R) * E < 65536, "u offsets must fit");
+
+  const int lane = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
+  const int tid = w * 64 + lane;
+  const int i0 = tx * TX, j0 = ty * TY;
+  const int x = i0 - 2 * R + lane;
+  const bool xin = x >= bx.xa0 && x < bx.xa1;
+  const bool xout = x >= bx.xo0 && x < bx.xo1;
+  const bool s2c = lane >= R && lane < W - R;
+  const bool s3c = lane >= 2 * R && lane < W - 2 * R;
+  const int xc = clampi(x, 0, nx - 1);
+  char* lb = (char*)lds;
+  // SEP: a compiler memory fence before every LDS read keeps each one a separate
+  // ds_read_b64 (2 LDS cycles per wave) instead of a merged ds_read2_b64 (8 cycles for
+  // the same two values: half the LDS read throughput, MI355X_MICROARCH.md §LDS)
+  auto ld = [&](int off) {
+    if constexpr (SEP) asm volatile("" ::: "memory");
+    return lds_ld<T>(lb, off);
+  };
+
+  // per row: global byte offset, LDS bases (u neighbourhood top-left; A own cell; A
+  // neighbourhood top-left for stages 2/3), lane masks
+  uint32_t goff[RPW];
+  int ub[RPW], aw[RPW], ar[RPW];
+  bool m1[RPW], m2[RPW], m3[RPW];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const int row = w + q * NW;
+    const int y = j0 - 2 * R + row;
+    const bool inxy = xin && y >= bx.ya0 && y < bx.ya1;
+    m1[q] = inxy;
+    m2[q] = inxy && s2c;
+    m3[q] = inxy && xout && y >= bx.yo0 && y < bx.yo1 && s3c;
+    goff[q] = (uint32_t)(clampi(y, 0, ny - 1) * (int)sy + xc) * (uint32_t)E;
+    ub[q] = (row * UW + lane) * E;                            // u(row-R+R.., lane-R+R..)
+    aw[q] = (G::OFF_A + R + row * W + lane) * E;               // A own cell, set 0
+    const int rc = clampi(row, R, S1R - R - 1);                 // in-bounds for masked rows
+    ar[q] = (G::OFF_A + R + (rc - R) * W + lane - (XS ? 0 : R)) * E;
+  }
+  uint32_t hoff[NH];
+  int hl[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    int idx = tid + h * NT;
+    hl[h] = -1;
+    hoff[h] = 0;
+    if (idx < NHALO) {
+      int ur, uc;
+      if (idx < R * UW) {
+        ur = idx / UW;
+        uc = idx - ur * UW;
+      } else if ((idx -= R * UW) < R * UW) {
+        ur = S1R + R + idx / UW;
+        uc = idx % UW;
+      } else {
+        idx -= R * UW;
+        ur = R + idx / (2 * R);
+        const int cc = idx % (2 * R);
+        uc = cc < R ? cc : W + cc;
+      }
+      hl[h] = (ur * UW + uc) * E;
+      hoff[h] = (uint32_t)(clampi(j0 - 3 * R + ur, 0, ny - 1) * (int)sy +
+                           clampi(i0 - 3 * R + uc, 0, nx - 1)) * (uint32_t)E;
+    }
+  }
+  const int64_t szb = sz * E;
+  auto plane = [&](int k) {  // buffer descriptor of plane k (clamped into the allocation)
+    return plane_rsrc((const char*)uin + (int64_t)clampi(k, 0, nz_alloc - 1) * szb);
+  };
+
+  T ru[RPW][NR], ra[RPW][NR], rb[RPW][NR], dl[RPW][R];
+  const int kst = kc0 - 4 * R;
+  {
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+#pragma unroll
+      for (int d = 0; d < R - 1; ++d) dl[q][d] = gld<T>(plane(kst + d), goff[q]);
+#pragma unroll
+      for (int s = 0; s < NR; ++s) {
+        const int pl = kst + R - 1 + s;
+        ru[q][pl - kst < NR ? pl - kst : pl - kst - NR] = gld<T>(plane(pl), goff[q]);
+        ra[q][s] = rb[q][s] = T(0);
+      }
+    }
+  }
+  // prefetch ring: slot f holds the planes of iteration k + f (f < PF): un = own column
+  // of u(k+f+3R) (enters the register ring), hv = the LDS rim of u(k+f+2R)
+  T hv[PF][NH], un[PF][RPW];
+#pragma unroll
+  for (int f = 0; f < PF; ++f) {  // planes of iterations kst .. kst+PF-1
+    const auto p2 = plane(kst + f + 2 * R);
+    const auto p3 = plane(kst + f + 3 * R);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) hv[f][h] = gld<T>(p2, hoff[h]);
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) un[f][q] = gld<T>(p3, goff[q]);
+  }
+  const T third = T(1.0 / 3.0);
+
+  // PH in [0, 2 NR): ring slots and the LDS buffer set (PH & 1) are compile-time
+  auto body = [&]<int PH>(int k) {
+    auto sl = [](int d) { return (PH + d + 4 * NR) % NR; };
+    constexpr int UIN = (PH + 3 * R) % NR;
+    constexpr int SET = PH & 1;
+    constexpr int UO = SET * USETB, AO = SET * ASETB;
+    // ---- top: new u plane enters the ring; LDS planes u(k+2R), A(k+R), B(k) ----
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      dl[q][R - 1] = ru[q][UIN];
+      ru[q][UIN] = un[0][q];
+      lds_st<T>(lb, ub[q] + UO + (R * UW + R) * E, ru[q][sl(2 * R)]);
+      lds_st<T>(lb, aw[q] + AO, ra[q][sl(R)]);
+      lds_st<T>(lb, aw[q] + AO + ABB, rb[q][sl(0)]);
+    }
+#pragma unroll
+    for (int h = 0; h < NH; ++h)  // the rim of u(k+2R)
+      if (hl[h] >= 0) lds_st<T>(lb, hl[h] + UO, hv[0][h]);
+    // shift the prefetch ring, issue plane k+PF
+#pragma unroll
+    for (int f = 0; f + 1 < PF; ++f) {
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) un[f][q] = un[f + 1][q];
+#pragma unroll
+      for (int h = 0; h < NH; ++h) hv[f][h] = hv[f + 1][h];
+    }
+    {
+      const auto p2 = plane(k + PF + 2 * R);
+      const auto p3 = plane(k + PF + 3 * R);
+#pragma unroll
+      for (int h = 0; h < NH; ++h) hv[PF - 1][h] = gld<T>(p2, hoff[h]);
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) un[PF - 1][q] = gld<T>(p3, goff[q]);
+    }
+    __syncthreads();
+    // ---- stage 1: A(k+2R) on S1 ----
+    const int pz1 = k + 2 * R;
+    const bool z1 = pz1 >= zlo && pz1 < zhi;
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int b = ub[q] + UO;
+      const T c = ru[q][sl(2 * R)];
+      T acc = fd_ctr(q1.kc, c);
+      if constexpr (R == 2) {
+        acc = fd4_axis(acc, q1.k[2], ru[q][sl(R)], ru[q][sl(R + 1)], ru[q][sl(3 * R - 1)],
+                       ru[q][sl(3 * R)]);
+        acc = fd4_axis(acc, q1.k[0], ld(b + (2 * UW + 0) * E),
+                       ld(b + (2 * UW + 1) * E), ld(b + (2 * UW + 3) * E),
+                       ld(b + (2 * UW + 4) * E));
+        acc = fd4_axis(acc, q1.k[1], ld(b + (0 * UW + 2) * E),
+                       ld(b + (1 * UW + 2) * E), ld(b + (3 * UW + 2) * E),
+                       ld(b + (4 * UW + 2) * E));
+      } else {
+        acc = fd2_axis(acc, q1.k[2], ru[q][sl(R)], ru[q][sl(3 * R)]);
+        acc = fd2_axis(acc, q1.k[0], ld(b + (UW + 0) * E),
+                       ld(b + (UW + 2) * E));
+        acc = fd2_axis(acc, q1.k[1], ld(b + 1 * E), ld(b + (2 * UW + 1) * E));
+      }
+      acc = pin(acc);
+      ra[q][sl(2 * R)] = (z1 && m1[q]) ? acc : c;
+    }
+    // ---- stage 2: B(k+R) on S2 ----
+    if (k >= kc0 - 2 * R) {
+      const int pz2 = k + R;
+      const bool z2 = pz2 >= zlo && pz2 < zhi;
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const int row = w + q * NW;
+        const T uo = ru[q][sl(R)];
+        if (row < R || row >= S1R - R) {  // scalar branch
+          rb[q][sl(R)] = uo;
+          continue;
+        }
+        const int b = ar[q] + AO;
+        const T c = ra[q][sl(R)];
+        T acc = fd_ctr(q2.kc, c, T(0.75) * uo);
+        constexpr int XC = XS ? 0 : R;  // column of the centre relative to the base
+        if constexpr (R == 2) {
+          acc = fd4_axis(acc, q2.k[2], ra[q][sl(0)], ra[q][sl(1)], ra[q][sl(3)], ra[q][sl(4)]);
+          T xm2, xm1, xp1, xp2;
+          if constexpr (XS) {
+            xm1 = wave_shr1(c);
+            xp1 = wave_shl1(c);
+            xm2 = wave_shr1(xm1);
+            xp2 = wave_shl1(xp1);
+          } else {
+            xm2 = ld(b + (2 * W + 0) * E);
+            xm1 = ld(b + (2 * W + 1) * E);
+            xp1 = ld(b + (2 * W + 3) * E);
+            xp2 = ld(b + (2 * W + 4) * E);
+          }
+          acc = fd4_axis(acc, q2.k[0], xm2, xm1, xp1, xp2);
+          acc = fd4_axis(acc, q2.k[1], ld(b + (0 * W + XC) * E),
+                         ld(b + (1 * W + XC) * E), ld(b + (3 * W + XC) * E),
+                         ld(b + (4 * W + XC) * E));
+        } else {
+          acc = fd2_axis(acc, q2.k[2], ra[q][sl(0)], ra[q][sl(2)]);
+          T xm1, xp1;
+          if constexpr (XS) {
+            xm1 = wave_shr1(c);
+            xp1 = wave_shl1(c);
+          } else {
+            xm1 = ld(b + (W + 0) * E);
+            xp1 = ld(b + (W + 2) * E);
+          }
+          acc = fd2_axis(acc, q2.k[0], xm1, xp1);
+          acc = fd2_axis(acc, q2.k[1], ld(b + XC * E),
+                         ld(b + (2 * W + XC) * E));
+        }
+        acc = pin(acc);
+        rb[q][sl(R)] = (z2 && m2[q]) ? acc : uo;
+      }
+    }
+    // ---- stage 3: u^{n+1}(k) on S3 ----
+    if (k >= kc0) {
+      const auto po = plane_rsrc((char*)uout + (int64_t)k * szb);
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const int row = w + q * NW;
+        if (row < 2 * R || row >= S1R - 2 * R) continue;  // scalar branch
+        const int b = ar[q] + AO + ABB;
+        const T c = rb[q][sl(0)];
+        T acc = fd_ctr(q3.kc, c, third * dl[q][0]);
+        constexpr int XC = XS ? 0 : R;
+        if constexpr (R == 2) {
+          acc = fd4_axis(acc, q3.k[2], rb[q][sl(-2)], rb[q][sl(-1)], rb[q][sl(1)], rb[q][sl(2)]);
+          T xm2, xm1, xp1, xp2;
+          if constexpr (XS) {
+            xm1 = wave_shr1(c);
+            xp1 = wave_shl1(c);
+            xm2 = wave_shr1(xm1);
+            xp2 = wave_shl1(xp1);
+          } else {
+            xm2 = ld(b + (2 * W + 0) * E);
+            xm1 = ld(b + (2 * W + 1) * E);
+            xp1 = ld(b + (2 * W + 3) * E);
+            xp2 = ld(b + (2 * W + 4) * E);
+          }
+          acc = fd4_axis(acc, q3.k[0], xm2, xm1, xp1, xp2);
+          acc = fd4_axis(acc, q3.k[1], ld(b + (0 * W + XC) * E),
+                         ld(b + (1 * W + XC) * E), ld(b + (3 * W + XC) * E),
+                         ld(b + (4 * W + XC) * E));
+        } else {
+          acc = fd2_axis(acc, q3.k[2], rb[q][sl(-1)], rb[q][sl(1)]);
+          T xm1, xp1;
+          if constexpr (XS) {
+            xm1 = wave_shr1(c);
+            xp1 = wave_shl1(c);
+          } else {
+            xm1 = ld(b + (W + 0) * E);
+            xp1 = ld(b + (W + 2) * E);
+          }
+          acc = fd2_axis(acc, q3.k[0], xm1, xp1);
+          acc = fd2_axis(acc, q3.k[1], ld(b + XC * E),
+                         ld(b + (2 * W + XC) * E));
+        }
+        acc = pin(acc);
+        if (m3[q]) gst<T>(po, goff[q], acc);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+#pragma unroll
+      for (int d = 0; d < R - 1; ++d) dl[q][d] = dl[q][d + 1];
+    }
+  };
+
+  // the LDS set of iteration k is (k - kst) & 1: unroll 2 NR so it is static
+  for (int kb = kst; kb < kc1; kb += 2 * NR) {
+    [&]<int... P>(std::integer_sequence<int, P...>) {
+      (void)((kb + P < kc1 ? (body.template operator()<P>(kb + P), true) : false) && ...);
+    }(std::make_integer_sequence<int, 2 * NR>{});
+  }
+}
+
 // Waves per SIMD to budget registers for (fp64): as many workgroups as the LDS admits
 // (FD4 16 waves: 1/CU -> 4; FD2 12 waves: 2/CU -> 6).  Without it the compiler spent 86
 // VGPRs on the FD2 step and lost the second workgroup per CU (-25 %).
@@ -340,25 +699,60 @@ constexpr int cring_min_waves() {
   return sizeof(T) == 8 ? (w > 8 ? 8 : (w < 1 ? 1 : w)) : 1;
 }
 
-template <typename T, int ORDER, int NW, int RPW, int XDPP, bool PERSIST>
+// Kernel variants: VAR < 16: cring march with XDPP = VAR; VAR >= 16: v3 march with
+// XS = VAR & 1 (DPP x-neighbours in stages 2/3), prefetch distance 1 + ((VAR >> 1) & 1)
+// and SEP = (VAR >> 2) & 1 (unmerged LDS reads).
+template <int VAR>
+struct StepVar {
+  static constexpr bool v3 = VAR >= 16;
+  static constexpr int xdpp = VAR & 15;
+  static constexpr int xs = VAR & 1;
+  static constexpr int pf = 1 + ((VAR >> 1) & 1);
+  static constexpr bool sep = (VAR >> 2) & 1;
+};
+
+template <typename T, int ORDER, int NW, int RPW, int VAR>
+__device__ __forceinline__ void march_var(T* lds, int tx, int ty, int kc0, int kc1,
+                                          const T* __restrict__ uin, T* __restrict__ uout,
+                                          int nx, int ny, int64_t sy, int64_t sz, int nz_alloc,
+                                          int zlo, int zhi, const Box2& bx, const FdCoef<T>& q1,
+                                          const FdCoef<T>& q2, const FdCoef<T>& q3) {
+  using V = StepVar<VAR>;
+  if constexpr (V::v3) {
+    v3_march<T, ORDER, NW, RPW, V::xs, V::pf, V::sep>(lds, tx, ty, kc0, kc1, uin, uout, nx, ny, sy, sz,
+                                              nz_alloc, zlo, zhi, bx, q1, q2, q3);
+  } else {
+    using Gm = CringGeom<ORDER, NW, RPW>;
+    cring_march<T, ORDER, NW, RPW, V::xdpp>(lds, lds + 2 * Gm::LDS_U,
+                                            lds + 2 * Gm::LDS_U + 2 * Gm::LDS_AB, tx, ty, kc0,
+                                            kc1, uin, uout, nx, ny, sy, sz, nz_alloc, zlo, zhi,
+                                            bx, q1, q2, q3);
+  }
+}
+
+template <typename T, int ORDER, int NW, int RPW, int VAR>
+constexpr int step_lds_elems() {
+  if constexpr (StepVar<VAR>::v3)
+    return V3Geom<T, ORDER, NW, RPW>::TOTAL;
+  else
+    return 2 * CringGeom<ORDER, NW, RPW>::LDS_U + 4 * CringGeom<ORDER, NW, RPW>::LDS_AB;
+}
+
+template <typename T, int ORDER, int NW, int RPW, int VAR, bool PERSIST>
 __global__ __launch_bounds__(64 * NW) __attribute__((
     amdgpu_waves_per_eu(cring_min_waves<T, ORDER, NW, RPW>()))) void diffusion3d_step_cring_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
     int nz_alloc, int k0, int k1, int k0b, int k1b, StepSched sc, int zlo, int zhi,
     Box2 bx, FdCoef<T> q1, FdCoef<T> q2, FdCoef<T> q3) {
-  using Gm = CringGeom<ORDER, NW, RPW>;
-  __shared__ T sU[2 * Gm::LDS_U];
-  __shared__ T sA[2 * Gm::LDS_AB];
-  __shared__ T sB[2 * Gm::LDS_AB];
+  __shared__ T lds[step_lds_elems<T, ORDER, NW, RPW, VAR>()];
   const Tile3 tile = xcd_tile();
   if constexpr (!PERSIST) {
     // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
     const bool second = tile.z >= sc.gza;
     const int kc0 = second ? k0b + (tile.z - sc.gza) * sc.zchunk : k0 + tile.z * sc.zchunk;
     const int kc1 = min(kc0 + sc.zchunk, second ? k1b : k1);
-    cring_march<T, ORDER, NW, RPW, XDPP>(sU, sA, sB, tile.x, tile.y, kc0, kc1, uin, uout,
-                                             nx, ny, sy, sz, nz_alloc, zlo, zhi, bx, q1, q2,
-                                             q3);
+    march_var<T, ORDER, NW, RPW, VAR>(lds, tile.x, tile.y, kc0, kc1, uin, uout, nx, ny, sy, sz,
+                                      nz_alloc, zlo, zhi, bx, q1, q2, q3);
   } else {
     // 1-D grid; tile.x = this group's XCD-contiguous logical id, so the groups of one XCD
     // march neighbouring tiles.  Group g owns the linear planes [s, e), s = g per +
@@ -373,12 +767,21 @@ __global__ __launch_bounds__(64 * NW) __attribute__((
       if (p0 < na) p1 = min(p1, na);  // a segment never spans both plane ranges
       const int kc0 = p0 < na ? k0 + p0 : k0b + (p0 - na);
       __syncthreads();  // nobody still reads the previous segment's last LDS planes
-      cring_march<T, ORDER, NW, RPW, XDPP>(sU, sA, sB, t % sc.gx, t / sc.gx, kc0,
-                                               kc0 + (p1 - p0), uin, uout, nx, ny, sy, sz,
-                                               nz_alloc, zlo, zhi, bx, q1, q2, q3);
+      march_var<T, ORDER, NW, RPW, VAR>(lds, t % sc.gx, t / sc.gx, kc0, kc0 + (p1 - p0), uin,
+                                        uout, nx, ny, sy, sz, nz_alloc, zlo, zhi, bx, q1, q2,
+                                        q3);
       s += p1 - p0;
     }
   }
+}
+
+// Persistent schedule for exclusive launches: ADVDIFF_STEP_PERSIST / advdiff_set_step_persist.
+// Off by default since the v3 march: at 512^3 the dynamically balanced grid of z chunks
+// is 9-11 % faster (FD4 760 vs 836 us, FD2 559 vs 745 us, profiles/step_variants_r2.log).
+static int g_step_persist = -1;
+static int step_persist() {
+  if (g_step_persist < 0) g_step_persist = knob("STEP_PERSIST", 0);
+  return g_step_persist;
 }
 
 struct SArgs {
@@ -411,7 +814,7 @@ static hipError_t launch_step(const SArgs& a) {
     return nb;
   }();
   static const int minc = knob("STEP_MIN_CHUNK", 32);
-  static const int persist = knob("STEP_PERSIST", 1);  // 0: grid schedule only (A/B)
+  const int persist = step_persist();  // 0 (default): grid schedule only
   static const int minseg = std::max(knob("STEP_MIN_SEG", 32), 1);
   const int na = std::max(a.k1 - a.k0, 0), nb = std::max(a.k1b - a.k0b, 0);
   const long long slots = (long long)device_cus() * per_cu;
@@ -464,17 +867,40 @@ static hipError_t dispatch_step(int cfg, const SArgs& a) {
     case 14: STEPV(12, 2, 1);    // 12 waves, DPP stages 2/3
     case 15: STEPV(12, 2, 2);    // 12 waves, DPP stages 1-3
     case 16: STEPV(16, 2, 1);    // 16 waves, DPP stages 2/3
-    default:  // FD4: 16 waves, DPP in all stages; FD2: 12 waves, stages 2/3
-      if constexpr (ORDER == 4) {
-        STEPV(16, 2, 2);
-      } else {
-        STEPV(12, 2, 1);
-      }
+    case 20: STEPV(16, 2, 16);   // v3, LDS x-neighbours, prefetch 1
+    case 21: STEPV(16, 2, 17);   // v3, DPP x in stages 2/3, prefetch 1
+    case 22: STEPV(16, 2, 18);   // v3, LDS x, prefetch 2
+    case 23: STEPV(16, 2, 19);   // v3, DPP x 2/3, prefetch 2
+    case 24: STEPV(16, 2, 20);   // v3, LDS x, prefetch 1, unmerged LDS reads
+    case 25: STEPV(16, 2, 21);   // v3, DPP x 2/3, prefetch 1, unmerged LDS reads
+    case 27: STEPV(16, 2, 23);   // v3, DPP x 2/3, prefetch 2, unmerged LDS reads
+    case 1: STEPV(16, 2, 2);     // round-1 default (cring, DPP in all stages)
+    default:  // v3, 16 waves, DPP x in stages 2/3, prefetch 2, unmerged LDS reads
+      STEPV(16, 2, 23);   // profiles/step_variants_r2.log: 760 us FD4 / 559 us FD2 at 512^3
   }
 #undef STEPV
 }
 
+// kernel variant of the 3-D fused step: ADVDIFF_STEP_CFG, or advdiff_set_step_cfg (tests)
+static int g_step_cfg = -1;
+static int step_cfg() {
+  if (g_step_cfg < 0) g_step_cfg = knob("STEP_CFG", 0);
+  return g_step_cfg;
+}
+
 }  // namespace advdiff
+
+extern "C" int advdiff_set_step_persist(int on) {
+  const int old = advdiff::step_persist();
+  advdiff::g_step_persist = on ? 1 : 0;
+  return old;
+}
+
+extern "C" int advdiff_set_step_cfg(int cfg) {
+  const int old = advdiff::step_cfg();
+  advdiff::g_step_cfg = cfg < 0 ? 0 : cfg;
+  return old;
+}
 
 extern "C" int advdiff_diffusion3d_step_box(int dtype, const void* uin, void* uout, int nx,
                                             int ny, int64_t sy, int64_t sz, int nz_alloc, int k0,
@@ -505,7 +931,7 @@ extern "C" int advdiff_diffusion3d_step_box_ex(int dtype, const void* uin, void*
   const Box2 bx{box[0], box[1], box[2], box[3], box[4], box[5], box[6], box[7]};
   const SArgs a{uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, k0b, k1b, zlo, zhi, bx,
                 cx, cy, cz, dt, (hipStream_t)stream, flags};
-  static const int cfg = knob("STEP_CFG", 0);
+  const int cfg = advdiff::step_cfg();
   if (dtype == ADVDIFF_F64) {
     if (order == 4) return dispatch_step<double, 4>(cfg, a);
     if (order == 2) return dispatch_step<double, 2>(cfg, a);

@@ -119,6 +119,10 @@ def _load():
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = c_int
+        lib.advdiff_set_step_cfg.argtypes = [c_int]
+        lib.advdiff_set_step_cfg.restype = c_int
+        lib.advdiff_set_step_persist.argtypes = [c_int]
+        lib.advdiff_set_step_persist.restype = c_int
         lib.advdiff_reduce_workspace_bytes.restype = c_sz
         lib.advdiff_reduce_workspace_bytes.argtypes = []
         lib.advdiff_build_info.restype = ctypes.c_char_p

@@ -62,6 +62,16 @@ def test_fused_step_bitwise_equals_per_stage(dtype, order, case):
 def test_fused_step_persistent_schedule_bitwise(order, case):
     """exclusive=True (one round of persistent groups marching segments of the linearised
     (tile, plane) space) == the grid of z chunks, bitwise; also with two plane ranges."""
+    from multigpu_advectiondiffusion_amd.ops import _lib
+    lib = _lib.require()
+    old = lib.advdiff_set_step_persist(1)
+    try:
+        _persistent_case(order, case)
+    finally:
+        lib.advdiff_set_step_persist(old)
+
+
+def _persistent_case(order, case):
     nz, ny, nx, sx, k0, k1, zlo, zhi, border = case
     g = torch.Generator().manual_seed(7)
     u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).cuda()
@@ -135,3 +145,36 @@ def test_fused_step_box_bounds_match_reference():
         ref.diffusion3d_step_box(cpu, out, nx, ny, 6, 34, 0, nz, box, 4, *c, dt)
         torch.cuda.synchronize()
         assert (got.cpu() - out).abs().max().item() < 1e-12, box
+
+
+STEP_VARIANTS = [0, 1, 16, 20, 21, 22, 23, 24, 25, 27]  # diffusion_fused.hip dispatch_step cfgs
+
+
+@pytest.mark.parametrize("cfg", STEP_VARIANTS)
+@pytest.mark.parametrize("order", [4, 2])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_fused_step_variants_bitwise(cfg, order, dtype):
+    """Every selectable kernel variant of the fused step (tile shape, x-neighbour source,
+    prefetch distance; grid and persistent schedules) is bit-identical to the per-stage
+    path on a sub-range with frozen planes and odd sizes."""
+    from multigpu_advectiondiffusion_amd.ops import _lib
+    lib = _lib.require()
+    nz, ny, nx, sx, k0, k1, zlo, zhi, border = (77, 53, 133, 136, 5, 70, 2, 74, 2)
+    g = torch.Generator().manual_seed(5)
+    u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).to(dtype).cuda()
+    c = (0.21, 0.17, 0.13)
+    dt = 0.9 / (2 * sum(c)) if order == 2 else 0.5 / sum(c)
+    exp = _per_stage(u, nx, ny, k0, k1, zlo, zhi, border, order, c, dt)
+    old = lib.advdiff_set_step_cfg(cfg)
+    oldp = lib.advdiff_set_step_persist(1)
+    try:
+        for exclusive in (False, True):
+            got = u.clone()
+            stencil.diffusion3d_step(u, got, nx=nx, ny=ny, k0=k0, k1=k1, zlo=zlo, zhi=zhi,
+                                     border=border, order=order, cx=c[0], cy=c[1], cz=c[2],
+                                     dt=dt, exclusive=exclusive)
+            torch.cuda.synchronize()
+            assert torch.equal(got, exp), (exclusive, (got - exp).abs().max().item())
+    finally:
+        lib.advdiff_set_step_cfg(old)
+        lib.advdiff_set_step_persist(oldp)
