@@ -8,9 +8,17 @@ solver at 256³ per GPU reported alongside.
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-One RK3 step = 3 fused stage kernels + 3 halo exchanges (no work skipped).  K steps are
-timed between a barrier + device sync on both sides; the max over ranks is reported.
-MLUPS = global cells x K / seconds / 1e6.  Rank 0 prints ONE JSON line.
+One RK3 step of the heat solver = ONE temporally blocked launch that computes all three
+SSP-RK3 stages (diffusion_fused.hip; bit-identical to three per-stage launches) + ONE halo
+exchange of 3R ghost planes per step when N > 1 (no work skipped).  Burgers steps are three
+fused WENO stage launches + three exchanges.  K steps are timed between a barrier + device
+sync on both sides; the max over ranks is reported.  MLUPS = global cells x K / seconds /
+1e6.  Rank 0 prints ONE JSON line.
+
+Self-validation (outside the timed region): after the timed steps the heat solution is
+compared with the exact decaying sine mode exp(-3 pi^2 K t) sin sin sin (L_inf, relative to
+the initial amplitude) and the run fails if it exceeds linf_bound().  The 7-point (FD2)
+Laplacian named by BASELINE.json is measured on the same grid and reported as `fd2_7pt`.
 """
 from __future__ import annotations
 
@@ -32,6 +40,25 @@ BASE_DIFFUSION = 927.2   # best published 3-D heat MLUPS (SingleGPU/Diffusion3d_
 BASE_BURGERS = 344.4     # best published 3-D Burgers MLUPS (SingleGPU/Burgers3d_WENO5_PitchedMem/Run.m:15-25)
 
 
+def linf_bound(grid, K: float, t: float, order: int) -> float:
+    """Bound of L_inf(u - exact) for the sine mode after time t (unit amplitude).
+
+    The scheme's truncation error is O(h^4) (FD4) / O(h^2) (FD2) ~ 1e-10 here; what
+    dominates is the reference's Dirichlet treatment: FD4 freezes the 2-cell border
+    (`MultiGPU/Diffusion3d_Baseline/Kernels.cu` updates [2, n-2)), so the cell at distance
+    h from a wall keeps its initial value sin(pi h) while the exact mode decays by
+    exp(-lam t): |error| <= sin(pi h)(1 - exp(-lam t)) there, less inside.  Twice that plus
+    the truncation allowance is the bound; a wrong stencil, halo plane or schedule gives
+    errors of O(dt/h^2 * |u|) ~ 1e-1 and fails it."""
+    import math
+    Ls = [(n - 1) * d for n, d in zip(grid.shape, grid.spacing)]
+    lam = K * math.pi ** 2 * sum(1.0 / L ** 2 for L in Ls)
+    h = max(d / L for d, L in zip(grid.spacing, Ls))
+    frozen = math.sin(math.pi * h) * (1.0 - math.exp(-lam * t)) if order == 4 else 0.0
+    trunc = 1e-9 if order == 4 else 10.0 * (math.pi * h) ** 2 * lam * t
+    return 2.0 * frozen + trunc
+
+
 def timed(solver: Solver, steps: int, warmup: int, dt: float) -> float:
     if warmup:
         solver.run(iters=warmup, dt=dt)
@@ -48,6 +75,7 @@ def main():
     ap.add_argument("--burgers-base", type=int, default=256, help="Burgers cells per GPU = base^3")
     ap.add_argument("--burgers-steps", type=int, default=None)
     ap.add_argument("--no-burgers", action="store_true")
+    ap.add_argument("--no-fd2", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--decomp", default=None, help="process grid (default: z-slabs)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
@@ -73,13 +101,19 @@ def main():
     dt = model.stable_dt()
     secs = timed(solver, args.steps, args.warmup, dt)
     mlups = grid.cells * args.steps / secs / 1e6
-    # sanity: the solution must stay finite and decay (sine mode)
+    # self-validation against the exact solution (outside the timed region)
     finite = solver.check_finite()
+    _, _, linf = solver.error_norms()
     pg = solver.pgrid
+    t_end = solver.t
     del solver
     if dev.type == "cuda":
         torch.cuda.empty_cache()
+    bound = linf_bound(grid, model.K, t_end, 4)
+    if not linf <= bound:
+        raise SystemExit(f"bench validation failed: L_inf vs exact = {linf:.3e} > {bound:.3e}")
 
+    link = "RCCL" if comm.backend == "nccl" else str(comm.backend)
     result = {
         "metric": METRIC,
         "value": round(mlups, 1),
@@ -96,11 +130,38 @@ def main():
         "config": {"model": "diffusion3d FD4 13-point + SSP-RK3", "global_batch": 1,
                    "seq_len": grid.cells, "grid": list(shape),
                    "parallelism": ("single GPU" if n == 1 else
-                                   f"z-slab{n} (RCCL halo, overlapped)" if pg[1:] == (1, 1) else
-                                   f"cartesian {'x'.join(map(str, pg))} (z,y,x; RCCL halo)"),
+                                   f"z-slab{n} ({link} halo, overlapped)" if pg[1:] == (1, 1) else
+                                   f"cartesian {'x'.join(map(str, pg))} (z,y,x; {link} halo)"),
                    "cells_per_gpu": grid.cells // n},
         "max_abs_u": finite,
+        "linf_vs_exact": float(f"{linf:.3e}"),
+        "linf_bound": float(f"{bound:.3e}"),
+        "t_end": t_end,
+        "rccl_world": n,
+        "comm_backend": comm.backend or "none (single process)",
+        "device_ids": comm.device_ids(),
     }
+
+    # ---- the 7-point (FD2) Laplacian named by BASELINE.json, same grid ----------------
+    if not args.no_fd2:
+        m2 = Diffusion(K=1.0, order=2)
+        s2 = Solver(m2, grid, comm, dtype=torch.float64, ic="sine",
+                    overlap=not args.no_overlap, decomp=args.decomp)
+        secs2 = timed(s2, args.steps, args.warmup, m2.stable_dt())
+        _, _, linf2 = s2.error_norms()
+        bound2 = linf_bound(grid, m2.K, s2.t, 2)
+        del s2
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        if not linf2 <= bound2:
+            raise SystemExit(f"bench validation failed: FD2 L_inf vs exact = {linf2:.3e} "
+                             f"> {bound2:.3e}")
+        ml2 = grid.cells * args.steps / secs2 / 1e6
+        result["fd2_7pt"] = {"value": round(ml2, 1), "unit": "MLUPS",
+                             "ms_per_step": round(secs2 / args.steps * 1e3, 4),
+                             "vs_baseline": round(ml2 / BASE_DIFFUSION, 2),
+                             "linf_vs_exact": float(f"{linf2:.3e}"),
+                             "model": "diffusion3d FD2 7-point + SSP-RK3"}
 
     # ---- secondary: 3-D Burgers WENO5-Z + C∇²u, fp64 ----------------------------------
     if not args.no_burgers:

@@ -97,6 +97,17 @@ class Comm:
     def distributed(self) -> bool:
         return self.size > 1
 
+    def device_ids(self) -> list:
+        """Device index of every rank (rank order), e.g. [0..7] on an 8-GPU node; proves
+        that each rank drove its own GPU.  CPU ranks report -1."""
+        mine = self.device.index if self.device.type == "cuda" else -1
+        if self.size == 1:
+            return [mine]
+        t = torch.tensor([mine], dtype=torch.int64, device=self._coll_device())
+        out = [torch.zeros_like(t) for _ in range(self.size)]
+        dist.all_gather(out, t)
+        return [int(x.item()) for x in out]
+
     # ---- collectives ---------------------------------------------------------------
     def barrier(self):
         if self.size > 1:
