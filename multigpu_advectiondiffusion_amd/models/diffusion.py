@@ -57,7 +57,8 @@ class Diffusion(Model):
              ny=None, box=None, exclusive=False):
         """Fused RK3 step on planes [lo, hi) (and [lo2, hi2) in the same launch).
         nx/ny/box: extents and explicit active/output bounds of a view (Cartesian blocks).
-        exclusive: the launch has the GPU to itself (3-D: persistent schedule)."""
+        exclusive: the launch has the GPU to itself (3-D: persistent schedule; the 2-D
+        step has one grid schedule — its y-march waves are independent — and ignores it)."""
         g = self.grid
         nx = g.nx if nx is None else nx
         ny = g.ny if ny is None else ny

@@ -310,7 +310,7 @@ class Solver:
             (vx0, vx1), (xa0, xa1), (xo0, xo1) = self._fused_view(1, x0, x1)
             sl = (slice(None), slice(vx0, vx1))
             self.model.step(self.u[sl], self.un[sl], y0, y1, self.zact[0], self.zact[1], dt,
-                            nx=vx1 - vx0, box=(xa0, xa1, xo0, xo1))
+                            nx=vx1 - vx0, box=(xa0, xa1, xo0, xo1), exclusive=exclusive)
         trace.sync_check(f"{self.model.name} fused step box {box}", self.device)
 
     def _step_fused(self, dt: float) -> None:
@@ -404,7 +404,9 @@ class Solver:
                 and not trace.TRACE)
 
     def _graph_for(self, dt: float):
-        key = (float(dt), self.GRAPH_STEPS)
+        # A graph bakes in the buffer addresses: the fused / LSRK paths ping-pong u <-> un,
+        # so after an odd number of eager steps the other parity needs its own graph.
+        key = (float(dt), self.GRAPH_STEPS, self.u.data_ptr())
         g = getattr(self, "_graphs", {}).get(key)
         if g is not None:
             return g

@@ -28,6 +28,22 @@ def test_graph_replay_bitwise(make):
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("fused", [True, False])
+def test_graph_replay_after_odd_eager_steps(fused):
+    """run(5) then run(20) (the bench's warm-up + timed pattern: the graph is captured in
+    the first call, replayed in the second at the other u/un parity) == 25 eager steps."""
+    g = Grid((40, 36, 34), (1.0, 1.0, 1.0))
+    outs = []
+    for graph in (False, True):
+        m = Diffusion(K=1.0, order=4, fused=fused)
+        s = Solver(m, g, dtype=torch.float64, device="cuda", ic="sine")
+        dt = m.stable_dt()
+        s.run(iters=5, dt=dt, graph=graph)
+        s.run(iters=20, dt=dt, graph=graph)
+        outs.append(s.gather())
+    assert np.array_equal(outs[0], outs[1])
+
+
 def test_torch_reference_kernel_path_on_gpu():
     """Solver(kernel="torch") runs the PyTorch reference ops on the GPU (naive A/B path)
     and agrees with the HIP kernels to rounding."""
