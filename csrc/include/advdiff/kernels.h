@@ -177,6 +177,11 @@ int advdiff_set_step_cfg(int cfg);
 // Allow (1) the persistent schedule for ADVDIFF_EXCLUSIVE 3-D fused launches (default 0:
 // grid of z chunks); returns the previous value.  Initialised from ADVDIFF_STEP_PERSIST.
 int advdiff_set_step_persist(int on);
+// 3-D WENO5 stage kernel version (1 = v1, 2 = v2 two barriers, 3 = v2 double-buffered);
+// returns the previous value.  Results agree to rounding (tests).
+int advdiff_set_b3_ver(int v);
+// rows per 3-D WENO tile (8 or 16); returns the previous value.
+int advdiff_set_b3_ty(int ty);
 // Library identification (build flags, arch) for diagnostics.
 const char* advdiff_build_info(void);
 // sha256 (first 16 hex digits) of the kernel sources this library was built from

@@ -186,6 +186,173 @@ __attribute__((amdgpu_waves_per_eu(W == 7 ? 4 : 1))) void burgers3d_stage_kernel
   }
 }
 
+// ------------------------------------------------------------------------------
+// WENO5 3-D stage, v2 (the default for WENO5-JS/Z):
+//   * 63-cell x tiles: lane l computes the face to the right of its cell from the LDS
+//     tile; the face to its left comes from lane l-1 by one DPP shift, so lane 0 only
+//     supplies that face and no wave computes an extra column of faces (v1: the last
+//     wave of the tile computed the tile's left faces with 8 of 64 lanes active);
+//   * y faces: the face above each row, plus the tile's bottom row of faces by wave 0;
+//   * z faces from the lane's register column (two of three curvatures reused);
+//   * scaled smoothness indicators (common.hpp w5_*): 32 instead of 40 fp64 ops per side;
+//   * the cell value and the z neighbours of the viscous term come from the register
+//     column, x/y neighbours from the LDS tile;
+//   * DB = false: 2 barriers per plane (faces | stage next tile | combine);
+//     DB = true: a double-buffered tile and ONE barrier per plane (2x the LDS).
+// Tiles are anchored at the active region (x: border-1, y: border), so a 256-wide grid
+// with border 3 takes 4 x tiles.
+// ------------------------------------------------------------------------------
+template <typename T, bool WZ, bool VISC, int MODE, int TY, bool DB, int WPE>
+__global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(WPE))) void burgers3d_w5_kernel(
+    const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
+    int k1, int zchunk, int border, T rdx, T rdy, T rdz, T vx, T vy, T vz, T dt, T a, T b) {
+  constexpr int R = 3, NP = 5, TX = 64, TXO = TX - 1;
+  constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NT = TX * TY, LT = LX * LY;
+  constexpr int NPT = (LT + NT - 1) / NT;
+  constexpr int NB = DB ? 2 : 1;
+  __shared__ T s_p[NB][LT];
+  __shared__ T s_m[NB][LT];
+  __shared__ T s_u[VISC ? NB : 1][VISC ? LT : 1];
+  __shared__ T s_fy[NB][(TY + 1) * TX];
+
+  const int tx = threadIdx.x, ty = threadIdx.y, tid = ty * TX + tx;
+  const int ib = border - 1 + (int)blockIdx.x * TXO;  // x of lane 0 (supplies a face only)
+  const int jb = border + (int)blockIdx.y * TY;       // y of wave 0
+  const int i = ib + tx, j = jb + ty;
+  const int kc0 = k0 + (int)blockIdx.z * zchunk;
+  const int kc1 = min(kc0 + zchunk, k1);
+  const bool active = tx >= 1 && i < nx - border && j < ny - border;
+  const int64_t own = (int64_t)min(j, ny - 1) * sy + min(i, nx - 1);
+  const int lc = (ty + R) * LX + tx + R;
+
+  int64_t toff[NPT];
+#pragma unroll
+  for (int r = 0; r < NPT; ++r) {
+    const int idx = min(tid + r * NT, LT - 1);
+    const int ly = idx / LX, lx = idx - ly * LX;
+    toff[r] = (int64_t)clampi(jb - R + ly, 0, ny - 1) * sy + clampi(ib - R + lx, 0, nx - 1);
+  }
+  T pre[NPT];
+  auto fetch_tile = [&](int k) {
+    const T* src = in + (int64_t)k * sz;
+#pragma unroll
+    for (int r = 0; r < NPT; ++r) pre[r] = src[toff[r]];
+  };
+  auto stage_tile = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < NPT; ++r) {
+      const int idx = tid + r * NT;
+      if (NPT * NT == LT || idx < LT) {
+        T p, m;
+        lf_split(pre[r], p, m);
+        s_p[buf][idx] = p;
+        s_m[buf][idx] = m;
+        if constexpr (VISC) s_u[buf][idx] = pre[r];
+      }
+    }
+  };
+  auto lds_face = [&](int buf, int c, int st) {
+    T pv[NP], mv[NP];
+#pragma unroll
+    for (int d = 0; d < NP; ++d) {
+      pv[d] = s_p[buf][c + (d - R + 1) * st];
+      mv[d] = s_m[buf][c + (d - R + 2) * st];
+    }
+    return w5_face<T, WZ>(pv, mv);
+  };
+
+  // ---- prologue: column window, the face below the first plane, the first tile ----
+  T P[NP], M[NP], U[NP];  // f+(k-2..k+2), f-(k-1..k+3) (last filled per plane), u(k-2..k+2)
+  T KP[3], KM[3];         // C of f+ centred on k-1..k+1, of f- centred on k..k+2
+  T fz_lo;
+  {
+    T uz[2 * R], fp[2 * R], fm[2 * R];
+#pragma unroll
+    for (int q = 0; q < 2 * R; ++q) {
+      uz[q] = in[(int64_t)(kc0 - R + q) * sz + own];
+      lf_split(uz[q], fp[q], fm[q]);
+    }
+    fz_lo = w5_face<T, WZ>(fp, fm + 1);  // face kc0-½
+    KP[0] = w5_curv(fp[1], fp[2], fp[3]);
+    KP[1] = w5_curv(fp[2], fp[3], fp[4]);
+    KM[0] = w5_curv(fm[2], fm[3], fm[4]);
+    KM[1] = w5_curv(fm[3], fm[4], fm[5]);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      P[q] = fp[q + 1];
+      U[q] = uz[q + 1];
+    }
+#pragma unroll
+    for (int q = 0; q < NP - 1; ++q) M[q] = fm[q + 2];
+  }
+  fetch_tile(kc0);
+  stage_tile(0);
+  if (kc0 + 1 < kc1) fetch_tile(kc0 + 1);
+  T unext = in[(int64_t)(kc0 + R) * sz + own];
+  __syncthreads();
+
+  for (int k = kc0; k < kc1; ++k) {
+    const int cb = DB ? ((k - kc0) & 1) : 0;
+    // own column: u(k+R) -> f-(k+R) now, f+(k+R)/u(k+R) after the shift
+    T pn, mn;
+    lf_split(unext, pn, mn);
+    M[NP - 1] = mn;
+    const T un = unext;
+    if (k + 1 < kc1) unext = in[(int64_t)(k + 1 + R) * sz + own];
+
+    const T fx = lds_face(cb, lc, 1);    // x face i+½
+    const T fy = lds_face(cb, lc, LX);   // y face j+½
+    T fyb = T(0);
+    if (ty == 0) fyb = lds_face(cb, (R - 1) * LX + tx + R, LX);  // y faces jb-½ (wave 0)
+    T d2x = T(0), d2y = T(0);
+    const T ctr = U[R - 1];
+    if constexpr (VISC) {
+      d2x = FD<4>::d2(s_u[cb][lc - 2], s_u[cb][lc - 1], ctr, s_u[cb][lc + 1], s_u[cb][lc + 2]);
+      d2y = FD<4>::d2(s_u[cb][lc - 2 * LX], s_u[cb][lc - LX], ctr, s_u[cb][lc + LX],
+                      s_u[cb][lc + 2 * LX]);
+    }
+    KP[2] = w5_curv(P[2], P[3], P[4]);
+    KM[2] = w5_curv(M[2], M[3], M[4]);
+    const T fz_hi = w5_face_k<T, WZ>(P, M, KP, KM);
+    KP[0] = KP[1];
+    KP[1] = KP[2];
+    KM[0] = KM[1];
+    KM[1] = KM[2];
+    s_fy[cb][(ty + 1) * TX + tx] = fy;
+    if (ty == 0) s_fy[cb][tx] = fyb;
+
+    if constexpr (!DB) __syncthreads();  // tile k fully read; y faces visible
+    if (k + 1 < kc1) {                   // stage tile k+1 (DB: into the other buffer)
+      stage_tile(DB ? cb ^ 1 : 0);
+      if (k + 2 < kc1) fetch_tile(k + 2);
+    }
+    if constexpr (DB) __syncthreads();  // y faces of k and tile k+1 visible
+
+    const T fyl = s_fy[cb][ty * TX + tx];
+    const T fxl = wave_shr1(fx);  // face i-½ from lane l-1 (lane 0: unused)
+    T L = -((fx - fxl) * rdx + (fy - fyl) * rdy + (fz_hi - fz_lo) * rdz);
+    if constexpr (VISC) {
+      L += vx * d2x + vy * d2y + vz * FD<4>::d2(U[R - 3], U[R - 2], ctr, U[R], U[R + 1]);
+    }
+    if (active) {
+      const int64_t o = (int64_t)k * sz + own;
+      T ax = T(0);
+      if constexpr (reads_aux<MODE>()) ax = aux[o];
+      stage_store<T, MODE>(out, aux, o, ax, ctr, L, dt, a, b);
+    }
+    fz_lo = fz_hi;
+#pragma unroll
+    for (int q = 0; q < NP - 1; ++q) {
+      P[q] = P[q + 1];
+      M[q] = M[q + 1];
+      U[q] = U[q + 1];
+    }
+    P[NP - 1] = pn;
+    U[NP - 1] = un;
+    if constexpr (!DB) __syncthreads();  // tile k+1 visible
+  }
+}
+
 template <typename T, int W, bool WZ, bool VISC, int MODE, int TX>
 __global__ __launch_bounds__(TX) void burgers2d_stage_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int64_t sy, int j0, int j1, int ychunk,
@@ -327,10 +494,52 @@ static hipError_t launch_b3_ty(const BArgs& p) {
   return hipGetLastError();
 }
 
+template <typename T, bool WZ, bool VISC, int MODE, int TY, bool DB, int WPE = 4>
+static hipError_t launch_b3_v2(const BArgs& p) {
+  const int gx = div_up(std::max(p.nx - 2 * p.border, 1), 63);
+  const int gy = div_up(std::max(p.ny - 2 * p.border, 1), TY);
+  const int zc = pick_chunk(p.hi - p.lo, (long long)gx * gy, 8, 256);
+  const int gz = div_up(p.hi - p.lo, zc);
+  const double s = 1.0 / 12.0;
+  hipLaunchKernelGGL((burgers3d_w5_kernel<T, WZ, VISC, MODE, TY, DB, WPE>), dim3(gx, gy, gz),
+                     dim3(64, TY, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx, p.ny,
+                     p.sy, p.sz, p.lo, p.hi, zc, p.border, T(p.rdx), T(p.rdy), T(p.rdz),
+                     T(p.vx * s), T(p.vy * s), T(p.vz * s), T(p.dt), T(p.a), T(p.b));
+  return hipGetLastError();
+}
+
+// 3-D WENO5 kernel version (ADVDIFF_B3_VER / advdiff_set_b3_ver): 1 = v1 (generic LDS
+// face kernel), 2 = v2 with two barriers per plane, 3 = v2 with a double-buffered tile
+// (default: 256^3 WENO5-Z + viscous stage 273 -> 242 us, profiles/burgers_variants_r2.log;
+// 9.8e7 instead of 1.11e8 VALU instructions per dispatch, profiles/pmc_r2_burgers_fused.md),
+// 4/5 = v2 at 6 waves/SIMD (spills; kept for the record).
+static int g_b3_ver = -1, g_b3_ty = -1;
+static int b3_ver() {
+  if (g_b3_ver < 0) g_b3_ver = knob("B3_VER", 3);
+  return g_b3_ver;
+}
+static int b3_ty() {  // rows (waves) per 3-D tile: 8 or 16 (ADVDIFF_B3_TY)
+  if (g_b3_ty < 0) g_b3_ty = knob("B3_TY", kBTY3);
+  return g_b3_ty;
+}
+
 template <typename T, int W, bool WZ, bool VISC, int MODE>
 static hipError_t launch_b3(const BArgs& p) {
-  static const int ty = knob("B3_TY", kBTY3);
-  if (W == 5 && ty == 16) return launch_b3_ty<T, W, WZ, VISC, MODE, 16>(p);
+  const int ty = b3_ty();
+  if constexpr (W == 5) {
+    const int v = b3_ver();
+    if (v == 2) {
+      return ty == 16 ? launch_b3_v2<T, WZ, VISC, MODE, 16, false>(p)
+                      : launch_b3_v2<T, WZ, VISC, MODE, 8, false>(p);
+    }
+    if (v == 3) {
+      return ty == 16 ? launch_b3_v2<T, WZ, VISC, MODE, 16, true>(p)
+                      : launch_b3_v2<T, WZ, VISC, MODE, 8, true>(p);
+    }
+    if (v == 4) return launch_b3_v2<T, WZ, VISC, MODE, 8, false, 6>(p);  // 6 waves/SIMD
+    if (v == 5) return launch_b3_v2<T, WZ, VISC, MODE, 4, false, 6>(p);
+    if (ty == 16) return launch_b3_ty<T, W, WZ, VISC, MODE, 16>(p);
+  }
   return launch_b3_ty<T, W, WZ, VISC, MODE, 8>(p);
 }
 
@@ -396,6 +605,18 @@ static hipError_t run_b(int dtype, bool three_d, int scheme, bool ls, const BArg
 }
 
 }  // namespace advdiff
+
+extern "C" int advdiff_set_b3_ver(int v) {
+  const int old = advdiff::b3_ver();
+  advdiff::g_b3_ver = v;
+  return old;
+}
+
+extern "C" int advdiff_set_b3_ty(int ty) {
+  const int old = advdiff::b3_ty();
+  advdiff::g_b3_ty = ty;
+  return old;
+}
 
 extern "C" int advdiff_burgers3d_stage(int dtype, const void* in, const void* u0, void* out,
                                        int nx, int ny, int64_t sy, int64_t sz, int k0, int k1,

@@ -292,6 +292,86 @@ __device__ __forceinline__ T weno5_face_k(const T* p, const T* m, const T* kp, c
   }
 }
 
+// ---------------------------------------------------------------------------------
+// WENO5 with SCALED smoothness indicators (the 3-D stage kernel's reconstruction).
+// Every indicator is carried as e_k = 4 (beta_k + eps) = t_k² + C_k, where t_k is the
+// first-derivative term (v0 - 4v1 + 3v2 etc.) and C_k = 13/3 c_k² + 4 eps folds the
+// curvature term and eps into one value per stencil centre (w5_curv: a z-marching lane
+// reuses two of three per side).  The common factor 4 leaves both weight families
+// unchanged (JS: alpha ∝ 1/e², a common 1/16; Z: tau/(beta+eps) is a ratio), and the
+// linear weights (0.1, 0.6, 0.3) become (1, 6, 3) — the 1/10 cancels in num/den.  Per
+// side this is 32 fp64 ops (Z) instead of 40, with the same results to rounding
+// (tests/test_kernels_gpu.py compares against the textbook fp64 form).
+// ---------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T w5_curv(T a, T b, T c) {
+#pragma clang fp contract(off)
+  const T t = fma(T(-2), b, a + c);
+  return fma(T(13.0 / 3.0) * t, t, T(4e-6));
+}
+
+// One side: numerator num = Σ w_k q_k (q_k = 6 x candidate) and S = Σ w_k, so the side's
+// value is num / (6 S).  C0..C2 = w5_curv centred on v1, v2, v3.
+template <typename T, bool ZVARIANT>
+__device__ __forceinline__ void w5_side(T v0, T v1, T v2, T v3, T v4, T C0, T C1, T C2,
+                                        T& num, T& S) {
+#pragma clang fp contract(off)
+  const T t0 = fma(T(3), v2, fma(T(-4), v1, v0));
+  const T t1 = v1 - v3;
+  const T t2 = fma(T(3), v2, fma(T(-4), v3, v4));
+  const T e0 = fma(t0, t0, C0), e1 = fma(t1, t1, C1), e2 = fma(t2, t2, C2);
+  const T q0 = fma(T(11), v2, fma(T(-7), v1, T(2) * v0));
+  const T q1 = fma(T(5), v2, fma(T(2), v3, -v1));
+  const T q2 = fma(T(5), v3, fma(T(2), v2, -v4));
+  T w0, w1, w2;
+  if constexpr (ZVARIANT) {
+    const T tau = fabs(e0 - e2);
+    w0 = (e0 + tau) * (e1 * e2);
+    w1 = (T(6) * (e1 + tau)) * (e0 * e2);
+    w2 = (T(3) * (e2 + tau)) * (e0 * e1);
+  } else {
+    const T s0 = e0 * e0, s1 = e1 * e1, s2 = e2 * e2;
+    w0 = s1 * s2;
+    w1 = T(6) * (s0 * s2);
+    w2 = T(3) * (s0 * s1);
+  }
+  num = fma(w0, q0, fma(w1, q1, w2 * q2));
+  S = (w0 + w1) + w2;
+}
+
+// Face flux from both sides: n1/(6 S1) + n2/(6 S2) = (n1 S2 + n2 S1) / (6 S1 S2) with one
+// division (fp64; S1 S2 >= ~1e-43 at eps = 1e-6 for the JS form); fp32 keeps two.
+template <typename T>
+__device__ __forceinline__ T w5_combine(T n1, T S1, T n2, T S2) {
+#pragma clang fp contract(off)
+  if constexpr (sizeof(T) == 8) {
+    return fast_div(fma(n1, S2, n2 * S1), (T(6) * S1) * S2);
+  } else {
+    return fast_div(n1, T(6) * S1) + fast_div(n2, T(6) * S2);
+  }
+}
+
+// Face i+½ from p = f⁺(i-2..i+2), m = f⁻(i-1..i+3), all curvatures computed here.
+template <typename T, bool ZVARIANT>
+__device__ __forceinline__ T w5_face(const T* p, const T* m) {
+  T n1, S1, n2, S2;
+  w5_side<T, ZVARIANT>(p[0], p[1], p[2], p[3], p[4], w5_curv(p[0], p[1], p[2]),
+                       w5_curv(p[1], p[2], p[3]), w5_curv(p[2], p[3], p[4]), n1, S1);
+  w5_side<T, ZVARIANT>(m[4], m[3], m[2], m[1], m[0], w5_curv(m[4], m[3], m[2]),
+                       w5_curv(m[3], m[2], m[1]), w5_curv(m[2], m[1], m[0]), n2, S2);
+  return w5_combine(n1, S1, n2, S2);
+}
+
+// The same face with the curvatures supplied: kp = C of f⁺ centred on p1, p2, p3 and
+// km = C of f⁻ centred on m1, m2, m3 (bit-identical to w5_face).
+template <typename T, bool ZVARIANT>
+__device__ __forceinline__ T w5_face_k(const T* p, const T* m, const T* kp, const T* km) {
+  T n1, S1, n2, S2;
+  w5_side<T, ZVARIANT>(p[0], p[1], p[2], p[3], p[4], kp[0], kp[1], kp[2], n1, S1);
+  w5_side<T, ZVARIANT>(m[4], m[3], m[2], m[1], m[0], km[2], km[1], km[0], n2, S2);
+  return w5_combine(n1, S1, n2, S2);
+}
+
 // Left-biased WENO7 (Jiang–Shu weights) at the right face of v3 from v0..v6 (= f at
 // i-3..i+3), as numerator/denominator.  Smoothness indicators and candidate stencils
 // exactly as the MATLAB prototype (Matlab_Prototipes/InviscidBurgersNd/WENO7resAdv1d.m;

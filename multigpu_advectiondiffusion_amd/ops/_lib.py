@@ -123,6 +123,10 @@ def _load():
         lib.advdiff_set_step_cfg.restype = c_int
         lib.advdiff_set_step_persist.argtypes = [c_int]
         lib.advdiff_set_step_persist.restype = c_int
+        lib.advdiff_set_b3_ver.argtypes = [c_int]
+        lib.advdiff_set_b3_ver.restype = c_int
+        lib.advdiff_set_b3_ty.argtypes = [c_int]
+        lib.advdiff_set_b3_ty.restype = c_int
         lib.advdiff_reduce_workspace_bytes.restype = c_sz
         lib.advdiff_reduce_workspace_bytes.argtypes = []
         lib.advdiff_build_info.restype = ctypes.c_char_p

@@ -185,3 +185,33 @@ def test_debug_print_kernel(capfd):
     torch.cuda.synchronize()
     out = capfd.readouterr().out
     assert "[k=1]" in out and "13.0000" in out and "18.0000" in out
+
+
+@pytest.mark.parametrize("ver,ty", [(1, 8), (1, 16), (2, 8), (2, 16), (3, 8), (3, 16), (4, 8), (5, 4)])
+@pytest.mark.parametrize("weno_z", [False, True])
+def test_burgers3d_stage_variants(ver, ty, weno_z):
+    """Every selectable 3-D WENO5 kernel variant (v1 generic, v2 two barriers, v3 double
+    buffer, v4/v5 6 waves/SIMD) against the fp64 reference, on a shape that leaves partial
+    tiles in x and y and a remainder z chunk."""
+    from multigpu_advectiondiffusion_amd.ops import _lib
+    lib = _lib.require()
+    nz, ny, nx, sx = 37, 45, 131, 136
+    inp = _smooth3(nz, ny, sx, 4, torch.float64)
+    u0 = _smooth3(nz, ny, sx, 5, torch.float64)
+    rd = (1 / 0.02, 1 / 0.03, 1 / 0.025)
+    vv = tuple(0.01 * r * r for r in rd)
+    kw = dict(nx=nx, ny=ny, k0=3, k1=nz - 3, border=3, weno_z=weno_z, rdx=rd[0], rdy=rd[1],
+              rdz=rd[2], vx=vv[0], vy=vv[1], vz=vv[2], dt=1e-3, a=0.75, b=0.25)
+    exp = u0.clone()
+    ref.burgers3d_stage(inp, u0, exp, nx, ny, 3, nz - 3, 3, weno_z, *rd, *vv, 1e-3, 0.75, 0.25)
+    old_v, old_t = lib.advdiff_set_b3_ver(ver), lib.advdiff_set_b3_ty(ty)
+    try:
+        g0 = u0.to(DEV)
+        gout = g0.clone()
+        stencil.burgers3d_stage(inp.to(DEV), g0, gout, **kw)
+        torch.cuda.synchronize()
+    finally:
+        lib.advdiff_set_b3_ver(old_v)
+        lib.advdiff_set_b3_ty(old_t)
+    err = (gout.cpu() - exp).abs().max().item()
+    assert err < 1e-11, err
