@@ -107,6 +107,24 @@ int advdiff_diffusion2d_stage_ls(int dtype, const void* in, void* du, void* out,
 // (WENO5) / 4 (WENO7): reads planes k0-R .. k1+R-1 and needs border >= R.
 // rdx = 1/dx ...; vx = C/dx² ... (all zero = inviscid, the viscous path is not
 // compiled in).
+// Burgers stages with the step size in device memory (adaptive CFL; nullptr: use dt).
+// ls != 0: low-storage stage (aux = du).  A device dt of 0 makes the stage out = in.
+int advdiff_burgers3d_stage_dt(int dtype, const void* in, void* aux, void* out, int nx, int ny,
+                               int64_t sy, int64_t sz, int k0, int k1, int border, int weno,
+                               double rdx, double rdy, double rdz, double vx, double vy,
+                               double vz, double dt, double a, double b, int ls,
+                               const double* dt_dev, void* stream);
+int advdiff_burgers2d_stage_dt(int dtype, const void* in, void* aux, void* out, int nx,
+                               int64_t sy, int j0, int j1, int border, int weno, double rdx,
+                               double rdy, double vx, double vy, double dt, double a, double b,
+                               int ls, const double* dt_dev, void* stream);
+// Adaptive CFL step on the device: red = advdiff_reduce_norms result (max|u| at [2], after
+// any cross-rank MAX), state = [t, dt, steps] (double[3], device): dt = min(cfl_h / max(
+// umax, 1e-300), dt_visc if > 0), clamped to t_end (has_tend) and 0 once t >= t_end; t and
+// steps advance with it.
+int advdiff_adaptive_dt(const double* red, double* state, double cfl_h, double dt_visc,
+                        double t_end, int has_tend, void* stream);
+
 int advdiff_burgers3d_stage(int dtype, const void* in, const void* u0, void* out,
                             int nx, int ny, int64_t sy, int64_t sz, int k0, int k1,
                             int border, int weno, double rdx, double rdy, double rdz,

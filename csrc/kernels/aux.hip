@@ -166,7 +166,35 @@ __global__ void scale_kernel(T* __restrict__ x, int64_t n, T s) {
     x[q] *= s;
 }
 
+// Adaptive-CFL step size on the device (one lane): the host loop of solver.py
+// (Burgers.stable_dt + the t_end clamp) evaluated in the same order, so the step
+// sequence is bit-identical to the host-driven path.  state = [t, dt, steps].
+__global__ void adaptive_dt_kernel(const double* __restrict__ red, double* state, double cfl_h,
+                                   double dt_visc, double t_end, int has_tend) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const double t = state[0];
+  double dt = 0.0;
+  if (!(has_tend && t >= t_end * (1.0 - 1e-14))) {
+    const double u = red[2] >= 1e-300 ? red[2] : 1e-300;  // max(umax, 1e-300)
+    dt = cfl_h / u;
+    if (dt_visc > 0.0 && dt_visc < dt) dt = dt_visc;
+    if (has_tend && t + dt > t_end) dt = t_end - t;
+  }
+  state[1] = dt;
+  if (dt != 0.0) {
+    state[0] = t + dt;
+    state[2] = state[2] + 1.0;
+  }
+}
+
 }  // namespace advdiff
+
+extern "C" int advdiff_adaptive_dt(const double* red, double* state, double cfl_h,
+                                   double dt_visc, double t_end, int has_tend, void* stream) {
+  hipLaunchKernelGGL(advdiff::adaptive_dt_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     red, state, cfl_h, dt_visc, t_end, has_tend);
+  return hipGetLastError();
+}
 
 extern "C" int advdiff_scale(int dtype, void* x, int64_t n, double s, void* stream) {
   using namespace advdiff;

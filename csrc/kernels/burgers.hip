@@ -38,7 +38,8 @@ template <typename T, int W, bool WZ, bool VISC, int MODE, int TX, int TY>
 __global__ __launch_bounds__(TX* TY)
 __attribute__((amdgpu_waves_per_eu(W == 7 ? 4 : 1))) void burgers3d_stage_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
-    int k1, int zchunk, int border, T rdx, T rdy, T rdz, T vx, T vy, T vz, T dt, T a, T b) {
+    int k1, int zchunk, int border, T rdx, T rdy, T rdz, T vx, T vy, T vz, T dt, T a, T b,
+    const double* __restrict__ dtp) {
   using Rc = Recon<T, W, WZ>;
   constexpr int R = Rc::R, NP = 2 * R - 1;
   constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NT = TX * TY;
@@ -58,6 +59,11 @@ __attribute__((amdgpu_waves_per_eu(W == 7 ? 4 : 1))) void burgers3d_stage_kernel
   const bool active = i >= border && i < nx - border && j >= border && j < ny - border;
   const int64_t own = (int64_t)min(j, ny - 1) * sy + min(i, nx - 1);
   const int lc = (ty + R) * LX + tx + R;
+  if (dtp != nullptr && !device_dt(dtp, dt)) {  // adaptive run at t_end: out = in
+    if (active)
+      for (int k = kc0; k < kc1; ++k) out[(int64_t)k * sz + own] = in[(int64_t)k * sz + own];
+    return;
+  }
 
   // Per-thread gather offsets of the tile (plane-relative), computed once.
   int64_t toff[NPT];
@@ -205,7 +211,8 @@ __attribute__((amdgpu_waves_per_eu(W == 7 ? 4 : 1))) void burgers3d_stage_kernel
 template <typename T, bool WZ, bool VISC, int MODE, int TY, bool DB, int WPE>
 __global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(WPE))) void burgers3d_w5_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
-    int k1, int zchunk, int border, T rdx, T rdy, T rdz, T vx, T vy, T vz, T dt, T a, T b) {
+    int k1, int zchunk, int border, T rdx, T rdy, T rdz, T vx, T vy, T vz, T dt, T a, T b,
+    const double* __restrict__ dtp) {
   constexpr int R = 3, NP = 5, TX = 64, TXO = TX - 1;
   constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NT = TX * TY, LT = LX * LY;
   constexpr int NPT = (LT + NT - 1) / NT;
@@ -224,6 +231,11 @@ __global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const bool active = tx >= 1 && i < nx - border && j < ny - border;
   const int64_t own = (int64_t)min(j, ny - 1) * sy + min(i, nx - 1);
   const int lc = (ty + R) * LX + tx + R;
+  if (dtp != nullptr && !device_dt(dtp, dt)) {  // adaptive run at t_end: out = in
+    if (active)
+      for (int k = kc0; k < kc1; ++k) out[(int64_t)k * sz + own] = in[(int64_t)k * sz + own];
+    return;
+  }
 
   int64_t toff[NPT];
 #pragma unroll
@@ -356,7 +368,7 @@ __global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(WPE))) 
 template <typename T, int W, bool WZ, bool VISC, int MODE, int TX>
 __global__ __launch_bounds__(TX) void burgers2d_stage_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int64_t sy, int j0, int j1, int ychunk,
-    int border, T rdx, T rdy, T vx, T vy, T dt, T a, T b) {
+    int border, T rdx, T rdy, T vx, T vy, T dt, T a, T b, const double* __restrict__ dtp) {
   using Rc = Recon<T, W, WZ>;
   constexpr int R = Rc::R, NP = 2 * R - 1, LX = TX + 2 * R;
   __shared__ T s_u[LX];
@@ -371,6 +383,11 @@ __global__ __launch_bounds__(TX) void burgers2d_stage_kernel(
   const bool active = i >= border && i < nx - border;
   const int ic = min(i, nx - 1);
   const int lc = tx + R;
+  if (dtp != nullptr && !device_dt(dtp, dt)) {  // adaptive run at t_end: out = in
+    if (active)
+      for (int jj = jc0; jj < jc1; ++jj) out[(int64_t)jj * sy + i] = in[(int64_t)jj * sy + i];
+    return;
+  }
   const int g0 = clampi(i0 - R + tx, 0, nx - 1);
   const int g1 = clampi(i0 - R + TX + tx, 0, nx - 1);
 
@@ -478,6 +495,7 @@ struct BArgs {
   int lo, hi, border;  // marched-axis range [lo, hi)
   double rdx, rdy, rdz, vx, vy, vz, dt, a, b;
   hipStream_t st;
+  const double* dtp;  // device dt (adaptive CFL) or nullptr: use dt
 };
 
 template <typename T, int W, bool WZ, bool VISC, int MODE, int TY>
@@ -490,7 +508,7 @@ static hipError_t launch_b3_ty(const BArgs& p) {
                      dim3(gx, gy, gz), dim3(kBTX3, TY, 1), 0, p.st, (const T*)p.in, (T*)p.aux,
                      (T*)p.out, p.nx, p.ny, p.sy, p.sz, p.lo, p.hi, zc, p.border, T(p.rdx),
                      T(p.rdy), T(p.rdz), T(p.vx * s), T(p.vy * s), T(p.vz * s), T(p.dt), T(p.a),
-                     T(p.b));
+                     T(p.b), p.dtp);
   return hipGetLastError();
 }
 
@@ -504,7 +522,7 @@ static hipError_t launch_b3_v2(const BArgs& p) {
   hipLaunchKernelGGL((burgers3d_w5_kernel<T, WZ, VISC, MODE, TY, DB, WPE>), dim3(gx, gy, gz),
                      dim3(64, TY, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx, p.ny,
                      p.sy, p.sz, p.lo, p.hi, zc, p.border, T(p.rdx), T(p.rdy), T(p.rdz),
-                     T(p.vx * s), T(p.vy * s), T(p.vz * s), T(p.dt), T(p.a), T(p.b));
+                     T(p.vx * s), T(p.vy * s), T(p.vz * s), T(p.dt), T(p.a), T(p.b), p.dtp);
   return hipGetLastError();
 }
 
@@ -552,7 +570,7 @@ static hipError_t launch_b2(const BArgs& p) {
   hipLaunchKernelGGL((burgers2d_stage_kernel<T, W, WZ, VISC, MODE, kBTX2>), dim3(gx, gy, 1),
                      dim3(kBTX2, 1, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx,
                      p.sy, p.lo, p.hi, yc, p.border, T(p.rdx), T(p.rdy), T(p.vx * s),
-                     T(p.vy * s), T(p.dt), T(p.a), T(p.b));
+                     T(p.vy * s), T(p.dt), T(p.a), T(p.b), p.dtp);
   return hipGetLastError();
 }
 
@@ -618,15 +636,41 @@ extern "C" int advdiff_set_b3_ty(int ty) {
   return old;
 }
 
+// dt_dev: device scalar with the step's dt (adaptive CFL, computed on the device by
+// advdiff_adaptive_dt) or nullptr (use dt).  A device dt of exactly 0 marks a step past
+// t_end: the stage becomes out = in on the active cells (aux untouched), so surplus steps
+// issued ahead of the host's next look at t are exact no-ops.
+extern "C" int advdiff_burgers3d_stage_dt(int dtype, const void* in, void* aux, void* out,
+                                          int nx, int ny, int64_t sy, int64_t sz, int k0,
+                                          int k1, int border, int weno, double rdx, double rdy,
+                                          double rdz, double vx, double vy, double vz,
+                                          double dt, double a, double b, int ls,
+                                          const double* dt_dev, void* stream) {
+  using namespace advdiff;
+  const BArgs p{in, aux, out, nx, ny, sy, sz, k0, k1, border, rdx, rdy, rdz,
+                vx, vy, vz, dt, a, b, (hipStream_t)stream, dt_dev};
+  return run_b(dtype, true, weno, ls != 0, p);
+}
+
+extern "C" int advdiff_burgers2d_stage_dt(int dtype, const void* in, void* aux, void* out,
+                                          int nx, int64_t sy, int j0, int j1, int border,
+                                          int weno, double rdx, double rdy, double vx,
+                                          double vy, double dt, double a, double b, int ls,
+                                          const double* dt_dev, void* stream) {
+  using namespace advdiff;
+  const BArgs p{in, aux, out, nx, 0, sy, 0, j0, j1, border, rdx, rdy, 0.0,
+                vx, vy, 0.0, dt, a, b, (hipStream_t)stream, dt_dev};
+  return run_b(dtype, false, weno, ls != 0, p);
+}
+
 extern "C" int advdiff_burgers3d_stage(int dtype, const void* in, const void* u0, void* out,
                                        int nx, int ny, int64_t sy, int64_t sz, int k0, int k1,
                                        int border, int weno, double rdx, double rdy,
                                        double rdz, double vx, double vy, double vz, double dt,
                                        double a, double b, void* stream) {
-  using namespace advdiff;
-  const BArgs p{in, const_cast<void*>(u0), out, nx, ny, sy, sz, k0, k1, border, rdx, rdy, rdz,
-                vx, vy, vz, dt, a, b, (hipStream_t)stream};
-  return run_b(dtype, true, weno, false, p);
+  return advdiff_burgers3d_stage_dt(dtype, in, const_cast<void*>(u0), out, nx, ny, sy, sz, k0,
+                                    k1, border, weno, rdx, rdy, rdz, vx, vy, vz, dt, a, b, 0,
+                                    nullptr, stream);
 }
 
 extern "C" int advdiff_burgers3d_stage_ls(int dtype, const void* in, void* du, void* out,
@@ -634,20 +678,17 @@ extern "C" int advdiff_burgers3d_stage_ls(int dtype, const void* in, void* du, v
                                           int k1, int border, int weno, double rdx, double rdy,
                                           double rdz, double vx, double vy, double vz,
                                           double dt, double A, double B, void* stream) {
-  using namespace advdiff;
-  const BArgs p{in, du, out, nx, ny, sy, sz, k0, k1, border, rdx, rdy, rdz,
-                vx, vy, vz, dt, A, B, (hipStream_t)stream};
-  return run_b(dtype, true, weno, true, p);
+  return advdiff_burgers3d_stage_dt(dtype, in, du, out, nx, ny, sy, sz, k0, k1, border, weno,
+                                    rdx, rdy, rdz, vx, vy, vz, dt, A, B, 1, nullptr, stream);
 }
 
 extern "C" int advdiff_burgers2d_stage(int dtype, const void* in, const void* u0, void* out,
                                        int nx, int64_t sy, int j0, int j1, int border,
                                        int weno, double rdx, double rdy, double vx, double vy,
                                        double dt, double a, double b, void* stream) {
-  using namespace advdiff;
-  const BArgs p{in, const_cast<void*>(u0), out, nx, 0, sy, 0, j0, j1, border, rdx, rdy, 0.0,
-                vx, vy, 0.0, dt, a, b, (hipStream_t)stream};
-  return run_b(dtype, false, weno, false, p);
+  return advdiff_burgers2d_stage_dt(dtype, in, const_cast<void*>(u0), out, nx, sy, j0, j1,
+                                    border, weno, rdx, rdy, vx, vy, dt, a, b, 0, nullptr,
+                                    stream);
 }
 
 extern "C" int advdiff_burgers2d_stage_ls(int dtype, const void* in, void* du, void* out,
@@ -655,8 +696,6 @@ extern "C" int advdiff_burgers2d_stage_ls(int dtype, const void* in, void* du, v
                                           int weno, double rdx, double rdy, double vx,
                                           double vy, double dt, double A, double B,
                                           void* stream) {
-  using namespace advdiff;
-  const BArgs p{in, du, out, nx, 0, sy, 0, j0, j1, border, rdx, rdy, 0.0,
-                vx, vy, 0.0, dt, A, B, (hipStream_t)stream};
-  return run_b(dtype, false, weno, true, p);
+  return advdiff_burgers2d_stage_dt(dtype, in, du, out, nx, sy, j0, j1, border, weno, rdx, rdy,
+                                    vx, vy, dt, A, B, 1, nullptr, stream);
 }

@@ -466,6 +466,16 @@ __device__ __forceinline__ T wave_shr1(T v) { return dpp_move<0x138>(v); }  // f
 template <typename T>
 __device__ __forceinline__ T wave_shl1(T v) { return dpp_move<0x130>(v); }  // from lane i+1
 
+// Adaptive-CFL step size read from device memory (advdiff_adaptive_dt): false when the
+// run has reached t_end (dt == 0), i.e. the stage is a no-op.
+template <typename T>
+__device__ __forceinline__ bool device_dt(const double* dtp, T& dt) {
+  const double d = *dtp;
+  if (d == 0.0) return false;
+  dt = T(d);
+  return true;
+}
+
 // ---------------------------------------------------------------------------------
 // Stage epilogues.  MODE selects the time integrator's per-stage update:
 //   kSsp1 : out = b (c + dt L)                      (SSP-RK3 stage 1)

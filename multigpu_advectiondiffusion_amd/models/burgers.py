@@ -10,8 +10,10 @@ Time step (`SingleGPU/Burgers3d_WENO5/main.cpp:130-133`, `MultiGPU/Burgers3d_Bas
     dt = min(CFL·min(d)/umax, 0.9 / (2C Σ 1/d²))
 The reference hard-codes umax = 1 (no reduction).  ``cfl_mode="fixed"``
 keeps that (default: matches the reference step count); ``"adaptive"`` uses the true
-global max|u| (device reduction + allreduce every step, as the MATLAB prototype
-`LFWENO5FDM3d.m:71`).
+global max|u| (as the MATLAB prototype `LFWENO5FDM3d.m:71`) computed ON THE DEVICE every
+step — norm reducer -> RCCL MAX allreduce on the stream -> ``advdiff_adaptive_dt`` ->
+the stage kernels read dt from device memory — so the step loop never waits for the
+host and single-process runs replay it as hipGraphs (solver.py ``_run_device_dt``).
 
 Deltas by design: each face flux is computed once (the reference's MultiGPU x-sweep
 starts at i=2 with a zero "old" flux — quirk #8 — and the SingleGPU y-sweep covers
@@ -64,8 +66,14 @@ class Burgers(Model):
             dt = min(dt, 0.9 / (2.0 * sum(self.visc)))
         return dt
 
+    def cfl_terms(self):
+        """(cfl * min(d), viscous dt limit or 0): stable_dt(umax) = min(cfl_h / umax, dv),
+        the two constants of the device-side adaptive step (ops/stencil.py adaptive_dt)."""
+        dv = 0.9 / (2.0 * sum(self.visc)) if self.C > 0 else 0.0
+        return self.cfl * min(self.grid.spacing), dv
+
     def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None, nx=None, ny=None,
-              border=None, ls=False):
+              border=None, ls=False, dt_dev=None):
         g = self.grid
         nx = g.nx if nx is None else nx
         ny = g.ny if ny is None else ny
@@ -76,11 +84,12 @@ class Burgers(Model):
                                     border=border, weno_z=z, rdx=self.rd[0],
                                     rdy=self.rd[1], rdz=self.rd[2], vx=self.visc[0],
                                     vy=self.visc[1], vz=self.visc[2], dt=dt, a=a, b=b,
-                                    stream=stream, ls=ls)
+                                    stream=stream, ls=ls, dt_dev=dt_dev)
         else:
             stencil.burgers2d_stage(inp, u0, out, nx=nx, j0=lo, j1=hi, border=border,
                                     weno_z=z, rdx=self.rd[0], rdy=self.rd[1], vx=self.visc[0],
-                                    vy=self.visc[1], dt=dt, a=a, b=b, stream=stream, ls=ls)
+                                    vy=self.visc[1], dt=dt, a=a, b=b, stream=stream, ls=ls,
+                                    dt_dev=dt_dev)
 
     def describe(self):
         d = super().describe()

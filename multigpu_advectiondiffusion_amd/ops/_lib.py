@@ -55,6 +55,13 @@ _SIGS = {
                                 c_dbl, c_dbl, c_dbl, c_vp],
     "advdiff_burgers2d_stage": [c_int, c_vp, c_vp, c_vp, c_int, c_i64, c_int, c_int, c_int,
                                 c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_vp],
+    "advdiff_burgers3d_stage_dt": [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_i64, c_i64, c_int,
+                                   c_int, c_int, c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl,
+                                   c_dbl, c_dbl, c_dbl, c_dbl, c_int, c_vp, c_vp],
+    "advdiff_burgers2d_stage_dt": [c_int, c_vp, c_vp, c_vp, c_int, c_i64, c_int, c_int, c_int,
+                                   c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_int,
+                                   c_vp, c_vp],
+    "advdiff_adaptive_dt": [c_vp, c_vp, c_dbl, c_dbl, c_dbl, c_int, c_vp],
     "advdiff_reduce_norms": [c_int, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int,
                              c_int, c_int, c_vp, c_vp, c_vp],
     "advdiff_init_ic": [c_int, c_int, c_vp, c_int, c_int, c_int, c_i64, c_i64, c_int, c_int,

@@ -170,9 +170,19 @@ def diffusion2d_stage(inp, u0, out, *, nx, j0, j1, border, order, cx, cy, dt, a,
         ref.diffusion2d_stage(inp, u0, out, nx, j0, j1, border, order, cx, cy, dt, a, b, ls)
 
 
+def _dt_of(dt, dt_dev):
+    """Host value of a device dt (torch/CPU paths only; the HIP kernels read it on device)."""
+    if dt_dev is None:
+        return dt, False
+    d = float(dt_dev.reshape(-1)[0])
+    return d, d == 0.0
+
+
 def burgers3d_stage(inp, u0, out, *, nx, ny, k0, k1, border, weno_z, rdx, rdy, rdz,
-                    vx=0.0, vy=0.0, vz=0.0, dt, a, b, stream=None, ls=False):
-    """weno_z: scheme — bool (WENO5 Z / JS) or "js" | "z" | "js7" (WENO7)."""
+                    vx=0.0, vy=0.0, vz=0.0, dt, a, b, stream=None, ls=False, dt_dev=None):
+    """weno_z: scheme — bool (WENO5 Z / JS) or "js" | "z" | "js7" (WENO7).
+    dt_dev: float64 device scalar holding dt (adaptive CFL: written on the device by
+    adaptive_dt, read by the kernel — no host sync); 0 there makes the stage out = in."""
     _check_layout(inp, u0, out)
     code_s, R = ref.scheme_code(weno_z), ref.scheme_radius(weno_z)
     if border < R:
@@ -180,18 +190,25 @@ def burgers3d_stage(inp, u0, out, *, nx, ny, k0, k1, border, weno_z, rdx, rdy, r
     if _native(inp):
         lib = _lib.require()
         assert k0 >= R and k1 + R <= inp.shape[0], "stencil planes out of bounds"
-        fn = lib.advdiff_burgers3d_stage_ls if ls else lib.advdiff_burgers3d_stage
-        code = fn(_dtype_code(inp), _ptr(inp), _aux_ptr(u0, a, ls), _ptr(out), nx, ny,
-                  inp.stride(1), inp.stride(0), k0, k1, border, code_s, rdx, rdy, rdz,
-                  vx, vy, vz, dt, a, b, _stream_ptr(stream))
+        code = lib.advdiff_burgers3d_stage_dt(
+            _dtype_code(inp), _ptr(inp), _aux_ptr(u0, a, ls), _ptr(out), nx, ny,
+            inp.stride(1), inp.stride(0), k0, k1, border, code_s, rdx, rdy, rdz, vx, vy, vz,
+            dt, a, b, 1 if ls else 0, None if dt_dev is None else dt_dev.data_ptr(),
+            _stream_ptr(stream))
         _lib.check(code, "burgers3d_stage")
     else:
+        dt, noop = _dt_of(dt, dt_dev)
+        if noop:
+            if k1 > k0:
+                sl = (slice(k0, k1), slice(border, ny - border), slice(border, nx - border))
+                out[sl] = inp[sl]
+            return
         ref.burgers3d_stage(inp, u0, out, nx, ny, k0, k1, border, code_s, rdx, rdy, rdz,
                             vx, vy, vz, dt, a, b, ls)
 
 
 def burgers2d_stage(inp, u0, out, *, nx, j0, j1, border, weno_z, rdx, rdy, vx=0.0, vy=0.0,
-                    dt, a, b, stream=None, ls=False):
+                    dt, a, b, stream=None, ls=False, dt_dev=None):
     _check_layout(inp, u0, out)
     code_s, R = ref.scheme_code(weno_z), ref.scheme_radius(weno_z)
     if border < R:
@@ -199,14 +216,45 @@ def burgers2d_stage(inp, u0, out, *, nx, j0, j1, border, weno_z, rdx, rdy, vx=0.
     if _native(inp):
         lib = _lib.require()
         assert j0 >= R and j1 + R <= inp.shape[0], "stencil rows out of bounds"
-        fn = lib.advdiff_burgers2d_stage_ls if ls else lib.advdiff_burgers2d_stage
-        code = fn(_dtype_code(inp), _ptr(inp), _aux_ptr(u0, a, ls), _ptr(out), nx,
-                  inp.stride(0), j0, j1, border, code_s, rdx, rdy, vx, vy, dt, a, b,
-                  _stream_ptr(stream))
+        code = lib.advdiff_burgers2d_stage_dt(
+            _dtype_code(inp), _ptr(inp), _aux_ptr(u0, a, ls), _ptr(out), nx, inp.stride(0),
+            j0, j1, border, code_s, rdx, rdy, vx, vy, dt, a, b, 1 if ls else 0,
+            None if dt_dev is None else dt_dev.data_ptr(), _stream_ptr(stream))
         _lib.check(code, "burgers2d_stage")
     else:
+        dt, noop = _dt_of(dt, dt_dev)
+        if noop:
+            if j1 > j0:
+                out[j0:j1, border:nx - border] = inp[j0:j1, border:nx - border]
+            return
         ref.burgers2d_stage(inp, u0, out, nx, j0, j1, border, code_s, rdx, rdy, vx, vy,
                             dt, a, b, ls)
+
+
+def adaptive_dt(red, state, *, cfl_h, dt_visc, t_end=None, stream=None):
+    """Device-side adaptive CFL step (see kernels.h advdiff_adaptive_dt): red = the norm
+    reducer's result tensor (max|u| at [2]), state = float64[3] device tensor [t, dt,
+    steps], updated in place."""
+    if state.is_cuda:
+        lib = _lib.require()
+        code = lib.advdiff_adaptive_dt(red.data_ptr(), state.data_ptr(), cfl_h, dt_visc,
+                                       0.0 if t_end is None else t_end,
+                                       0 if t_end is None else 1, _stream_ptr(stream))
+        _lib.check(code, "adaptive_dt")
+        return
+    t = float(state[0])
+    dt = 0.0
+    if not (t_end is not None and t >= t_end * (1 - 1e-14)):
+        u = max(float(red[2]), 1e-300)
+        dt = cfl_h / u
+        if dt_visc > 0.0 and dt_visc < dt:
+            dt = dt_visc
+        if t_end is not None and t + dt > t_end:
+            dt = t_end - t
+    state[1] = dt
+    if dt != 0.0:
+        state[0] = t + dt
+        state[2] = float(state[2]) + 1.0
 
 
 class NormReducer:

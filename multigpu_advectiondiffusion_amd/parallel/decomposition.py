@@ -185,6 +185,57 @@ def parse_proc_grid(spec, world: int, shape_array: tuple, ghost: int) -> tuple:
     return p
 
 
+def halo_link_bytes(shape_array: tuple, pgrid: tuple, ghost: int, elem: int,
+                    corners: bool) -> float:
+    """Bytes one rank moves over its busiest xGMI link per exchange (upper bound over
+    ranks).  Every neighbour pair has its own point-to-point link, so messages to
+    different neighbours overlap; with corners (the fused step's phased exchange: axis by
+    axis, fastest first, each phase carrying the ghosts of the axes before it) the
+    phases run one after another, so their per-phase maxima add up."""
+    dims = len(shape_array)
+    local = [-(-n // p) for n, p in zip(shape_array, pgrid)]  # largest block
+    split = [a for a in range(dims) if pgrid[a] > 1]
+    done = set()
+    per_phase = []
+    for a in sorted(split, reverse=True):
+        face = ghost
+        for b in range(dims):
+            if b == a:
+                continue
+            face *= (local[b] + 2 * ghost) if (corners and b in done) else local[b]
+        per_phase.append(face * elem)
+        done.add(a)
+    if not per_phase:
+        return 0.0
+    return float(sum(per_phase) if corners else max(per_phase))
+
+
+def candidate_proc_grids(world: int, shape_array: tuple, ghost: int, elem: int = 8,
+                         corners: bool = False, keep: int = 3) -> list:
+    """Process grids worth trying on an xGMI node, best first by `halo_link_bytes`: the
+    slab, plus grids that split only the two slowest axes (a split of the contiguous x
+    axis makes the strided x faces AND boundary boxes a few cells wide, which waste
+    most of a 64-lane x tile: +16 % compute at (2,2,2), profiles/multigpu_readiness.md)
+    that move fewer bytes per link than the slab."""
+    dims = len(shape_array)
+    slab = (world,) + (1,) * (dims - 1)
+    out = [slab]
+    if dims < 2 or world == 1:
+        return out
+    scored = []
+    for p in _factorisations(world, dims):
+        if p == slab or p[-1] > 1:
+            continue
+        if any(n // q < max(ghost, 1) for n, q in zip(shape_array, p)):
+            continue
+        scored.append((halo_link_bytes(shape_array, p, ghost, elem, corners), p))
+    base = halo_link_bytes(shape_array, slab, ghost, elem, corners)
+    for b, p in sorted(scored):
+        if b < 0.9 * base and len(out) < keep:
+            out.append(p)
+    return out
+
+
 def _factorisations(n: int, dims: int):
     if dims == 1:
         yield (n,)

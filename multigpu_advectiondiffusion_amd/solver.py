@@ -68,14 +68,18 @@ class Solver:
                  dtype=torch.float64, device=None, ic: str = "sine", ic_params=None,
                  overlap: bool = True, pad_rows: bool = True, t0: float = 0.0,
                  check_every: int = 0, fused: bool | None = None, decomp=None,
-                 integrator: str = "ssprk3", kernel: str = "native"):
+                 integrator: str = "ssprk3", kernel: str = "native",
+                 device_dt: bool | None = None):
         """decomp: process grid — None/"slab" (split the slowest axis only, the
         reference's layout), "auto" (smallest halo surface) or "PZxPYxPX" / a tuple in
         array axis order ((pz, py, px) in 3-D, (py, px) in 2-D).
         integrator: "ssprk3" (3 stages, the C++/CUDA apps) or "lsrk45" (low-storage
         RK4(5), 5 stages, the MATLAB WENO7 prototypes).
         kernel: "native" (the gfx950 HIP kernels) or "torch" (the PyTorch reference ops on
-        the same device — the naive A/B baseline; same launch ranges and schedule)."""
+        the same device — the naive A/B baseline; same launch ranges and schedule).
+        device_dt: adaptive-CFL models compute dt on the device (no per-step host sync;
+        graph-replayable); None = on for the native GPU path, False = the host-driven
+        loop (bitwise the same step sequence, tests/test_adaptive_dt.py)."""
         if kernel not in ("native", "torch"):
             raise ValueError("kernel must be 'native' or 'torch'")
         self.kernel = kernel
@@ -144,6 +148,11 @@ class Solver:
         self.zact = (max(0, model.border - off), min(self.d.alloc, grid.n_decomposed - model.border - off))
         self._pending = {}
         self._reducer = None
+        self._dt_dev = None  # device dt of the step being issued (adaptive CFL)
+        self._dts = None     # device [t, dt, steps] of the adaptive loop
+        if device_dt is None:
+            device_dt = self.device.type == "cuda" and kernel == "native"
+        self.device_dt = bool(device_dt) and model.needs_umax
 
     def _initial_field(self, ic, params):
         """IC of the local slab incl. ghosts (ghosts = the neighbours' planes at t0).
@@ -224,7 +233,8 @@ class Solver:
             return
         lo, hi = rng
         if hi > lo:
-            self.model.stage(inp, u0, out, lo, hi, dt, a, b, ls=ls)
+            kw = {} if self._dt_dev is None else {"dt_dev": self._dt_dev}
+            self.model.stage(inp, u0, out, lo, hi, dt, a, b, ls=ls, **kw)
             trace.sync_check(f"{self.model.name} stage [{lo},{hi})", self.device)
 
     def _launch_box(self, inp, u0, out, box, dt, a, b, ls=False):
@@ -244,6 +254,8 @@ class Solver:
             sl = (slice(None), slice(x0 - R, x1 + R))
             kw = dict(nx=x1 - x0 + 2 * R, border=R)
         v = (lambda t: None if t is None else t[sl])
+        if self._dt_dev is not None:
+            kw["dt_dev"] = self._dt_dev
         self.model.stage(v(inp), v(u0), v(out), z0, z1, dt, a, b, ls=ls, **kw)
         trace.sync_check(f"{self.model.name} stage box {box}", self.device)
 
@@ -355,16 +367,15 @@ class Solver:
             for A, Bc in zip(LSRK45_A, LSRK45_B):
                 self._stage(self.u, self.du, self.un, A, Bc, dt, ls=True)
                 self.u, self.un = self.un, self.u
+        else:
+            u, A, B = self.u, self.A, self.B
+            (a1, b1), (a2, b2), (a3, b3) = RK3
+            self._stage(u, None, A, a1, b1, dt)
+            self._stage(A, u, B, a2, b2, dt)
+            self._stage(B, u, u, a3, b3, dt)
+        if self._dt_dev is None:  # device-dt steps keep t / it on the device
             self.t += dt
             self.it += 1
-            return
-        u, A, B = self.u, self.A, self.B
-        (a1, b1), (a2, b2), (a3, b3) = RK3
-        self._stage(u, None, A, a1, b1, dt)
-        self._stage(A, u, B, a2, b2, dt)
-        self._stage(B, u, u, a3, b3, dt)
-        self.t += dt
-        self.it += 1
 
     def sync_halos(self):
         """Complete every in-flight exchange (stream-ordered)."""
@@ -403,10 +414,11 @@ class Solver:
         return (self.device.type == "cuda" and self.comm.size == 1 and not trace.SYNC_DEBUG
                 and not trace.TRACE)
 
-    def _graph_for(self, dt: float):
+    def _graph_for(self, dt: float | None, t_end: float | None = None):
+        """dt=None: a graph of device-dt (adaptive CFL) steps towards t_end."""
         # A graph bakes in the buffer addresses: the fused / LSRK paths ping-pong u <-> un,
         # so after an odd number of eager steps the other parity needs its own graph.
-        key = (float(dt), self.GRAPH_STEPS, self.u.data_ptr())
+        key = (None if dt is None else float(dt), t_end, self.GRAPH_STEPS, self.u.data_ptr())
         g = getattr(self, "_graphs", {}).get(key)
         if g is not None:
             return g
@@ -420,7 +432,10 @@ class Solver:
         with torch.cuda.stream(side):
             with torch.cuda.graph(graph, stream=side):
                 for _ in range(self.GRAPH_STEPS):
-                    self.step(dt)
+                    if dt is None:
+                        self._step_device_dt(t_end)
+                    else:
+                        self.step(dt)
         torch.cuda.current_stream().wait_stream(side)
         self.t, self.it = t, it
         self._graphs[key] = graph
@@ -438,6 +453,62 @@ class Solver:
         for _ in range(n):
             self.step(dt)
 
+    # ------------------------------------------------------------------------------
+    # adaptive CFL on the device: max|u| (norm reducer) -> RCCL MAX allreduce on the
+    # stream -> advdiff_adaptive_dt -> stage kernels read dt from device memory.  The
+    # host learns t only at chunk ends; steps issued past t_end get dt = 0 and are exact
+    # no-ops.  Same step sequence as the host-driven loop (bitwise; tests).
+    # ------------------------------------------------------------------------------
+    def _allreduce_max_device(self, red):
+        import torch.distributed as dist
+        v = red[2:3]
+        if self.comm.backend == "nccl":
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)  # on-stream, no host sync
+        else:  # gloo (CPU / one-GPU tests): host round trip
+            h = v.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.MAX)
+            v.copy_(h)
+
+    def _step_device_dt(self, t_end):
+        red = self.reducer()(self.u, None, self._owned_xyz_box(), sync=False)
+        if self.comm.size > 1:
+            self._allreduce_max_device(red)
+        cfl_h, dv = self.model.cfl_terms()
+        stencil.adaptive_dt(red, self._dts, cfl_h=cfl_h, dt_visc=dv, t_end=t_end)
+        self._dt_dev = self._dts[1:2]
+        try:
+            self.step(0.0)  # the kernels take dt from _dt_dev
+        finally:
+            self._dt_dev = None
+
+    def _issue_device_dt(self, n, t_end, use_graph):
+        if use_graph and n >= self.GRAPH_STEPS:
+            g = self._graph_for(None, t_end)
+            for _ in range(n // self.GRAPH_STEPS):
+                g.replay()
+            n %= self.GRAPH_STEPS
+        for _ in range(n):
+            self._step_device_dt(t_end)
+
+    def _advance_device_dt(self, iters, t_end, use_graph):
+        import math
+        if self._dts is None:
+            self._dts = torch.zeros(3, dtype=torch.float64, device=self.device)
+        self._dts.copy_(torch.tensor([self.t, 0.0, 0.0], dtype=torch.float64))
+        it0 = self.it
+        if iters is not None:
+            self._issue_device_dt(iters, None, use_graph)
+            t, _, steps = self._dts.tolist()
+        else:
+            n = 1
+            while True:
+                self._issue_device_dt(n, t_end, use_graph)
+                t, dt_last, steps = self._dts.tolist()  # the chunk's only host sync
+                if t >= t_end * (1 - 1e-14) or dt_last == 0.0:
+                    break
+                n = int(min(max(math.ceil((t_end - t) / dt_last), 1), 64))
+        self.t, self.it = t, it0 + int(steps)
+
     def run(self, iters: int | None = None, t_end: float | None = None, dt: float | None = None,
             callback=None, graph: bool | None = None) -> RunStats:
         """Advance `iters` steps (fixed dt) or until `t_end`. Times the loop with a
@@ -447,15 +518,24 @@ class Solver:
         if iters is None and t_end is None:
             raise ValueError("give iters or t_end")
         fixed_dt = dt if dt is not None else (None if self.model.needs_umax else self.dt())
-        use_graph = (self.graph_capable() and fixed_dt is not None and callback is None
-                     and not self.check_every) if graph is None else graph
-        if use_graph:
-            self._graph_for(fixed_dt)  # capture outside the timed region (like a warm-up)
+        dev_dt = (fixed_dt is None and self.device_dt and callback is None
+                  and not self.check_every and _FAULT is None)
+        use_graph = (self.graph_capable() and (fixed_dt is not None or dev_dt)
+                     and callback is None and not self.check_every) if graph is None else graph
+        if use_graph:  # capture outside the timed region (like a warm-up)
+            if fixed_dt is not None:
+                self._graph_for(fixed_dt)
+            elif dev_dt:
+                if self._dts is None:
+                    self._dts = torch.zeros(3, dtype=torch.float64, device=self.device)
+                self._graph_for(None, t_end if iters is None else None)
         self._sync()
         self.comm.barrier()
         t_start = time.perf_counter()
         steps0 = self.it
-        if use_graph:
+        if dev_dt:
+            self._advance_device_dt(iters, t_end, use_graph)
+        elif use_graph:
             if iters is not None:
                 n = iters
             else:  # full steps that fit before t_end, then a short last step
@@ -463,7 +543,7 @@ class Solver:
                 while n > 0 and self.t + n * fixed_dt > t_end:
                     n -= 1
             self._advance(n, fixed_dt, True)
-        while True:
+        while not dev_dt:
             if iters is not None and self.it - steps0 >= iters:
                 break
             if t_end is not None and self.t >= t_end * (1 - 1e-14):

@@ -209,3 +209,22 @@ def test_cartesian_fused_step_bitwise(kind, world, decomp):
     ref = _serial(kind, 3)
     out = spawn_local(world, _run_cart_fused, kind, 3, decomp, True)[0]
     assert np.array_equal(out, ref), np.abs(out - ref).max()
+
+
+def test_candidate_proc_grids_xgmi_model():
+    """Busiest-link bytes of the fused heat exchange (3R = 6 ghosts, phased corners) at
+    the weak-scaling grids: the slab moves 50 MB per link at N = 8, the z/y grids 38 MB;
+    x is never split; at N = 2 / 4 the slab is the only candidate."""
+    from multigpu_advectiondiffusion_amd.parallel.decomposition import (
+        candidate_proc_grids, halo_link_bytes)
+    g8 = (1024, 1024, 1024)
+    assert round(halo_link_bytes(g8, (8, 1, 1), 6, 8, True) / 1e6, 1) == 50.3
+    assert round(halo_link_bytes(g8, (2, 4, 1), 6, 8, True) / 1e6, 1) == 38.3
+    c8 = candidate_proc_grids(8, g8, 6, 8, corners=True)
+    assert c8[0] == (8, 1, 1) and set(c8[1:]) == {(2, 4, 1), (4, 2, 1)}
+    assert all(p[2] == 1 for p in c8)
+    assert candidate_proc_grids(2, (1024, 512, 512), 6, 8, corners=True) == [(2, 1, 1)]
+    assert candidate_proc_grids(4, (1024, 1024, 512), 6, 8, corners=True) == [(4, 1, 1)]
+    assert candidate_proc_grids(1, g8, 6) == [(1, 1, 1)]
+    # faces only (per-stage WENO exchange): messages to different neighbours overlap
+    assert halo_link_bytes((512,) * 3, (2, 2, 2), 3, 8, False) == 3 * 256 * 256 * 8
