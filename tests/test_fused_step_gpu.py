@@ -178,3 +178,33 @@ def test_fused_step_variants_bitwise(cfg, order, dtype):
     finally:
         lib.advdiff_set_step_cfg(old)
         lib.advdiff_set_step_persist(oldp)
+
+
+@pytest.mark.parametrize("order", [4, 2])
+def test_fused_step_production_size_bitwise(order):
+    """The bench's launch at production size (512^3, fp64, the default variant): the grid
+    schedule and the persistent schedule (L = tiles x planes near its int32 guard's scale,
+    per/rem split over CUs x occupancy groups) are bitwise equal to three per-stage
+    launches over the whole grid."""
+    from multigpu_advectiondiffusion_amd.ops import _lib
+    lib = _lib.require()
+    n, R = 512, order // 2
+    g = torch.Generator(device="cuda").manual_seed(5)
+    u = torch.rand((n, n, n), generator=g, dtype=torch.float64, device="cuda")
+    c = (0.21, 0.17, 0.13)
+    dt = 0.9 / (2 * sum(c)) if order == 2 else 0.5 / sum(c)
+    kw = dict(nx=n, ny=n, k0=R, k1=n - R, zlo=R, zhi=n - R, border=R, order=order, cx=c[0],
+              cy=c[1], cz=c[2], dt=dt)
+    exp = _per_stage(u, n, n, R, n - R, R, n - R, R, order, c, dt)
+    got = u.clone()
+    stencil.diffusion3d_step(u, got, exclusive=True, **kw)  # default: grid schedule
+    torch.cuda.synchronize()
+    assert torch.equal(got, exp), (got - exp).abs().max().item()
+    old = lib.advdiff_set_step_persist(1)
+    try:
+        got.copy_(u)
+        stencil.diffusion3d_step(u, got, exclusive=True, **kw)
+        torch.cuda.synchronize()
+    finally:
+        lib.advdiff_set_step_persist(old)
+    assert torch.equal(got, exp), (got - exp).abs().max().item()
