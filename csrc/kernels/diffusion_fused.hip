@@ -519,32 +519,27 @@ __device__ __forceinline__ void v3_march(
     constexpr int SET = PH & 1;
     constexpr int UO = SET * USETB, AO = SET * ASETB;
     // ---- top: new u plane enters the ring; LDS planes u(k+2R), A(k+R), B(k) ----
+    // the prefetch ring (PF slots) and the delay line (R slots) rotate by renaming:
+    // iteration PH consumes prefetch slot PF0 and refills it with plane k+PF
+    constexpr int PF0 = PH % PF;
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
-      dl[q][R - 1] = ru[q][UIN];
-      ru[q][UIN] = un[0][q];
+      dl[q][(PH + R - 1) % R] = ru[q][UIN];
+      ru[q][UIN] = un[PF0][q];
       lds_st<T>(lb, ub[q] + UO + (R * UW + R) * E, ru[q][sl(2 * R)]);
       lds_st<T>(lb, aw[q] + AO, ra[q][sl(R)]);
       lds_st<T>(lb, aw[q] + AO + ABB, rb[q][sl(0)]);
     }
 #pragma unroll
     for (int h = 0; h < NH; ++h)  // the rim of u(k+2R)
-      if (hl[h] >= 0) lds_st<T>(lb, hl[h] + UO, hv[0][h]);
-    // shift the prefetch ring, issue plane k+PF
-#pragma unroll
-    for (int f = 0; f + 1 < PF; ++f) {
-#pragma unroll
-      for (int q = 0; q < RPW; ++q) un[f][q] = un[f + 1][q];
-#pragma unroll
-      for (int h = 0; h < NH; ++h) hv[f][h] = hv[f + 1][h];
-    }
+      if (hl[h] >= 0) lds_st<T>(lb, hl[h] + UO, hv[PF0][h]);
     {
       const auto p2 = plane(k + PF + 2 * R);
       const auto p3 = plane(k + PF + 3 * R);
 #pragma unroll
-      for (int h = 0; h < NH; ++h) hv[PF - 1][h] = gld<T>(p2, hoff[h]);
+      for (int h = 0; h < NH; ++h) hv[PF0][h] = gld<T>(p2, hoff[h]);
 #pragma unroll
-      for (int q = 0; q < RPW; ++q) un[PF - 1][q] = gld<T>(p3, goff[q]);
+      for (int q = 0; q < RPW; ++q) un[PF0][q] = gld<T>(p3, goff[q]);
     }
     __syncthreads();
     // ---- stage 1: A(k+2R) on S1 ----
@@ -634,7 +629,7 @@ __device__ __forceinline__ void v3_march(
         if (row < 2 * R || row >= S1R - 2 * R) continue;  // scalar branch
         const int b = ar[q] + AO + ABB;
         const T c = rb[q][sl(0)];
-        T acc = fd_ctr(q3.kc, c, third * dl[q][0]);
+        T acc = fd_ctr(q3.kc, c, third * dl[q][PH % R]);
         constexpr int XC = XS ? 0 : R;
         if constexpr (R == 2) {
           acc = fd4_axis(acc, q3.k[2], rb[q][sl(-2)], rb[q][sl(-1)], rb[q][sl(1)], rb[q][sl(2)]);
@@ -672,12 +667,8 @@ __device__ __forceinline__ void v3_march(
         if (m3[q]) gst<T>(po, goff[q], acc);
       }
     }
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-#pragma unroll
-      for (int d = 0; d < R - 1; ++d) dl[q][d] = dl[q][d + 1];
-    }
   };
+  static_assert((2 * NR) % PF == 0 && (2 * NR) % R == 0, "ring phases must repeat");
 
   // the LDS set of iteration k is (k - kst) & 1: unroll 2 NR so it is static
   for (int kb = kst; kb < kc1; kb += 2 * NR) {
