@@ -9,7 +9,8 @@
 // plus named options (runtime replacements of the reference's #defines, §2.7):
 //   --ic NAME  --order 2|4  --safety S  --weno js|z|js7  --visc C  --fp32  --no-overlap
 //   --integrator ssprk3|lsrk45  --no-fused  --transport rccl|socket  --write FILE
-//   --error-norms
+//   --error-norms  --decomp slab|PZxPYxPX|PYxPX (process grid in array order: Cartesian
+//   blocks, cart.cpp; default z-slabs as the reference)
 // Launch one process per GPU with torchrun-style env vars (RANK/WORLD_SIZE/LOCAL_RANK/
 // MASTER_ADDR/MASTER_PORT), e.g. via `python -m multigpu_advectiondiffusion_amd.launch`.
 #include <chrono>
@@ -55,7 +56,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
               << (diff ? (dims == 3 ? " K L W H Nx Ny Nz iters [bx by bz]" : " K L W Nx Ny iters [bx by]")
                        : (dims == 3 ? " tEnd CFL L W H Nx Ny Nz [bx by bz]" : " tEnd CFL L W Nx Ny [bx by]"))
               << " [--ic NAME] [--order 2|4] [--weno js|z|js7] [--integrator ssprk3|lsrk45] [--no-fused] [--visc C] [--fp32] [--no-overlap]"
-                 " [--transport rccl|socket] [--write FILE] [--error-norms]\n";
+                 " [--transport rccl|socket] [--decomp slab|PZxPYxPX|PYxPX] [--write FILE] [--error-norms]\n";
     return 1;
   }
   Problem p;
@@ -93,6 +94,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   if (opt.count("--visc")) p.C = std::stod(opt["--visc"]);
   if (opt.count("--fp32")) p.dtype = ADVDIFF_F32;
   if (opt.count("--no-overlap")) p.overlap = false;
+  std::string decomp = opt.count("--decomp") ? opt["--decomp"] : "slab";
   std::string ic = opt.count("--ic") ? opt["--ic"] : (diff ? "heat" : "gaussian");
   p.ic = ic_code(ic);
   if (p.ic == 3) {
@@ -113,6 +115,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   if (env.size > ndev && tk != "socket")
     throw std::runtime_error("more ranks than GPUs: one process per GPU (or --transport socket)");
   HIP_CHECK(hipSetDevice(env.local_rank % ndev));
+  if (decomp != "slab") parse_pgrid(decomp, dims, env.size, p.pgrid);
   auto tr = make_transport(env, tk);
   Engine eng(p, tr.get(), env);
   Stats st = diff ? eng.run_iters(iters) : eng.run_until(tEnd + p.t0);
@@ -120,6 +123,11 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
       std::string(diff ? "Diffusion-" : "Burgers-") + (dims == 3 ? "3D" : "2D") +
       (diff ? (p.order == 4 ? " MI355X-FD4" : " MI355X-FD2") : (p.weno == 1 ? " MI355X-WENO5Z" : p.weno == 0 ? " MI355X-WENO5JS" : " MI355X-WENO7JS"));
   std::string optname = std::string("Fused LDS z-march + RK3 (gfx950), transport=") + tr->name();
+  if (eng.cartesian()) {
+    optname += ", decomp=" + std::to_string(eng.cart().pgrid[0]) + "x" +
+               std::to_string(eng.cart().pgrid[1]);
+    if (dims == 3) optname += "x" + std::to_string(eng.cart().pgrid[2]);
+  }
   double l1 = 0, l2 = 0, li = 0;
   const bool norms = opt.count("--error-norms") && (p.ic == 2 || p.ic == 3);
   if (norms) eng.error_norms(l1, l2, li);

@@ -49,27 +49,49 @@ static double now_s() {
 }
 
 Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_(tr), env_(env) {
-  slab_.n = p.n_decomposed();
-  slab_.size = env.size;
-  slab_.rank = env.rank;
   const int R = p.radius();
-  fused_ = p.fused && p.physics == Physics::Diffusion && p.integrator == 0 &&
-           slab_.n / slab_.size >= 3 * R;
-  slab_.ghost = fused_ ? 3 * R : R;
-  if (slab_.n < slab_.size * slab_.ghost)
-    throw std::runtime_error("slab thinner than the ghost width: use fewer ranks");
+  // process grid (array order); default: slabs along the slowest axis
+  cd_.dims = p.dims;
+  cd_.rank = env.rank;
+  if (p.dims == 3) {
+    cd_.shape[0] = p.nz;
+    cd_.shape[1] = p.ny;
+    cd_.shape[2] = p.nx;
+  } else {
+    cd_.shape[0] = p.ny;
+    cd_.shape[1] = p.nx;
+  }
+  if (p.pgrid[0] > 0) {
+    for (int a = 0; a < 3; ++a) cd_.pgrid[a] = a < p.dims ? p.pgrid[a] : 1;
+  } else {
+    cd_.pgrid[0] = env.size;
+  }
+  if (cd_.size() != env.size) throw std::runtime_error("process grid does not match WORLD_SIZE");
+  cart_ = !cd_.is_slab();
+  // fused: blocks at least 3R thick on every split axis (else per-stage, solver.py)
+  bool thick = true;
+  for (int a = 0; a < p.dims; ++a)
+    if (cd_.pgrid[a] > 1 && cd_.shape[a] / cd_.pgrid[a] < 3 * R) thick = false;
+  fused_ = p.fused && p.physics == Physics::Diffusion && p.integrator == 0 && thick;
+  cd_.ghost = fused_ ? 3 * R : R;
+  for (int a = 0; a < p.dims; ++a)
+    if (cd_.shape[a] < cd_.pgrid[a] * std::max(cd_.ghost_of_axis(a), 1))
+      throw std::runtime_error("block thinner than the ghost width: use fewer ranks");
+  slab_ = cd_.axis(0);
+  for (int a = 0; a < p.dims; ++a) alloc_[a] = cd_.axis(a).alloc();
   elem_ = p.dtype == ADVDIFF_F64 ? 8 : 4;
   const int per = 256 / (int)elem_;
-  const int sx = (p.nx + per - 1) / per * per;  // 256-B row pitch
+  const int ax = alloc_[p.dims - 1];
+  const int sx = (ax + per - 1) / per * per;  // 256-B row pitch
   sy_ = sx;
   if (p.dims == 3) {
-    sz_ = (int64_t)p.ny * sx;
+    sz_ = (int64_t)alloc_[1] * sx;
     plane_bytes_ = (size_t)sz_ * elem_;
   } else {
     sz_ = sx;
     plane_bytes_ = (size_t)sx * elem_;
   }
-  field_bytes_ = plane_bytes_ * (size_t)slab_.alloc();
+  field_bytes_ = plane_bytes_ * (size_t)alloc_[0];
   HIP_CHECK(hipMalloc(&u_, field_bytes_));
   HIP_CHECK(hipMalloc(&A_, field_bytes_));
   HIP_CHECK(hipMalloc(&B_, field_bytes_));
@@ -80,15 +102,27 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   HIP_CHECK(hipStreamCreateWithPriority(&comm_, hipStreamNonBlocking, hi_pri));
   HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&halo_done_, hipEventDisableTiming));
-  // initial condition on the device, ghosts included (they equal the neighbours' planes)
-  const int kg0 = slab_.start() - slab_.ghost;
-  if (p.dims == 3)
-    KERNEL_CHECK(advdiff_init_ic(p.dtype, p.ic, u_, p.nx, p.ny, slab_.alloc(), sy_, sz_, kg0,
+  // initial condition on the device, ghosts included (they equal the neighbours' cells)
+  int off[3] = {0, 0, 0};
+  for (int a = 0; a < p.dims; ++a) {
+    const Slab s = cd_.axis(a);
+    off[a] = s.start() - s.ghost;
+  }
+  if (!cart_ && p.dims == 3)
+    KERNEL_CHECK(advdiff_init_ic(p.dtype, p.ic, u_, p.nx, p.ny, slab_.alloc(), sy_, sz_, off[0],
                                  p.nx, p.ny, p.nz, p.dx(), p.dy(), p.dz(), p.ic_p0, p.ic_p1,
                                  compute_));
-  else
-    KERNEL_CHECK(advdiff_init_ic(p.dtype, p.ic, u_, p.nx, slab_.alloc(), 1, sy_, sz_, kg0, p.nx,
+  else if (!cart_)
+    KERNEL_CHECK(advdiff_init_ic(p.dtype, p.ic, u_, p.nx, slab_.alloc(), 1, sy_, sz_, off[0], p.nx,
                                  p.ny, 1, p.dx(), p.dy(), 0.0, p.ic_p0, p.ic_p1, compute_));
+  else if (p.dims == 3)
+    KERNEL_CHECK(advdiff_init_ic_box(p.dtype, p.ic, u_, alloc_[2], alloc_[1], alloc_[0], sy_, sz_,
+                                     off[2], off[1], off[0], p.nx, p.ny, p.nz, p.dx(), p.dy(),
+                                     p.dz(), p.ic_p0, p.ic_p1, compute_));
+  else
+    KERNEL_CHECK(advdiff_init_ic_box(p.dtype, p.ic, u_, alloc_[1], alloc_[0], 1, sy_, sz_, off[1],
+                                     off[0], 0, p.nx, p.ny, 1, p.dx(), p.dy(), 0.0, p.ic_p0,
+                                     p.ic_p1, compute_));
   HIP_CHECK(hipMemcpyAsync(A_, u_, field_bytes_, hipMemcpyDeviceToDevice, compute_));
   if (p.integrator == 1)
     HIP_CHECK(hipMemsetAsync(B_, 0, field_bytes_, compute_));  // du
@@ -97,8 +131,10 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   HIP_CHECK(hipStreamSynchronize(compute_));
   full_ = slab_.compute_range(p.border());
   slab_.split(p.border(), slab_.ghost, interior_, blo_, bhi_);
-  const int off = slab_.start() - slab_.ghost;
-  zact_ = {std::max(0, p.border() - off), std::min(slab_.alloc(), slab_.n - p.border() - off)};
+  full_box_ = cd_.compute_box(p.border());
+  cd_.split_boxes(p.border(), cd_.ghost, interior_box_, boundary_boxes_);
+  const int zoff = slab_.start() - slab_.ghost;
+  zact_ = {std::max(0, p.border() - zoff), std::min(slab_.alloc(), slab_.n - p.border() - zoff)};
   t_ = p.t0;
 }
 
@@ -112,6 +148,8 @@ Engine::~Engine() {
   (void)hipFree(u_);
   (void)hipFree(A_);
   (void)hipFree(B_);
+  for (void* b : hbufs_)
+    if (b) (void)hipFree(b);
 }
 
 double Engine::stable_dt() const {
@@ -132,46 +170,50 @@ double Engine::stable_dt() const {
 
 void Engine::launch(const void* in, void* aux, void* out, Range r, double dt, double a,
                     double b, bool ls) {
+  launch_view(in, aux, out, p_.nx, p_.ny, r, p_.border(), dt, a, b, ls);
+}
+
+void Engine::launch_view(const void* in, void* aux, void* out, int nx, int ny, Range r, int B,
+                         double dt, double a, double b, bool ls) {
   if (r.empty()) return;
   const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
-  const int B = p_.border();
   if (p_.physics == Physics::Diffusion) {
     const double cx = p_.K / (dx * dx), cy = p_.K / (dy * dy), cz = p_.K / (dz * dz);
     if (p_.dims == 3) {
       if (ls)
-        KERNEL_CHECK(advdiff_diffusion3d_stage_ls(p_.dtype, in, aux, out, p_.nx, p_.ny, sy_, sz_,
+        KERNEL_CHECK(advdiff_diffusion3d_stage_ls(p_.dtype, in, aux, out, nx, ny, sy_, sz_,
                                                   r.lo, r.hi, B, p_.order, cx, cy, cz, dt, a, b,
                                                   compute_));
       else
-        KERNEL_CHECK(advdiff_diffusion3d_stage(p_.dtype, in, aux, out, p_.nx, p_.ny, sy_, sz_,
+        KERNEL_CHECK(advdiff_diffusion3d_stage(p_.dtype, in, aux, out, nx, ny, sy_, sz_,
                                                r.lo, r.hi, B, p_.order, cx, cy, cz, dt, a, b,
                                                compute_));
     } else {
       if (ls)
-        KERNEL_CHECK(advdiff_diffusion2d_stage_ls(p_.dtype, in, aux, out, p_.nx, sy_, r.lo, r.hi,
+        KERNEL_CHECK(advdiff_diffusion2d_stage_ls(p_.dtype, in, aux, out, nx, sy_, r.lo, r.hi,
                                                   B, p_.order, cx, cy, dt, a, b, compute_));
       else
-        KERNEL_CHECK(advdiff_diffusion2d_stage(p_.dtype, in, aux, out, p_.nx, sy_, r.lo, r.hi, B,
+        KERNEL_CHECK(advdiff_diffusion2d_stage(p_.dtype, in, aux, out, nx, sy_, r.lo, r.hi, B,
                                                p_.order, cx, cy, dt, a, b, compute_));
     }
   } else {
     const double vx = p_.C / (dx * dx), vy = p_.C / (dy * dy), vz = p_.C / (dz * dz);
     if (p_.dims == 3) {
       if (ls)
-        KERNEL_CHECK(advdiff_burgers3d_stage_ls(p_.dtype, in, aux, out, p_.nx, p_.ny, sy_, sz_,
+        KERNEL_CHECK(advdiff_burgers3d_stage_ls(p_.dtype, in, aux, out, nx, ny, sy_, sz_,
                                                 r.lo, r.hi, B, p_.weno, 1.0 / dx, 1.0 / dy,
                                                 1.0 / dz, vx, vy, vz, dt, a, b, compute_));
       else
-        KERNEL_CHECK(advdiff_burgers3d_stage(p_.dtype, in, aux, out, p_.nx, p_.ny, sy_, sz_, r.lo,
+        KERNEL_CHECK(advdiff_burgers3d_stage(p_.dtype, in, aux, out, nx, ny, sy_, sz_, r.lo,
                                              r.hi, B, p_.weno, 1.0 / dx, 1.0 / dy, 1.0 / dz, vx,
                                              vy, vz, dt, a, b, compute_));
     } else {
       if (ls)
-        KERNEL_CHECK(advdiff_burgers2d_stage_ls(p_.dtype, in, aux, out, p_.nx, sy_, r.lo, r.hi, B,
+        KERNEL_CHECK(advdiff_burgers2d_stage_ls(p_.dtype, in, aux, out, nx, sy_, r.lo, r.hi, B,
                                                 p_.weno, 1.0 / dx, 1.0 / dy, vx, vy, dt, a, b,
                                                 compute_));
       else
-        KERNEL_CHECK(advdiff_burgers2d_stage(p_.dtype, in, aux, out, p_.nx, sy_, r.lo, r.hi, B,
+        KERNEL_CHECK(advdiff_burgers2d_stage(p_.dtype, in, aux, out, nx, sy_, r.lo, r.hi, B,
                                              p_.weno, 1.0 / dx, 1.0 / dy, vx, vy, dt, a, b,
                                              compute_));
     }
@@ -199,6 +241,10 @@ void Engine::launch_fused(Range r, double dt, Range r2, bool exclusive) {
 }
 
 void Engine::step_fused(double dt) {
+  if (cart_) {
+    step_fused_cart(dt);
+    return;
+  }
   if (env_.size == 1) {
     launch_fused(full_, dt, Range{}, true);
   } else if (p_.overlap) {
@@ -226,6 +272,10 @@ void Engine::start_halo(void* field) {
 }
 
 void Engine::stage(void* in, void* aux, void* out, double a, double b, double dt, bool ls) {
+  if (cart_) {
+    stage_cart(in, aux, out, a, b, dt, ls);
+    return;
+  }
   if (env_.size == 1) {
     launch(in, aux, out, full_, dt, a, b, ls);
     return;
@@ -310,19 +360,15 @@ Stats Engine::run_until(double t_end) {
 }
 
 void Engine::error_norms(double& l1, double& l2, double& linf) {
+  if (cart_) {
+    error_norms_cart(l1, l2, linf);
+    return;
+  }
   const int G = slab_.ghost, c = slab_.count();
   void* ex = nullptr;
   HIP_CHECK(hipMalloc(&ex, plane_bytes_ * c));
-  double scale = 1.0;
+  const double scale = exact_scale();
   const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
-  if (p_.ic == 2) {  // sine: separable decay
-    const double Lx = (p_.nx - 1) * dx, Ly = (p_.ny - 1) * dy;
-    double lam = 1.0 / (Lx * Lx) + 1.0 / (Ly * Ly);
-    if (p_.dims == 3) lam += 1.0 / std::pow((p_.nz - 1) * dz, 2);
-    scale = std::exp(-p_.K * M_PI * M_PI * lam * t_);
-  } else if (p_.ic == 3) {  // heat kernel from t0 = ic_p1
-    scale = std::pow(p_.ic_p1 / t_, p_.dims / 2.0);
-  }
   const double p0 = p_.ic == 3 ? p_.K : p_.ic_p0, p1 = p_.ic == 3 ? t_ : p_.ic_p1;
   if (p_.dims == 3)
     KERNEL_CHECK(advdiff_init_ic(p_.dtype, p_.ic, ex, p_.nx, p_.ny, c, sy_, sz_, slab_.start(),
@@ -353,9 +399,22 @@ void Engine::error_norms(double& l1, double& l2, double& linf) {
   linf = tr_->allreduce_max(h[2]);
 }
 
+double Engine::exact_scale() const {
+  const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
+  if (p_.ic == 2) {  // sine: separable decay
+    const double Lx = (p_.nx - 1) * dx, Ly = (p_.ny - 1) * dy;
+    double lam = 1.0 / (Lx * Lx) + 1.0 / (Ly * Ly);
+    if (p_.dims == 3) lam += 1.0 / std::pow((p_.nz - 1) * dz, 2);
+    return std::exp(-p_.K * M_PI * M_PI * lam * t_);
+  }
+  if (p_.ic == 3) return std::pow(p_.ic_p1 / t_, p_.dims / 2.0);  // heat kernel from t0
+  return 1.0;
+}
+
 std::vector<float> Engine::gather_float32() {
   HIP_CHECK(hipStreamSynchronize(comm_));
   HIP_CHECK(hipStreamSynchronize(compute_));
+  if (cart_) return gather_cart();
   const int G = slab_.ghost, c = slab_.count();
   std::vector<char> raw(plane_bytes_ * c);
   HIP_CHECK(hipMemcpy(raw.data(), plane(u_, G), raw.size(), hipMemcpyDeviceToHost));

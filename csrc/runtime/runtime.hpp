@@ -54,10 +54,21 @@ struct ProcEnv {
 // ------------------------------------------------------------------------------------
 // Transport: how ghost planes and scalars move between ranks.
 // ------------------------------------------------------------------------------------
+// One point-to-point message of an exchange: `bytes` from `send` to rank `peer`, and
+// `bytes` from `peer` into `recv` (neighbour pairs exchange equal-sized blocks).
+struct Msg {
+  int peer = -1;
+  const void* send = nullptr;
+  void* recv = nullptr;
+  size_t bytes = 0;
+};
+
 class Transport {
  public:
   virtual ~Transport() = default;
   virtual const char* name() const = 0;
+  // Enqueue a set of messages to distinct peers on `stream` (one grouped RCCL call).
+  virtual void exchange(const std::vector<Msg>& msgs, hipStream_t stream) = 0;
   // Enqueue the exchange of G-plane slabs (bytes each) with the lower/upper neighbour
   // (-1 = none) on `stream`: send_lo -> lower's recv_hi, send_hi -> upper's recv_lo.
   virtual void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
@@ -97,12 +108,48 @@ struct Slab {
 };
 
 // ------------------------------------------------------------------------------------
+// Cartesian block decomposition (mirror of parallel/decomposition.py
+// CartesianDecomposition): array axis order (z, y, x) in 3-D, (y, x) in 2-D; ranks are
+// row-major over the process grid.  Axis 0 always carries G ghost layers, the other
+// axes only when split.  pgrid = (P, 1, 1) is exactly the slab layout.
+// ------------------------------------------------------------------------------------
+struct Box {
+  Range r[3];
+  bool empty(int dims) const {
+    for (int a = 0; a < dims; ++a)
+      if (r[a].empty()) return true;
+    return false;
+  }
+};
+
+struct Cart {
+  int dims = 3;
+  int shape[3] = {1, 1, 1};  // global extents, array order
+  int pgrid[3] = {1, 1, 1};
+  int rank = 0, ghost = 0;
+  int size() const { return pgrid[0] * pgrid[1] * (dims == 3 ? pgrid[2] : 1); }
+  void coords_of(int r, int* c) const;
+  int rank_of(const int* c) const;
+  int ghost_of_axis(int a) const { return (a == 0 || pgrid[a] > 1) ? ghost : 0; }
+  Slab axis(int a, int r = -1) const;
+  int neighbor(int a, int side) const;  // -1 at the domain edge
+  bool is_slab() const { return pgrid[1] == 1 && (dims == 2 || pgrid[2] == 1); }
+  Box compute_box(int border) const;
+  // interior (computable while the halo is in flight) + at most 2*dims boundary boxes
+  void split_boxes(int border, int width, Box& interior, std::vector<Box>& boundary) const;
+};
+
+// "PZxPYxPX" / "PYxPX" -> pgrid (array order); throws on a mismatch with dims / world
+void parse_pgrid(const std::string& spec, int dims, int world, int* pgrid);
+
+// ------------------------------------------------------------------------------------
 // Problem + engine
 // ------------------------------------------------------------------------------------
 enum class Physics { Diffusion, Burgers };
 
 struct Problem {
   Physics physics = Physics::Diffusion;
+  int pgrid[3] = {0, 0, 0};        // process grid (array order); 0 = slab (P, 1, 1)
   int dims = 3;
   int nx = 0, ny = 0, nz = 1;     // global grid
   double L = 1, W = 1, H = 1;     // domain lengths
@@ -153,10 +200,15 @@ class Engine {
   int iteration() const { return it_; }
   const Slab& slab() const { return slab_; }
   bool fused() const { return fused_; }
+  bool cartesian() const { return cart_; }
+  const Cart& cart() const { return cd_; }
 
  private:
   void launch(const void* in, void* aux, void* out, Range r, double dt, double a, double b,
               bool ls);
+  // stage kernel on a view of nx (x ny) cells with frozen border `border`, planes r
+  void launch_view(const void* in, void* aux, void* out, int nx, int ny, Range r, int border,
+                   double dt, double a, double b, bool ls);
   void stage(void* in, void* aux, void* out, double a, double b, double dt, bool ls = false);
   // exclusive: nothing runs beside the launch (single rank / full range after the halo
   // wait) -> persistent schedule of the 3-D step kernel (ADVDIFF_EXCLUSIVE)
@@ -164,6 +216,21 @@ class Engine {
   void step_fused(double dt);
   void start_halo(void* field);
   void* plane(void* base, int l) const { return (char*)base + (size_t)l * plane_bytes_; }
+  // ---- Cartesian blocks (cart_): kernels on views, phased / face halo exchange ----
+  void* at(void* base, int z, int y, int x) const {
+    return (char*)base + ((size_t)z * sz_ + (size_t)y * sy_ + (size_t)x) * elem_;
+  }
+  void launch_box(void* in, void* aux, void* out, const Box& b, double dt, double a, double b_,
+                  bool ls);
+  void launch_fused_box(const Box& b, double dt, bool exclusive);
+  void fused_view(int a, int lo, int hi, Range& view, Range& act, Range& outr) const;
+  void stage_cart(void* in, void* aux, void* out, double a, double b, double dt, bool ls);
+  void step_fused_cart(double dt);
+  void start_halo_cart(void* field);
+  void* halo_buf(size_t i, size_t bytes);
+  void error_norms_cart(double& l1, double& l2, double& linf);
+  std::vector<float> gather_cart();
+  double exact_scale() const;  // decay factor of the exact solution at t_ (sine / heat ICs)
 
   Problem p_;
   Transport* tr_;
@@ -175,6 +242,13 @@ class Engine {
   void *u_ = nullptr, *A_ = nullptr, *B_ = nullptr;
   bool fused_ = false;
   Range zact_;  // fused: local planes whose intermediate stages are updated
+  bool cart_ = false;
+  Cart cd_;
+  int alloc_[3] = {1, 1, 1};  // local extents incl. ghosts (array order)
+  Box full_box_, interior_box_;
+  std::vector<Box> boundary_boxes_;
+  std::vector<void*> hbufs_;
+  std::vector<size_t> hcap_;
   hipStream_t compute_ = nullptr, comm_ = nullptr;
   hipEvent_t ready_ = nullptr, halo_done_ = nullptr;
   bool halo_pending_ = false;

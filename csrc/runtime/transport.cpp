@@ -7,7 +7,7 @@
 //    be held by a torchrun agent's store).
 //  * RcclTransport: grouped ncclSend/ncclRecv of the ghost slabs straight from/into the
 //    device fields on the caller's stream (RCCL over xGMI, zero copy).
-//  * SocketTransport: host-staged neighbour exchange over TCP.  It lets several ranks
+//  * SocketTransport: host-staged exchange over a TCP full mesh.  It lets several ranks
 //    share ONE GPU (RCCL refuses that), so the native multi-rank path is testable on a
 //    single-GPU box; it is also the reference's own transport pattern (D2H -> send ->
 //    recv -> H2D, main.c:209-288).
@@ -182,6 +182,15 @@ class Star {
   int hub_ = -1;
 };
 
+// the two messages of a slab exchange (lower / upper neighbour; -1 = none)
+static std::vector<Msg> neighbour_msgs(const void* send_lo, void* recv_lo, const void* send_hi,
+                                       void* recv_hi, size_t bytes, int lower, int upper) {
+  std::vector<Msg> m;
+  if (lower >= 0) m.push_back(Msg{lower, send_lo, recv_lo, bytes});
+  if (upper >= 0) m.push_back(Msg{upper, send_hi, recv_hi, bytes});
+  return m;
+}
+
 // ---------------------------------------------------------------- RCCL
 #define NCCL_CHECK(expr)                                                              \
   do {                                                                                \
@@ -205,18 +214,18 @@ class RcclTransport final : public Transport {
     if (comm_) ncclCommDestroy(comm_);
   }
   const char* name() const override { return "rccl"; }
-  void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
-            size_t bytes, int lower, int upper, hipStream_t s) override {
+  void exchange(const std::vector<Msg>& msgs, hipStream_t s) override {
+    if (msgs.empty()) return;
     NCCL_CHECK(ncclGroupStart());
-    if (lower >= 0) {
-      NCCL_CHECK(ncclSend(send_lo, bytes, ncclChar, lower, comm_, s));
-      NCCL_CHECK(ncclRecv(recv_lo, bytes, ncclChar, lower, comm_, s));
-    }
-    if (upper >= 0) {
-      NCCL_CHECK(ncclSend(send_hi, bytes, ncclChar, upper, comm_, s));
-      NCCL_CHECK(ncclRecv(recv_hi, bytes, ncclChar, upper, comm_, s));
+    for (const Msg& m : msgs) {
+      NCCL_CHECK(ncclSend(m.send, m.bytes, ncclChar, m.peer, comm_, s));
+      NCCL_CHECK(ncclRecv(m.recv, m.bytes, ncclChar, m.peer, comm_, s));
     }
     NCCL_CHECK(ncclGroupEnd());
+  }
+  void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
+            size_t bytes, int lower, int upper, hipStream_t s) override {
+    exchange(neighbour_msgs(send_lo, recv_lo, send_hi, recv_hi, bytes, lower, upper), s);
   }
   double allreduce_max(double v) override { return star_.reduce(v, true); }
   double allreduce_sum(double v) override { return star_.reduce(v, false); }
@@ -232,56 +241,72 @@ class RcclTransport final : public Transport {
 // ---------------------------------------------------------------- host-staged TCP
 class SocketTransport final : public Transport {
  public:
+  // full mesh: rank j > i connects to rank i's listener (port MASTER_PORT+1+i), so any
+  // pair of ranks (slab neighbours, Cartesian faces) has its own socket
   explicit SocketTransport(const ProcEnv& e) : star_(e), env_(e) {
     if (e.size == 1) return;
+    fds_.assign(e.size, -1);
     const int base = e.master_port + 1;
     int lfd = -1;
     if (e.rank < e.size - 1) lfd = listen_on(base + e.rank);
     star_.reduce(0.0, false);  // every listener is up
-    if (e.rank > 0) {
-      lo_ = connect_to("127.0.0.1", base + e.rank - 1);
-      send_all(lo_, &e.rank, sizeof(int));
+    for (int q = 0; q < e.rank; ++q) {
+      fds_[q] = connect_to("127.0.0.1", base + q);
+      send_all(fds_[q], &e.rank, sizeof(int));
     }
-    if (lfd >= 0) {
-      hi_ = ::accept(lfd, nullptr, nullptr);
-      int r;
-      recv_all(hi_, &r, sizeof(r));
-      ::close(lfd);
+    for (int n = e.rank + 1; n < e.size; ++n) {
+      int fd = ::accept(lfd, nullptr, nullptr);
+      if (fd < 0) die("accept");
+      int r = -1;
+      recv_all(fd, &r, sizeof(r));
+      if (r <= e.rank || r >= e.size) die("bad peer rank");
+      fds_[r] = fd;
     }
+    if (lfd >= 0) ::close(lfd);
   }
   ~SocketTransport() override {
-    if (lo_ >= 0) ::close(lo_);
-    if (hi_ >= 0) ::close(hi_);
+    for (int fd : fds_)
+      if (fd >= 0) ::close(fd);
     if (h_send_) (void)hipHostFree(h_send_);
     if (h_recv_) (void)hipHostFree(h_recv_);
   }
   const char* name() const override { return "socket"; }
-  void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
-            size_t bytes, int lower, int upper, hipStream_t s) override {
-    if (bytes > cap_) {
+  void exchange(const std::vector<Msg>& msgs, hipStream_t s) override {
+    if (msgs.empty()) return;
+    size_t total = 0;
+    for (const Msg& m : msgs) total += m.bytes;
+    if (total > cap_) {
       if (h_send_) (void)hipHostFree(h_send_);
       if (h_recv_) (void)hipHostFree(h_recv_);
-      HIP_CHECK(hipHostMalloc(&h_send_, 2 * bytes));
-      HIP_CHECK(hipHostMalloc(&h_recv_, 2 * bytes));
-      cap_ = bytes;
+      HIP_CHECK(hipHostMalloc(&h_send_, total));
+      HIP_CHECK(hipHostMalloc(&h_recv_, total));
+      cap_ = total;
     }
-    char* sl = (char*)h_send_;
-    char* sh = sl + bytes;
-    char* rl = (char*)h_recv_;
-    char* rh = rl + bytes;
-    if (lower >= 0) HIP_CHECK(hipMemcpyAsync(sl, send_lo, bytes, hipMemcpyDeviceToHost, s));
-    if (upper >= 0) HIP_CHECK(hipMemcpyAsync(sh, send_hi, bytes, hipMemcpyDeviceToHost, s));
+    std::vector<size_t> off(msgs.size());
+    size_t o = 0;
+    for (size_t q = 0; q < msgs.size(); ++q) {
+      off[q] = o;
+      HIP_CHECK(hipMemcpyAsync((char*)h_send_ + o, msgs[q].send, msgs[q].bytes,
+                               hipMemcpyDeviceToHost, s));
+      o += msgs[q].bytes;
+    }
     HIP_CHECK(hipStreamSynchronize(s));
-    std::thread tx([&] {
-      if (lower >= 0) send_all(lo_, sl, bytes);
-      if (upper >= 0) send_all(hi_, sh, bytes);
-    });
-    if (lower >= 0) recv_all(lo_, rl, bytes);
-    if (upper >= 0) recv_all(hi_, rh, bytes);
-    tx.join();
-    if (lower >= 0) HIP_CHECK(hipMemcpyAsync(recv_lo, rl, bytes, hipMemcpyHostToDevice, s));
-    if (upper >= 0) HIP_CHECK(hipMemcpyAsync(recv_hi, rh, bytes, hipMemcpyHostToDevice, s));
+    // one sender thread per message: a send that blocks on a full socket never stalls
+    // the receives below, whatever order the peers read in
+    std::vector<std::thread> tx;
+    for (size_t q = 0; q < msgs.size(); ++q)
+      tx.emplace_back([&, q] { send_all(fds_[msgs[q].peer], (char*)h_send_ + off[q], msgs[q].bytes); });
+    for (size_t q = 0; q < msgs.size(); ++q)
+      recv_all(fds_[msgs[q].peer], (char*)h_recv_ + off[q], msgs[q].bytes);
+    for (auto& t : tx) t.join();
+    for (size_t q = 0; q < msgs.size(); ++q)
+      HIP_CHECK(hipMemcpyAsync(msgs[q].recv, (char*)h_recv_ + off[q], msgs[q].bytes,
+                               hipMemcpyHostToDevice, s));
     HIP_CHECK(hipStreamSynchronize(s));  // staging buffers are reused next call
+  }
+  void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
+            size_t bytes, int lower, int upper, hipStream_t s) override {
+    exchange(neighbour_msgs(send_lo, recv_lo, send_hi, recv_hi, bytes, lower, upper), s);
   }
   double allreduce_max(double v) override { return star_.reduce(v, true); }
   double allreduce_sum(double v) override { return star_.reduce(v, false); }
@@ -291,7 +316,7 @@ class SocketTransport final : public Transport {
  private:
   Star star_;
   ProcEnv env_;
-  int lo_ = -1, hi_ = -1;
+  std::vector<int> fds_;
   void *h_send_ = nullptr, *h_recv_ = nullptr;
   size_t cap_ = 0;
 };
@@ -300,6 +325,7 @@ class SocketTransport final : public Transport {
 class LocalTransport final : public Transport {
  public:
   const char* name() const override { return "local"; }
+  void exchange(const std::vector<Msg>&, hipStream_t) override {}
   void halo(const void*, void*, const void*, void*, size_t, int, int, hipStream_t) override {}
   double allreduce_max(double v) override { return v; }
   double allreduce_sum(double v) override { return v; }

@@ -4,6 +4,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cassert>
 #include <cstdio>
 #include <cstdlib>
@@ -106,8 +107,83 @@ static void test_summary_block() {
          std::string::npos);
 }
 
+// Cartesian blocks: over all ranks, interior + boundary boxes cover every non-frozen
+// cell exactly once; the interior box never reaches a split face's ghost layers; a
+// rank's neighbours are symmetric; parse_pgrid validates the product
+static void test_cart_partition() {
+  const int shapes[][3] = {{30, 26, 41}, {17, 40, 33}};
+  const int grids[][3] = {{1, 2, 2}, {2, 1, 2}, {2, 2, 2}, {3, 2, 1}, {1, 1, 4}};
+  for (const auto& sh : shapes)
+    for (const auto& pg : grids)
+      for (int ghost : {2, 6}) {
+        Cart c;
+        c.dims = 3;
+        for (int a = 0; a < 3; ++a) {
+          c.shape[a] = sh[a];
+          c.pgrid[a] = pg[a];
+        }
+        c.ghost = ghost;
+        bool fits = true;
+        for (int a = 0; a < 3; ++a)
+          if (c.shape[a] < c.pgrid[a] * std::max(c.ghost_of_axis(a), 1)) fits = false;
+        if (!fits) continue;
+        const int border = 2;
+        std::vector<int> hits((size_t)sh[0] * sh[1] * sh[2], 0);
+        for (int r = 0; r < c.size(); ++r) {
+          c.rank = r;
+          Slab ax[3];
+          for (int a = 0; a < 3; ++a) ax[a] = c.axis(a);
+          Box in;
+          std::vector<Box> bnd;
+          c.split_boxes(border, ghost, in, bnd);
+          std::vector<Box> all(bnd);
+          all.push_back(in);
+          for (const Box& b : all) {
+            if (b.empty(3)) continue;
+            for (int k = b.r[0].lo; k < b.r[0].hi; ++k)
+              for (int j = b.r[1].lo; j < b.r[1].hi; ++j)
+                for (int i = b.r[2].lo; i < b.r[2].hi; ++i) {
+                  const int g[3] = {ax[0].start() - ax[0].ghost + k, ax[1].start() - ax[1].ghost + j,
+                                    ax[2].start() - ax[2].ghost + i};
+                  ++hits[((size_t)g[0] * sh[1] + g[1]) * sh[2] + g[2]];
+                }
+          }
+          for (int a = 0; a < 3; ++a) {
+            if (in.empty(3) || c.pgrid[a] == 1) continue;
+            if (c.neighbor(a, -1) >= 0) EXPECT(in.r[a].lo >= ax[a].ghost + ghost);
+            if (c.neighbor(a, 1) >= 0) EXPECT(in.r[a].hi <= ax[a].ghost + ax[a].count() - ghost);
+            for (int side : {-1, 1}) {
+              const int nb = c.neighbor(a, side);
+              if (nb < 0) continue;
+              Cart o = c;
+              o.rank = nb;
+              EXPECT(o.neighbor(a, -side) == r);
+            }
+          }
+        }
+        for (int z = 0; z < sh[0]; ++z)
+          for (int y = 0; y < sh[1]; ++y)
+            for (int x = 0; x < sh[2]; ++x) {
+              const bool act = z >= border && z < sh[0] - border && y >= border &&
+                               y < sh[1] - border && x >= border && x < sh[2] - border;
+              EXPECT(hits[((size_t)z * sh[1] + y) * sh[2] + x] == (act ? 1 : 0));
+            }
+      }
+  int pg[3];
+  parse_pgrid("2x2x1", 3, 4, pg);
+  EXPECT(pg[0] == 2 && pg[1] == 2 && pg[2] == 1);
+  bool threw = false;
+  try {
+    parse_pgrid("2x2", 3, 4, pg);
+  } catch (const std::exception&) {
+    threw = true;
+  }
+  EXPECT(threw);
+}
+
 int main() {
   test_slab_partition();
+  test_cart_partition();
   test_star_collectives();
   test_summary_block();
   if (failures) {

@@ -124,3 +124,39 @@ def test_native_fused_equals_per_stage_and_multirank(tmp_path):
     _run("diffusion3d", args, c, world=3, extra=["--ic", "sine", "--transport", "socket"])
     fa, fb, fc = (np.fromfile(p, dtype=np.float32) for p in (a, b, c))
     assert np.array_equal(fa, fb) and np.array_equal(fa, fc)
+
+
+@pytest.mark.parametrize("app,args,shape,world,decomp,extra", [
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 66, 40, 45, 12], (45, 40, 66), 4, "1x2x2",
+     ["--ic", "sine"]),                                   # fused step, x and y split
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 66, 40, 45, 12], (45, 40, 66), 4, "2x2x1",
+     ["--ic", "sine", "--no-fused"]),                     # per-stage kernels on views
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 50, 44, 46, 9], (46, 44, 50), 8, "2x2x2",
+     ["--ic", "sine", "--no-overlap"]),
+    ("burgers3d", [0.03, 0.3, 2.0, 2.0, 2.0, 40, 36, 41], (41, 36, 40), 4, "2x1x2", []),
+    ("diffusion2d", [1.0, 1.0, 1.0, 130, 90, 30], (90, 130), 4, "2x2", ["--ic", "disc"]),
+    ("burgers2d", [0.1, 0.4, 2.0, 2.0, 140, 100], (100, 140), 2, "1x2",
+     ["--weno", "js", "--visc", "0"]),
+])
+def test_native_cartesian_socket_bitwise(tmp_path, app, args, shape, world, decomp, extra):
+    """Native Cartesian blocks (csrc/runtime/cart.cpp: kernels on views, face / phased
+    corner exchange over the socket full mesh, ranks sharing the GPU) == the 1-rank run."""
+    one, many = tmp_path / "one.bin", tmp_path / "many.bin"
+    _run(app, args, one, extra=extra)
+    txt = _run(app, args, many, world=world,
+               extra=extra + ["--transport", "socket", "--decomp", decomp])
+    assert f"decomp={decomp}" in txt, txt
+    a = np.fromfile(one, dtype=np.float32).reshape(shape)
+    b = np.fromfile(many, dtype=np.float32).reshape(shape)
+    assert np.array_equal(a, b), np.abs(a - b).max()
+
+
+def test_native_cartesian_error_norms(tmp_path):
+    """--error-norms on Cartesian blocks == the slab run's norms."""
+    base = [1.0, 10.0, 10.0, 10.0, 41, 41, 41, 30]
+    t1 = _run("diffusion3d", base, tmp_path / "a.bin", extra=["--error-norms"])
+    t4 = _run("diffusion3d", base, tmp_path / "b.bin", world=4,
+              extra=["--error-norms", "--transport", "socket", "--decomp", "1x2x2"])
+    pick = lambda t, k: float([l for l in t.splitlines() if l.startswith(k)][0].split(":")[1])  # noqa
+    for k in ("L1 norm", "L2 norm", "Linf norm"):
+        assert abs(pick(t1, k) - pick(t4, k)) <= 1e-12 * max(abs(pick(t1, k)), 1e-30), k

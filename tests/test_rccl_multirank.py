@@ -152,12 +152,20 @@ def _native(app, args, out, world, transport):
     ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 66, 40, 64, 12], (64, 40, 66), ["--ic", "sine"]),
     ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 66, 40, 64, 12], (64, 40, 66), ["--ic", "sine", "--no-fused"]),
     ("burgers3d", [0.03, 0.3, 2.0, 2.0, 2.0, 40, 36, 64], (64, 36, 40), []),
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 66, 64, 64, 12], (64, 64, 66), ["--ic", "sine", "--decomp", "cart"]),
+    ("burgers3d", [0.03, 0.3, 2.0, 2.0, 2.0, 40, 64, 64], (64, 64, 40), ["--decomp", "cart"]),
 ])
 def test_native_rccl_multirank_bitwise(tmp_path, world, app, args, shape, extra):
     if _ngpu() < world:
         pytest.skip(f"needs {world} GPUs")
     one, many = tmp_path / "one.bin", tmp_path / "many.bin"
-    _native(app, args + extra, one, 1, "rccl")
+    if "cart" in extra:  # Cartesian blocks of the native engine (y and z split)
+        i = extra.index("cart")
+        extra = extra[:i] + [{2: "1x2x1", 4: "2x2x1", 8: "2x4x1"}[world]] + extra[i + 1:]
+        _native(app, args + [e for e in extra if e not in ("--decomp",) and "x" not in e],
+                one, 1, "rccl")
+    else:
+        _native(app, args + extra, one, 1, "rccl")
     txt = _native(app, args + extra, many, world, "rccl")
     assert "transport=rccl" in txt
     a = np.fromfile(one, dtype=np.float32).reshape(shape)
