@@ -3,7 +3,8 @@
 Two entry points:
 
 * CLI: ``python -m multigpu_advectiondiffusion_amd.launch -np 8 diffusion3d 1 2 2 2 512 512 512 100``
-  starts P child processes of ``python -m multigpu_advectiondiffusion_amd`` with the
+  starts P child processes of ``python -m multigpu_advectiondiffusion_amd`` (``--native``:
+  of the C++ executable ``bin/<app>``) with the
   torchrun environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1,
   MASTER_PORT) — one process per GPU; ``--cpu`` runs P gloo ranks on the CPU (the
   oversubscription / no-cluster test mode of SURVEY.md §4, done properly).
@@ -41,15 +42,22 @@ def _child_env(rank: int, world: int, port: int, cpu: bool) -> dict:
 
 
 def launch(np_: int, argv: list[str], cpu: bool = False, timeout: float | None = None,
-           poll_s: float = 0.2) -> int:
+           poll_s: float = 0.2, native: bool = False) -> int:
     """Run P ranks; fail fast: the first rank that exits non-zero (or the wall-clock
     `timeout`, rc 124) terminates the others, so a crashed rank never leaves its peers
     blocked in a halo exchange until the collective timeout.  Returns the first
     non-zero exit code (0 if all succeed)."""
     import time
     port = free_port()
-    cmd = [sys.executable, "-m", "multigpu_advectiondiffusion_amd"] + argv
-    if cpu and "--device" not in argv:
+    if native:  # the C++ executables: bin/<app> <args...> (RCCL or --transport socket)
+        from pathlib import Path
+        exe = Path(__file__).resolve().parent.parent / "bin" / argv[0]
+        if not exe.exists():
+            raise FileNotFoundError(f"{exe} not built (make -C csrc apps)")
+        cmd = [str(exe)] + argv[1:]
+    else:
+        cmd = [sys.executable, "-m", "multigpu_advectiondiffusion_amd"] + argv
+    if cpu and not native and "--device" not in argv:
         cmd += ["--device", "cpu"]
     procs = [subprocess.Popen(cmd, env=_child_env(r, np_, port, cpu)) for r in range(np_)]
     deadline = None if timeout is None else time.monotonic() + timeout
@@ -137,9 +145,11 @@ def main(argv=None) -> int:
     ap.add_argument("-np", "--nproc", type=int, required=True)
     ap.add_argument("--cpu", action="store_true", help="gloo ranks on the CPU")
     ap.add_argument("--timeout", type=float, default=None)
+    ap.add_argument("--native", action="store_true",
+                    help="run the native executable bin/<app> instead of the Python front end")
     ap.add_argument("rest", nargs=argparse.REMAINDER)
     ns = ap.parse_args(argv)
-    return launch(ns.nproc, ns.rest, cpu=ns.cpu, timeout=ns.timeout)
+    return launch(ns.nproc, ns.rest, cpu=ns.cpu, timeout=ns.timeout, native=ns.native)
 
 
 if __name__ == "__main__":
