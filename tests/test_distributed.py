@@ -228,3 +228,36 @@ def test_candidate_proc_grids_xgmi_model():
     assert candidate_proc_grids(1, g8, 6) == [(1, 1, 1)]
     # faces only (per-stage WENO exchange): messages to different neighbours overlap
     assert halo_link_bytes((512,) * 3, (2, 2, 2), 3, 8, False) == 3 * 256 * 256 * 8
+
+
+def _bench_tune(comm):
+    import bench
+    from multigpu_advectiondiffusion_amd import Diffusion, Grid, Solver
+    from multigpu_advectiondiffusion_amd.parallel.decomposition import candidate_proc_grids
+    grid = Grid((96, 96, 48), (1.0, 1.0, 1.0))
+    model = Diffusion(K=1.0, order=4)
+    model.bind(grid)
+    dt = model.stable_dt()
+
+    def make(p):
+        return Solver(model, grid, comm, dtype=torch.float64, ic="sine", decomp=p)
+    cands = candidate_proc_grids(comm.size, (48, 96, 96), 6, 8, corners=True, keep=3)
+    best, trials = bench.tune_decomp(make, cands, dt, comm.device)
+    s = make(best)
+    s.run(iters=3, dt=dt)
+    diag = bench.halo_diag(s)
+    return best, trials, diag, cands
+
+
+def test_bench_decomposition_tuning_gloo():
+    """bench.py's N>1 machinery over 4 gloo ranks: every candidate grid runs, all ranks
+    pick the same fastest grid, candidates agree with the slab, halo diagnostics report."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    out = spawn_local(4, _bench_tune, device="cpu", backend="gloo")
+    assert all(o[0] == out[0][0] for o in out)
+    best, trials, diag, cands = out[0]
+    assert tuple(best) in [tuple(c) for c in cands] and len(cands) == 3
+    assert len(trials) == len(cands) and all(isinstance(v, float) for v in trials.values())
+    assert diag["halo_exchange_ms"] > 0 and diag["halo_link_MB"] > 0
