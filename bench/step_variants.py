@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--cfgs", default="0,21,23,24,25,27")
     ap.add_argument("--orders", default="4,2")
+    ap.add_argument("--rounds", type=int, default=1,
+                    help="interleave the configs over this many rounds (median): clock drift "
+                         "between configs cancels")
     args = ap.parse_args()
     lib = _lib.require()
     n = args.n
@@ -44,27 +47,35 @@ def main():
     v = torch.empty_like(u)
     ref = {}
     out = {}
+    import statistics
     for order in [int(o) for o in args.orders.split(",")]:
         R = order // 2
         kw = dict(nx=n, ny=n, k0=R, k1=n - R, zlo=R, zhi=n - R, border=R, order=order,
                   cx=1.0, cy=1.0, cz=1.0, dt=0.01)
-        for cfg in [int(c) for c in args.cfgs.split(",")]:
-            lib.advdiff_set_step_cfg(cfg)
-            for excl in (True, False):
-                lib.advdiff_set_step_persist(1 if excl else 0)
-                t = timeit(lambda: stencil.diffusion3d_step(u, v, exclusive=excl, **kw),
-                           args.reps)
-                torch.cuda.synchronize()
-                key = (order, excl)
-                if key not in ref:
-                    ref[key] = v.clone()
-                    same = True
-                else:
-                    same = bool(torch.equal(ref[key], v))
-                tag = f"fd{order}_cfg{cfg}_{'persist' if excl else 'grid'}"
-                out[tag] = {"us": round(t * 1e6, 1), "mlups": round(n ** 3 / t / 1e6, 1),
-                            "bitwise_vs_first": same}
-                print(tag, out[tag], flush=True)
+        cfgs = [int(c) for c in args.cfgs.split(",")]
+        times = {}
+        for _ in range(args.rounds):
+            for cfg in cfgs:
+                lib.advdiff_set_step_cfg(cfg)
+                for excl in (True, False):
+                    lib.advdiff_set_step_persist(1 if excl else 0)
+                    t = timeit(lambda: stencil.diffusion3d_step(u, v, exclusive=excl, **kw),
+                               args.reps)
+                    torch.cuda.synchronize()
+                    key = (order, excl)
+                    tag = f"fd{order}_cfg{cfg}_{'persist' if excl else 'grid'}"
+                    if key not in ref:
+                        ref[key] = v.clone()
+                        same = True
+                    else:
+                        same = bool(torch.equal(ref[key], v))
+                    times.setdefault(tag, []).append(t)
+                    out[tag] = {"us": round(statistics.median(times[tag]) * 1e6, 1),
+                                "mlups": round(n ** 3 / statistics.median(times[tag]) / 1e6, 1),
+                                "bitwise_vs_first": same and out.get(tag, {}).get(
+                                    "bitwise_vs_first", True)}
+        for tag in [t for t in out if t.startswith(f"fd{order}_")]:
+            print(tag, out[tag], flush=True)
     lib.advdiff_set_step_cfg(0)
     lib.advdiff_set_step_persist(0)
     print(json.dumps(out))

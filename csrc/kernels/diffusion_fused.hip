@@ -729,9 +729,22 @@ constexpr int step_lds_elems() {
     return 2 * CringGeom<ORDER, NW, RPW>::LDS_U + 4 * CringGeom<ORDER, NW, RPW>::LDS_AB;
 }
 
+// waves per SIMD to budget registers for, from the LDS footprint of the variant
+template <typename T, int ORDER, int NW, int RPW, int VAR>
+constexpr int step_min_waves() {
+  if constexpr (StepVar<VAR>::v3) {
+    constexpr int lds = (int)sizeof(T) * V3Geom<T, ORDER, NW, RPW>::TOTAL;
+    constexpr int wgs = 163840 / lds;
+    constexpr int w = wgs * NW / 4;
+    return sizeof(T) == 8 ? (w > 8 ? 8 : (w < 1 ? 1 : w)) : 1;
+  } else {
+    return cring_min_waves<T, ORDER, NW, RPW>();
+  }
+}
+
 template <typename T, int ORDER, int NW, int RPW, int VAR, bool PERSIST>
 __global__ __launch_bounds__(64 * NW) __attribute__((
-    amdgpu_waves_per_eu(cring_min_waves<T, ORDER, NW, RPW>()))) void diffusion3d_step_cring_kernel(
+    amdgpu_waves_per_eu(step_min_waves<T, ORDER, NW, RPW, VAR>()))) void diffusion3d_step_cring_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
     int nz_alloc, int k0, int k1, int k0b, int k1b, StepSched sc, int zlo, int zhi,
     Box2 bx, FdCoef<T> q1, FdCoef<T> q2, FdCoef<T> q3) {
@@ -865,9 +878,17 @@ static hipError_t dispatch_step(int cfg, const SArgs& a) {
     case 24: STEPV(16, 2, 20);   // v3, LDS x, prefetch 1, unmerged LDS reads
     case 25: STEPV(16, 2, 21);   // v3, DPP x 2/3, prefetch 1, unmerged LDS reads
     case 27: STEPV(16, 2, 23);   // v3, DPP x 2/3, prefetch 2, unmerged LDS reads
+    case 30: STEPV(12, 3, 23);   // taller tiles: 36 stage-1 rows (TY 28 for FD4)
+    case 31: STEPV(8, 5, 23);    // 40 rows (TY 32), 8 waves x 5 rows
+    case 32: STEPV(8, 4, 23);    // 32 rows, 8 waves x 4 rows
+    case 33: STEPV(10, 4, 23);   // 40 rows, 10 waves x 4 rows
+    case 29: STEPV(16, 2, 23);   // round-2 default before the taller tiles
     case 1: STEPV(16, 2, 2);     // round-1 default (cring, DPP in all stages)
-    default:  // v3, 16 waves, DPP x in stages 2/3, prefetch 2, unmerged LDS reads
-      STEPV(16, 2, 23);   // profiles/step_variants_r2.log: 760 us FD4 / 559 us FD2 at 512^3
+    default:  // v3, 12 waves x 3 rows (36 stage-1 rows), DPP x in stages 2/3, prefetch 2,
+              // unmerged LDS reads: vs 16 x 2 rows, interleaved medians at 512^3
+              // FD4 793 -> 761 us, FD2 598 -> 566 us (profiles/step_variants_r2_tiles.log);
+              // 48 rows overflow the 16-bit DS offsets, 10 x 4 spills at 168 VGPRs
+      STEPV(12, 3, 23);
   }
 #undef STEPV
 }

@@ -147,7 +147,7 @@ def test_fused_step_box_bounds_match_reference():
         assert (got.cpu() - out).abs().max().item() < 1e-12, box
 
 
-STEP_VARIANTS = [0, 1, 16, 20, 21, 22, 23, 24, 25, 27]  # diffusion_fused.hip dispatch_step cfgs
+STEP_VARIANTS = [0, 1, 16, 20, 21, 22, 23, 24, 25, 27, 29, 30, 31, 32, 33]  # diffusion_fused.hip dispatch_step cfgs
 
 
 @pytest.mark.parametrize("cfg", STEP_VARIANTS)
