@@ -359,44 +359,6 @@ struct V3Geom {
   static constexpr int TOTAL = OFF_B + 2 * ASET;
 };
 
-template <typename T>
-__device__ __forceinline__ T lds_ld(const char* base, int byte_off) {
-  return *(const T*)(base + byte_off);
-}
-template <typename T>
-__device__ __forceinline__ void lds_st(char* base, int byte_off, T v) {
-  *(T*)(base + byte_off) = v;
-}
-// Plane-relative global access through a raw buffer resource: the plane base lives in
-// the (scalar) descriptor and the per-lane part is a 32-bit byte offset, so a load or
-// store costs no VALU address arithmetic (gfx9 descriptor word 3 = 0x00020000; the range
-// check is disabled by num_records = 2^32 - 1; offsets stay inside one plane < 2^31 B).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
-}
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-template <typename T>
-__device__ __forceinline__ T gld(__amdgpu_buffer_rsrc_t r, uint32_t boff) {
-  if constexpr (sizeof(T) == 8)
-    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, (int)boff, 0, 0));
-  else
-    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, (int)boff, 0, 0));
-}
-template <typename T>
-__device__ __forceinline__ void gst(__amdgpu_buffer_rsrc_t r, uint32_t boff, T v) {
-  if constexpr (sizeof(T) == 8)
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)boff, 0, 0);
-  else
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)boff, 0, 0);
-}
-// keep a value computed on every lane (no exec-masked skip of the computation): the
-// frozen-cell choice below it must be a v_cndmask, not a branch around the stencil
-template <typename T>
-__device__ __forceinline__ T pin(T v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
-
 template <typename T, int ORDER, int NW, int RPW, int XS, int PF, bool SEP>
 __device__ __forceinline__ void v3_march(
     T* lds, int tx, int ty, int kc0, int kc1, const T* __restrict__ uin,

@@ -14,7 +14,7 @@ SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAI
       "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum")
 [ -n "$PMC_SETS_OVERRIDE" ] && eval "SETS=($PMC_SETS_OVERRIDE)"
 for job in ${PMC_JOBS:-burgers:ADVDIFF_B3_VER=2}; do
-  tgt=${job%%:*}; envs=${job#*:}
+  tgt=${job%%:*}; envs=${job#*:}; envs=${envs//,/ }
   tag="${tgt}_$(echo "$envs" | tr -c 'A-Za-z0-9\n' '_' | sed 's/ADVDIFF_//g')"
   i=0
   for set in "${SETS[@]}"; do

@@ -187,11 +187,13 @@ def test_debug_print_kernel(capfd):
     assert "[k=1]" in out and "13.0000" in out and "18.0000" in out
 
 
-@pytest.mark.parametrize("ver,ty", [(1, 8), (1, 16), (2, 8), (2, 16), (3, 8), (3, 16), (4, 8), (5, 4)])
+@pytest.mark.parametrize("ver,ty", [(1, 8), (1, 16), (2, 8), (2, 16), (3, 8), (3, 16), (4, 8), (5, 4),
+                                    (6, 8), (6, 16), (7, 8), (8, 8)])
 @pytest.mark.parametrize("weno_z", [False, True])
 def test_burgers3d_stage_variants(ver, ty, weno_z):
     """Every selectable 3-D WENO5 kernel variant (v1 generic, v2 two barriers, v3 double
-    buffer, v4/v5 6 waves/SIMD) against the fp64 reference, on a shape that leaves partial
+    buffer, v4/v5 6 waves/SIMD, v6/v7 renamed rings with / without the rotating bottom
+    faces) against the fp64 reference, on a shape that leaves partial
     tiles in x and y and a remainder z chunk."""
     from multigpu_advectiondiffusion_amd.ops import _lib
     lib = _lib.require()
