@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--cfgs", default="0,21,23,24,25,27")
     ap.add_argument("--orders", default="4,2")
+    ap.add_argument("--edges", default="1", help="v3 edge tiles on/off values to A/B (1,0)")
+    ap.add_argument("--schedules", default="persist,grid")
     ap.add_argument("--rounds", type=int, default=1,
                     help="interleave the configs over this many rounds (median): clock drift "
                          "between configs cancels")
@@ -55,15 +57,17 @@ def main():
         cfgs = [int(c) for c in args.cfgs.split(",")]
         times = {}
         for _ in range(args.rounds):
-            for cfg in cfgs:
+            for cfg, edge in [(c, e) for c in cfgs for e in map(int, args.edges.split(","))]:
                 lib.advdiff_set_step_cfg(cfg)
-                for excl in (True, False):
+                lib.advdiff_set_step_edge(edge)
+                for excl in [s == "persist" for s in args.schedules.split(",")]:
                     lib.advdiff_set_step_persist(1 if excl else 0)
                     t = timeit(lambda: stencil.diffusion3d_step(u, v, exclusive=excl, **kw),
                                args.reps)
                     torch.cuda.synchronize()
                     key = (order, excl)
-                    tag = f"fd{order}_cfg{cfg}_{'persist' if excl else 'grid'}"
+                    tag = (f"fd{order}_cfg{cfg}{'' if edge else '_noedge'}_"
+                           f"{'persist' if excl else 'grid'}")
                     if key not in ref:
                         ref[key] = v.clone()
                         same = True
@@ -78,6 +82,7 @@ def main():
             print(tag, out[tag], flush=True)
     lib.advdiff_set_step_cfg(0)
     lib.advdiff_set_step_persist(0)
+    lib.advdiff_set_step_edge(1)
     print(json.dumps(out))
 
 

@@ -195,6 +195,8 @@ int advdiff_set_step_cfg(int cfg);
 // Allow (1) the persistent schedule for ADVDIFF_EXCLUSIVE 3-D fused launches (default 0:
 // grid of z chunks); returns the previous value.  Initialised from ADVDIFF_STEP_PERSIST.
 int advdiff_set_step_persist(int on);
+// v3 fused step: boundary-anchored edge tiles (1, default) or the plain partition (0)
+int advdiff_set_step_edge(int on);
 // 3-D WENO5 stage kernel version (1 = v1, 2 = v2 two barriers, 3 = v2 double-buffered);
 // returns the previous value.  Results agree to rounding (tests).
 int advdiff_set_b3_ver(int v);

@@ -53,7 +53,69 @@ struct StepSched {
   int gx, gy;       // tiles along x / y
   int gza, zchunk;  // grid mode
   int per, rem;     // persistent mode: L = per G + rem
+  int edge;         // v3: boundary-anchored edge tiles (axis_tile)
 };
+
+// Tile placement along one axis of the v3 march (span W = 64 lanes in x, S1R rows in y;
+// interior tiles output W - 4R cells, lanes/rows [2R, W-2R)).  Tiles cover the output
+// range [P0, P1) = [o0,o1) ∩ [a0,a1) of the launch.  Edge tiles (edge = 1): when P0 is
+// the active range's own start a0 (a Dirichlet boundary — the R cells below it are
+// frozen, so their stage-1/2 values are exact copies of u), the first tile is anchored
+// with its lanes [0,R) on those frozen cells and outputs [R, W-2R): R more cells than an
+// interior tile; likewise the last tile at a1.  At 512^3 FD4 this takes 9 x 18 instead
+// of 10 x 19 tiles (-15 % stage-1/2/3 work).  The last tile is anchored at P1 and writes
+// only from wlo, where the previous tile stopped, so every cell has exactly one writer.
+// edge = 0: the same partition without the R-cell extensions (the pre-edge layout).
+struct AxisTile {
+  int org;      // coordinate of lane / row 0
+  int lo, hi;   // stage-3 (output) lanes / rows [lo, hi)
+  int wlo;      // first coordinate this tile writes
+};
+
+struct AxisSpan {
+  int p0, p1, lol, hir;
+};
+__host__ __device__ inline AxisSpan axis_span(int W, int R, int a0, int a1, int o0, int o1,
+                                              int nmax, int edge) {
+  AxisSpan s;
+  s.p0 = o0 > a0 ? o0 : a0;
+  s.p1 = o1 < a1 ? o1 : a1;
+  const bool el = edge && s.p0 == a0 && a0 - R >= 0;
+  const bool er = edge && s.p1 == a1 && a1 + R <= nmax;
+  s.lol = el ? R : 2 * R;
+  s.hir = er ? W - R : W - 2 * R;
+  return s;
+}
+
+__host__ __device__ inline int axis_tile_count(int W, int R, int a0, int a1, int o0, int o1,
+                                               int nmax, int edge) {
+  const AxisSpan s = axis_span(W, R, a0, a1, o0, o1, nmax, edge);
+  const int L = s.p1 - s.p0, TO = W - 4 * R;
+  if (L <= s.hir - s.lol) return 1;
+  const int rest = L - (W - 2 * R - s.lol) - (s.hir - 2 * R);
+  return 2 + (rest > 0 ? (rest + TO - 1) / TO : 0);
+}
+
+__device__ __forceinline__ AxisTile axis_tile(int t, int n, int W, int R, int a0, int a1,
+                                              int o0, int o1, int nmax, int edge) {
+  const AxisSpan s = axis_span(W, R, a0, a1, o0, o1, nmax, edge);
+  const int TO = W - 4 * R;
+  const int e0 = s.p0 + (W - 2 * R - s.lol);  // end of tile 0's outputs
+  AxisTile a;
+  a.lo = t == 0 ? s.lol : 2 * R;
+  a.hi = t == n - 1 ? s.hir : W - 2 * R;
+  if (t == 0) {
+    a.org = s.p0 - s.lol;
+    a.wlo = s.p0;
+  } else if (t == n - 1) {
+    a.org = s.p1 - s.hir;
+    a.wlo = e0 + (t - 1) * TO;
+  } else {
+    a.wlo = e0 + (t - 1) * TO;
+    a.org = a.wlo - 2 * R;
+  }
+  return a;
+}
 
 // Compact rings: every z-window is a ring of exactly NR = 2R+1 registers (u(k+R..k+3R),
 // A(k..k+2R), B(k-R..k+R)) and the march is unrolled NR times; u(k..k+R-1), still needed
@@ -361,9 +423,10 @@ struct V3Geom {
 
 template <typename T, int ORDER, int NW, int RPW, int XS, int PF, bool SEP>
 __device__ __forceinline__ void v3_march(
-    T* lds, int tx, int ty, int kc0, int kc1, const T* __restrict__ uin,
-    T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz, int nz_alloc, int zlo,
-    int zhi, const Box2& bx, const FdCoef<T>& q1, const FdCoef<T>& q2, const FdCoef<T>& q3) {
+    T* lds, int tx, int ty, int gx, int gy, int edge, int kc0, int kc1,
+    const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
+    int nz_alloc, int zlo, int zhi, const Box2& bx, const FdCoef<T>& q1, const FdCoef<T>& q2,
+    const FdCoef<T>& q3) {
   using G = V3Geom<T, ORDER, NW, RPW>;
   constexpr int R = G::R, NR = 2 * R + 1, W = G::W, S1R = G::S1R, UW = G::UW, UH = G::UH;
   constexpr int TX = W - 4 * R, TY = S1R - 4 * R;
@@ -379,12 +442,16 @@ __device__ __forceinline__ void v3_march(
   const int lane = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
   const int tid = w * 64 + lane;
-  const int i0 = tx * TX, j0 = ty * TY;
-  const int x = i0 - 2 * R + lane;
+  static_assert(TX > 0, "tile too narrow");
+  const AxisTile atx = axis_tile(tx, gx, W, R, bx.xa0, bx.xa1, bx.xo0, bx.xo1, nx, edge);
+  const AxisTile aty = axis_tile(ty, gy, S1R, R, bx.ya0, bx.ya1, bx.yo0, bx.yo1, ny, edge);
+  const int x = atx.org + lane;
   const bool xin = x >= bx.xa0 && x < bx.xa1;
-  const bool xout = x >= bx.xo0 && x < bx.xo1;
+  const bool xout = x >= max(bx.xo0, atx.wlo) && x < bx.xo1;
+  const int ywlo = max(bx.yo0, aty.wlo);
+  // lanes of a frozen edge column carry A = B = u, so s2c needs no edge case
   const bool s2c = lane >= R && lane < W - R;
-  const bool s3c = lane >= 2 * R && lane < W - 2 * R;
+  const bool s3c = lane >= atx.lo && lane < atx.hi;
   const int xc = clampi(x, 0, nx - 1);
   char* lb = (char*)lds;
   // SEP: a compiler memory fence before every LDS read keeps each one a separate
@@ -403,11 +470,11 @@ __device__ __forceinline__ void v3_march(
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
     const int row = w + q * NW;
-    const int y = j0 - 2 * R + row;
+    const int y = aty.org + row;
     const bool inxy = xin && y >= bx.ya0 && y < bx.ya1;
     m1[q] = inxy;
     m2[q] = inxy && s2c;
-    m3[q] = inxy && xout && y >= bx.yo0 && y < bx.yo1 && s3c;
+    m3[q] = inxy && xout && y >= ywlo && y < bx.yo1 && s3c;
     goff[q] = (uint32_t)(clampi(y, 0, ny - 1) * (int)sy + xc) * (uint32_t)E;
     ub[q] = (row * UW + lane) * E;                            // u(row-R+R.., lane-R+R..)
     aw[q] = (G::OFF_A + R + row * W + lane) * E;               // A own cell, set 0
@@ -436,8 +503,8 @@ __device__ __forceinline__ void v3_march(
         uc = cc < R ? cc : W + cc;
       }
       hl[h] = (ur * UW + uc) * E;
-      hoff[h] = (uint32_t)(clampi(j0 - 3 * R + ur, 0, ny - 1) * (int)sy +
-                           clampi(i0 - 3 * R + uc, 0, nx - 1)) * (uint32_t)E;
+      hoff[h] = (uint32_t)(clampi(aty.org - R + ur, 0, ny - 1) * (int)sy +
+                           clampi(atx.org - R + uc, 0, nx - 1)) * (uint32_t)E;
     }
   }
   const int64_t szb = sz * E;
@@ -588,7 +655,7 @@ __device__ __forceinline__ void v3_march(
 #pragma unroll
       for (int q = 0; q < RPW; ++q) {
         const int row = w + q * NW;
-        if (row < 2 * R || row >= S1R - 2 * R) continue;  // scalar branch
+        if (row < aty.lo || row >= aty.hi) continue;  // scalar branch
         const int b = ar[q] + AO + ABB;
         const T c = rb[q][sl(0)];
         T acc = fd_ctr(q3.kc, c, third * dl[q][PH % R]);
@@ -665,15 +732,17 @@ struct StepVar {
 };
 
 template <typename T, int ORDER, int NW, int RPW, int VAR>
-__device__ __forceinline__ void march_var(T* lds, int tx, int ty, int kc0, int kc1,
+__device__ __forceinline__ void march_var(T* lds, int tx, int ty, const StepSched& sc,
+                                          int kc0, int kc1,
                                           const T* __restrict__ uin, T* __restrict__ uout,
                                           int nx, int ny, int64_t sy, int64_t sz, int nz_alloc,
                                           int zlo, int zhi, const Box2& bx, const FdCoef<T>& q1,
                                           const FdCoef<T>& q2, const FdCoef<T>& q3) {
   using V = StepVar<VAR>;
   if constexpr (V::v3) {
-    v3_march<T, ORDER, NW, RPW, V::xs, V::pf, V::sep>(lds, tx, ty, kc0, kc1, uin, uout, nx, ny, sy, sz,
-                                              nz_alloc, zlo, zhi, bx, q1, q2, q3);
+    v3_march<T, ORDER, NW, RPW, V::xs, V::pf, V::sep>(lds, tx, ty, sc.gx, sc.gy, sc.edge, kc0,
+                                                      kc1, uin, uout, nx, ny, sy, sz, nz_alloc,
+                                                      zlo, zhi, bx, q1, q2, q3);
   } else {
     using Gm = CringGeom<ORDER, NW, RPW>;
     cring_march<T, ORDER, NW, RPW, V::xdpp>(lds, lds + 2 * Gm::LDS_U,
@@ -717,8 +786,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((
     const bool second = tile.z >= sc.gza;
     const int kc0 = second ? k0b + (tile.z - sc.gza) * sc.zchunk : k0 + tile.z * sc.zchunk;
     const int kc1 = min(kc0 + sc.zchunk, second ? k1b : k1);
-    march_var<T, ORDER, NW, RPW, VAR>(lds, tile.x, tile.y, kc0, kc1, uin, uout, nx, ny, sy, sz,
-                                      nz_alloc, zlo, zhi, bx, q1, q2, q3);
+    march_var<T, ORDER, NW, RPW, VAR>(lds, tile.x, tile.y, sc, kc0, kc1, uin, uout, nx, ny, sy,
+                                      sz, nz_alloc, zlo, zhi, bx, q1, q2, q3);
   } else {
     // 1-D grid; tile.x = this group's XCD-contiguous logical id, so the groups of one XCD
     // march neighbouring tiles.  Group g owns the linear planes [s, e), s = g per +
@@ -733,7 +802,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((
       if (p0 < na) p1 = min(p1, na);  // a segment never spans both plane ranges
       const int kc0 = p0 < na ? k0 + p0 : k0b + (p0 - na);
       __syncthreads();  // nobody still reads the previous segment's last LDS planes
-      march_var<T, ORDER, NW, RPW, VAR>(lds, t % sc.gx, t / sc.gx, kc0, kc0 + (p1 - p0), uin,
+      march_var<T, ORDER, NW, RPW, VAR>(lds, t % sc.gx, t / sc.gx, sc, kc0, kc0 + (p1 - p0), uin,
                                         uout, nx, ny, sy, sz, nz_alloc, zlo, zhi, bx, q1, q2,
                                         q3);
       s += p1 - p0;
@@ -744,6 +813,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((
 // Persistent schedule for exclusive launches: ADVDIFF_STEP_PERSIST / advdiff_set_step_persist.
 // Off by default since the v3 march: at 512^3 the dynamically balanced grid of z chunks
 // is 9-11 % faster (FD4 760 vs 836 us, FD2 559 vs 745 us, profiles/step_variants_r2.log).
+static int g_step_edge = -1;
+static int step_edge() {  // v3 edge tiles (axis_tile): ADVDIFF_STEP_EDGE / advdiff_set_step_edge
+  if (g_step_edge < 0) g_step_edge = knob("STEP_EDGE", 1);
+  return g_step_edge;
+}
+
 static int g_step_persist = -1;
 static int step_persist() {
   if (g_step_persist < 0) g_step_persist = knob("STEP_PERSIST", 0);
@@ -768,7 +843,13 @@ template <typename T, int ORDER, int NW, int RPW, int XDPP = 0>
 static hipError_t launch_step(const SArgs& a) {
   constexpr int R = ORDER / 2;
   constexpr int TX = 64 - 4 * R, TY = NW * RPW - 4 * R;
-  const int gx = div_up(a.nx, TX), gy = div_up(a.ny, TY);
+  const int edge = StepVar<XDPP>::v3 ? step_edge() : 0;
+  const int gx = StepVar<XDPP>::v3
+                     ? axis_tile_count(64, R, a.bx.xa0, a.bx.xa1, a.bx.xo0, a.bx.xo1, a.nx, edge)
+                     : div_up(a.nx, TX);
+  const int gy = StepVar<XDPP>::v3 ? axis_tile_count(NW * RPW, R, a.bx.ya0, a.bx.ya1, a.bx.yo0,
+                                                     a.bx.yo1, a.ny, edge)
+                                   : div_up(a.ny, TY);
   // z chunks: minimise (rounds of resident workgroups) x (chunk + 4R warm-up planes);
   // resident workgroups = CUs x occupancy of this instance (LDS / VGPR bound: 1-2 per CU)
   static const int target = knob("STEP_TARGET_BLOCKS", 0);  // >0: legacy fixed target
@@ -784,7 +865,7 @@ static hipError_t launch_step(const SArgs& a) {
   static const int minseg = std::max(knob("STEP_MIN_SEG", 32), 1);
   const int na = std::max(a.k1 - a.k0, 0), nb = std::max(a.k1b - a.k0b, 0);
   const long long slots = (long long)device_cus() * per_cu;
-  StepSched sc{gx, gy, 0, 0, 0, 0};
+  StepSched sc{gx, gy, 0, 0, 0, 0, edge};
   dim3 grid;
   const long long L = (long long)gx * gy * (na + nb);
   const bool persistent = persist && (a.flags & ADVDIFF_EXCLUSIVE) && L < (1LL << 31);
@@ -867,6 +948,12 @@ static int step_cfg() {
 extern "C" int advdiff_set_step_persist(int on) {
   const int old = advdiff::step_persist();
   advdiff::g_step_persist = on ? 1 : 0;
+  return old;
+}
+
+extern "C" int advdiff_set_step_edge(int on) {
+  const int old = advdiff::step_edge();
+  advdiff::g_step_edge = on ? 1 : 0;
   return old;
 }
 

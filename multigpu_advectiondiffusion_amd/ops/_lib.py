@@ -130,6 +130,8 @@ def _load():
         lib.advdiff_set_step_cfg.restype = c_int
         lib.advdiff_set_step_persist.argtypes = [c_int]
         lib.advdiff_set_step_persist.restype = c_int
+        lib.advdiff_set_step_edge.argtypes = [c_int]
+        lib.advdiff_set_step_edge.restype = c_int
         lib.advdiff_set_b3_ver.argtypes = [c_int]
         lib.advdiff_set_b3_ver.restype = c_int
         lib.advdiff_set_b3_ty.argtypes = [c_int]

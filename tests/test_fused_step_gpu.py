@@ -208,3 +208,46 @@ def test_fused_step_production_size_bitwise(order):
     finally:
         lib.advdiff_set_step_persist(old)
     assert torch.equal(got, exp), (got - exp).abs().max().item()
+
+
+@pytest.mark.parametrize("order", [4, 2])
+@pytest.mark.parametrize("boxkind", ["slab", "interior", "edge_hi_x_lo_y", "edge_lo_x_hi_y"])
+@pytest.mark.parametrize("shape", [(40, 44, 70, 72), (24, 130, 300, 320), (20, 37, 61, 64)])
+def test_fused_step_edge_tiles_bitwise(order, boxkind, shape):
+    """Boundary-anchored edge tiles (axis_tile, the default) vs the plain partition: the
+    same values on every cell, no cell written twice or left out (output initialised with
+    a sentinel), for slab and Cartesian-view boxes (output >= 3R inside view edges that
+    are not global boundaries, as the solver's boxes are)."""
+    from multigpu_advectiondiffusion_amd.ops import _lib
+    lib = _lib.require()
+    nz, ny, nx, sx = shape
+    box = {"slab": None,
+           "interior": (0, nx, 0, ny, 6, nx - 6, 6, ny - 6),
+           "edge_hi_x_lo_y": (0, nx - 3, 3, ny, 6, nx, 3, ny - 6),
+           "edge_lo_x_hi_y": (3, nx, 0, ny - 3, 3, nx - 6, 6, ny)}[boxkind]
+    g = torch.Generator().manual_seed(13)
+    u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).cuda()
+    c = (0.21, 0.17, 0.13)
+    dt = 0.9 / (2 * sum(c)) if order == 2 else 0.5 / sum(c)
+    kw = dict(nx=nx, ny=ny, k0=3, k1=nz - 3, zlo=2, zhi=nz - 2, border=3, order=order,
+              cx=c[0], cy=c[1], cz=c[2], dt=dt, box=box)
+    outs = []
+    old = lib.advdiff_set_step_edge(1)
+    try:
+        for edge in (1, 0):
+            lib.advdiff_set_step_edge(edge)
+            got = torch.full_like(u, float("nan"))
+            stencil.diffusion3d_step(u, got, **kw)
+            torch.cuda.synchronize()
+            outs.append(got)
+    finally:
+        lib.advdiff_set_step_edge(old)
+    assert torch.equal(outs[0].isnan(), outs[1].isnan())
+    assert torch.equal(torch.nan_to_num(outs[0], 7.0), torch.nan_to_num(outs[1], 7.0))
+    if box is not None:
+        cpu = u.cpu()
+        ref_out = torch.full_like(cpu, float("nan"))
+        ref.diffusion3d_step_box(cpu, ref_out, nx, ny, 3, nz - 3, 2, nz - 2, box, order, *c, dt)
+        written = ~outs[0].isnan().cpu()
+        assert torch.equal(written, ~ref_out.isnan())
+        assert (outs[0].cpu()[written] - ref_out[written]).abs().max().item() < 1e-12
