@@ -927,10 +927,12 @@ static hipError_t dispatch_step(int cfg, const SArgs& a) {
     case 33: STEPV(10, 4, 23);   // 40 rows, 10 waves x 4 rows
     case 29: STEPV(16, 2, 23);   // round-2 default before the taller tiles
     case 1: STEPV(16, 2, 2);     // round-1 default (cring, DPP in all stages)
-    default:  // v3, 12 waves x 3 rows (36 stage-1 rows), DPP x in stages 2/3, prefetch 2,
-              // unmerged LDS reads: vs 16 x 2 rows, interleaved medians at 512^3
-              // FD4 793 -> 761 us, FD2 598 -> 566 us (profiles/step_variants_r2_tiles.log);
-              // 48 rows overflow the 16-bit DS offsets, 10 x 4 spills at 168 VGPRs
+    default:  // v3, DPP x in stages 2/3, prefetch 2, unmerged LDS reads.  With the edge
+              // tiles (axis_tile), interleaved medians at 512^3: FD4 16 waves x 2 rows
+              // (32 stage-1 rows) 662 us vs 715 us for 12 x 3; FD2 12 x 3 rows 535 us vs
+              // 549 us for 16 x 2 (profiles/step_cfgs_edge_r2.log).  48 rows overflow the
+              // 16-bit DS offsets, 10 x 4 spills at 168 VGPRs
+      if constexpr (ORDER == 4) STEPV(16, 2, 23);
       STEPV(12, 3, 23);
   }
 #undef STEPV

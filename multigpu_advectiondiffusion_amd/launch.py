@@ -30,6 +30,28 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def free_port_block(n: int, tries: int = 64) -> int:
+    """A base port b with b .. b+n all bindable right now: the native socket transport
+    listens on ADVDIFF_PORT (rendezvous) and ADVDIFF_PORT+1+i (rank i of the full mesh),
+    so a lone free port is not enough on a busy host."""
+    import random
+    for _ in range(tries):
+        b = random.randint(20000, 60000 - n - 1)
+        socks = []
+        try:
+            for q in range(b, b + n + 1):
+                s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+                socks.append(s)
+                s.bind(("0.0.0.0", q))
+            return b
+        except OSError:
+            continue
+        finally:
+            for s in socks:
+                s.close()
+    return free_port()
+
+
 def _child_env(rank: int, world: int, port: int, cpu: bool) -> dict:
     env = dict(os.environ)
     env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
@@ -48,7 +70,8 @@ def launch(np_: int, argv: list[str], cpu: bool = False, timeout: float | None =
     blocked in a halo exchange until the collective timeout.  Returns the first
     non-zero exit code (0 if all succeed)."""
     import time
-    port = free_port()
+    # native ranks listen on MASTER_PORT+17 (rendezvous) and MASTER_PORT+18+i (socket mesh)
+    port = free_port_block(np_ + 18) if native else free_port()
     if native:  # the C++ executables: bin/<app> <args...> (RCCL or --transport socket)
         from pathlib import Path
         exe = Path(__file__).resolve().parent.parent / "bin" / argv[0]

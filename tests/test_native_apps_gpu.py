@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from multigpu_advectiondiffusion_amd import Burgers, Diffusion, Grid, Solver
-from multigpu_advectiondiffusion_amd.launch import free_port
+from multigpu_advectiondiffusion_amd.launch import free_port_block
 
 pytestmark = pytest.mark.gpu
 
@@ -22,7 +22,7 @@ BIN = ROOT / "bin"
 def _run(app, args, out, world=1, extra=()):
     exe = BIN / app
     assert exe.exists(), f"{exe} not built (make -C csrc apps)"
-    port = free_port()
+    port = free_port_block(world + 1)
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),

@@ -19,7 +19,7 @@ import pytest
 import torch
 
 from multigpu_advectiondiffusion_amd import Burgers, Diffusion, Grid, Solver
-from multigpu_advectiondiffusion_amd.launch import free_port, spawn_local
+from multigpu_advectiondiffusion_amd.launch import free_port_block, spawn_local
 
 ROOT = Path(__file__).resolve().parent.parent
 
@@ -128,7 +128,7 @@ def test_rccl_multirank_bitwise(world):
 def _native(app, args, out, world, transport):
     exe = ROOT / "bin" / app
     assert exe.exists(), f"{exe} not built (make -C csrc apps)"
-    port = free_port()
+    port = free_port_block(world + 1)
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
