@@ -12,6 +12,8 @@ for tgt in sorted({p.split("/")[-2].rsplit("_", 1)[0] for p in glob.glob(f"{root
     agg = collections.defaultdict(list)
     kname = ""
     for f in sorted(glob.glob(f"{root}/{tgt}_*/p_counter_collection.csv")):
+        if not f.split("/")[-2][len(tgt) + 1:].isdigit():  # another target sharing the prefix
+            continue
         for r in csv.DictReader(open(f)):
             if "advdiff" in r["Kernel_Name"]:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
