@@ -382,7 +382,9 @@ __global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(WPE))) 
 //     holds the others at the per-plane barrier (the y analogue of the x halo lane);
 //   * faces are carried as 6 x flux (the 1/6 of the candidate polynomials is folded
 //     into rd*/6 by the launcher) and the one division per face uses one Newton step
-//     on v_rcp_f64 plus a residual correction (w5_face6: 2 fp64 ops fewer per face).
+//     on v_rcp_f64 plus a residual correction (w5_face6: 2 fp64 ops fewer per face;
+//     correctly rounded on 4M random operand pairs, bench/native/divtest.hip — without
+//     the Newton step up to 18 ulp).
 // Requires a plane (sy * ny elements) below 2^31 bytes; the launcher falls back to v3.
 // ------------------------------------------------------------------------------
 template <typename T>

@@ -320,7 +320,8 @@ __device__ __forceinline__ void w5_side(T v0, T v1, T v2, T v3, T v4, T C0, T C1
   const T t1 = v1 - v3;
   const T t2 = fma(T(3), v2, fma(T(-4), v3, v4));
   const T e0 = fma(t0, t0, C0), e1 = fma(t1, t1, C1), e2 = fma(t2, t2, C2);
-  const T q0 = fma(T(11), v2, fma(T(-7), v1, T(2) * v0));
+  // 2 v0 - 7 v1 + 11 v2 = 2 t0 + v1 + 5 v2: one op fewer than the direct form
+  const T q0 = fma(T(2), t0, fma(T(5), v2, v1));
   const T q1 = fma(T(5), v2, fma(T(2), v3, -v1));
   const T q2 = fma(T(5), v3, fma(T(2), v2, -v4));
   T w0, w1, w2;
