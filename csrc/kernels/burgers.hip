@@ -381,10 +381,9 @@ __global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(WPE))) 
 //     above its row — every other wave does exactly 3 faces per plane, so no wave
 //     holds the others at the per-plane barrier (the y analogue of the x halo lane);
 //   * faces are carried as 6 x flux (the 1/6 of the candidate polynomials is folded
-//     into rd*/6 by the launcher) and the one division per face uses one Newton step
-//     on v_rcp_f64 plus a residual correction (w5_face6: 2 fp64 ops fewer per face;
-//     correctly rounded on 4M random operand pairs, bench/native/divtest.hip — without
-//     the Newton step up to 18 ulp).
+//     into rd*/6 by the launcher) and the one division per face is a product with a
+//     reciprocal refined by one Newton step (w5_combine6: 4 fp64 ops fewer per face
+//     than the IEEE-exact fast_div; bench/native/divtest.hip measures the variants).
 // Requires a plane (sy * ny elements) below 2^31 bytes; the launcher falls back to v3.
 // ------------------------------------------------------------------------------
 template <typename T>
@@ -400,12 +399,18 @@ __device__ __forceinline__ T fast_div1(T n, T d) {
   }
 }
 
-// 6 x the face flux from the two sides (w5_side numerators / weight sums)
+// 6 x the face flux from the two sides (w5_side numerators / weight sums): the common
+// numerator times a reciprocal refined by one Newton step (relative error ~2^-46, i.e.
+// ~1e-14 of the flux; fast_div1's residual correction to a correctly rounded quotient
+// costs 2 more fp64 ops per face and buys nothing the scheme can see)
 template <typename T>
 __device__ __forceinline__ T w5_combine6(T n1, T S1, T n2, T S2) {
 #pragma clang fp contract(off)
   if constexpr (sizeof(T) == 8) {
-    return fast_div1(fma(n1, S2, n2 * S1), S1 * S2);
+    const T d = S1 * S2;
+    T r = __builtin_amdgcn_rcp(d);
+    r = fma(fma(-d, r, T(1)), r, r);
+    return fma(n1, S2, n2 * S1) * r;
   } else {
     return fast_div1(n1, S1) + fast_div1(n2, S2);
   }

@@ -326,10 +326,13 @@ __device__ __forceinline__ void w5_side(T v0, T v1, T v2, T v3, T v4, T C0, T C1
   const T q2 = fma(T(5), v3, fma(T(2), v2, -v4));
   T w0, w1, w2;
   if constexpr (ZVARIANT) {
+    // (e_k + tau) * prod_{j!=k} e_j = P + tau * prod_{j!=k} e_j with P = e0 e1 e2:
+    // 4 products + 3 fma instead of 3 products, 3 adds and 3 more products
     const T tau = fabs(e0 - e2);
-    w0 = (e0 + tau) * (e1 * e2);
-    w1 = (T(6) * (e1 + tau)) * (e0 * e2);
-    w2 = (T(3) * (e2 + tau)) * (e0 * e1);
+    const T e12 = e1 * e2, e02 = e0 * e2, e01 = e0 * e1, P = e0 * e12;
+    w0 = fma(tau, e12, P);
+    w1 = T(6) * fma(tau, e02, P);
+    w2 = T(3) * fma(tau, e01, P);
   } else {
     const T s0 = e0 * e0, s1 = e1 * e1, s2 = e2 * e2;
     w0 = s1 * s2;
