@@ -605,6 +605,209 @@ __global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(4))) vo
   }
 }
 
+// ------------------------------------------------------------------------------
+// WENO5 3-D stage, v9: v6 (YM = 1, TY = 8) with the per-plane overhead taken out.
+//   * the march is unrolled by 10 planes (ring length 5 x buffer-set parity 2), so the
+//     LDS buffer set of every plane is a compile-time constant: each LDS access is a
+//     loop-invariant lane base + an immediate offset.  The lane's read base sits at the
+//     lowest cell any of its reads touches (own cell - 2 rows - 2 columns), so every
+//     offset is non-negative and fits the 16-bit DS offset (v6 spends ~15 v_add_u32
+//     per plane rebuilding bases);
+//   * every prefetch is unconditional: plane indices past the chunk are clamped (SALU)
+//     to its last plane, so no branch and no phi copies (v_mov_b64) around the loads;
+//     the extra tile staged after the last plane lands in the idle buffer set;
+//   * x and y faces use w5_side_h (common.hpp): 37 instead of 41 fp64 ops per side,
+//     carried as 3 x the flux; z faces keep w5_side on the z rings (6 x the flux).
+// Requires a plane below 2^31 bytes (v6_fits); TY = 8 only (offsets < 64 KiB).
+// ------------------------------------------------------------------------------
+template <typename T, bool WZ, bool VISC, int MODE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void burgers3d_w5s_kernel(
+    const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
+    int k1, int zchunk, int border, T rdx3, T rdy3, T rdz6, T vx, T vy, T vz, T dt, T a, T b,
+    const double* __restrict__ dtp) {
+  constexpr int TY = 8, R = 3, NR = 5, TX = 64, TXO = TX - 1;
+  constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NT = TX * TY, LT = LX * LY;
+  constexpr int NPT = (LT + NT - 1) / NT;
+  constexpr int E = (int)sizeof(T);
+  constexpr int NARR = VISC ? 3 : 2;                 // staged arrays: f+, f- [, u]
+  constexpr int SET = NARR * LT + (TY + 1) * TX;     // elements per buffer set (+ y faces)
+  constexpr int OM = LT * E, OU = 2 * LT * E, OFY = NARR * LT * E, SETB = SET * E;
+  constexpr int XO = 2 * LX * E + 2 * E;             // own cell - lane read base
+  static_assert(SETB + XO + NARR * LT * E + 3 * LX * E < 65536, "DS immediate offsets");
+  __shared__ T lds[2 * SET];
+  char* lb = (char*)lds;
+  const W5Sgpr<T> kk;  // fp64 constants in SGPRs (VOP3 operands, no v_fmac copies)
+
+  const int tx = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
+  const int tid = w * TX + tx;
+  const int ib = border - 1 + (int)blockIdx.x * TXO;  // x of lane 0 (supplies a face only)
+  const int jb = border + (int)blockIdx.y * TY;       // y of wave 0
+  const int i = ib + tx, j = jb + w;
+  const int kc0 = k0 + (int)blockIdx.z * zchunk;
+  const int kc1 = min(kc0 + zchunk, k1);
+  const int klast = kc1 - 1;
+  const bool active = tx >= 1 && i < nx - border && j < ny - border;
+  const uint32_t goff = (uint32_t)(min(j, ny - 1) * (int)sy + min(i, nx - 1)) * (uint32_t)E;
+  const int64_t szb = sz * E;
+  auto plane = [&](const T* base, int k) {
+    return plane_rsrc((const char*)base + (int64_t)k * szb);
+  };
+  if (dtp != nullptr && !device_dt(dtp, dt)) {  // adaptive run at t_end: out = in
+    if (active)
+      for (int k = kc0; k < kc1; ++k) gst<T>(plane(out, k), goff, gld<T>(plane(in, k), goff));
+    return;
+  }
+
+  uint32_t toff[NPT];
+#pragma unroll
+  for (int r = 0; r < NPT; ++r) {
+    const int idx = min(tid + r * NT, LT - 1);
+    const int ly = idx / LX, lx = idx - ly * LX;
+    toff[r] = (uint32_t)(clampi(jb - R + ly, 0, ny - 1) * (int)sy +
+                         clampi(ib - R + lx, 0, nx - 1)) * (uint32_t)E;
+  }
+  // loop-invariant LDS lane bases (byte addresses); everything else is an immediate
+  const int lrb = ((w + R) * LX + tx + R) * E - XO;  // own-cell reads
+  const int brb = tx * E;                            // bottom y faces (row R-1) + its store
+  const int fyb = ((w + 1) * TX + tx) * E;           // y face above the own cell
+  const int stb = tid * E;                           // tile staging
+  T pre[NPT];
+  auto fetch_tile = [&](int k) {
+    const auto rs = plane(in, k);
+#pragma unroll
+    for (int r = 0; r < NPT; ++r) pre[r] = gld<T>(rs, toff[r]);
+  };
+  auto stage_tile = [&]<int SB>() {  // SB: byte offset of the buffer set
+#pragma unroll
+    for (int r = 0; r < NPT; ++r) {
+      const int idx = tid + r * NT;
+      if (NPT * NT == LT || idx < LT) {
+        T p, m;
+        lf_split(pre[r], p, m);
+        lds_st<T>(lb + stb, SB + r * NT * E, p);
+        lds_st<T>(lb + stb, SB + OM + r * NT * E, m);
+        if constexpr (VISC) lds_st<T>(lb + stb, SB + OU + r * NT * E, pre[r]);
+      }
+    }
+  };
+  // 3 x flux at the face to the right of the cell at immediate offset c (relative to the
+  // base pointer bp) along stride st
+  auto lds_face3 = [&](const char* bp, int c, int st) {
+    T pv[5], mv[5];
+#pragma unroll
+    for (int d = 0; d < 5; ++d) {
+      pv[d] = lds_ld<T>(bp, c + (d - 2) * st);
+      mv[d] = lds_ld<T>(bp, c + OM + (d - 1) * st);
+    }
+    T n1, S1, n2, S2;
+    w5_face3_sides<T, WZ>(pv, mv, n1, S1, n2, S2, kk);
+    return w5_combine6(n1, S1, n2, S2);
+  };
+
+  // ---- rings: plane p lives in slot (p - kc0 + 2 NR) % NR ----
+  T rp[NR], rm[NR], ru[NR], cp[NR], cm[NR], fz[NR];  // f+, f-, u, C(f+), C(f-), 6 x z face
+  {
+    T uz[2 * R], fp[2 * R], fm[2 * R];  // planes kc0-3 .. kc0+2
+#pragma unroll
+    for (int q = 0; q < 2 * R; ++q) {
+      uz[q] = gld<T>(plane(in, kc0 - R + q), goff);
+      lf_split(uz[q], fp[q], fm[q]);
+    }
+    auto sl = [](int p) { return (p + 2 * NR) % NR; };  // slot of plane kc0 + p
+    {  // face kc0-½: the march's z-face arithmetic (bit-identical to it)
+      T n1, S1, n2, S2;
+      w5_side<T, WZ>(fp[0], fp[1], fp[2], fp[3], fp[4], w5_curv(fp[0], fp[1], fp[2], kk),
+                     w5_curv(fp[1], fp[2], fp[3], kk), w5_curv(fp[2], fp[3], fp[4], kk), n1, S1, kk);
+      w5_side<T, WZ>(fm[5], fm[4], fm[3], fm[2], fm[1], w5_curv(fm[5], fm[4], fm[3], kk),
+                     w5_curv(fm[4], fm[3], fm[2], kk), w5_curv(fm[3], fm[2], fm[1], kk), n2, S2, kk);
+      fz[sl(-1)] = w5_combine6(n1, S1, n2, S2);
+    }
+    cp[sl(-1)] = w5_curv(fp[1], fp[2], fp[3], kk);
+    cp[sl(0)] = w5_curv(fp[2], fp[3], fp[4], kk);
+    cm[sl(0)] = w5_curv(fm[2], fm[3], fm[4], kk);
+    cm[sl(1)] = w5_curv(fm[3], fm[4], fm[5], kk);
+#pragma unroll
+    for (int q = 1; q < 2 * R; ++q) {  // planes kc0-2 .. kc0+2
+      rp[sl(q - R)] = fp[q];
+      ru[sl(q - R)] = uz[q];
+    }
+#pragma unroll
+    for (int q = 2; q < 2 * R; ++q) rm[sl(q - R)] = fm[q];  // kc0-1 .. kc0+2
+  }
+  fetch_tile(kc0);
+  stage_tile.template operator()<0>();
+  fetch_tile(min(kc0 + 1, klast));
+  T un = gld<T>(plane(in, kc0 + R), goff);  // u(k+3) of the current iteration
+  T ax = T(0);
+  if constexpr (reads_aux<MODE>()) ax = gld<T>(plane(aux, kc0), goff);
+  __syncthreads();
+
+  auto body = [&]<int PH>(int k) {
+    auto sl = [](int d) { return (PH + d + 2 * NR) % NR; };  // slot of plane k + d
+    constexpr int SB = (PH & 1) * SETB, SBN = SETB - SB;    // this / the other set
+    // new plane k+3 of the own column: f-(k+3) now; f+(k+3) and u(k+3) after their use
+    T pn, mn;
+    lf_split(un, pn, mn);
+    rm[sl(3)] = mn;
+    const T unew = un;
+    un = gld<T>(plane(in, min(k + 1, klast) + R), goff);
+    T axk = ax;
+    if constexpr (reads_aux<MODE>()) ax = gld<T>(plane(aux, min(k + 1, klast)), goff);
+
+    const T fy = lds_face3(lb + lrb, SB + XO, LX * E);  // y face j+½
+    if (w == (k - kc0) % TY)  // the tile's bottom y faces rotate over the waves
+      lds_st<T>(lb + brb, SB + OFY, lds_face3(lb + brb, SB + ((R - 1) * LX + R) * E, LX * E));
+    lds_st<T>(lb + fyb, SB + OFY, fy);
+    const T ctr = ru[sl(0)];
+    T d2x = T(0), d2y = T(0), d2z = T(0);
+    const T fx = lds_face3(lb + lrb, SB + XO, E);  // x face i+½
+    if constexpr (VISC) {
+      const int c = SB + OU + XO;
+      const char* bp = lb + lrb;
+      d2x = fd4_d2k(lds_ld<T>(bp, c - 2 * E), lds_ld<T>(bp, c - E), ctr,
+                    lds_ld<T>(bp, c + E), lds_ld<T>(bp, c + 2 * E), kk);
+      d2y = fd4_d2k(lds_ld<T>(bp, c - 2 * LX * E), lds_ld<T>(bp, c - LX * E), ctr,
+                    lds_ld<T>(bp, c + LX * E), lds_ld<T>(bp, c + 2 * LX * E), kk);
+      d2z = fd4_d2k(ru[sl(-2)], ru[sl(-1)], ctr, ru[sl(1)], ru[sl(2)], kk);
+    }
+    cp[sl(1)] = w5_curv(rp[sl(0)], rp[sl(1)], rp[sl(2)], kk);
+    cm[sl(2)] = w5_curv(rm[sl(1)], rm[sl(2)], rm[sl(3)], kk);
+    {
+      T n1, S1, n2, S2;
+      w5_side<T, WZ>(rp[sl(-2)], rp[sl(-1)], rp[sl(0)], rp[sl(1)], rp[sl(2)], cp[sl(-1)],
+                     cp[sl(0)], cp[sl(1)], n1, S1, kk);
+      w5_side<T, WZ>(rm[sl(3)], rm[sl(2)], rm[sl(1)], rm[sl(0)], rm[sl(-1)], cm[sl(2)],
+                     cm[sl(1)], cm[sl(0)], n2, S2, kk);
+      fz[sl(0)] = w5_combine6(n1, S1, n2, S2);  // face k+½
+    }
+
+    // stage tile k+1 into the other buffer set, fetch tile k+2 (past the chunk: its last
+    // plane again, staged into the idle set and never read)
+    stage_tile.template operator()<SBN>();
+    fetch_tile(min(k + 2, klast));
+    __syncthreads();  // y faces of k and tile k+1 visible
+
+    const T fyl = lds_ld<T>(lb + fyb, SB + OFY - TX * E);
+    const T fxl = wave_shr1(fx);  // face i-½ from lane l-1 (lane 0: unused)
+    T L = -(((fx - fxl) * rdx3 + (fy - fyl) * rdy3) + (fz[sl(0)] - fz[sl(-1)]) * rdz6);
+    if constexpr (VISC) L += vx * d2x + vy * d2y + vz * d2z;
+    T dnew = T(0);
+    const T v = stage_value<T, MODE>(axk, ctr, L, dt, a, b, dnew);
+    if (active) {
+      gst<T>(plane(out, k), goff, v);
+      if constexpr (MODE == kLs1 || MODE == kLs) gst<T>(plane(aux, k), goff, dnew);
+    }
+    rp[sl(3)] = pn;  // f+(k+3), u(k+3) replace f+(k-2), u(k-2)
+    ru[sl(3)] = unew;
+  };
+  for (int kb = kc0; kb < kc1; kb += 2 * NR) {
+    [&]<int... P>(std::integer_sequence<int, P...>) {
+      (void)((kb + P < kc1 ? (body.template operator()<P>(kb + P), true) : false) && ...);
+    }(std::make_integer_sequence<int, 2 * NR>{});
+  }
+}
+
 template <typename T, int W, bool WZ, bool VISC, int MODE, int TX>
 __global__ __launch_bounds__(TX) void burgers2d_stage_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int64_t sy, int j0, int j1, int ychunk,
@@ -781,7 +984,21 @@ static hipError_t launch_b3_v6(const BArgs& p) {
   return hipGetLastError();
 }
 
-// v6 addresses a plane with 32-bit byte offsets
+template <typename T, bool WZ, bool VISC, int MODE>
+static hipError_t launch_b3_v9(const BArgs& p) {
+  const int gx = div_up(std::max(p.nx - 2 * p.border, 1), 63);
+  const int gy = div_up(std::max(p.ny - 2 * p.border, 1), 8);
+  const int zc = pick_chunk(p.hi - p.lo, (long long)gx * gy, 8, 256);
+  const int gz = div_up(p.hi - p.lo, zc);
+  const double s = 1.0 / 12.0;
+  hipLaunchKernelGGL((burgers3d_w5s_kernel<T, WZ, VISC, MODE>), dim3(gx, gy, gz), dim3(64, 8, 1),
+                     0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx, p.ny, p.sy, p.sz,
+                     p.lo, p.hi, zc, p.border, T(p.rdx / 3.0), T(p.rdy / 3.0), T(p.rdz / 6.0),
+                     T(p.vx * s), T(p.vy * s), T(p.vz * s), T(p.dt), T(p.a), T(p.b), p.dtp);
+  return hipGetLastError();
+}
+
+// v6 / v9 address a plane with 32-bit byte offsets
 template <typename T>
 static bool v6_fits(const BArgs& p) {
   return (int64_t)p.sy * p.ny * (int64_t)sizeof(T) < (int64_t(1) << 31);
@@ -794,11 +1011,14 @@ static bool v6_fits(const BArgs& p) {
 // 4/5 = v2 at 6 waves/SIMD (spills; kept for the record), 6 = the renamed-ring v6 kernel
 // with rotating bottom faces (default: 242 -> 227 us, 9.06e7 VALU per dispatch, in-solver
 // 20.3k -> 21.7k MLUPS; profiles/burgers_v6_r2.md), 7 = v6 with wave 0 fixed, 8 = v6
-// with a halo wave row (7 of 8 rows output: more workgroups, slower).  ADVDIFF_B3_TY=16
+// with a halo wave row (7 of 8 rows output: more workgroups, slower), 9 = v6 with
+// compile-time LDS sets, unconditional prefetches, SGPR constants and w5_side_h x/y faces
+// (default: 226 -> 195 us, SQ_INSTS_VALU 8.46e7 -> 7.62e7 = 290 lane-ops per cell,
+// profiles/burgers_v9_r2.md).  ADVDIFF_B3_TY=16
 // gives v3/v6 16-row tiles.
 static int g_b3_ver = -1, g_b3_ty = -1;
 static int b3_ver() {
-  if (g_b3_ver < 0) g_b3_ver = knob("B3_VER", 6);
+  if (g_b3_ver < 0) g_b3_ver = knob("B3_VER", 9);
   return g_b3_ver;
 }
 static int b3_ty() {  // rows (waves) per 3-D tile: 8 or 16 (ADVDIFF_B3_TY)
@@ -819,6 +1039,7 @@ static hipError_t launch_b3(const BArgs& p) {
       return ty == 16 ? launch_b3_v2<T, WZ, VISC, MODE, 16, true>(p)
                       : launch_b3_v2<T, WZ, VISC, MODE, 8, true>(p);
     }
+    if (v == 9 && v6_fits<T>(p)) return launch_b3_v9<T, WZ, VISC, MODE>(p);
     if (v >= 6 && v <= 8 && v6_fits<T>(p)) {
       if (ty == 16) return launch_b3_v6<T, WZ, VISC, MODE, 1, 16>(p);
       return v == 6 ? launch_b3_v6<T, WZ, VISC, MODE, 1>(p)

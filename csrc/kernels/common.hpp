@@ -168,9 +168,11 @@ __device__ __forceinline__ T fd2_axis(T acc, T k, T m1, T p1) {
 template <typename T>
 __device__ __forceinline__ void lf_split(T u, T& fp, T& fm) {
 #pragma clang fp contract(off)
-  const T s = (T(0.5) * fabs(u)) * u;
-  fp = fma(T(0.25) * u, u, s);
-  fm = fma(T(0.25) * u, u, -s);
+  // h = u/2: h·h = u²/4 exactly as (u/4)·u, |h|·u = (|u|/2)·u — 4 ops instead of 5
+  const T h = T(0.5) * u;
+  const T s = fabs(h) * u;
+  fp = fma(h, h, s);
+  fm = fma(h, h, -s);
 }
 
 // Division without the IEEE div_scale/div_fmas/div_fixup sequence: hardware reciprocal
@@ -293,6 +295,40 @@ __device__ __forceinline__ T weno5_face_k(const T* p, const T* m, const T* kp, c
 }
 
 // ---------------------------------------------------------------------------------
+// Non-inline fp64 constants of the WENO5 / FD4 helpers.  gfx9 VOP3 (v_fma_f64) cannot
+// encode a literal, so fma(3.0, x, y) becomes the 2-address v_fmac_f64_e32 with the
+// literal — plus a v_mov_b64 whenever the accumulator is still live.  W5Lit (default)
+// keeps the literals; W5Sgpr holds the same values in SGPRs (laundered once per kernel),
+// which VOP3 takes as an operand, so no copy is needed.  The values are identical, so
+// both give bit-identical results.
+// ---------------------------------------------------------------------------------
+template <typename T>
+struct W5Lit {
+  static constexpr T k3 = T(3), k5 = T(5), k6 = T(6), k1_5 = T(1.5), k13_3 = T(13.0 / 3.0),
+                     k4em6 = T(4e-6), k16 = T(16), km30 = T(-30);
+};
+template <typename T>
+__device__ __forceinline__ T sgpr_const(T v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+template <typename T>
+struct W5Sgpr {
+  T k3, k5, k6, k1_5, k13_3, k4em6, k16, km30;
+  __device__ __forceinline__ W5Sgpr()
+      : k3(sgpr_const(T(3))), k5(sgpr_const(T(5))), k6(sgpr_const(T(6))),
+        k1_5(sgpr_const(T(1.5))), k13_3(sgpr_const(T(13.0 / 3.0))),
+        k4em6(sgpr_const(T(4e-6))), k16(sgpr_const(T(16))), km30(sgpr_const(T(-30))) {}
+};
+
+// FD<4>::d2 with the constants from K (bit-identical)
+template <typename T, class K>
+__device__ __forceinline__ T fd4_d2k(T m2, T m1, T c, T p1, T p2, const K& kk) {
+#pragma clang fp contract(off)
+  return fma(kk.km30, c, fma(kk.k16, m1 + p1, -(m2 + p2)));
+}
+
+// ---------------------------------------------------------------------------------
 // WENO5 with SCALED smoothness indicators (the 3-D stage kernel's reconstruction).
 // Every indicator is carried as e_k = 4 (beta_k + eps) = t_k² + C_k, where t_k is the
 // first-derivative term (v0 - 4v1 + 3v2 etc.) and C_k = 13/3 c_k² + 4 eps folds the
@@ -303,27 +339,27 @@ __device__ __forceinline__ T weno5_face_k(const T* p, const T* m, const T* kp, c
 // side this is 32 fp64 ops (Z) instead of 40, with the same results to rounding
 // (tests/test_kernels_gpu.py compares against the textbook fp64 form).
 // ---------------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ T w5_curv(T a, T b, T c) {
+template <typename T, class K = W5Lit<T>>
+__device__ __forceinline__ T w5_curv(T a, T b, T c, const K& kk = K{}) {
 #pragma clang fp contract(off)
   const T t = fma(T(-2), b, a + c);
-  return fma(T(13.0 / 3.0) * t, t, T(4e-6));
+  return fma(kk.k13_3 * t, t, kk.k4em6);
 }
 
 // One side: numerator num = Σ w_k q_k (q_k = 6 x candidate) and S = Σ w_k, so the side's
 // value is num / (6 S).  C0..C2 = w5_curv centred on v1, v2, v3.
-template <typename T, bool ZVARIANT>
+template <typename T, bool ZVARIANT, class K = W5Lit<T>>
 __device__ __forceinline__ void w5_side(T v0, T v1, T v2, T v3, T v4, T C0, T C1, T C2,
-                                        T& num, T& S) {
+                                        T& num, T& S, const K& kk = K{}) {
 #pragma clang fp contract(off)
-  const T t0 = fma(T(3), v2, fma(T(-4), v1, v0));
+  const T t0 = fma(kk.k3, v2, fma(T(-4), v1, v0));
   const T t1 = v1 - v3;
-  const T t2 = fma(T(3), v2, fma(T(-4), v3, v4));
+  const T t2 = fma(kk.k3, v2, fma(T(-4), v3, v4));
   const T e0 = fma(t0, t0, C0), e1 = fma(t1, t1, C1), e2 = fma(t2, t2, C2);
   // 2 v0 - 7 v1 + 11 v2 = 2 t0 + v1 + 5 v2: one op fewer than the direct form
-  const T q0 = fma(T(2), t0, fma(T(5), v2, v1));
-  const T q1 = fma(T(5), v2, fma(T(2), v3, -v1));
-  const T q2 = fma(T(5), v3, fma(T(2), v2, -v4));
+  const T q0 = fma(T(2), t0, fma(kk.k5, v2, v1));
+  const T q1 = fma(kk.k5, v2, fma(T(2), v3, -v1));
+  const T q2 = fma(kk.k5, v3, fma(T(2), v2, -v4));
   T w0, w1, w2;
   if constexpr (ZVARIANT) {
     // (e_k + tau) * prod_{j!=k} e_j = P + tau * prod_{j!=k} e_j with P = e0 e1 e2:
@@ -331,13 +367,13 @@ __device__ __forceinline__ void w5_side(T v0, T v1, T v2, T v3, T v4, T C0, T C1
     const T tau = fabs(e0 - e2);
     const T e12 = e1 * e2, e02 = e0 * e2, e01 = e0 * e1, P = e0 * e12;
     w0 = fma(tau, e12, P);
-    w1 = T(6) * fma(tau, e02, P);
-    w2 = T(3) * fma(tau, e01, P);
+    w1 = kk.k6 * fma(tau, e02, P);
+    w2 = kk.k3 * fma(tau, e01, P);
   } else {
     const T s0 = e0 * e0, s1 = e1 * e1, s2 = e2 * e2;
     w0 = s1 * s2;
-    w1 = T(6) * (s0 * s2);
-    w2 = T(3) * (s0 * s1);
+    w1 = kk.k6 * (s0 * s2);
+    w2 = kk.k3 * (s0 * s1);
   }
   num = fma(w0, q0, fma(w1, q1, w2 * q2));
   S = (w0 + w1) + w2;
@@ -374,6 +410,57 @@ __device__ __forceinline__ T w5_face_k(const T* p, const T* m, const T* kp, cons
   w5_side<T, ZVARIANT>(p[0], p[1], p[2], p[3], p[4], kp[0], kp[1], kp[2], n1, S1);
   w5_side<T, ZVARIANT>(m[4], m[3], m[2], m[1], m[0], km[2], km[1], km[0], n2, S2);
   return w5_combine(n1, S1, n2, S2);
+}
+
+// ---------------------------------------------------------------------------------
+// One side of an x/y face of the v9 3-D stage, curvatures included, around the
+// differences a = v2 - v1, b = v2 - v3 and the raw curvatures c_k (centred on v1, v2,
+// v3):   t0 = c0 + 2a,  t2 = c2 + 2b,  t1 = b - a,  c1 = -(a + b);
+//        Σ w_k q_k = S q1 + w0 (q0 - q1) + w2 (q2 - q1)   with
+//        q0 - q1 = 2 (c0 - c1),  q2 - q1 = c1 - c2,  q1 / 2 = 3 v2 - b + a / 2,
+// and (w0, w1, w2) = (g0, 6 g1, 3 g2) folded into S = g0 + 6 g1 + 3 g2.  The numerator
+// is returned HALVED (numh = Σ w_k q_k / 2), so w5_combine6 of two such sides is 3 x
+// the face flux.  37 fp64 ops per side (w5_side + its three w5_curv: 41).
+// ---------------------------------------------------------------------------------
+template <typename T, bool ZVARIANT, class K = W5Lit<T>>
+__device__ __forceinline__ void w5_side_h(T v0, T v1, T v2, T v3, T v4, T& numh, T& S,
+                                          const K& kk = K{}) {
+#pragma clang fp contract(off)
+  const T a = v2 - v1, b = v2 - v3;
+  const T c0 = fma(T(-2), v1, v0 + v2);
+  const T c2 = fma(T(-2), v3, v2 + v4);
+  const T c1n = a + b;  // = -c1
+  const T t0 = fma(T(2), a, c0), t1 = b - a, t2 = fma(T(2), b, c2);
+  const T e0 = fma(t0, t0, fma(kk.k13_3 * c0, c0, kk.k4em6));
+  const T e1 = fma(t1, t1, fma(kk.k13_3 * c1n, c1n, kk.k4em6));
+  const T e2 = fma(t2, t2, fma(kk.k13_3 * c2, c2, kk.k4em6));
+  const T q1h = fma(T(0.5), a, fma(kk.k3, v2, -b));
+  const T d01 = c0 + c1n;     // c0 - c1
+  const T d21n = c1n + c2;    // -(c1 - c2)
+  T g0, g1, g2;
+  if constexpr (ZVARIANT) {
+    const T tau = fabs(e0 - e2);
+    const T e12 = e1 * e2, P = e0 * e12;
+    g0 = fma(tau, e12, P);
+    g1 = fma(tau, e0 * e2, P);
+    g2 = fma(tau, e0 * e1, P);
+  } else {
+    const T s0 = e0 * e0, s1 = e1 * e1, s2 = e2 * e2;
+    g0 = s1 * s2;
+    g1 = s0 * s2;
+    g2 = s0 * s1;
+  }
+  S = fma(kk.k6, g1, fma(kk.k3, g2, g0));
+  numh = fma(S, q1h, fma(g0, d01, -((kk.k1_5 * g2) * d21n)));
+}
+
+// Both sides of x/y face i+½ from p = f⁺(i-2..i+2), m = f⁻(i-1..i+3); w5_combine6 of
+// them is 3 x the face flux.
+template <typename T, bool ZVARIANT, class K = W5Lit<T>>
+__device__ __forceinline__ void w5_face3_sides(const T* p, const T* m, T& n1, T& S1, T& n2,
+                                               T& S2, const K& kk = K{}) {
+  w5_side_h<T, ZVARIANT>(p[0], p[1], p[2], p[3], p[4], n1, S1, kk);
+  w5_side_h<T, ZVARIANT>(m[4], m[3], m[2], m[1], m[0], n2, S2, kk);
 }
 
 // Left-biased WENO7 (Jiang–Shu weights) at the right face of v3 from v0..v6 (= f at

@@ -10,8 +10,16 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--csv", default=None)
     ap.add_argument("--top", type=int, default=20)
+    ap.add_argument("--instances", default=None,
+                    help="substring of a kernel name: print that kernel's per-launch times "
+                         "in launch order (µs) instead of the summary")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
+    if a.instances:
+        rows = c.execute("select duration/1000.0 from kernels where name like ? order by start",
+                         (f"%{a.instances}%",)).fetchall()
+        print(" ".join(f"{r[0]:.1f}" for r in rows))
+        return
     rows = c.execute("select name, count(*), avg(duration)/1000.0, sum(duration)/1e6, "
                      "min(duration)/1000.0, max(duration)/1000.0, max(vgpr_count), "
                      "max(lds_size), grid_x, grid_y, grid_z, workgroup_x, workgroup_y "

@@ -188,7 +188,7 @@ def test_debug_print_kernel(capfd):
 
 
 @pytest.mark.parametrize("ver,ty", [(1, 8), (1, 16), (2, 8), (2, 16), (3, 8), (3, 16), (4, 8), (5, 4),
-                                    (6, 8), (6, 16), (7, 8), (8, 8)])
+                                    (6, 8), (6, 16), (7, 8), (8, 8), (9, 8)])
 @pytest.mark.parametrize("weno_z", [False, True])
 def test_burgers3d_stage_variants(ver, ty, weno_z):
     """Every selectable 3-D WENO5 kernel variant (v1 generic, v2 two barriers, v3 double
