@@ -217,3 +217,42 @@ def test_burgers3d_stage_variants(ver, ty, weno_z):
         lib.advdiff_set_b3_ty(old_t)
     err = (gout.cpu() - exp).abs().max().item()
     assert err < 1e-11, err
+
+
+@pytest.mark.parametrize("k0,k1", [(3, 4), (3, 5), (7, 18), (3, 58)])
+@pytest.mark.parametrize("mode", ["ssp1", "ssp", "ls"])
+def test_burgers3d_v9_plane_ranges(k0, k1, mode):
+    """The default 3-D WENO5 kernel (v9: 10-plane unroll, clamped unconditional
+    prefetches) on plane ranges of 1, 2, 11 and 55 planes — chunks shorter than, equal to
+    and not a multiple of the unroll — in every stage epilogue, against the fp64
+    reference; cells outside [k0, k1) must be untouched."""
+    nz, ny, nx, sx = 61, 21, 70, 72
+    inp = _smooth3(nz, ny, sx, 7, torch.float64)
+    u0 = _smooth3(nz, ny, sx, 8, torch.float64)
+    aux = _smooth3(nz, ny, sx, 9, torch.float64)
+    rd = (1 / 0.02, 1 / 0.03, 1 / 0.025)
+    vv = tuple(0.01 * r * r for r in rd)
+    a, b = {"ssp1": (0.0, 1.0), "ssp": (0.75, 0.25), "ls": (-0.4, 0.3)}[mode]
+    ls = mode == "ls"
+    exp_out, exp_aux = u0.clone(), aux.clone()
+    if ls:
+        ref.burgers3d_stage(inp, exp_aux, exp_out, nx, ny, k0, k1, 3, True, *rd, *vv, 1e-3, a, b,
+                            ls=True)
+    else:
+        ref.burgers3d_stage(inp, u0, exp_out, nx, ny, k0, k1, 3, True, *rd, *vv, 1e-3, a, b)
+    lib = _lib.require()
+    old = lib.advdiff_set_b3_ver(9)
+    try:
+        gout, gaux = u0.to(DEV), aux.to(DEV)
+        kw = dict(nx=nx, ny=ny, k0=k0, k1=k1, border=3, weno_z=True, rdx=rd[0], rdy=rd[1],
+                  rdz=rd[2], vx=vv[0], vy=vv[1], vz=vv[2], dt=1e-3, a=a, b=b)
+        if ls:
+            stencil.burgers3d_stage(inp.to(DEV), gaux, gout, ls=True, **kw)
+        else:
+            stencil.burgers3d_stage(inp.to(DEV), gout.clone(), gout, **kw)
+        torch.cuda.synchronize()
+    finally:
+        lib.advdiff_set_b3_ver(old)
+    assert (gout.cpu() - exp_out).abs().max().item() < 1e-11
+    if ls:
+        assert (gaux.cpu() - exp_aux).abs().max().item() < 1e-11
