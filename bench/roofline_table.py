@@ -13,7 +13,7 @@ KEYS = {"copy_box": "copy_box_kernel", "stage1": "diffusion3d_stage_kernel<doubl
         "stage2": "diffusion3d_stage_kernel<double, 4, 64, 16, 1>",
         "fused_fd4": "diffusion3d_step_cring_kernel<double, 4,",
         "fused_fd2": "diffusion3d_step_cring_kernel<double, 2,",
-        "weno5_stage": "burgers3d_w5r_kernel<double, true, true, 1,"}
+        "weno5_stage": "burgers3d_w5s_kernel<double, true, true, 1"}
 meta = json.loads([l for l in open(f"{root}/trace.log") if l.startswith("{")][-1])
 
 
