@@ -19,6 +19,12 @@ Self-validation (outside the timed region): after the timed steps the heat solut
 compared with the exact decaying sine mode exp(-3 pi^2 K t) sin sin sin (L_inf, relative to
 the initial amplitude) and the run fails if it exceeds linf_bound().  The 7-point (FD2)
 Laplacian named by BASELINE.json is measured on the same grid and reported as `fd2_7pt`.
+
+`sustained` (informational, AFTER the K timed steps; the headline `value` is the K-step
+number): --sustained-steps more steps of the same solver, timed the same way.  The fp64
+stencil load runs the chip at its power limit and the clock controller dips for a few ms
+after a load starts, so a 20-step window (15 ms) mostly sees that dip; 200 steps show the
+settled rate (profiles/launch_times_r2s5.txt has the per-launch times).
 """
 from __future__ import annotations
 
@@ -65,6 +71,16 @@ def timed(solver: Solver, steps: int, warmup: int, dt: float) -> float:
         solver.run(iters=warmup, dt=dt)
     st = solver.run(iters=steps, dt=dt)  # barrier + sync on both sides, max over ranks
     return st.compute_s
+
+
+def sustained(solver: Solver, steps: int, dt: float, cells: int) -> dict | None:
+    """Informational settled-clock rate: `steps` more steps right after the headline
+    window, timed the same way (barrier + sync both sides, max over ranks)."""
+    if steps <= 0:
+        return None
+    st = solver.run(iters=steps, dt=dt)
+    return {"steps": steps, "value": round(cells * steps / st.compute_s / 1e6, 1),
+            "ms_per_step": round(st.compute_s / steps * 1e3, 4)}
 
 
 def _free(dev):
@@ -153,6 +169,9 @@ def main():
                     help="weak: base^3 cells per GPU (default); strong: the 8-GPU grid "
                          "(2*base)^3 on any N")
     ap.add_argument("--device", default=None)
+    ap.add_argument("--sustained-steps", type=int, default=200,
+                    help="extra steps timed after the headline window (informational "
+                         "'sustained' fields; 0 = off)")
     args = ap.parse_args()
 
     comm = Comm.from_env(device=args.device)
@@ -183,6 +202,7 @@ def main():
     solver = make_heat(decomp)
     secs = timed(solver, args.steps, args.warmup, dt)
     mlups = grid.cells * args.steps / secs / 1e6
+    sust = sustained(solver, args.sustained_steps, dt, grid.cells)
     # self-validation against the exact solution (outside the timed region)
     finite = solver.check_finite()
     _, _, linf = solver.error_norms()
@@ -216,6 +236,7 @@ def main():
                                    f"cartesian {'x'.join(map(str, pg))} (z,y,x; {link} halo)"),
                    "cells_per_gpu": grid.cells // n},
         "max_abs_u": finite,
+        **({"sustained": sust} if sust else {}),
         "linf_vs_exact": float(f"{linf:.3e}"),
         "linf_bound": float(f"{bound:.3e}"),
         "t_end": t_end,
@@ -267,13 +288,15 @@ def main():
         bsteps = args.burgers_steps or args.steps
         bsecs = timed(bsolver, bsteps, args.warmup, bmodel.stable_dt())
         bml = bgrid.cells * bsteps / bsecs / 1e6
+        bsust = sustained(bsolver, args.sustained_steps, bmodel.stable_dt(), bgrid.cells)
         bsolver.check_finite()
         result["burgers3d"] = {"value": round(bml, 1), "unit": "MLUPS", "grid": list(bshape),
                                "steps": bsteps, "ms_per_step": round(bsecs / bsteps * 1e3, 4),
                                "vs_baseline": round(bml / BASE_BURGERS, 2),
                                "model": "burgers3d WENO5-Z + FD4 viscous (C=1e-5) + SSP-RK3",
                                "pgrid": list(bsolver.pgrid),
-                               "decomp_trials_ms_per_step": btrials}
+                               "decomp_trials_ms_per_step": btrials,
+                               **({"sustained": bsust} if bsust else {})}
         del bsolver
 
     if comm.rank == 0:
