@@ -114,6 +114,13 @@ int advdiff_burgers3d_stage_dt(int dtype, const void* in, void* aux, void* out, 
                                double rdx, double rdy, double rdz, double vx, double vy,
                                double vz, double dt, double a, double b, int ls,
                                const double* dt_dev, void* stream);
+// The 3-D stage on two plane ranges [k0, k1) and [k0b, k1b) (either may be empty): one
+// launch with the default WENO5 kernel (a slab rank's two boundary slabs), else two.
+int advdiff_burgers3d_stage2_dt(int dtype, const void* in, void* aux, void* out, int nx, int ny,
+                                int64_t sy, int64_t sz, int k0, int k1, int k0b, int k1b,
+                                int border, int weno, double rdx, double rdy, double rdz,
+                                double vx, double vy, double vz, double dt, double a, double b,
+                                int ls, const double* dt_dev, void* stream);
 int advdiff_burgers2d_stage_dt(int dtype, const void* in, void* aux, void* out, int nx,
                                int64_t sy, int j0, int j1, int border, int weno, double rdx,
                                double rdy, double vx, double vy, double dt, double a, double b,

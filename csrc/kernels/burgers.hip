@@ -623,8 +623,8 @@ __global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(4))) vo
 template <typename T, bool WZ, bool VISC, int MODE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void burgers3d_w5s_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
-    int k1, int zchunk, int border, T rdx3, T rdy3, T rdz6, T vx, T vy, T vz, T dt, T a, T b,
-    const double* __restrict__ dtp) {
+    int k1, int k0b, int k1b, int gza, int zchunk, int border, T rdx3, T rdy3, T rdz6, T vx,
+    T vy, T vz, T dt, T a, T b, const double* __restrict__ dtp) {
   constexpr int TY = 8, R = 3, NR = 5, TX = 64, TXO = TX - 1;
   constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NT = TX * TY, LT = LX * LY;
   constexpr int NPT = (LT + NT - 1) / NT;
@@ -644,8 +644,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
   const int ib = border - 1 + (int)blockIdx.x * TXO;  // x of lane 0 (supplies a face only)
   const int jb = border + (int)blockIdx.y * TY;       // y of wave 0
   const int i = ib + tx, j = jb + w;
-  const int kc0 = k0 + (int)blockIdx.z * zchunk;
-  const int kc1 = min(kc0 + zchunk, k1);
+  // z chunks of the first plane range [k0, k1), then (blockIdx.z >= gza) of the second
+  // [k0b, k1b): both boundary slabs of a rank in ONE launch
+  const bool second = (int)blockIdx.z >= gza;
+  const int kc0 = second ? k0b + ((int)blockIdx.z - gza) * zchunk : k0 + (int)blockIdx.z * zchunk;
+  const int kc1 = min(kc0 + zchunk, second ? k1b : k1);
   const int klast = kc1 - 1;
   const bool active = tx >= 1 && i < nx - border && j < ny - border;
   const uint32_t goff = (uint32_t)(min(j, ny - 1) * (int)sy + min(i, nx - 1)) * (uint32_t)E;
@@ -939,6 +942,7 @@ struct BArgs {
   double rdx, rdy, rdz, vx, vy, vz, dt, a, b;
   hipStream_t st;
   const double* dtp;  // device dt (adaptive CFL) or nullptr: use dt
+  int lo2 = 0, hi2 = 0;  // optional second marched-axis range (3-D: v9 in the same launch)
 };
 
 template <typename T, int W, bool WZ, bool VISC, int MODE, int TY>
@@ -988,13 +992,16 @@ template <typename T, bool WZ, bool VISC, int MODE>
 static hipError_t launch_b3_v9(const BArgs& p) {
   const int gx = div_up(std::max(p.nx - 2 * p.border, 1), 63);
   const int gy = div_up(std::max(p.ny - 2 * p.border, 1), 8);
-  const int zc = pick_chunk(p.hi - p.lo, (long long)gx * gy, 8, 256);
-  const int gz = div_up(p.hi - p.lo, zc);
+  const int na = std::max(p.hi - p.lo, 0), nb = std::max(p.hi2 - p.lo2, 0);
+  const int zc = pick_chunk(na + nb, (long long)gx * gy, 8, 256);
+  const int gza = div_up(na, zc);
+  const int gz = gza + div_up(nb, zc);
   const double s = 1.0 / 12.0;
   hipLaunchKernelGGL((burgers3d_w5s_kernel<T, WZ, VISC, MODE>), dim3(gx, gy, gz), dim3(64, 8, 1),
                      0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx, p.ny, p.sy, p.sz,
-                     p.lo, p.hi, zc, p.border, T(p.rdx / 3.0), T(p.rdy / 3.0), T(p.rdz / 6.0),
-                     T(p.vx * s), T(p.vy * s), T(p.vz * s), T(p.dt), T(p.a), T(p.b), p.dtp);
+                     p.lo, p.hi, p.lo2, p.hi2, gza, zc, p.border, T(p.rdx / 3.0),
+                     T(p.rdy / 3.0), T(p.rdz / 6.0), T(p.vx * s), T(p.vy * s), T(p.vz * s),
+                     T(p.dt), T(p.a), T(p.b), p.dtp);
   return hipGetLastError();
 }
 
@@ -1099,11 +1106,28 @@ static hipError_t dispatch_b(int scheme, bool visc, int mode, const BArgs& p) {
 static int scheme_radius(int scheme) { return scheme == 2 ? 4 : 3; }
 
 static hipError_t run_b(int dtype, bool three_d, int scheme, bool ls, const BArgs& p) {
-  if (p.hi <= p.lo) return hipSuccess;
+  const bool two = p.hi2 > p.lo2;
+  if (p.hi <= p.lo) {
+    if (!two) return hipSuccess;
+    BArgs q = p;  // only the second range: it becomes the first
+    q.lo = p.lo2, q.hi = p.hi2, q.lo2 = q.hi2 = 0;
+    return run_b(dtype, three_d, scheme, ls, q);
+  }
   const int R = scheme_radius(scheme);
   if (scheme < 0 || scheme > 2 || p.lo < R || p.nx <= 0 || (three_d && p.ny <= 0) ||
-      p.border < R || p.in == p.out || (ls && (p.in == p.aux || p.out == p.aux)))
+      p.border < R || p.in == p.out || (ls && (p.in == p.aux || p.out == p.aux)) ||
+      (two && p.lo2 < R))
     return hipErrorInvalidValue;
+  // two plane ranges in one launch: the 3-D WENO5 v9 kernel; everything else launches
+  // the ranges one after the other
+  if (two && !(three_d && scheme != 2 && b3_ver() == 9 &&
+               (dtype == ADVDIFF_F64 ? v6_fits<double>(p) : v6_fits<float>(p)))) {
+    BArgs p1 = p, p2 = p;
+    p1.lo2 = p1.hi2 = 0;
+    p2.lo = p.lo2, p2.hi = p.hi2, p2.lo2 = p2.hi2 = 0;
+    const hipError_t e = run_b(dtype, three_d, scheme, ls, p1);
+    return e != hipSuccess ? e : run_b(dtype, three_d, scheme, ls, p2);
+  }
   const bool visc = p.vx != 0.0 || p.vy != 0.0 || (three_d && p.vz != 0.0);
   const int mode = ls ? (p.a != 0.0 ? kLs : kLs1) : (p.a != 0.0 ? kSsp : kSsp1);
   if (dtype == ADVDIFF_F64)
@@ -1142,6 +1166,23 @@ extern "C" int advdiff_burgers3d_stage_dt(int dtype, const void* in, void* aux, 
   using namespace advdiff;
   const BArgs p{in, aux, out, nx, ny, sy, sz, k0, k1, border, rdx, rdy, rdz,
                 vx, vy, vz, dt, a, b, (hipStream_t)stream, dt_dev};
+  return run_b(dtype, true, weno, ls != 0, p);
+}
+
+// The same stage on two marched-axis ranges [k0, k1) and [k0b, k1b) (a slab rank's two
+// boundary slabs after the halo wait): one launch with the default 3-D WENO5 kernel (v9),
+// two launches otherwise.  Either range may be empty.
+extern "C" int advdiff_burgers3d_stage2_dt(int dtype, const void* in, void* aux, void* out,
+                                           int nx, int ny, int64_t sy, int64_t sz, int k0,
+                                           int k1, int k0b, int k1b, int border, int weno,
+                                           double rdx, double rdy, double rdz, double vx,
+                                           double vy, double vz, double dt, double a, double b,
+                                           int ls, const double* dt_dev, void* stream) {
+  using namespace advdiff;
+  BArgs p{in, aux, out, nx, ny, sy, sz, k0, k1, border, rdx, rdy, rdz,
+          vx, vy, vz, dt, a, b, (hipStream_t)stream, dt_dev};
+  p.lo2 = k0b;
+  p.hi2 = k1b;
   return run_b(dtype, true, weno, ls != 0, p);
 }
 

@@ -283,8 +283,16 @@ void Engine::stage(void* in, void* aux, void* out, double a, double b, double dt
   if (p_.overlap) {
     launch(in, aux, out, interior_, dt, a, b, ls);
     if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
-    launch(in, aux, out, blo_, dt, a, b, ls);
-    launch(in, aux, out, bhi_, dt, a, b, ls);
+    if (p_.physics == Physics::Burgers && p_.dims == 3) {  // both boundary slabs, one launch
+      const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
+      KERNEL_CHECK(advdiff_burgers3d_stage2_dt(
+          p_.dtype, in, aux, out, p_.nx, p_.ny, sy_, sz_, blo_.lo, blo_.hi, bhi_.lo, bhi_.hi,
+          p_.border(), p_.weno, 1.0 / dx, 1.0 / dy, 1.0 / dz, p_.C / (dx * dx),
+          p_.C / (dy * dy), p_.C / (dz * dz), dt, a, b, ls ? 1 : 0, nullptr, compute_));
+    } else {
+      launch(in, aux, out, blo_, dt, a, b, ls);
+      launch(in, aux, out, bhi_, dt, a, b, ls);
+    }
   } else {
     if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
     launch(in, aux, out, full_, dt, a, b, ls);

@@ -72,8 +72,12 @@ class Burgers(Model):
         dv = 0.9 / (2.0 * sum(self.visc)) if self.C > 0 else 0.0
         return self.cfl * min(self.grid.spacing), dv
 
+    # stage() takes a second plane range (lo2, hi2): the 3-D kernel serves both boundary
+    # slabs of a slab rank in one launch
+    two_range_stage = True
+
     def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None, nx=None, ny=None,
-              border=None, ls=False, dt_dev=None):
+              border=None, ls=False, dt_dev=None, lo2=0, hi2=0):
         g = self.grid
         nx = g.nx if nx is None else nx
         ny = g.ny if ny is None else ny
@@ -84,12 +88,14 @@ class Burgers(Model):
                                     border=border, weno_z=z, rdx=self.rd[0],
                                     rdy=self.rd[1], rdz=self.rd[2], vx=self.visc[0],
                                     vy=self.visc[1], vz=self.visc[2], dt=dt, a=a, b=b,
-                                    stream=stream, ls=ls, dt_dev=dt_dev)
+                                    stream=stream, ls=ls, dt_dev=dt_dev, k0b=lo2, k1b=hi2)
         else:
-            stencil.burgers2d_stage(inp, u0, out, nx=nx, j0=lo, j1=hi, border=border,
-                                    weno_z=z, rdx=self.rd[0], rdy=self.rd[1], vx=self.visc[0],
-                                    vy=self.visc[1], dt=dt, a=a, b=b, stream=stream, ls=ls,
-                                    dt_dev=dt_dev)
+            for j0, j1 in ((lo, hi), (lo2, hi2)):
+                if j1 > j0:
+                    stencil.burgers2d_stage(inp, u0, out, nx=nx, j0=j0, j1=j1, border=border,
+                                            weno_z=z, rdx=self.rd[0], rdy=self.rd[1],
+                                            vx=self.visc[0], vy=self.visc[1], dt=dt, a=a, b=b,
+                                            stream=stream, ls=ls, dt_dev=dt_dev)
 
     def describe(self):
         d = super().describe()

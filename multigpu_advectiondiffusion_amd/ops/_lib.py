@@ -58,6 +58,10 @@ _SIGS = {
     "advdiff_burgers3d_stage_dt": [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_i64, c_i64, c_int,
                                    c_int, c_int, c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl,
                                    c_dbl, c_dbl, c_dbl, c_dbl, c_int, c_vp, c_vp],
+    "advdiff_burgers3d_stage2_dt": [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_i64, c_i64, c_int,
+                                    c_int, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_dbl,
+                                    c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_int, c_vp,
+                                    c_vp],
     "advdiff_burgers2d_stage_dt": [c_int, c_vp, c_vp, c_vp, c_int, c_i64, c_int, c_int, c_int,
                                    c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_int,
                                    c_vp, c_vp],

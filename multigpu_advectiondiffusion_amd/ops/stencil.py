@@ -179,32 +179,37 @@ def _dt_of(dt, dt_dev):
 
 
 def burgers3d_stage(inp, u0, out, *, nx, ny, k0, k1, border, weno_z, rdx, rdy, rdz,
-                    vx=0.0, vy=0.0, vz=0.0, dt, a, b, stream=None, ls=False, dt_dev=None):
+                    vx=0.0, vy=0.0, vz=0.0, dt, a, b, stream=None, ls=False, dt_dev=None,
+                    k0b=0, k1b=0):
     """weno_z: scheme — bool (WENO5 Z / JS) or "js" | "z" | "js7" (WENO7).
     dt_dev: float64 device scalar holding dt (adaptive CFL: written on the device by
-    adaptive_dt, read by the kernel — no host sync); 0 there makes the stage out = in."""
+    adaptive_dt, read by the kernel — no host sync); 0 there makes the stage out = in.
+    [k0b, k1b): an optional second plane range (a slab rank's other boundary slab),
+    served by the same launch (advdiff_burgers3d_stage2_dt)."""
     _check_layout(inp, u0, out)
     code_s, R = ref.scheme_code(weno_z), ref.scheme_radius(weno_z)
     if border < R:
         raise ValueError(f"WENO needs a frozen border of at least {R} cells")
+    ranges = [(lo, hi) for lo, hi in ((k0, k1), (k0b, k1b)) if hi > lo]
     if _native(inp):
         lib = _lib.require()
-        assert k0 >= R and k1 + R <= inp.shape[0], "stencil planes out of bounds"
-        code = lib.advdiff_burgers3d_stage_dt(
+        for lo, hi in ranges:
+            assert lo >= R and hi + R <= inp.shape[0], "stencil planes out of bounds"
+        code = lib.advdiff_burgers3d_stage2_dt(
             _dtype_code(inp), _ptr(inp), _aux_ptr(u0, a, ls), _ptr(out), nx, ny,
-            inp.stride(1), inp.stride(0), k0, k1, border, code_s, rdx, rdy, rdz, vx, vy, vz,
-            dt, a, b, 1 if ls else 0, None if dt_dev is None else dt_dev.data_ptr(),
+            inp.stride(1), inp.stride(0), k0, k1, k0b, k1b, border, code_s, rdx, rdy, rdz, vx,
+            vy, vz, dt, a, b, 1 if ls else 0, None if dt_dev is None else dt_dev.data_ptr(),
             _stream_ptr(stream))
         _lib.check(code, "burgers3d_stage")
     else:
         dt, noop = _dt_of(dt, dt_dev)
-        if noop:
-            if k1 > k0:
-                sl = (slice(k0, k1), slice(border, ny - border), slice(border, nx - border))
+        for lo, hi in ranges:
+            if noop:
+                sl = (slice(lo, hi), slice(border, ny - border), slice(border, nx - border))
                 out[sl] = inp[sl]
-            return
-        ref.burgers3d_stage(inp, u0, out, nx, ny, k0, k1, border, code_s, rdx, rdy, rdz,
-                            vx, vy, vz, dt, a, b, ls)
+            else:
+                ref.burgers3d_stage(inp, u0, out, nx, ny, lo, hi, border, code_s, rdx, rdy,
+                                    rdz, vx, vy, vz, dt, a, b, ls)
 
 
 def burgers2d_stage(inp, u0, out, *, nx, j0, j1, border, weno_z, rdx, rdy, vx=0.0, vy=0.0,

@@ -227,15 +227,17 @@ class Solver:
     # ------------------------------------------------------------------------------
     # stepping
     # ------------------------------------------------------------------------------
-    def _launch(self, inp, u0, out, rng, dt, a, b, ls=False):
+    def _launch(self, inp, u0, out, rng, dt, a, b, ls=False, rng2=(0, 0)):
         if self.cart:
             self._launch_box(inp, u0, out, rng, dt, a, b, ls)
             return
-        lo, hi = rng
-        if hi > lo:
+        (lo, hi), (lo2, hi2) = rng, rng2
+        if hi > lo or hi2 > lo2:
             kw = {} if self._dt_dev is None else {"dt_dev": self._dt_dev}
+            if hi2 > lo2:
+                kw.update(lo2=lo2, hi2=hi2)
             self.model.stage(inp, u0, out, lo, hi, dt, a, b, ls=ls, **kw)
-            trace.sync_check(f"{self.model.name} stage [{lo},{hi})", self.device)
+            trace.sync_check(f"{self.model.name} stage [{lo},{hi}) [{lo2},{hi2})", self.device)
 
     def _launch_box(self, inp, u0, out, box, dt, a, b, ls=False):
         """Stage on a local box (array order).  The kernels update [border, n-border) of
@@ -271,8 +273,12 @@ class Solver:
                 if pend is not None:
                     pend.wait()
             with trace.range_("boundary"):
-                for rng in self.boundary:
-                    self._launch(inp, u0, out, rng, dt, a, b, ls)
+                if not self.cart and getattr(self.model, "two_range_stage", False):
+                    # both boundary slabs in ONE launch
+                    self._launch(inp, u0, out, self.boundary[0], dt, a, b, ls, self.boundary[1])
+                else:
+                    for rng in self.boundary:
+                        self._launch(inp, u0, out, rng, dt, a, b, ls)
         else:
             if pend is not None:
                 pend.wait()
