@@ -256,3 +256,32 @@ def test_burgers3d_v9_plane_ranges(k0, k1, mode):
     assert (gout.cpu() - exp_out).abs().max().item() < 1e-11
     if ls:
         assert (gaux.cpu() - exp_aux).abs().max().item() < 1e-11
+
+
+@pytest.mark.parametrize("ver", [9, 6])
+@pytest.mark.parametrize("r1,r2", [((3, 6), (40, 43)), ((3, 20), (21, 58)), ((0, 0), (9, 12)),
+                                   ((5, 9), (0, 0))])
+def test_burgers3d_two_range_launch(ver, r1, r2):
+    """advdiff_burgers3d_stage2_dt (a slab rank's two boundary slabs): one launch with v9,
+    two launches with the other kernels — bitwise equal to two single-range launches."""
+    nz, ny, nx, sx = 61, 21, 70, 72
+    inp = _smooth3(nz, ny, sx, 11, torch.float64).to(DEV)
+    u0 = _smooth3(nz, ny, sx, 12, torch.float64).to(DEV)
+    rd = (1 / 0.02, 1 / 0.03, 1 / 0.025)
+    vv = tuple(0.01 * r * r for r in rd)
+    kw = dict(nx=nx, ny=ny, border=3, weno_z=True, rdx=rd[0], rdy=rd[1], rdz=rd[2], vx=vv[0],
+              vy=vv[1], vz=vv[2], dt=1e-3, a=0.75, b=0.25)
+    lib = _lib.require()
+    old = lib.advdiff_set_b3_ver(ver)
+    try:
+        one = u0.clone()
+        stencil.burgers3d_stage(inp, u0, one, k0=r1[0], k1=r1[1], k0b=r2[0], k1b=r2[1], **kw)
+        two = u0.clone()
+        for lo, hi in (r1, r2):
+            if hi > lo:
+                stencil.burgers3d_stage(inp, u0, two, k0=lo, k1=hi, **kw)
+        torch.cuda.synchronize()
+    finally:
+        lib.advdiff_set_b3_ver(old)
+    assert torch.equal(one, two)
+    assert not torch.equal(one, u0)
