@@ -62,6 +62,9 @@ class Comm:
         """
         if timeout_s is None:  # collective timeout (a dead peer surfaces as an error)
             timeout_s = float(os.environ.get("ADVDIFF_COMM_TIMEOUT", "600"))
+        # ADVDIFF_BACKEND=gloo: host-staged device halos (rehearsing multi-rank runs with
+        # several ranks on one GPU together with ADVDIFF_SHARE_GPU=1; RCCL refuses that)
+        backend = backend or os.environ.get("ADVDIFF_BACKEND") or None
         size = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
