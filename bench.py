@@ -135,7 +135,7 @@ def tune_decomp(make, cands, dt, dev, trial_steps=3, rounds=3):
     return best[1], trials
 
 
-def halo_diag(s, reps=5):
+def halo_diag(s, reps=5, dt=None):
     """Exchange-only timing of the timed configuration (N > 1): ms per full exchange
     (all phases, stream-ordered, max over ranks) and the implied rate of the busiest
     link — the xGMI bandwidth this run actually saw."""
@@ -155,8 +155,21 @@ def halo_diag(s, reps=5):
     ms = s.comm.allreduce_max((_t.perf_counter() - t0) / reps * 1e3)
     link = halo_link_bytes(s.cd.shape, s.pgrid, s.ghost, s.u.element_size(),
                            corners=s.cart and s.fused)
+    # the same steps with the exchange switched off (ghosts go stale — run LAST, after
+    # the validation): the compute-only step time; the timed ms/step minus this is the
+    # part of the exchange the overlap did not hide
+    dt = s.model.stable_dt() if dt is None else dt
+    s.sync_halos()
+    start = s.halo.start
+    s.halo.start = lambda *a, **k: None
+    try:
+        s.run(iters=2, dt=dt)
+        nohalo = s.run(iters=reps, dt=dt).compute_s / reps * 1e3
+    finally:
+        s.halo.start = start
     return {"halo_exchange_ms": round(ms, 4), "halo_link_MB": round(link / 1e6, 2),
-            "halo_link_GBps": round(link / (ms * 1e-3) / 1e9, 1) if ms > 0 else None}
+            "halo_link_GBps": round(link / (ms * 1e-3) / 1e9, 1) if ms > 0 else None,
+            "step_ms_without_exchange": round(nohalo, 4)}
 
 
 def main():
@@ -217,7 +230,7 @@ def main():
     _, _, linf = solver.error_norms()
     pg = solver.pgrid
     t_end = solver.t
-    diag = halo_diag(solver)
+    diag = halo_diag(solver, dt=dt)
     del solver
     _free(dev)
     bound = linf_bound(grid, model.K, t_end, 4)

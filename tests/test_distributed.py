@@ -261,3 +261,4 @@ def test_bench_decomposition_tuning_gloo():
     assert tuple(best) in [tuple(c) for c in cands] and len(cands) == 3
     assert len(trials) == len(cands) and all(isinstance(v, float) for v in trials.values())
     assert diag["halo_exchange_ms"] > 0 and diag["halo_link_MB"] > 0
+    assert diag["step_ms_without_exchange"] > 0
