@@ -215,6 +215,10 @@ const char* advdiff_build_info(void);
 // (csrc/Makefile SRC_HASH); the Python loader refuses a library that does not match the tree
 const char* advdiff_source_hash(void);
 
+// Load the code objects of every kernel file now (the runtime otherwise loads each at its
+// first launch, ~20 ms for the WENO5 file); call once after selecting the device.
+int advdiff_preload(void);
+
 #ifdef __cplusplus
 }
 #endif

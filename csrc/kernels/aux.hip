@@ -353,3 +353,21 @@ extern "C" const char* advdiff_build_info(void) {
   return "libadvdiff gfx950 (CDNA4) HIP kernels: diffusion{2,3}d FD2/FD4 fused SSP-RK3, "
          "burgers{2,3}d WENO5-JS/Z fused SSP-RK3, norms, init, copy_box";
 }
+
+// Load every kernel translation unit's code object now (outside any timed region).  With
+// deferred loading (the HIP default) a code object is loaded at the first launch of one
+// of its kernels — for the WENO5 file (many template instances) ~20-25 ms, which landed
+// inside the first timed step of a run (profiles/native_apps_r2.log).
+extern "C" int advdiff_preload_burgers(void);
+extern "C" int advdiff_preload_diffusion(void);
+extern "C" int advdiff_preload_diffusion_fused(void);
+extern "C" int advdiff_preload_diffusion2d_fused(void);
+extern "C" int advdiff_preload(void) {
+  hipFuncAttributes a;
+  int e = hipFuncGetAttributes(&a, (const void*)advdiff::init_ic_kernel<double>);
+  if (e == hipSuccess) e = advdiff_preload_diffusion();
+  if (e == hipSuccess) e = advdiff_preload_diffusion_fused();
+  if (e == hipSuccess) e = advdiff_preload_diffusion2d_fused();
+  if (e == hipSuccess) e = advdiff_preload_burgers();
+  return e;
+}

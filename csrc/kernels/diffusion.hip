@@ -302,3 +302,10 @@ extern "C" int advdiff_diffusion2d_stage_ls(int dtype, const void* in, void* du,
                 (hipStream_t)stream};
   return run_d(dtype, false, order, true, p);
 }
+
+// Code-object preload (see advdiff_preload in aux.hip).
+extern "C" int advdiff_preload_diffusion(void) {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(
+      &a, (const void*)advdiff::diffusion3d_stage_kernel<double, 4, advdiff::kTX3, advdiff::kTY3, 0>);
+}

@@ -224,3 +224,9 @@ extern "C" int advdiff_diffusion2d_step(int dtype, const void* uin, void* uout, 
   return advdiff_diffusion2d_step_box(dtype, uin, uout, nx, sy, ny_alloc, j0, j1, ylo, yhi, box,
                                       order, cx, cy, dt, stream);
 }
+
+// Code-object preload (see advdiff_preload in aux.hip).
+extern "C" int advdiff_preload_diffusion2d_fused(void) {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, (const void*)advdiff::diffusion2d_step_kernel<double, 4>);
+}

@@ -1022,3 +1022,10 @@ extern "C" int advdiff_diffusion3d_step(int dtype, const void* uin, void* uout, 
   return advdiff_diffusion3d_step2(dtype, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, 0, 0, zlo,
                                    zhi, border, order, cx, cy, cz, dt, stream);
 }
+
+// Code-object preload (see advdiff_preload in aux.hip).
+extern "C" int advdiff_preload_diffusion_fused(void) {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(
+      &a, (const void*)advdiff::diffusion3d_step_cring_kernel<double, 4, 16, 2, 23, false>);
+}

@@ -115,6 +115,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   if (env.size > ndev && tk != "socket")
     throw std::runtime_error("more ranks than GPUs: one process per GPU (or --transport socket)");
   HIP_CHECK(hipSetDevice(env.local_rank % ndev));
+  HIP_CHECK((hipError_t)advdiff_preload());  // code objects loaded before the timed loop
   if (decomp != "slab") parse_pgrid(decomp, dims, env.size, p.pgrid);
   auto tr = make_transport(env, tk);
   Engine eng(p, tr.get(), env);

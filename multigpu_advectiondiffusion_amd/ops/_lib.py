@@ -65,6 +65,7 @@ _SIGS = {
     "advdiff_burgers2d_stage_dt": [c_int, c_vp, c_vp, c_vp, c_int, c_i64, c_int, c_int, c_int,
                                    c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_int,
                                    c_vp, c_vp],
+    "advdiff_preload": [],
     "advdiff_adaptive_dt": [c_vp, c_vp, c_dbl, c_dbl, c_dbl, c_int, c_vp],
     "advdiff_reduce_norms": [c_int, c_vp, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_int,
                              c_int, c_int, c_vp, c_vp, c_vp],
@@ -165,6 +166,22 @@ def require():
     if lib is None:
         raise RuntimeError(f"advdiff native kernels unavailable: {_err}")
     return lib
+
+
+_preloaded = set()
+
+
+def preload(device_index: int) -> None:
+    """Load every kernel file's code object on `device_index` now (advdiff_preload): the
+    HIP runtime otherwise loads each at its first launch (~20 ms for the WENO5 file),
+    inside whatever the caller is timing.  Once per device and process."""
+    if device_index in _preloaded:
+        return
+    import torch
+    lib = require()
+    with torch.cuda.device(device_index):
+        check(lib.advdiff_preload(), "advdiff_preload")
+    _preloaded.add(device_index)
 
 
 def check(code: int, what: str) -> None:

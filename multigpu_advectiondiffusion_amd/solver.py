@@ -92,6 +92,10 @@ class Solver:
                 comm.device = torch.device("cuda", torch.cuda.current_device())
         self.comm = comm
         self.device = comm.device
+        if self.device.type == "cuda" and kernel != "torch":
+            from .ops import _lib
+            if _lib.available():
+                _lib.preload(self.device.index)  # code objects loaded outside any timing
         self.model = model
         self.grid = grid
         self.dtype = dtype
