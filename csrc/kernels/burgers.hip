@@ -1064,7 +1064,12 @@ static hipError_t launch_b3(const BArgs& p) {
 template <typename T, int W, bool WZ, bool VISC, int MODE>
 static hipError_t launch_b2(const BArgs& p) {
   const int gx = div_up(p.nx, kBTX2);
-  const int yc = pick_chunk(p.hi - p.lo, gx, 4, 256);
+  // fewest rows per y chunk: 1 — small grids (the reference's 400x406 rows) are latency-
+  // bound, and a wave walking fewer rows in sequence wins there (400x406 WENO5-JS step
+  // 23.4 -> 20.4 us with 4 -> 1, profiles/small2d_r2.log); from ~1000^2 up the chunk
+  // comes from the block target and this floor is inactive
+  static const int minc = std::max(knob("B2_MINC", 1), 1);
+  const int yc = pick_chunk(p.hi - p.lo, gx, minc, 256);
   const int gy = div_up(p.hi - p.lo, yc);
   const double s = 1.0 / 12.0;
   hipLaunchKernelGGL((burgers2d_stage_kernel<T, W, WZ, VISC, MODE, kBTX2>), dim3(gx, gy, 1),
