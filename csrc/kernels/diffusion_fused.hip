@@ -860,7 +860,10 @@ static hipError_t launch_step(const SArgs& a) {
       nb = 1;
     return nb;
   }();
-  static const int minc = knob("STEP_MIN_CHUNK", 32);
+  // chunk floor 16 (was 32): lets small grids fill one round of CUs (201x199x200 FD4:
+  // 6 -> 7 chunks, 216 -> 252 groups, 51.6 -> 45.1 us per step); 512^3 and 400x200x206
+  // pick the same chunking either way (profiles/heat3d_min_chunk_r2.log)
+  static const int minc = knob("STEP_MIN_CHUNK", 16);
   const int persist = step_persist();  // 0 (default): grid schedule only
   static const int minseg = std::max(knob("STEP_MIN_SEG", 32), 1);
   const int na = std::max(a.k1 - a.k0, 0), nb = std::max(a.k1b - a.k0b, 0);
