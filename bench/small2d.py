@@ -22,11 +22,12 @@ CASES = [
     ("burgers2d_js_1001x1001", lambda: Burgers(viscosity=0.0, weno="js", cfl=0.4), (1001, 1001), "gaussian", 200),
     ("burgers2d_z_visc_2048x2048", lambda: Burgers(viscosity=1e-5, weno="z", cfl=0.3), (2048, 2048), "gaussian", 100),
     ("heat2d_fd4_400x406", lambda: Diffusion(K=1.0, order=4, safety=0.8), (400, 406), "disc", 2000),
+    ("heat2d_fd4_1001x1001", lambda: Diffusion(K=1.0, order=4), (1001, 1001), "heat", 2000),
 ]
 
 
 def main():
-    out = {"B2_MINC": os.environ.get("ADVDIFF_B2_MINC", "default")}
+    out = {"knobs": {k: v for k, v in os.environ.items() if k.startswith("ADVDIFF_")}}
     for name, mk, shape, ic, steps in CASES:
         m = mk()
         g = Grid(shape, (2.0,) * len(shape))
