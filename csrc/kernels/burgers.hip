@@ -624,7 +624,7 @@ template <typename T, bool WZ, bool VISC, int MODE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void burgers3d_w5s_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
     int k1, int k0b, int k1b, int gza, int zchunk, int border, T rdx3, T rdy3, T rdz6, T vx,
-    T vy, T vz, T dt, T a, T b, const double* __restrict__ dtp) {
+    T vy, T vz, T dt, T a, T b, const double* __restrict__ dtp, int xcdmap) {
   constexpr int TY = 8, R = 3, NR = 5, TX = 64, TXO = TX - 1;
   constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NT = TX * TY, LT = LX * LY;
   constexpr int NPT = (LT + NT - 1) / NT;
@@ -641,13 +641,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
   const int tx = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
   const int tid = w * TX + tx;
-  const int ib = border - 1 + (int)blockIdx.x * TXO;  // x of lane 0 (supplies a face only)
-  const int jb = border + (int)blockIdx.y * TY;       // y of wave 0
+  // xcdmap: XCD-contiguous tile order (common.hpp xcd_tile), so y-adjacent tiles — which
+  // share 6 of their 14 staged rows — run together on one XCD's L2
+  const Tile3 tl = xcdmap ? xcd_tile() : Tile3{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+  const int ib = border - 1 + tl.x * TXO;  // x of lane 0 (supplies a face only)
+  const int jb = border + tl.y * TY;       // y of wave 0
   const int i = ib + tx, j = jb + w;
-  // z chunks of the first plane range [k0, k1), then (blockIdx.z >= gza) of the second
+  // z chunks of the first plane range [k0, k1), then (tile z >= gza) of the second
   // [k0b, k1b): both boundary slabs of a rank in ONE launch
-  const bool second = (int)blockIdx.z >= gza;
-  const int kc0 = second ? k0b + ((int)blockIdx.z - gza) * zchunk : k0 + (int)blockIdx.z * zchunk;
+  const bool second = tl.z >= gza;
+  const int kc0 = second ? k0b + (tl.z - gza) * zchunk : k0 + tl.z * zchunk;
   const int kc1 = min(kc0 + zchunk, second ? k1b : k1);
   const int klast = kc1 - 1;
   const bool active = tx >= 1 && i < nx - border && j < ny - border;
@@ -990,6 +993,9 @@ static hipError_t launch_b3_v6(const BArgs& p) {
 
 template <typename T, bool WZ, bool VISC, int MODE>
 static hipError_t launch_b3_v9(const BArgs& p) {
+  // XCD-contiguous tile order (default): 256^3 WENO5-Z + viscous step 0.584 -> 0.564 ms
+  // (+3.7 %, 3 interleaved rounds, bitwise identical; profiles/burgers3d_xcd_r2.log)
+  static const int xcdmap = knob("B3_XCD", 1);
   const int gx = div_up(std::max(p.nx - 2 * p.border, 1), 63);
   const int gy = div_up(std::max(p.ny - 2 * p.border, 1), 8);
   const int na = std::max(p.hi - p.lo, 0), nb = std::max(p.hi2 - p.lo2, 0);
@@ -1001,7 +1007,7 @@ static hipError_t launch_b3_v9(const BArgs& p) {
                      0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx, p.ny, p.sy, p.sz,
                      p.lo, p.hi, p.lo2, p.hi2, gza, zc, p.border, T(p.rdx / 3.0),
                      T(p.rdy / 3.0), T(p.rdz / 6.0), T(p.vx * s), T(p.vy * s), T(p.vz * s),
-                     T(p.dt), T(p.a), T(p.b), p.dtp);
+                     T(p.dt), T(p.a), T(p.b), p.dtp, xcdmap);
   return hipGetLastError();
 }
 
