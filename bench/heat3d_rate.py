@@ -3,7 +3,7 @@
 bench grid under the current ADVDIFF_* launch knobs — one JSON line per process, for
 interleaved A/B runs of a knob (knobs are read once per process):
 
-    ADVDIFF_STEP_MIN_CHUNK=16 python bench/heat3d_rate.py
+    ADVDIFF_STEP_MIN_CHUNK=16 python bench/heat3d_rate.py [order: 4 (default) | 2]
 """
 import json
 import os
@@ -18,9 +18,11 @@ SHAPES = [(201, 199, 200), (400, 200, 206), (512, 512, 512)]
 
 
 def main():
-    out = {"knobs": {k: v for k, v in os.environ.items() if k.startswith("ADVDIFF_")}}
+    order = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    out = {"knobs": {k: v for k, v in os.environ.items() if k.startswith("ADVDIFF_")},
+           "order": order}
     for shape in SHAPES:
-        m = Diffusion(K=1.0, order=4)
+        m = Diffusion(K=1.0, order=order)
         g = Grid(shape, (1.0, 1.0, 1.0))
         m.bind(g)
         s = Solver(m, g, dtype=torch.float64, ic="sine")
