@@ -148,7 +148,13 @@ def test_native_cartesian_socket_bitwise(tmp_path, app, args, shape, world, deco
     assert f"decomp={decomp}" in txt, txt
     a = np.fromfile(one, dtype=np.float32).reshape(shape)
     b = np.fromfile(many, dtype=np.float32).reshape(shape)
-    assert np.array_equal(a, b), np.abs(a - b).max()
+    if not np.array_equal(a, b):
+        # locate the wrong region (which block / face / corner) for the failure report
+        bad = np.argwhere(a != b)
+        lo, hi = bad.min(axis=0), bad.max(axis=0)
+        pytest.fail(f"{len(bad)} cells differ, max {np.abs(a - b).max()}, box {lo}..{hi} "
+                    f"of {shape}; zero cells in the {world}-rank run: {int((b == 0).sum())} "
+                    f"vs {int((a == 0).sum())}\n{txt[-2000:]}")
 
 
 def test_native_cartesian_error_norms(tmp_path):
