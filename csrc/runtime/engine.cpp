@@ -95,7 +95,11 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   HIP_CHECK(hipMalloc(&u_, field_bytes_));
   HIP_CHECK(hipMalloc(&A_, field_bytes_));
   HIP_CHECK(hipMalloc(&B_, field_bytes_));
+  // all three zeroed: cells a step never writes (ghost edges / corners at physical faces of a
+  // Cartesian block) are packed and sent, and a reused allocation would carry stale values
   HIP_CHECK(hipMemset(u_, 0, field_bytes_));
+  HIP_CHECK(hipMemset(A_, 0, field_bytes_));
+  HIP_CHECK(hipMemset(B_, 0, field_bytes_));
   int lo_pri = 0, hi_pri = 0;
   HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri));
   HIP_CHECK(hipStreamCreateWithPriority(&compute_, hipStreamNonBlocking, lo_pri));
