@@ -66,14 +66,10 @@ int advdiff_diffusion3d_step_box(int dtype, const void* uin, void* uout, int nx,
                                  int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int k0b,
                                  int k1b, int zlo, int zhi, const int* box, int order,
                                  double cx, double cy, double cz, double dt, void* stream);
-// Launch-policy flags of the _ex entry.
+// Launch-policy flags of the _ex entry (placement hints only, results are bit-identical).
 //   ADVDIFF_EXCLUSIVE: the launch has the GPU to itself (single rank, or a full-range
-//   launch after the halo wait): the fused step then runs as ONE round of persistent
-//   workgroups (CUs x occupancy), each marching an equal contiguous share of the
-//   linearised (tile, plane) space — no round quantisation, ~2 z warm-ups per group
-//   instead of one per chunk.  Without it (an interior launch that overlaps RCCL copy
-//   kernels, which may hold CUs for the whole launch) the grid of z chunks keeps the
-//   dispatcher's dynamic load balancing.  Placement only: results are bit-identical.
+//   launch after the halo wait).  Currently every launch uses the grid of z chunks (the
+//   persistent schedule it used to select measured slower and was removed).
 #define ADVDIFF_EXCLUSIVE 1
 int advdiff_diffusion3d_step_box_ex(int dtype, const void* uin, void* uout, int nx, int ny,
                                     int64_t sy, int64_t sz, int nz_alloc, int k0, int k1,
@@ -196,19 +192,34 @@ int advdiff_debug_print(int dtype, const void* u, int64_t sy, int64_t sz, int i0
 int advdiff_device_info(int dev, int64_t* out, int n);
 // Peer topology: can_access (hipDeviceCanAccessPeer), HSA link type (4 = xGMI), hop count.
 int advdiff_peer_info(int a, int b, int* can_access, int* link_type, int* hops);
-// Select the 3-D fused-step kernel variant (0 = default; A/B and tests); returns the
-// previous value.  Initialised from ADVDIFF_STEP_CFG.
-int advdiff_set_step_cfg(int cfg);
-// Allow (1) the persistent schedule for ADVDIFF_EXCLUSIVE 3-D fused launches (default 0:
-// grid of z chunks); returns the previous value.  Initialised from ADVDIFF_STEP_PERSIST.
-int advdiff_set_step_persist(int on);
 // v3 fused step: boundary-anchored edge tiles (1, default) or the plain partition (0)
 int advdiff_set_step_edge(int on);
-// 3-D WENO5 stage kernel version (1 = v1, 2 = v2 two barriers, 3 = v2 double-buffered);
-// returns the previous value.  Results agree to rounding (tests).
+// 3-D WENO5 stage kernel version (9 = default, 3 = the v3 fallback used for planes of
+// 2 GiB and more); returns the previous value.  Results agree to rounding (tests).
 int advdiff_set_b3_ver(int v);
-// rows per 3-D WENO tile (8 or 16); returns the previous value.
-int advdiff_set_b3_ty(int ty);
+// ---------------------------------------------------------------------------------
+// Peer transport of one node (ipc.hip): hipIpc-mapped device memory + device flags.  A
+// rank puts boundary cells straight into a neighbour's ghost cells (advdiff_copy_box with
+// a mapped destination), raises the neighbour's flag (advdiff_ipc_signal) and makes its
+// stream wait for its own flags (advdiff_ipc_wait).  All stream-ordered kernels: no host
+// synchronisation, hipGraph-capturable.  Works across the GPUs of a node (xGMI) and
+// between several processes on one GPU.
+typedef struct advdiff_ipc advdiff_ipc;
+typedef struct advdiff_ipc_addr {
+  unsigned char handle[64];  // hipIpcMemHandle_t of the allocation
+  uint64_t offset;           // byte offset of the address in it
+  uint64_t bytes;            // allocation size
+} advdiff_ipc_addr;
+int advdiff_ipc_create(int world, int rank, advdiff_ipc** out);
+int advdiff_ipc_destroy(advdiff_ipc* c);
+int advdiff_ipc_describe(advdiff_ipc* c, const void* ptr, advdiff_ipc_addr* out);
+int advdiff_ipc_flags_addr(advdiff_ipc* c, advdiff_ipc_addr* out);
+int advdiff_ipc_map(advdiff_ipc* c, const advdiff_ipc_addr* a, void** ptr);
+int advdiff_ipc_set_peer(advdiff_ipc* c, int peer, const advdiff_ipc_addr* peer_flags);
+int advdiff_ipc_signal(advdiff_ipc* c, const int* peers, int n, void* stream);
+int advdiff_ipc_wait(advdiff_ipc* c, const int* peers, int n, void* stream);
+int advdiff_ipc_errors(advdiff_ipc* c, long long* timeouts);
+
 // Library identification (build flags, arch) for diagnostics.
 const char* advdiff_build_info(void);
 // sha256 (first 16 hex digits) of the kernel sources this library was built from

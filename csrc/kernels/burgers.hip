@@ -368,23 +368,11 @@ __global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(WPE))) 
 }
 
 // ------------------------------------------------------------------------------
-// WENO5 3-D stage, v6: the v3 algorithm (63-cell x tiles, DPP left x face, register
-// z column, double-buffered LDS tile, one barrier per plane) reshaped for issue:
-//   * the z march is unrolled by the ring length (5): the f+/f-/u/curvature/z-face
-//     rings rotate by renaming (v3 spends ~21 v_mov_b64 per plane shifting them);
-//   * the wave index is scalar (readfirstlane): per-wave choices are scalar branches;
-//   * global traffic through per-plane buffer resources + 32-bit lane byte offsets (no
-//     64-bit VALU address math); u^n (aux) is prefetched one plane ahead;
-//   * the tile's bottom row of y faces (one extra face evaluation per plane): YM = 0:
-//     wave 0 computes it (as v3); YM = 1: it rotates over the waves plane by plane;
-//     YM = 2: wave 0 is a halo row (7 output rows of 8) that computes ONLY the y face
-//     above its row — every other wave does exactly 3 faces per plane, so no wave
-//     holds the others at the per-plane barrier (the y analogue of the x halo lane);
-//   * faces are carried as 6 x flux (the 1/6 of the candidate polynomials is folded
-//     into rd*/6 by the launcher) and the one division per face is a product with a
-//     reciprocal refined by one Newton step (w5_combine6: 4 fp64 ops fewer per face
-//     than the IEEE-exact fast_div; bench/native/divtest.hip measures the variants).
-// Requires a plane (sy * ny elements) below 2^31 bytes; the launcher falls back to v3.
+// Division helpers of the v9 stage.  Faces are carried as a multiple of the flux (the
+// 1/6 or 1/3 of the candidate polynomials is folded into rd* by the launcher) and the one
+// division per face is a product with a reciprocal refined by one Newton step
+// (w5_combine6: 4 fp64 ops fewer per face than the IEEE-exact fast_div;
+// bench/native/divtest.hip measures the variants).
 // ------------------------------------------------------------------------------
 template <typename T>
 __device__ __forceinline__ T fast_div1(T n, T d) {
@@ -416,197 +404,11 @@ __device__ __forceinline__ T w5_combine6(T n1, T S1, T n2, T S2) {
   }
 }
 
-template <typename T, bool WZ>
-__device__ __forceinline__ T w5_face6(const T* p, const T* m) {
-  T n1, S1, n2, S2;
-  w5_side<T, WZ>(p[0], p[1], p[2], p[3], p[4], w5_curv(p[0], p[1], p[2]),
-                 w5_curv(p[1], p[2], p[3]), w5_curv(p[2], p[3], p[4]), n1, S1);
-  w5_side<T, WZ>(m[4], m[3], m[2], m[1], m[0], w5_curv(m[4], m[3], m[2]),
-                 w5_curv(m[3], m[2], m[1]), w5_curv(m[2], m[1], m[0]), n2, S2);
-  return w5_combine6(n1, S1, n2, S2);
-}
-
-template <typename T, bool WZ, bool VISC, int MODE, int TY, int YM>
-__global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(4))) void burgers3d_w5r_kernel(
-    const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
-    int k1, int zchunk, int border, T rdx6, T rdy6, T rdz6, T vx, T vy, T vz, T dt, T a, T b,
-    const double* __restrict__ dtp) {
-  constexpr int R = 3, NR = 5, TX = 64, TXO = TX - 1;
-  constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NT = TX * TY, LT = LX * LY;
-  constexpr int NPT = (LT + NT - 1) / NT;
-  constexpr int E = (int)sizeof(T);
-  constexpr int NARR = VISC ? 3 : 2;                 // staged arrays: f+, f- [, u]
-  constexpr int SET = NARR * LT + (TY + 1) * TX;     // elements per buffer set (+ y faces)
-  constexpr int OM = LT * E, OU = 2 * LT * E, OFY = NARR * LT * E, SETB = SET * E;
-  static_assert(SETB < 65536, "LDS byte offsets within a set must fit the DS offset");
-  __shared__ T lds[2 * SET];
-  char* lb = (char*)lds;
-
-  const int tx = threadIdx.x;
-  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
-  const int tid = w * TX + tx;
-  const int ib = border - 1 + (int)blockIdx.x * TXO;  // x of lane 0 (supplies a face only)
-  constexpr int TYO = YM == 2 ? TY - 1 : TY;  // output rows per tile
-  const int jb = border - (YM == 2) + (int)blockIdx.y * TYO;  // y of wave 0
-  const int i = ib + tx, j = jb + w;
-  const int kc0 = k0 + (int)blockIdx.z * zchunk;
-  const int kc1 = min(kc0 + zchunk, k1);
-  const bool hrow = YM == 2 && w == 0;  // halo row: supplies its top y face only
-  const bool active = !hrow && tx >= 1 && i < nx - border && j < ny - border;
-  const uint32_t goff = (uint32_t)(min(j, ny - 1) * (int)sy + min(i, nx - 1)) * (uint32_t)E;
-  const int64_t szb = sz * E;
-  auto plane = [&](const T* base, int k) {
-    return plane_rsrc((const char*)base + (int64_t)k * szb);
-  };
-  if (dtp != nullptr && !device_dt(dtp, dt)) {  // adaptive run at t_end: out = in
-    if (active)
-      for (int k = kc0; k < kc1; ++k) gst<T>(plane(out, k), goff, gld<T>(plane(in, k), goff));
-    return;
-  }
-
-  uint32_t toff[NPT];
-#pragma unroll
-  for (int r = 0; r < NPT; ++r) {
-    const int idx = min(tid + r * NT, LT - 1);
-    const int ly = idx / LX, lx = idx - ly * LX;
-    toff[r] = (uint32_t)(clampi(jb - R + ly, 0, ny - 1) * (int)sy +
-                         clampi(ib - R + lx, 0, nx - 1)) * (uint32_t)E;
-  }
-  T pre[NPT];
-  auto fetch_tile = [&](int k) {
-    const auto rs = plane(in, k);
-#pragma unroll
-    for (int r = 0; r < NPT; ++r) pre[r] = gld<T>(rs, toff[r]);
-  };
-  auto stage_tile = [&](int sb) {  // sb: byte offset of the buffer set
-#pragma unroll
-    for (int r = 0; r < NPT; ++r) {
-      const int idx = tid + r * NT;
-      if (NPT * NT == LT || idx < LT) {
-        T p, m;
-        lf_split(pre[r], p, m);
-        lds_st<T>(lb, sb + idx * E, p);
-        lds_st<T>(lb, sb + OM + idx * E, m);
-        if constexpr (VISC) lds_st<T>(lb, sb + OU + idx * E, pre[r]);
-      }
-    }
-  };
-  // 6 x flux at the face to the right of the LDS cell at byte offset c along stride st
-  auto lds_face = [&](int c, int st) {
-    T pv[5], mv[5];
-#pragma unroll
-    for (int d = 0; d < 5; ++d) {
-      pv[d] = lds_ld<T>(lb, c + (d - 2) * st);
-      mv[d] = lds_ld<T>(lb, c + OM + (d - 1) * st);
-    }
-    return w5_face6<T, WZ>(pv, mv);
-  };
-  const int lcb = ((w + R) * LX + tx + R) * E;         // the lane's cell
-  const int bcb = ((R - 1) * LX + tx + R) * E;         // the cell below the tile's row 0
-  const int fyw = OFY + ((w + (YM == 2 ? 0 : 1)) * TX + tx) * E;  // y face above the cell
-
-  // ---- rings: plane p lives in slot (p - kc0 + 2 NR) % NR ----
-  T rp[NR], rm[NR], ru[NR], cp[NR], cm[NR], fz[NR];  // f+, f-, u, C(f+), C(f-), 6 x z face
-  {
-    T uz[2 * R], fp[2 * R], fm[2 * R];  // planes kc0-3 .. kc0+2
-#pragma unroll
-    for (int q = 0; q < 2 * R; ++q) {
-      uz[q] = gld<T>(plane(in, kc0 - R + q), goff);
-      lf_split(uz[q], fp[q], fm[q]);
-    }
-    auto sl = [](int p) { return (p + 2 * NR) % NR; };  // slot of plane kc0 + p
-    fz[sl(-1)] = w5_face6<T, WZ>(fp, fm + 1);            // face kc0-½
-    cp[sl(-1)] = w5_curv(fp[1], fp[2], fp[3]);
-    cp[sl(0)] = w5_curv(fp[2], fp[3], fp[4]);
-    cm[sl(0)] = w5_curv(fm[2], fm[3], fm[4]);
-    cm[sl(1)] = w5_curv(fm[3], fm[4], fm[5]);
-#pragma unroll
-    for (int q = 1; q < 2 * R; ++q) {  // planes kc0-2 .. kc0+2
-      rp[sl(q - R)] = fp[q];
-      ru[sl(q - R)] = uz[q];
-    }
-#pragma unroll
-    for (int q = 2; q < 2 * R; ++q) rm[sl(q - R)] = fm[q];  // kc0-1 .. kc0+2
-  }
-  fetch_tile(kc0);
-  stage_tile(0);
-  if (kc0 + 1 < kc1) fetch_tile(kc0 + 1);
-  T un = gld<T>(plane(in, kc0 + R), goff);  // u(k+3) of the current iteration
-  T ax = T(0);
-  if constexpr (reads_aux<MODE>()) ax = gld<T>(plane(aux, kc0), goff);
-  __syncthreads();
-
-  auto body = [&]<int PH>(int k) {
-    auto sl = [](int d) { return (PH + d + 2 * NR) % NR; };  // slot of plane k + d
-    const int sb = ((k - kc0) & 1) * SETB;
-    // new plane k+3 of the own column: f-(k+3) now; f+(k+3) and u(k+3) after their use
-    T pn, mn;
-    lf_split(un, pn, mn);
-    rm[sl(3)] = mn;
-    const T unew = un;
-    if (k + 1 < kc1) un = gld<T>(plane(in, k + 1 + R), goff);
-    T axk = ax;
-    if constexpr (reads_aux<MODE>())
-      if (k + 1 < kc1) ax = gld<T>(plane(aux, k + 1), goff);
-
-    const T fy = lds_face(sb + lcb, LX * E);  // y face j+½
-    if constexpr (YM != 2) {
-      const int bw = YM == 1 ? (k - kc0) % TY : 0;  // wave computing the bottom faces
-      if (w == bw) lds_st<T>(lb, sb + OFY + tx * E, lds_face(sb + bcb, LX * E));
-    }
-    lds_st<T>(lb, sb + fyw, fy);
-    const T ctr = ru[sl(0)];
-    T fx = T(0), d2x = T(0), d2y = T(0), d2z = T(0);
-    if (!hrow) {  // scalar branch
-      fx = lds_face(sb + lcb, E);  // x face i+½
-      if constexpr (VISC) {
-        const int c = sb + OU + lcb;
-        d2x = FD<4>::d2(lds_ld<T>(lb, c - 2 * E), lds_ld<T>(lb, c - E), ctr,
-                        lds_ld<T>(lb, c + E), lds_ld<T>(lb, c + 2 * E));
-        d2y = FD<4>::d2(lds_ld<T>(lb, c - 2 * LX * E), lds_ld<T>(lb, c - LX * E), ctr,
-                        lds_ld<T>(lb, c + LX * E), lds_ld<T>(lb, c + 2 * LX * E));
-        d2z = FD<4>::d2(ru[sl(-2)], ru[sl(-1)], ctr, ru[sl(1)], ru[sl(2)]);
-      }
-      cp[sl(1)] = w5_curv(rp[sl(0)], rp[sl(1)], rp[sl(2)]);
-      cm[sl(2)] = w5_curv(rm[sl(1)], rm[sl(2)], rm[sl(3)]);
-      T n1, S1, n2, S2;
-      w5_side<T, WZ>(rp[sl(-2)], rp[sl(-1)], rp[sl(0)], rp[sl(1)], rp[sl(2)], cp[sl(-1)],
-                     cp[sl(0)], cp[sl(1)], n1, S1);
-      w5_side<T, WZ>(rm[sl(3)], rm[sl(2)], rm[sl(1)], rm[sl(0)], rm[sl(-1)], cm[sl(2)],
-                     cm[sl(1)], cm[sl(0)], n2, S2);
-      fz[sl(0)] = w5_combine6(n1, S1, n2, S2);  // face k+½
-    }
-
-    if (k + 1 < kc1) {  // stage tile k+1 into the other buffer set, fetch tile k+2
-      stage_tile(sb ^ SETB);
-      if (k + 2 < kc1) fetch_tile(k + 2);
-    }
-    __syncthreads();  // y faces of k and tile k+1 visible
-
-    if (!hrow) {
-      const T fyl = lds_ld<T>(lb, sb + fyw - TX * E);
-      const T fxl = wave_shr1(fx);  // face i-½ from lane l-1 (lane 0: unused)
-      T L = -((fx - fxl) * rdx6 + (fy - fyl) * rdy6 + (fz[sl(0)] - fz[sl(-1)]) * rdz6);
-      if constexpr (VISC) L += vx * d2x + vy * d2y + vz * d2z;
-      T dnew = T(0);
-      const T v = stage_value<T, MODE>(axk, ctr, L, dt, a, b, dnew);
-      if (active) {
-        gst<T>(plane(out, k), goff, v);
-        if constexpr (MODE == kLs1 || MODE == kLs) gst<T>(plane(aux, k), goff, dnew);
-      }
-    }
-    rp[sl(3)] = pn;  // f+(k+3), u(k+3) replace f+(k-2), u(k-2)
-    ru[sl(3)] = unew;
-  };
-  for (int kb = kc0; kb < kc1; kb += NR) {
-    [&]<int... P>(std::integer_sequence<int, P...>) {
-      (void)((kb + P < kc1 ? (body.template operator()<P>(kb + P), true) : false) && ...);
-    }(std::make_integer_sequence<int, NR>{});
-  }
-}
-
 // ------------------------------------------------------------------------------
-// WENO5 3-D stage, v9: v6 (YM = 1, TY = 8) with the per-plane overhead taken out.
+// WENO5 3-D stage, v9 (default): the v3 algorithm (63-cell x tiles, DPP left x face,
+// register z column, double-buffered LDS tile, one barrier per plane) with the z rings
+// rotated by renaming (march unrolled by the ring length), the tile's bottom y faces
+// rotating over the waves plane by plane, and the per-plane overhead taken out:
 //   * the march is unrolled by 10 planes (ring length 5 x buffer-set parity 2), so the
 //     LDS buffer set of every plane is a compile-time constant: each LDS access is a
 //     loop-invariant lane base + an immediate offset.  The lane's read base sits at the
@@ -618,7 +420,7 @@ __global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(4))) vo
 //     the extra tile staged after the last plane lands in the idle buffer set;
 //   * x and y faces use w5_side_h (common.hpp): 37 instead of 41 fp64 ops per side,
 //     carried as 3 x the flux; z faces keep w5_side on the z rings (6 x the flux).
-// Requires a plane below 2^31 bytes (v6_fits); TY = 8 only (offsets < 64 KiB).
+// Requires a plane below 2^31 bytes (v9_fits); TY = 8 only (offsets < 64 KiB).
 // ------------------------------------------------------------------------------
 template <typename T, bool WZ, bool VISC, int MODE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void burgers3d_w5s_kernel(
@@ -948,46 +750,33 @@ struct BArgs {
   int lo2 = 0, hi2 = 0;  // optional second marched-axis range (3-D: v9 in the same launch)
 };
 
-template <typename T, int W, bool WZ, bool VISC, int MODE, int TY>
-static hipError_t launch_b3_ty(const BArgs& p) {
-  const int gx = div_up(p.nx, kBTX3), gy = div_up(p.ny, TY);
+// generic scheme kernel (WENO7; 64 x 8 tiles)
+template <typename T, int W, bool WZ, bool VISC, int MODE>
+static hipError_t launch_b3_generic(const BArgs& p) {
+  const int gx = div_up(p.nx, kBTX3), gy = div_up(p.ny, kBTY3);
   const int zc = pick_chunk(p.hi - p.lo, (long long)gx * gy, 8, 256);
   const int gz = div_up(p.hi - p.lo, zc);
   const double s = 1.0 / 12.0;
-  hipLaunchKernelGGL((burgers3d_stage_kernel<T, W, WZ, VISC, MODE, kBTX3, TY>),
-                     dim3(gx, gy, gz), dim3(kBTX3, TY, 1), 0, p.st, (const T*)p.in, (T*)p.aux,
-                     (T*)p.out, p.nx, p.ny, p.sy, p.sz, p.lo, p.hi, zc, p.border, T(p.rdx),
-                     T(p.rdy), T(p.rdz), T(p.vx * s), T(p.vy * s), T(p.vz * s), T(p.dt), T(p.a),
-                     T(p.b), p.dtp);
+  hipLaunchKernelGGL((burgers3d_stage_kernel<T, W, WZ, VISC, MODE, kBTX3, kBTY3>),
+                     dim3(gx, gy, gz), dim3(kBTX3, kBTY3, 1), 0, p.st, (const T*)p.in,
+                     (T*)p.aux, (T*)p.out, p.nx, p.ny, p.sy, p.sz, p.lo, p.hi, zc, p.border,
+                     T(p.rdx), T(p.rdy), T(p.rdz), T(p.vx * s), T(p.vy * s), T(p.vz * s),
+                     T(p.dt), T(p.a), T(p.b), p.dtp);
   return hipGetLastError();
 }
 
-template <typename T, bool WZ, bool VISC, int MODE, int TY, bool DB, int WPE = 4>
-static hipError_t launch_b3_v2(const BArgs& p) {
+// v3: 63-cell x tiles, double-buffered LDS tile, 64-bit addressing (planes of any size)
+template <typename T, bool WZ, bool VISC, int MODE>
+static hipError_t launch_b3_v3(const BArgs& p) {
   const int gx = div_up(std::max(p.nx - 2 * p.border, 1), 63);
-  const int gy = div_up(std::max(p.ny - 2 * p.border, 1), TY);
+  const int gy = div_up(std::max(p.ny - 2 * p.border, 1), kBTY3);
   const int zc = pick_chunk(p.hi - p.lo, (long long)gx * gy, 8, 256);
   const int gz = div_up(p.hi - p.lo, zc);
   const double s = 1.0 / 12.0;
-  hipLaunchKernelGGL((burgers3d_w5_kernel<T, WZ, VISC, MODE, TY, DB, WPE>), dim3(gx, gy, gz),
-                     dim3(64, TY, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx, p.ny,
-                     p.sy, p.sz, p.lo, p.hi, zc, p.border, T(p.rdx), T(p.rdy), T(p.rdz),
+  hipLaunchKernelGGL((burgers3d_w5_kernel<T, WZ, VISC, MODE, kBTY3, true, 4>), dim3(gx, gy, gz),
+                     dim3(64, kBTY3, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx,
+                     p.ny, p.sy, p.sz, p.lo, p.hi, zc, p.border, T(p.rdx), T(p.rdy), T(p.rdz),
                      T(p.vx * s), T(p.vy * s), T(p.vz * s), T(p.dt), T(p.a), T(p.b), p.dtp);
-  return hipGetLastError();
-}
-
-template <typename T, bool WZ, bool VISC, int MODE, int YM, int TY = 8>
-static hipError_t launch_b3_v6(const BArgs& p) {
-  const int gx = div_up(std::max(p.nx - 2 * p.border, 1), 63);
-  const int gy = div_up(std::max(p.ny - 2 * p.border, 1), YM == 2 ? TY - 1 : TY);
-  const int zc = pick_chunk(p.hi - p.lo, (long long)gx * gy, 8, 256);
-  const int gz = div_up(p.hi - p.lo, zc);
-  const double s = 1.0 / 12.0, s6 = 1.0 / 6.0;
-  hipLaunchKernelGGL((burgers3d_w5r_kernel<T, WZ, VISC, MODE, TY, YM>), dim3(gx, gy, gz),
-                     dim3(64, TY, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx, p.ny,
-                     p.sy, p.sz, p.lo, p.hi, zc, p.border, T(p.rdx * s6), T(p.rdy * s6),
-                     T(p.rdz * s6), T(p.vx * s), T(p.vy * s), T(p.vz * s), T(p.dt), T(p.a),
-                     T(p.b), p.dtp);
   return hipGetLastError();
 }
 
@@ -1011,60 +800,33 @@ static hipError_t launch_b3_v9(const BArgs& p) {
   return hipGetLastError();
 }
 
-// v6 / v9 address a plane with 32-bit byte offsets
+// v9 addresses a plane with 32-bit byte offsets
 template <typename T>
-static bool v6_fits(const BArgs& p) {
+static bool v9_fits(const BArgs& p) {
   return (int64_t)p.sy * p.ny * (int64_t)sizeof(T) < (int64_t(1) << 31);
 }
 
-// 3-D WENO5 kernel version (ADVDIFF_B3_VER / advdiff_set_b3_ver): 1 = v1 (generic LDS
-// face kernel), 2 = v2 with two barriers per plane, 3 = v2 with a double-buffered tile
-// (256^3 WENO5-Z + viscous stage 273 -> 242 us, profiles/burgers_variants_r2.log; 9.8e7
-// instead of 1.11e8 VALU instructions per dispatch, profiles/pmc_r2_burgers_fused.md),
-// 4/5 = v2 at 6 waves/SIMD (spills; kept for the record), 6 = the renamed-ring v6 kernel
-// with rotating bottom faces (default: 242 -> 227 us, 9.06e7 VALU per dispatch, in-solver
-// 20.3k -> 21.7k MLUPS; profiles/burgers_v6_r2.md), 7 = v6 with wave 0 fixed, 8 = v6
-// with a halo wave row (7 of 8 rows output: more workgroups, slower), 9 = v6 with
-// compile-time LDS sets, unconditional prefetches, SGPR constants and w5_side_h x/y faces
-// (default: 226 -> 195 us, SQ_INSTS_VALU 8.46e7 -> 7.62e7 = 290 lane-ops per cell,
-// profiles/burgers_v9_r2.md).  ADVDIFF_B3_TY=16
-// gives v3/v6 16-row tiles.
-static int g_b3_ver = -1, g_b3_ty = -1;
+// 3-D WENO5 kernel version (ADVDIFF_B3_VER / advdiff_set_b3_ver): 9 (default) = the v9
+// kernel (ring renaming, compile-time LDS sets, unconditional prefetches, SGPR constants,
+// w5_side_h x/y faces: 256^3 WENO5-Z + viscous stage 195 us, 290 lane-ops per cell,
+// profiles/burgers_v9_r2.md); 3 = v3 (double-buffered tile, one barrier per plane, 242
+// us), also the fallback for planes of 2 GiB and more.  The round-1/2 variants v1, v2,
+// v4-v8 and the 16-row tiles were removed after their A/Bs (profiles/burgers_variants_r2.log,
+// profiles/burgers_v6_r2.md, docs/DESIGN.md); WENO7 runs the generic scheme kernel.
+static int g_b3_ver = -1;
 static int b3_ver() {
   if (g_b3_ver < 0) g_b3_ver = knob("B3_VER", 9);
   return g_b3_ver;
 }
-static int b3_ty() {  // rows (waves) per 3-D tile: 8 or 16 (ADVDIFF_B3_TY)
-  if (g_b3_ty < 0) g_b3_ty = knob("B3_TY", kBTY3);
-  return g_b3_ty;
-}
 
 template <typename T, int W, bool WZ, bool VISC, int MODE>
 static hipError_t launch_b3(const BArgs& p) {
-  const int ty = b3_ty();
   if constexpr (W == 5) {
-    const int v = b3_ver();
-    if (v == 2) {
-      return ty == 16 ? launch_b3_v2<T, WZ, VISC, MODE, 16, false>(p)
-                      : launch_b3_v2<T, WZ, VISC, MODE, 8, false>(p);
-    }
-    if (v == 3) {
-      return ty == 16 ? launch_b3_v2<T, WZ, VISC, MODE, 16, true>(p)
-                      : launch_b3_v2<T, WZ, VISC, MODE, 8, true>(p);
-    }
-    if (v == 9 && v6_fits<T>(p)) return launch_b3_v9<T, WZ, VISC, MODE>(p);
-    if (v >= 6 && v <= 8 && v6_fits<T>(p)) {
-      if (ty == 16) return launch_b3_v6<T, WZ, VISC, MODE, 1, 16>(p);
-      return v == 6 ? launch_b3_v6<T, WZ, VISC, MODE, 1>(p)
-             : v == 7 ? launch_b3_v6<T, WZ, VISC, MODE, 0>(p)
-                      : launch_b3_v6<T, WZ, VISC, MODE, 2>(p);
-    }
-    if (v >= 6) return launch_b3_v2<T, WZ, VISC, MODE, 8, true>(p);  // v3 fallback
-    if (v == 4) return launch_b3_v2<T, WZ, VISC, MODE, 8, false, 6>(p);  // 6 waves/SIMD
-    if (v == 5) return launch_b3_v2<T, WZ, VISC, MODE, 4, false, 6>(p);
-    if (ty == 16) return launch_b3_ty<T, W, WZ, VISC, MODE, 16>(p);
+    if (b3_ver() == 9 && v9_fits<T>(p)) return launch_b3_v9<T, WZ, VISC, MODE>(p);
+    return launch_b3_v3<T, WZ, VISC, MODE>(p);
+  } else {
+    return launch_b3_generic<T, W, WZ, VISC, MODE>(p);
   }
-  return launch_b3_ty<T, W, WZ, VISC, MODE, 8>(p);
 }
 
 template <typename T, int W, bool WZ, bool VISC, int MODE>
@@ -1132,7 +894,7 @@ static hipError_t run_b(int dtype, bool three_d, int scheme, bool ls, const BArg
   // two plane ranges in one launch: the 3-D WENO5 v9 kernel; everything else launches
   // the ranges one after the other
   if (two && !(three_d && scheme != 2 && b3_ver() == 9 &&
-               (dtype == ADVDIFF_F64 ? v6_fits<double>(p) : v6_fits<float>(p)))) {
+               (dtype == ADVDIFF_F64 ? v9_fits<double>(p) : v9_fits<float>(p)))) {
     BArgs p1 = p, p2 = p;
     p1.lo2 = p1.hi2 = 0;
     p2.lo = p.lo2, p2.hi = p.hi2, p2.lo2 = p2.hi2 = 0;
@@ -1155,12 +917,6 @@ static hipError_t run_b(int dtype, bool three_d, int scheme, bool ls, const BArg
 extern "C" int advdiff_set_b3_ver(int v) {
   const int old = advdiff::b3_ver();
   advdiff::g_b3_ver = v;
-  return old;
-}
-
-extern "C" int advdiff_set_b3_ty(int ty) {
-  const int old = advdiff::b3_ty();
-  advdiff::g_b3_ty = ty;
   return old;
 }
 

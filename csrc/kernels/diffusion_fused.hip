@@ -38,21 +38,15 @@ struct Box2 {
   int xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1;
 };
 
-// Work split of a launch.
-//   Grid mode (persistent = 0): blockIdx -> (x tile, y tile, z chunk of `zchunk` planes;
-//   chunks z >= gza belong to the second plane range), as many rounds of resident groups
-//   as the grid needs — the dispatcher balances the load dynamically.
-//   Persistent mode (compact-ring kernel, PERSIST = true): a 1-D grid of G = CUs x
-//   occupancy groups; the (tile, plane) space is linearised tile-major (tile index
-//   t = ty gx + tx, then the planes of range 1 followed by those of range 2), L = tiles x
-//   planes, and group g marches an equal share of it (per or per + 1 planes) as 1-3 z
-//   segments (a segment ends at a tile or range boundary and pays the 4R-plane warm-up
-//   again).  512³: 220 tiles x 512 planes = 440 planes per group + ~2 warm-ups, against
-//   7 rounds x (64 + 8) planes in grid mode.
+// Work split of a launch: blockIdx -> (x tile, y tile, z chunk of `zchunk` planes; chunks
+// z >= gza belong to the second plane range), as many rounds of resident groups as the
+// grid needs — the dispatcher balances the load dynamically.  (A persistent schedule —
+// one round of groups each marching an equal share of the linearised (tile, plane) space
+// — measured 9-11 % slower at 512^3 and was removed: profiles/step_variants_r2.log.)
 struct StepSched {
   int gx, gy;       // tiles along x / y
-  int gza, zchunk;  // grid mode
-  int per, rem;     // persistent mode: L = per G + rem
+  int gza, zchunk;  // chunks of the first range, planes per chunk
+  int per, rem;     // unused (ABI of the kernel argument block)
   int edge;         // v3: boundary-anchored edge tiles (axis_tile)
 };
 
@@ -117,281 +111,6 @@ __device__ __forceinline__ AxisTile axis_tile(int t, int n, int W, int R, int a0
   return a;
 }
 
-// Compact rings: every z-window is a ring of exactly NR = 2R+1 registers (u(k+R..k+3R),
-// A(k..k+2R), B(k-R..k+R)) and the march is unrolled NR times; u(k..k+R-1), still needed
-// as the u^n term of stage 3, move to a short delay line when their ring slot is reused.
-// 17 instead of 24 window values per row (R = 2) leave room for the stage-1 DPP path.
-template <int ORDER, int NW, int RPW>
-struct CringGeom {
-  static constexpr int R = FD<ORDER>::R;
-  static constexpr int W = 64;
-  static constexpr int TX = W - 4 * R;
-  static constexpr int S1R = NW * RPW;
-  static constexpr int TY = S1R - 4 * R;
-  static constexpr int UW = W + 2 * R, UH = S1R + 2 * R;
-  static constexpr int LDS_U = UH * UW, LDS_AB = S1R * W;  // per buffer set
-};
-
-// One z segment [kc0, kc1) of output tile (tx, ty): warm-up + march (the whole
-// algorithm; sU/sA/sB are the workgroup's double-buffered LDS planes).
-template <typename T, int ORDER, int NW, int RPW, int XDPP>
-__device__ __forceinline__ void cring_march(
-    T* sU, T* sA, T* sB, int tx, int ty, int kc0, int kc1, const T* __restrict__ uin,
-    T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz, int nz_alloc, int zlo,
-    int zhi, const Box2& bx, const FdCoef<T>& q1, const FdCoef<T>& q2, const FdCoef<T>& q3) {
-  constexpr int R = FD<ORDER>::R;
-  constexpr int NR = 2 * R + 1;
-  constexpr int W = 64;
-  constexpr int TX = W - 4 * R;
-  constexpr int S1R = NW * RPW;
-  constexpr int TY = S1R - 4 * R;
-  constexpr int UW = W + 2 * R, UH = S1R + 2 * R;
-  constexpr int NT = 64 * NW;
-  constexpr int NHALO = UW * UH - W * S1R;
-  constexpr int NH = (NHALO + NT - 1) / NT;
-  static_assert(TY > 0, "tile too small");
-
-  const int lane = threadIdx.x, w = threadIdx.y, tid = w * 64 + lane;
-  const int i0 = tx * TX, j0 = ty * TY;
-  const int x = i0 - 2 * R + lane;
-  const bool xin = x >= bx.xa0 && x < bx.xa1;   // non-frozen columns
-  const bool xout = x >= bx.xo0 && x < bx.xo1;  // columns this launch writes
-  const bool s2c = lane >= R && lane < W - R;
-  const bool s3c = lane >= 2 * R && lane < W - 2 * R;
-  const int xc = clampi(x, 0, nx - 1);
-
-  int row[RPW], off[RPW];
-  bool inxy[RPW], outq[RPW], s2r[RPW], s3r[RPW];
-#pragma unroll
-  for (int q = 0; q < RPW; ++q) {
-    row[q] = w + q * NW;  // interleaved: every wave has <= 1 masked halo row per stage
-    const int y = j0 - 2 * R + row[q];
-    inxy[q] = xin && y >= bx.ya0 && y < bx.ya1;
-    outq[q] = inxy[q] && xout && y >= bx.yo0 && y < bx.yo1;
-    s2r[q] = row[q] >= R && row[q] < S1R - R;
-    s3r[q] = row[q] >= 2 * R && row[q] < S1R - 2 * R;
-    off[q] = clampi(y, 0, ny - 1) * (int)sy + xc;
-  }
-  int hl[NH], ho[NH];
-#pragma unroll
-  for (int h = 0; h < NH; ++h) {
-    int idx = tid + h * NT;
-    hl[h] = -1;
-    ho[h] = 0;
-    if (idx < NHALO) {
-      int ur, uc;
-      if (idx < R * UW) {
-        ur = idx / UW;
-        uc = idx - ur * UW;
-      } else if ((idx -= R * UW) < R * UW) {
-        ur = S1R + R + idx / UW;
-        uc = idx % UW;
-      } else {
-        idx -= R * UW;
-        ur = R + idx / (2 * R);
-        const int cc = idx % (2 * R);
-        uc = cc < R ? cc : W + cc;
-      }
-      hl[h] = ur * UW + uc;
-      ho[h] = clampi(j0 - 3 * R + ur, 0, ny - 1) * (int)sy + clampi(i0 - 3 * R + uc, 0, nx - 1);
-    }
-  }
-  auto plane = [&](int k) { return uin + (int64_t)clampi(k, 0, nz_alloc - 1) * sz; };
-
-  // plane p lives in ring slot (p - kst) % NR.  At the start of iteration k the u ring
-  // holds u(k+R-1 .. k+3R-1) and the delay line dl[0..R-2] holds u(k .. k+R-2).
-  T ru[RPW][NR], ra[RPW][NR], rb[RPW][NR], dl[RPW][R];
-  const int kst = kc0 - 4 * R;
-#pragma unroll
-  for (int q = 0; q < RPW; ++q) {
-#pragma unroll
-    for (int d = 0; d < R - 1; ++d) dl[q][d] = plane(kst + d)[off[q]];
-#pragma unroll
-    for (int s = 0; s < NR; ++s) {
-      const int pl = kst + R - 1 + s;  // planes kst+R-1 .. kst+3R-1
-      ru[q][pl - kst < NR ? pl - kst : pl - kst - NR] = plane(pl)[off[q]];
-      ra[q][s] = rb[q][s] = T(0);
-    }
-  }
-  // Global prefetch, one plane ahead: un = own column of u(k+3R) (enters the ring at the
-  // top of iteration k), hv = rim of u(k+1+2R).  The LDS u plane of iteration k+1 is
-  // written at the END of iteration k and A/B right after they are computed, so the LDS
-  // stores overlap the VALU work instead of forming a burst in front of the barrier.
-  T hv[NH], un[RPW];
-  {  // LDS u plane of the first iteration: u(kst+2R) (ring slot 2R) and its rim
-    T* pU = sU + (kst & 1) * (UH * UW);
-#pragma unroll
-    for (int h = 0; h < NH; ++h) hv[h] = plane(kst + 2 * R)[ho[h]];
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) pU[(row[q] + R) * UW + lane + R] = ru[q][2 * R];
-#pragma unroll
-    for (int h = 0; h < NH; ++h)
-      if (hl[h] >= 0) pU[hl[h]] = hv[h];
-  }
-#pragma unroll
-  for (int q = 0; q < RPW; ++q) un[q] = plane(kst + 3 * R)[off[q]];
-  const T third = T(1.0 / 3.0);
-
-  auto body = [&]<int PH>(int k) {
-    auto sl = [](int d) { return (PH + d + 4 * NR) % NR; };  // slot of plane k+d
-    constexpr int UIN = (PH + 3 * R) % NR;                    // u(k+3R) replaces u(k+R-1)
-    const int set = k & 1;
-    T* pU = sU + set * (UH * UW);
-    T* pA = sA + set * (S1R * W);
-    T* pB = sB + set * (S1R * W);
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-      dl[q][R - 1] = ru[q][UIN];  // u(k+R-1) -> delay line
-      ru[q][UIN] = un[q];
-      pU[(row[q] + R) * UW + lane + R] = ru[q][sl(2 * R)];
-      pA[row[q] * W + lane] = ra[q][sl(R)];
-      pB[row[q] * W + lane] = rb[q][sl(0)];
-    }
-#pragma unroll
-    for (int h = 0; h < NH; ++h)
-      if (hl[h] >= 0) pU[hl[h]] = hv[h];
-    if (k + 1 < kc1) {
-#pragma unroll
-      for (int h = 0; h < NH; ++h) hv[h] = plane(k + 1 + 2 * R)[ho[h]];
-#pragma unroll
-      for (int q = 0; q < RPW; ++q) un[q] = plane(k + 1 + 3 * R)[off[q]];
-    }
-    __syncthreads();
-    // stage 1: A(k+2R)
-    const int p1 = k + 2 * R;
-    const bool z1 = p1 >= zlo && p1 < zhi;
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-      const T c = ru[q][sl(2 * R)];
-      const int l = (row[q] + R) * UW + lane + R;
-      T acc = fd_ctr(q1.kc, c);  // order: centre, z, x, y (as the per-stage kernel)
-      if constexpr (R == 2) {
-        T m1, m2, p1v, p2v;
-        if constexpr (XDPP >= 2) {
-          m1 = wave_shr1(c);
-          p1v = wave_shl1(c);
-          m2 = wave_shr1(m1);
-          p2v = wave_shl1(p1v);
-          if (lane < R) {
-            m1 = pU[l - 1];
-            m2 = pU[l - 2];
-          } else if (lane >= W - R) {
-            p1v = pU[l + 1];
-            p2v = pU[l + 2];
-          }
-        } else {
-          m2 = pU[l - 2];
-          m1 = pU[l - 1];
-          p1v = pU[l + 1];
-          p2v = pU[l + 2];
-        }
-        acc = fd4_axis(acc, q1.k[2], ru[q][sl(R)], ru[q][sl(R + 1)], ru[q][sl(3 * R - 1)],
-                       ru[q][sl(3 * R)]);
-        acc = fd4_axis(acc, q1.k[0], m2, m1, p1v, p2v);
-        acc = fd4_axis(acc, q1.k[1], pU[l - 2 * UW], pU[l - UW], pU[l + UW], pU[l + 2 * UW]);
-      } else {
-        acc = fd2_axis(acc, q1.k[2], ru[q][sl(R)], ru[q][sl(3 * R)]);
-        acc = fd2_axis(acc, q1.k[0], pU[l - 1], pU[l + 1]);
-        acc = fd2_axis(acc, q1.k[1], pU[l - UW], pU[l + UW]);
-      }
-      const T v = acc;
-      ra[q][sl(2 * R)] = (z1 && inxy[q]) ? v : c;
-    }
-    // stage 2: B(k+R)
-    if (k >= kc0 - 2 * R) {
-      const int p2 = k + R;
-      const bool z2 = p2 >= zlo && p2 < zhi;
-#pragma unroll
-      for (int q = 0; q < RPW; ++q) {
-        const T uo = ru[q][sl(R)];
-        if (!s2r[q]) {
-          rb[q][sl(R)] = uo;
-          continue;
-        }
-        const int l = row[q] * W + lane;
-        const T c = ra[q][sl(R)];
-        T acc = fd_ctr(q2.kc, c, T(0.75) * uo);
-        if constexpr (R == 2) {
-          T m1, m2, p1v, p2v;
-          if constexpr (XDPP >= 1) {
-            m1 = wave_shr1(c);
-            p1v = wave_shl1(c);
-            m2 = wave_shr1(m1);
-            p2v = wave_shl1(p1v);
-          } else {
-            m2 = pA[l - 2];
-            m1 = pA[l - 1];
-            p1v = pA[l + 1];
-            p2v = pA[l + 2];
-          }
-          acc = fd4_axis(acc, q2.k[2], ra[q][sl(0)], ra[q][sl(1)], ra[q][sl(3)], ra[q][sl(4)]);
-          acc = fd4_axis(acc, q2.k[0], m2, m1, p1v, p2v);
-          acc = fd4_axis(acc, q2.k[1], pA[l - 2 * W], pA[l - W], pA[l + W], pA[l + 2 * W]);
-        } else {
-          const T m1 = XDPP >= 1 ? wave_shr1(c) : pA[l - 1];
-          const T p1v = XDPP >= 1 ? wave_shl1(c) : pA[l + 1];
-          acc = fd2_axis(acc, q2.k[2], ra[q][sl(0)], ra[q][sl(2)]);
-          acc = fd2_axis(acc, q2.k[0], m1, p1v);
-          acc = fd2_axis(acc, q2.k[1], pA[l - W], pA[l + W]);
-        }
-        const T v = acc;
-        rb[q][sl(R)] = (z2 && inxy[q] && s2c) ? v : uo;
-      }
-    }
-    // stage 3: u^{n+1}(k)
-    if (k >= kc0) {
-#pragma unroll
-      for (int q = 0; q < RPW; ++q) {
-        if (!s3r[q]) continue;
-        const int l = row[q] * W + lane;
-        const T c = rb[q][sl(0)];
-        const T uo = dl[q][0];
-        T acc = fd_ctr(q3.kc, c, third * uo);
-        if constexpr (R == 2) {
-          T m1, m2, p1v, p2v;
-          if constexpr (XDPP >= 1) {
-            m1 = wave_shr1(c);
-            p1v = wave_shl1(c);
-            m2 = wave_shr1(m1);
-            p2v = wave_shl1(p1v);
-          } else {
-            m2 = pB[l - 2];
-            m1 = pB[l - 1];
-            p1v = pB[l + 1];
-            p2v = pB[l + 2];
-          }
-          acc = fd4_axis(acc, q3.k[2], rb[q][sl(-2)], rb[q][sl(-1)], rb[q][sl(1)], rb[q][sl(2)]);
-          acc = fd4_axis(acc, q3.k[0], m2, m1, p1v, p2v);
-          acc = fd4_axis(acc, q3.k[1], pB[l - 2 * W], pB[l - W], pB[l + W], pB[l + 2 * W]);
-        } else {
-          const T m1 = XDPP >= 1 ? wave_shr1(c) : pB[l - 1];
-          const T p1v = XDPP >= 1 ? wave_shl1(c) : pB[l + 1];
-          acc = fd2_axis(acc, q3.k[2], rb[q][sl(-1)], rb[q][sl(1)]);
-          acc = fd2_axis(acc, q3.k[0], m1, p1v);
-          acc = fd2_axis(acc, q3.k[1], pB[l - W], pB[l + W]);
-        }
-        const T v = acc;
-        if (outq[q] && s3c) uout[(int64_t)k * sz + off[q]] = v;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-#pragma unroll
-      for (int d = 0; d < R - 1; ++d) dl[q][d] = dl[q][d + 1];
-    }
-  };
-
-  for (int kb = kst; kb < kc1; kb += NR) {
-    body.template operator()<0>(kb);
-    if (kb + 1 < kc1) body.template operator()<1>(kb + 1);
-    if (kb + 2 < kc1) body.template operator()<2>(kb + 2);
-    if constexpr (NR > 3) {
-      if (kb + 3 < kc1) body.template operator()<3>(kb + 3);
-      if (kb + 4 < kc1) body.template operator()<4>(kb + 4);
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------------
 // v3 march: the same algorithm (compact rings, trapezoid, one barrier per plane) with
 // the code shaped for the gfx950 issue model:
@@ -406,7 +125,9 @@ __device__ __forceinline__ void cring_march(
 //     form: no 64-bit VALU address math in the march);
 //   * PF: prefetch distance in planes (1 or 2).
 // The arithmetic (fd_ctr / fd4_axis / fd2_axis in the fixed order centre, z, x, y) is
-// unchanged, so v3 is bit-identical to the cring march and to the per-stage kernels.
+// that of the per-stage kernels, so the step is bit-identical to three stage launches.
+// (The round-1 "compact ring" march with per-iteration LDS pointers and the 8-slot ring
+// kernels were removed after their A/Bs: profiles/kbench_fused_*.log, step_cfgs_*.)
 // ---------------------------------------------------------------------------------
 template <typename T, int ORDER, int NW, int RPW>
 struct V3Geom {
@@ -711,118 +432,37 @@ __device__ __forceinline__ void v3_march(
 // (FD4 16 waves: 1/CU -> 4; FD2 12 waves: 2/CU -> 6).  Without it the compiler spent 86
 // VGPRs on the FD2 step and lost the second workgroup per CU (-25 %).
 template <typename T, int ORDER, int NW, int RPW>
-constexpr int cring_min_waves() {
-  using Gm = CringGeom<ORDER, NW, RPW>;
-  constexpr int lds = (int)sizeof(T) * 2 * (Gm::LDS_U + 2 * Gm::LDS_AB);
+constexpr int step_min_waves() {
+  constexpr int lds = (int)sizeof(T) * V3Geom<T, ORDER, NW, RPW>::TOTAL;
   constexpr int wgs = 163840 / lds;
   constexpr int w = wgs * NW / 4;
   return sizeof(T) == 8 ? (w > 8 ? 8 : (w < 1 ? 1 : w)) : 1;
 }
 
-// Kernel variants: VAR < 16: cring march with XDPP = VAR; VAR >= 16: v3 march with
-// XS = VAR & 1 (DPP x-neighbours in stages 2/3), prefetch distance 1 + ((VAR >> 1) & 1)
-// and SEP = (VAR >> 2) & 1 (unmerged LDS reads).
-template <int VAR>
-struct StepVar {
-  static constexpr bool v3 = VAR >= 16;
-  static constexpr int xdpp = VAR & 15;
-  static constexpr int xs = VAR & 1;
-  static constexpr int pf = 1 + ((VAR >> 1) & 1);
-  static constexpr bool sep = (VAR >> 2) & 1;
-};
-
-template <typename T, int ORDER, int NW, int RPW, int VAR>
-__device__ __forceinline__ void march_var(T* lds, int tx, int ty, const StepSched& sc,
-                                          int kc0, int kc1,
-                                          const T* __restrict__ uin, T* __restrict__ uout,
-                                          int nx, int ny, int64_t sy, int64_t sz, int nz_alloc,
-                                          int zlo, int zhi, const Box2& bx, const FdCoef<T>& q1,
-                                          const FdCoef<T>& q2, const FdCoef<T>& q3) {
-  using V = StepVar<VAR>;
-  if constexpr (V::v3) {
-    v3_march<T, ORDER, NW, RPW, V::xs, V::pf, V::sep>(lds, tx, ty, sc.gx, sc.gy, sc.edge, kc0,
-                                                      kc1, uin, uout, nx, ny, sy, sz, nz_alloc,
-                                                      zlo, zhi, bx, q1, q2, q3);
-  } else {
-    using Gm = CringGeom<ORDER, NW, RPW>;
-    cring_march<T, ORDER, NW, RPW, V::xdpp>(lds, lds + 2 * Gm::LDS_U,
-                                            lds + 2 * Gm::LDS_U + 2 * Gm::LDS_AB, tx, ty, kc0,
-                                            kc1, uin, uout, nx, ny, sy, sz, nz_alloc, zlo, zhi,
-                                            bx, q1, q2, q3);
-  }
-}
-
-template <typename T, int ORDER, int NW, int RPW, int VAR>
-constexpr int step_lds_elems() {
-  if constexpr (StepVar<VAR>::v3)
-    return V3Geom<T, ORDER, NW, RPW>::TOTAL;
-  else
-    return 2 * CringGeom<ORDER, NW, RPW>::LDS_U + 4 * CringGeom<ORDER, NW, RPW>::LDS_AB;
-}
-
-// waves per SIMD to budget registers for, from the LDS footprint of the variant
-template <typename T, int ORDER, int NW, int RPW, int VAR>
-constexpr int step_min_waves() {
-  if constexpr (StepVar<VAR>::v3) {
-    constexpr int lds = (int)sizeof(T) * V3Geom<T, ORDER, NW, RPW>::TOTAL;
-    constexpr int wgs = 163840 / lds;
-    constexpr int w = wgs * NW / 4;
-    return sizeof(T) == 8 ? (w > 8 ? 8 : (w < 1 ? 1 : w)) : 1;
-  } else {
-    return cring_min_waves<T, ORDER, NW, RPW>();
-  }
-}
-
-template <typename T, int ORDER, int NW, int RPW, int VAR, bool PERSIST>
+// The march variant: DPP x neighbours in stages 2/3 (XS = 1), prefetch distance 2,
+// unmerged LDS reads (SEP).  The other (XS, PF, SEP) combinations measured 1-9 % slower
+// at 512^3 (profiles/step_variants_r2.log, step_cfgs_edge_r2.log) and were removed.
+template <typename T, int ORDER, int NW, int RPW>
 __global__ __launch_bounds__(64 * NW) __attribute__((
-    amdgpu_waves_per_eu(step_min_waves<T, ORDER, NW, RPW, VAR>()))) void diffusion3d_step_cring_kernel(
+    amdgpu_waves_per_eu(step_min_waves<T, ORDER, NW, RPW>()))) void diffusion3d_step_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
     int nz_alloc, int k0, int k1, int k0b, int k1b, StepSched sc, int zlo, int zhi,
     Box2 bx, FdCoef<T> q1, FdCoef<T> q2, FdCoef<T> q3) {
-  __shared__ T lds[step_lds_elems<T, ORDER, NW, RPW, VAR>()];
+  __shared__ T lds[V3Geom<T, ORDER, NW, RPW>::TOTAL];
   const Tile3 tile = xcd_tile();
-  if constexpr (!PERSIST) {
-    // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
-    const bool second = tile.z >= sc.gza;
-    const int kc0 = second ? k0b + (tile.z - sc.gza) * sc.zchunk : k0 + tile.z * sc.zchunk;
-    const int kc1 = min(kc0 + sc.zchunk, second ? k1b : k1);
-    march_var<T, ORDER, NW, RPW, VAR>(lds, tile.x, tile.y, sc, kc0, kc1, uin, uout, nx, ny, sy,
-                                      sz, nz_alloc, zlo, zhi, bx, q1, q2, q3);
-  } else {
-    // 1-D grid; tile.x = this group's XCD-contiguous logical id, so the groups of one XCD
-    // march neighbouring tiles.  Group g owns the linear planes [s, e), s = g per +
-    // min(g, rem) (32-bit: the host keeps L < 2^31).  Wave-uniform (scalar) loop.
-    const int g = tile.x;
-    const int na = k1 - k0, P = na + (k1b - k0b);
-    int s = g * sc.per + min(g, sc.rem);
-    const int e = s + sc.per + (g < sc.rem ? 1 : 0);
-    while (s < e) {
-      const int t = s / P, p0 = s - t * P;
-      int p1 = min(P, e - t * P);
-      if (p0 < na) p1 = min(p1, na);  // a segment never spans both plane ranges
-      const int kc0 = p0 < na ? k0 + p0 : k0b + (p0 - na);
-      __syncthreads();  // nobody still reads the previous segment's last LDS planes
-      march_var<T, ORDER, NW, RPW, VAR>(lds, t % sc.gx, t / sc.gx, sc, kc0, kc0 + (p1 - p0), uin,
-                                        uout, nx, ny, sy, sz, nz_alloc, zlo, zhi, bx, q1, q2,
-                                        q3);
-      s += p1 - p0;
-    }
-  }
+  // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
+  const bool second = tile.z >= sc.gza;
+  const int kc0 = second ? k0b + (tile.z - sc.gza) * sc.zchunk : k0 + tile.z * sc.zchunk;
+  const int kc1 = min(kc0 + sc.zchunk, second ? k1b : k1);
+  v3_march<T, ORDER, NW, RPW, 1, 2, true>(lds, tile.x, tile.y, sc.gx, sc.gy, sc.edge, kc0, kc1,
+                                           uin, uout, nx, ny, sy, sz, nz_alloc, zlo, zhi, bx,
+                                           q1, q2, q3);
 }
 
-// Persistent schedule for exclusive launches: ADVDIFF_STEP_PERSIST / advdiff_set_step_persist.
-// Off by default since the v3 march: at 512^3 the dynamically balanced grid of z chunks
-// is 9-11 % faster (FD4 760 vs 836 us, FD2 559 vs 745 us, profiles/step_variants_r2.log).
 static int g_step_edge = -1;
 static int step_edge() {  // v3 edge tiles (axis_tile): ADVDIFF_STEP_EDGE / advdiff_set_step_edge
   if (g_step_edge < 0) g_step_edge = knob("STEP_EDGE", 1);
   return g_step_edge;
-}
-
-static int g_step_persist = -1;
-static int step_persist() {
-  if (g_step_persist < 0) g_step_persist = knob("STEP_PERSIST", 0);
-  return g_step_persist;
 }
 
 struct SArgs {
@@ -836,26 +476,19 @@ struct SArgs {
   Box2 bx;
   double cx, cy, cz, dt;
   hipStream_t st;
-  int flags;  // ADVDIFF_EXCLUSIVE: persistent schedule allowed
 };
 
-template <typename T, int ORDER, int NW, int RPW, int XDPP = 0>
+template <typename T, int ORDER, int NW, int RPW>
 static hipError_t launch_step(const SArgs& a) {
   constexpr int R = ORDER / 2;
-  constexpr int TX = 64 - 4 * R, TY = NW * RPW - 4 * R;
-  const int edge = StepVar<XDPP>::v3 ? step_edge() : 0;
-  const int gx = StepVar<XDPP>::v3
-                     ? axis_tile_count(64, R, a.bx.xa0, a.bx.xa1, a.bx.xo0, a.bx.xo1, a.nx, edge)
-                     : div_up(a.nx, TX);
-  const int gy = StepVar<XDPP>::v3 ? axis_tile_count(NW * RPW, R, a.bx.ya0, a.bx.ya1, a.bx.yo0,
-                                                     a.bx.yo1, a.ny, edge)
-                                   : div_up(a.ny, TY);
+  const int edge = step_edge();
+  const int gx = axis_tile_count(64, R, a.bx.xa0, a.bx.xa1, a.bx.xo0, a.bx.xo1, a.nx, edge);
+  const int gy = axis_tile_count(NW * RPW, R, a.bx.ya0, a.bx.ya1, a.bx.yo0, a.bx.yo1, a.ny, edge);
   // z chunks: minimise (rounds of resident workgroups) x (chunk + 4R warm-up planes);
   // resident workgroups = CUs x occupancy of this instance (LDS / VGPR bound: 1-2 per CU)
-  static const int target = knob("STEP_TARGET_BLOCKS", 0);  // >0: legacy fixed target
   static const int per_cu = [] {
     int nb = 0;
-    const void* fn = (const void*)diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, false>;
+    const void* fn = (const void*)diffusion3d_step_kernel<T, ORDER, NW, RPW>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * NW, 0) != hipSuccess || nb < 1)
       nb = 1;
     return nb;
@@ -864,107 +497,40 @@ static hipError_t launch_step(const SArgs& a) {
   // 6 -> 7 chunks, 216 -> 252 groups, 51.6 -> 45.1 us per step); 512^3 and 400x200x206
   // pick the same chunking either way (profiles/heat3d_min_chunk_r2.log)
   static const int minc = knob("STEP_MIN_CHUNK", 16);
-  const int persist = step_persist();  // 0 (default): grid schedule only
-  static const int minseg = std::max(knob("STEP_MIN_SEG", 32), 1);
   const int na = std::max(a.k1 - a.k0, 0), nb = std::max(a.k1b - a.k0b, 0);
   const long long slots = (long long)device_cus() * per_cu;
   StepSched sc{gx, gy, 0, 0, 0, 0, edge};
-  dim3 grid;
-  const long long L = (long long)gx * gy * (na + nb);
-  const bool persistent = persist && (a.flags & ADVDIFF_EXCLUSIVE) && L < (1LL << 31);
-  if (persistent) {
-    // one round of resident groups; small launches keep >= minseg planes per group
-    const long long G = std::max(1LL, std::min(slots, (L + minseg - 1) / minseg));
-    sc.per = (int)(L / G);
-    sc.rem = (int)(L % G);
-    grid = dim3((unsigned)G, 1, 1);
-  } else {
-    int zc;
-    if (target > 0) {
-      long long chunks = (target + (long long)gx * gy - 1) / ((long long)gx * gy);
-      zc = std::max(div_up(na + nb, std::max<long long>(chunks, 1)), minc);
-    } else {
-      zc = pick_chunk_rounds(na + nb, (long long)gx * gy, slots, 4 * R, minc);
-    }
-    sc.gza = na > 0 ? div_up(na, zc) : 0;
-    sc.zchunk = zc;
-    grid = dim3(gx, gy, sc.gza + (nb > 0 ? div_up(nb, zc) : 0));
-  }
+  const int zc = pick_chunk_rounds(na + nb, (long long)gx * gy, slots, 4 * R, minc);
+  sc.gza = na > 0 ? div_up(na, zc) : 0;
+  sc.zchunk = zc;
+  const dim3 grid(gx, gy, sc.gza + (nb > 0 ? div_up(nb, zc) : 0));
   // SSP-RK3 stage coefficients b = 1, 1/4, 2/3: exactly the per-stage path's (FdCoef)
   const FdCoef<T> q1 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 1.0, true);
   const FdCoef<T> q2 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 0.25, true);
   const FdCoef<T> q3 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 2.0 / 3.0, true);
-#define STEP_ARGS                                                                              \
-  grid, dim3(64, NW, 1), 0, a.st, (const T*)a.uin, (T*)a.uout, a.nx, a.ny, a.sy, a.sz,        \
-      a.nz_alloc, a.k0, a.k1, a.k0b, a.k1b, sc, a.zlo, a.zhi, a.bx, q1, q2, q3
-  if (persistent)
-    hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, true>),
-                       STEP_ARGS);
-  else
-    hipLaunchKernelGGL((diffusion3d_step_cring_kernel<T, ORDER, NW, RPW, XDPP, false>),
-                       STEP_ARGS);
-#undef STEP_ARGS
+  hipLaunchKernelGGL((diffusion3d_step_kernel<T, ORDER, NW, RPW>), grid, dim3(64, NW, 1), 0,
+                     a.st, (const T*)a.uin, (T*)a.uout, a.nx, a.ny, a.sy, a.sz, a.nz_alloc,
+                     a.k0, a.k1, a.k0b, a.k1b, sc, a.zlo, a.zhi, a.bx, q1, q2, q3);
   return hipGetLastError();
 }
 
-// Tile/schedule variants (A/B via ADVDIFF_STEP_CFG; measurements in profiles/).  The
-// plain register-shifting and 8-slot-ring kernels measured in profiles/kbench_fused_*.log
-// were slower and are gone; the compact-ring variants stay selectable.
+// Tile shape per order.  With the edge tiles (axis_tile), interleaved medians at 512^3:
+// FD4 16 waves x 2 rows (32 stage-1 rows) 662 us vs 715 us for 12 x 3; FD2 12 x 3 rows
+// 535 us vs 549 us for 16 x 2 (profiles/step_cfgs_edge_r2.log).  48 rows overflow the
+// 16-bit DS offsets, 10 x 4 spills at 168 VGPRs.
 template <typename T, int ORDER>
-static hipError_t dispatch_step(int cfg, const SArgs& a) {
-#define STEPV(NW, RPW, ...) return launch_step<T, ORDER, NW, RPW, ##__VA_ARGS__>(a)
-  switch (cfg) {
-    case 14: STEPV(12, 2, 1);    // 12 waves, DPP stages 2/3
-    case 15: STEPV(12, 2, 2);    // 12 waves, DPP stages 1-3
-    case 16: STEPV(16, 2, 1);    // 16 waves, DPP stages 2/3
-    case 20: STEPV(16, 2, 16);   // v3, LDS x-neighbours, prefetch 1
-    case 21: STEPV(16, 2, 17);   // v3, DPP x in stages 2/3, prefetch 1
-    case 22: STEPV(16, 2, 18);   // v3, LDS x, prefetch 2
-    case 23: STEPV(16, 2, 19);   // v3, DPP x 2/3, prefetch 2
-    case 24: STEPV(16, 2, 20);   // v3, LDS x, prefetch 1, unmerged LDS reads
-    case 25: STEPV(16, 2, 21);   // v3, DPP x 2/3, prefetch 1, unmerged LDS reads
-    case 27: STEPV(16, 2, 23);   // v3, DPP x 2/3, prefetch 2, unmerged LDS reads
-    case 30: STEPV(12, 3, 23);   // taller tiles: 36 stage-1 rows (TY 28 for FD4)
-    case 31: STEPV(8, 5, 23);    // 40 rows (TY 32), 8 waves x 5 rows
-    case 32: STEPV(8, 4, 23);    // 32 rows, 8 waves x 4 rows
-    case 33: STEPV(10, 4, 23);   // 40 rows, 10 waves x 4 rows
-    case 29: STEPV(16, 2, 23);   // round-2 default before the taller tiles
-    case 1: STEPV(16, 2, 2);     // round-1 default (cring, DPP in all stages)
-    default:  // v3, DPP x in stages 2/3, prefetch 2, unmerged LDS reads.  With the edge
-              // tiles (axis_tile), interleaved medians at 512^3: FD4 16 waves x 2 rows
-              // (32 stage-1 rows) 662 us vs 715 us for 12 x 3; FD2 12 x 3 rows 535 us vs
-              // 549 us for 16 x 2 (profiles/step_cfgs_edge_r2.log).  48 rows overflow the
-              // 16-bit DS offsets, 10 x 4 spills at 168 VGPRs
-      if constexpr (ORDER == 4) STEPV(16, 2, 23);
-      STEPV(12, 3, 23);
-  }
-#undef STEPV
-}
-
-// kernel variant of the 3-D fused step: ADVDIFF_STEP_CFG, or advdiff_set_step_cfg (tests)
-static int g_step_cfg = -1;
-static int step_cfg() {
-  if (g_step_cfg < 0) g_step_cfg = knob("STEP_CFG", 0);
-  return g_step_cfg;
+static hipError_t dispatch_step(const SArgs& a) {
+  if constexpr (ORDER == 4)
+    return launch_step<T, ORDER, 16, 2>(a);
+  else
+    return launch_step<T, ORDER, 12, 3>(a);
 }
 
 }  // namespace advdiff
 
-extern "C" int advdiff_set_step_persist(int on) {
-  const int old = advdiff::step_persist();
-  advdiff::g_step_persist = on ? 1 : 0;
-  return old;
-}
-
 extern "C" int advdiff_set_step_edge(int on) {
   const int old = advdiff::step_edge();
   advdiff::g_step_edge = on ? 1 : 0;
-  return old;
-}
-
-extern "C" int advdiff_set_step_cfg(int cfg) {
-  const int old = advdiff::step_cfg();
-  advdiff::g_step_cfg = cfg < 0 ? 0 : cfg;
   return old;
 }
 
@@ -995,15 +561,15 @@ extern "C" int advdiff_diffusion3d_step_box_ex(int dtype, const void* uin, void*
     return hipErrorInvalidValue;
   if (sy * (int64_t)ny >= (int64_t(1) << 31)) return hipErrorInvalidValue;
   const Box2 bx{box[0], box[1], box[2], box[3], box[4], box[5], box[6], box[7]};
+  (void)flags;  // placement hints (ADVDIFF_EXCLUSIVE): the grid schedule serves all launches
   const SArgs a{uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, k0b, k1b, zlo, zhi, bx,
-                cx, cy, cz, dt, (hipStream_t)stream, flags};
-  const int cfg = advdiff::step_cfg();
+                cx, cy, cz, dt, (hipStream_t)stream};
   if (dtype == ADVDIFF_F64) {
-    if (order == 4) return dispatch_step<double, 4>(cfg, a);
-    if (order == 2) return dispatch_step<double, 2>(cfg, a);
+    if (order == 4) return dispatch_step<double, 4>(a);
+    if (order == 2) return dispatch_step<double, 2>(a);
   } else if (dtype == ADVDIFF_F32) {
-    if (order == 4) return dispatch_step<float, 4>(cfg, a);
-    if (order == 2) return dispatch_step<float, 2>(cfg, a);
+    if (order == 4) return dispatch_step<float, 4>(a);
+    if (order == 2) return dispatch_step<float, 2>(a);
   }
   return hipErrorInvalidValue;
 }
@@ -1030,5 +596,5 @@ extern "C" int advdiff_diffusion3d_step(int dtype, const void* uin, void* uout, 
 extern "C" int advdiff_preload_diffusion_fused(void) {
   hipFuncAttributes a;
   return hipFuncGetAttributes(
-      &a, (const void*)advdiff::diffusion3d_step_cring_kernel<double, 4, 16, 2, 23, false>);
+      &a, (const void*)advdiff::diffusion3d_step_kernel<double, 4, 16, 2>);
 }

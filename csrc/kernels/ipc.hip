@@ -1,0 +1,222 @@
+// Peer-to-peer transport primitives of one node: hipIpc-mapped device memory + device-side
+// flags.  This is the P2PComm of SURVEY.md §7.1 ("peer-mapped xGMI puts"): a rank writes
+// its boundary cells STRAIGHT INTO the neighbour's ghost cells (a copy kernel whose
+// destination is the neighbour's field, mapped into this process with
+// hipIpcOpenMemHandle), then raises the neighbour's flag with a release store; the
+// neighbour's stream waits on its own flag with an acquire spin.  Every step of an
+// exchange is a kernel on a stream: no host synchronisation, no staging buffer, no pack or
+// unpack, and the whole exchange can be captured into a hipGraph (the counters live in
+// device memory, so replays keep counting).
+//
+// It replaces the reference's host-staged choreography (MultiGPU/Diffusion3d_Baseline/
+// main.c:209-288: pack kernel -> D2H -> host-blocking stream sync -> MPI_Isend/Irecv ->
+// MPI_Wait -> H2D -> unpack kernel).  Across GPUs the puts travel over xGMI (the mapping is
+// a peer mapping); with several ranks on ONE GPU (the test configuration of a 1-GPU box,
+// where RCCL refuses two ranks per device) the same code runs as same-device IPC.
+//
+// Flags block of a rank (device memory, exported): recv[world] (written by the peers: the
+// number of messages peer q has delivered), sent[world] (messages delivered to q, local),
+// expect[world] (messages consumed from q, local), err (wait timeouts).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "advdiff/kernels.h"
+
+struct advdiff_ipc {
+  int world = 1, rank = 0;
+  uint64_t* block = nullptr;          // recv | sent | expect | err
+  std::vector<uint64_t*> peer_cell;   // peer q's recv[rank] (mapped), or nullptr
+  std::map<std::string, void*> opened;  // IPC handle bytes -> mapped base
+  std::map<uintptr_t, hipIpcMemHandle_t> exported;  // allocation base -> handle
+  std::mutex mu;
+  uint64_t* recv() const { return block; }
+  uint64_t* sent() const { return block + world; }
+  uint64_t* expect() const { return block + 2 * world; }
+  unsigned long long* err() const { return (unsigned long long*)(block + 3 * world); }
+};
+
+namespace advdiff {
+
+constexpr int kIpcMaxPeers = 16;
+
+struct IpcSignalArgs {
+  uint64_t* remote[kIpcMaxPeers];  // peer's recv[rank]
+  uint64_t* sent[kIpcMaxPeers];    // own sent[peer]
+  int n;
+};
+
+struct IpcWaitArgs {
+  const uint64_t* flag[kIpcMaxPeers];  // own recv[peer]
+  uint64_t* expect[kIpcMaxPeers];      // own expect[peer]
+  int n;
+  unsigned long long* err;
+  uint64_t timeout_ticks;  // s_memrealtime runs at 100 MHz
+};
+
+// lane q: sent[q] += 1, then publish it to the peer with a system-scope release store
+// (the puts before it on this stream are complete and written back by then)
+__global__ void ipc_signal_kernel(IpcSignalArgs a) {
+  const int q = threadIdx.x;
+  if (q >= a.n) return;
+  const uint64_t v = a.sent[q][0] + 1;
+  a.sent[q][0] = v;
+  __hip_atomic_store(a.remote[q], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// lane q: expect[q] += 1, then spin (acquire loads, s_sleep) until recv[q] reaches it.
+// Bounded: after timeout_ticks the lane records a timeout and leaves, so the grid always
+// drains even if a peer died (the host checks advdiff_ipc_errors at its sync points).
+__global__ void ipc_wait_kernel(IpcWaitArgs a) {
+  const int q = threadIdx.x;
+  if (q >= a.n) return;
+  const uint64_t e = a.expect[q][0] + 1;
+  a.expect[q][0] = e;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(a.flag[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+    __builtin_amdgcn_s_sleep(4);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+      atomicAdd(a.err, 1ull);
+      break;
+    }
+  }
+}
+
+static uint64_t wait_timeout_ticks() {
+  static const uint64_t t = [] {
+    const char* v = std::getenv("ADVDIFF_IPC_TIMEOUT_S");
+    const double s = v ? std::atof(v) : 120.0;
+    return (uint64_t)(s * 1e8);
+  }();
+  return t;
+}
+
+}  // namespace advdiff
+
+extern "C" int advdiff_ipc_create(int world, int rank, advdiff_ipc** out) {
+  if (world < 1 || rank < 0 || rank >= world || out == nullptr) return hipErrorInvalidValue;
+  auto* c = new advdiff_ipc;
+  c->world = world;
+  c->rank = rank;
+  c->peer_cell.assign(world, nullptr);
+  const size_t bytes = (3 * (size_t)world + 1) * sizeof(uint64_t);
+  hipError_t e = hipMalloc(&c->block, bytes < 4096 ? 4096 : bytes);
+  if (e == hipSuccess) e = hipMemset(c->block, 0, bytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();  // setup only: zeroed before any peer maps it
+  if (e != hipSuccess) {
+    delete c;
+    return e;
+  }
+  *out = c;
+  return hipSuccess;
+}
+
+extern "C" int advdiff_ipc_destroy(advdiff_ipc* c) {
+  if (c == nullptr) return hipSuccess;
+  (void)hipDeviceSynchronize();
+  for (auto& kv : c->opened) (void)hipIpcCloseMemHandle(kv.second);
+  (void)hipFree(c->block);
+  delete c;
+  return hipSuccess;
+}
+
+// address of `ptr` as (IPC handle of its allocation, byte offset)
+extern "C" int advdiff_ipc_describe(advdiff_ipc* c, const void* ptr, advdiff_ipc_addr* out) {
+  if (c == nullptr || ptr == nullptr || out == nullptr) return hipErrorInvalidValue;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> g(c->mu);
+  auto it = c->exported.find((uintptr_t)base);
+  if (it == c->exported.end()) {
+    hipIpcMemHandle_t h;
+    e = hipIpcGetMemHandle(&h, base);
+    if (e != hipSuccess) return e;
+    it = c->exported.emplace((uintptr_t)base, h).first;
+  }
+  static_assert(sizeof(hipIpcMemHandle_t) <= sizeof(out->handle), "IPC handle size");
+  std::memset(out, 0, sizeof(*out));
+  std::memcpy(out->handle, &it->second, sizeof(hipIpcMemHandle_t));
+  out->offset = (uint64_t)((const char*)ptr - (const char*)base);
+  out->bytes = (uint64_t)size;
+  return hipSuccess;
+}
+
+extern "C" int advdiff_ipc_flags_addr(advdiff_ipc* c, advdiff_ipc_addr* out) {
+  return advdiff_ipc_describe(c, c ? c->recv() : nullptr, out);
+}
+
+// map a peer's address into this process (handles are opened once and cached)
+extern "C" int advdiff_ipc_map(advdiff_ipc* c, const advdiff_ipc_addr* a, void** ptr) {
+  if (c == nullptr || a == nullptr || ptr == nullptr) return hipErrorInvalidValue;
+  const std::string key((const char*)a->handle, sizeof(hipIpcMemHandle_t));
+  std::lock_guard<std::mutex> g(c->mu);
+  auto it = c->opened.find(key);
+  if (it == c->opened.end()) {
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, a->handle, sizeof(h));
+    void* base = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return e;
+    it = c->opened.emplace(key, base).first;
+  }
+  *ptr = (char*)it->second + a->offset;
+  return hipSuccess;
+}
+
+extern "C" int advdiff_ipc_set_peer(advdiff_ipc* c, int peer, const advdiff_ipc_addr* flags) {
+  if (c == nullptr || peer < 0 || peer >= c->world || peer == c->rank) return hipErrorInvalidValue;
+  void* base = nullptr;
+  const int e = advdiff_ipc_map(c, flags, &base);
+  if (e != hipSuccess) return e;
+  c->peer_cell[peer] = (uint64_t*)base + c->rank;  // the peer's recv[rank]
+  return hipSuccess;
+}
+
+extern "C" int advdiff_ipc_signal(advdiff_ipc* c, const int* peers, int n, void* stream) {
+  using namespace advdiff;
+  if (n <= 0) return hipSuccess;
+  if (c == nullptr || peers == nullptr || n > kIpcMaxPeers) return hipErrorInvalidValue;
+  IpcSignalArgs a{};
+  a.n = n;
+  for (int q = 0; q < n; ++q) {
+    const int p = peers[q];
+    if (p < 0 || p >= c->world || c->peer_cell[p] == nullptr) return hipErrorInvalidValue;
+    a.remote[q] = c->peer_cell[p];
+    a.sent[q] = c->sent() + p;
+  }
+  hipLaunchKernelGGL(ipc_signal_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
+  return hipGetLastError();
+}
+
+extern "C" int advdiff_ipc_wait(advdiff_ipc* c, const int* peers, int n, void* stream) {
+  using namespace advdiff;
+  if (n <= 0) return hipSuccess;
+  if (c == nullptr || peers == nullptr || n > kIpcMaxPeers) return hipErrorInvalidValue;
+  IpcWaitArgs a{};
+  a.n = n;
+  a.err = c->err();
+  a.timeout_ticks = wait_timeout_ticks();
+  for (int q = 0; q < n; ++q) {
+    const int p = peers[q];
+    if (p < 0 || p >= c->world || p == c->rank) return hipErrorInvalidValue;
+    a.flag[q] = c->recv() + p;
+    a.expect[q] = c->expect() + p;
+  }
+  hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
+  return hipGetLastError();
+}
+
+// wait timeouts so far (synchronous read: call at a sync point)
+extern "C" int advdiff_ipc_errors(advdiff_ipc* c, long long* timeouts) {
+  if (c == nullptr || timeouts == nullptr) return hipErrorInvalidValue;
+  unsigned long long h = 0;
+  const hipError_t e = hipMemcpy(&h, c->err(), sizeof(h), hipMemcpyDeviceToHost);
+  *timeouts = (long long)h;
+  return e;
+}

@@ -8,9 +8,12 @@
 //
 // plus named options (runtime replacements of the reference's #defines, §2.7):
 //   --ic NAME  --order 2|4  --safety S  --weno js|z|js7  --visc C  --fp32  --no-overlap
-//   --integrator ssprk3|lsrk45  --no-fused  --transport rccl|socket  --write FILE
-//   --error-norms  --decomp slab|PZxPYxPX|PYxPX (process grid in array order: Cartesian
-//   blocks, cart.cpp; default z-slabs as the reference)
+//   --integrator ssprk3|lsrk45  --no-fused  --transport rccl|ipc|socket  --write FILE
+//   --write-ghosts FILE (the reference's multi-GPU result.bin: every rank's slab WITH its
+//   ghost planes, MultiGPU/Diffusion3d_Baseline/main.c:341)  --error-norms
+//   --decomp slab|PZxPYxPX|PYxPX (process grid in array order: Cartesian blocks, cart.cpp;
+//   default z-slabs as the reference)  --geometry (print every rank's launch / halo
+//   geometry as JSON lines and exit; no GPU work)
 // Launch one process per GPU with torchrun-style env vars (RANK/WORLD_SIZE/LOCAL_RANK/
 // MASTER_ADDR/MASTER_PORT), e.g. via `python -m multigpu_advectiondiffusion_amd.launch`.
 #include <chrono>
@@ -39,7 +42,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
     std::string a = argv[q];
     if (a.rfind("--", 0) == 0) {
       const bool flag = a == "--fp32" || a == "--no-overlap" || a == "--error-norms" ||
-                        a == "--no-fused";
+                        a == "--no-fused" || a == "--geometry";
       if (flag || q + 1 >= argc) {
         opt[a] = "1";
       } else {
@@ -56,7 +59,8 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
               << (diff ? (dims == 3 ? " K L W H Nx Ny Nz iters [bx by bz]" : " K L W Nx Ny iters [bx by]")
                        : (dims == 3 ? " tEnd CFL L W H Nx Ny Nz [bx by bz]" : " tEnd CFL L W Nx Ny [bx by]"))
               << " [--ic NAME] [--order 2|4] [--weno js|z|js7] [--integrator ssprk3|lsrk45] [--no-fused] [--visc C] [--fp32] [--no-overlap]"
-                 " [--transport rccl|socket] [--decomp slab|PZxPYxPX|PYxPX] [--write FILE] [--error-norms]\n";
+                 " [--transport rccl|ipc|socket] [--decomp slab|PZxPYxPX|PYxPX] [--write FILE]"
+                 " [--write-ghosts FILE] [--error-norms] [--geometry]\n";
     return 1;
   }
   Problem p;
@@ -94,7 +98,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   if (opt.count("--visc")) p.C = std::stod(opt["--visc"]);
   if (opt.count("--fp32")) p.dtype = ADVDIFF_F32;
   if (opt.count("--no-overlap")) p.overlap = false;
-  std::string decomp = opt.count("--decomp") ? opt["--decomp"] : "slab";
+  const std::string decomp = opt.count("--decomp") ? opt["--decomp"] : "slab";
   std::string ic = opt.count("--ic") ? opt["--ic"] : (diff ? "heat" : "gaussian");
   p.ic = ic_code(ic);
   if (p.ic == 3) {
@@ -108,12 +112,17 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   }
 
   ProcEnv env = ProcEnv::from_env();
+  if (opt.count("--geometry")) {  // host-only: the geometry every rank would use
+    if (decomp != "slab") parse_pgrid(decomp, dims, env.size, p.pgrid);
+    for (int r = 0; r < env.size; ++r) std::cout << geometry_json(p, r, env.size) << "\n";
+    return 0;
+  }
   int ndev = 0;
   HIP_CHECK(hipGetDeviceCount(&ndev));
   if (ndev == 0) throw std::runtime_error("no HIP device");
   const std::string tk = opt.count("--transport") ? opt["--transport"] : "rccl";
-  if (env.size > ndev && tk != "socket")
-    throw std::runtime_error("more ranks than GPUs: one process per GPU (or --transport socket)");
+  if (env.size > ndev && tk != "socket" && tk != "ipc")
+    throw std::runtime_error("more ranks than GPUs: one process per GPU (or --transport ipc|socket)");
   HIP_CHECK(hipSetDevice(env.local_rank % ndev));
   HIP_CHECK((hipError_t)advdiff_preload());  // code objects loaded before the timed loop
   if (decomp != "slab") parse_pgrid(decomp, dims, env.size, p.pgrid);
@@ -132,11 +141,21 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   double l1 = 0, l2 = 0, li = 0;
   const bool norms = opt.count("--error-norms") && (p.ic == 2 || p.ic == 3);
   if (norms) eng.error_norms(l1, l2, li);
-  const double tw = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-  std::vector<float> g;
-  if (opt.count("--write")) g = eng.gather_float32();
-  st.dtoh = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() - tw;
+  // DtH: the barrier-fenced copy of the result to the host and its gather to rank 0
+  // (the reference's timed DtH + Merge_domains, MultiGPU/Diffusion3d_Baseline/main.c:313-335)
+  auto wall = [] {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  tr->barrier();
+  const double tw = wall();
+  std::vector<float> g = eng.gather_float32();
+  tr->barrier();
+  st.dtoh = tr->allreduce_max(wall() - tw);
+  std::vector<float> gg;
+  if (opt.count("--write-ghosts")) gg = eng.gather_float32_ghosts();
   if (env.rank == 0) {
+    std::cout << "advdiff native build: runtime " << advdiff_runtime_hash() << ", kernels "
+              << advdiff_source_hash() << "\n";
     if (pos.size() > need) std::cout << "(block sizes ignored: gfx950 tiles are fixed)\n";
     std::cout << summary_multigpu(title, optname, st, p, env.size);
     if (norms) {
@@ -145,6 +164,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
       std::printf("Linf norm                                     :  %e\n", li);
     }
     if (opt.count("--write")) write_binary(opt["--write"], g);
+    if (opt.count("--write-ghosts")) write_binary(opt["--write-ghosts"], gg);
     std::cout.flush();
   }
   tr->barrier();

@@ -88,6 +88,161 @@ void parse_pgrid(const std::string& spec, int dims, int world, int* pgrid) {
 }
 
 // ------------------------------------------------------------------------------------
+// Host-only geometry (shared by the Engine and the geometry dump)
+// ------------------------------------------------------------------------------------
+Cart make_cart(const Problem& p, int rank, int size, bool* fused) {
+  const int R = p.radius();
+  Cart cd;
+  cd.dims = p.dims;
+  cd.rank = rank;
+  if (p.dims == 3) {
+    cd.shape[0] = p.nz;
+    cd.shape[1] = p.ny;
+    cd.shape[2] = p.nx;
+  } else {
+    cd.shape[0] = p.ny;
+    cd.shape[1] = p.nx;
+  }
+  if (p.pgrid[0] > 0) {
+    for (int a = 0; a < 3; ++a) cd.pgrid[a] = a < p.dims ? p.pgrid[a] : 1;
+  } else {
+    cd.pgrid[0] = size;
+  }
+  if (cd.size() != size) throw std::runtime_error("process grid does not match WORLD_SIZE");
+  // fused: blocks at least 3R thick on every split axis (else per-stage, solver.py)
+  bool thick = true;
+  for (int a = 0; a < p.dims; ++a)
+    if (cd.pgrid[a] > 1 && cd.shape[a] / cd.pgrid[a] < 3 * R) thick = false;
+  const bool f = p.fused && p.physics == Physics::Diffusion && p.integrator == 0 && thick;
+  cd.ghost = f ? 3 * R : R;
+  for (int a = 0; a < p.dims; ++a)
+    if (cd.shape[a] < cd.pgrid[a] * std::max(cd.ghost_of_axis(a), 1))
+      throw std::runtime_error("block thinner than the ghost width: use fewer ranks");
+  if (fused) *fused = f;
+  return cd;
+}
+
+void fused_view(const Cart& cd, int radius, int border, int a, int lo, int hi, Range& view,
+                Range& act, Range& outr) {
+  const int R3 = 3 * radius;
+  const Slab ax = cd.axis(a);
+  view = {std::max(0, lo - R3), std::min(ax.alloc(), hi + R3)};
+  const int origin = ax.start() - ax.ghost + view.lo;
+  const int N = cd.shape[a];
+  act = {std::max(0, border - origin), std::min(view.hi - view.lo, N - border - origin)};
+  outr = {lo - view.lo, hi - view.lo};
+}
+
+std::vector<std::vector<HaloPlanMsg>> halo_plan(const Cart& cd, bool corners) {
+  const int dims = cd.dims, G = cd.ghost;
+  std::vector<std::vector<int>> phases;
+  std::vector<int> split;
+  for (int a = dims - 1; a >= 0; --a)
+    if (cd.pgrid[a] > 1) split.push_back(a);
+  if (corners)
+    for (int a : split) phases.push_back({a});
+  else if (!split.empty())
+    phases.push_back(split);
+  Range own[3], alloc[3];
+  for (int a = 0; a < dims; ++a) {
+    const Slab s = cd.axis(a);
+    own[a] = {s.ghost, s.ghost + s.count()};
+    alloc[a] = {0, s.alloc()};
+  }
+  std::vector<std::vector<HaloPlanMsg>> out;
+  for (const auto& axes : phases) {
+    std::vector<HaloPlanMsg> ph;
+    for (int a : axes)
+      for (int side : {-1, 1}) {
+        const int peer = cd.neighbor(a, side);
+        if (peer < 0) continue;
+        HaloPlanMsg m;
+        m.peer = peer;
+        m.axis = a;
+        m.side = side;
+        for (int q = 0; q < dims; ++q) {
+          const bool carried = corners && q > a;  // exchanged in an earlier phase
+          m.send.r[q] = m.recv.r[q] = carried ? alloc[q] : own[q];
+        }
+        m.send.r[a] = side < 0 ? Range{own[a].lo, own[a].lo + G} : Range{own[a].hi - G, own[a].hi};
+        m.recv.r[a] = side < 0 ? Range{0, G} : Range{own[a].hi, own[a].hi + G};
+        ph.push_back(m);
+      }
+    for (size_t i = 0; i < ph.size(); ++i)  // distinct peers per phase (one message each)
+      for (size_t j = i + 1; j < ph.size(); ++j)
+        if (ph[i].peer == ph[j].peer)
+          throw std::runtime_error("halo phase with two messages to one peer (a process-grid axis of 2 with periodic wrap?)");
+    out.push_back(ph);
+  }
+  return out;
+}
+
+static std::string jrange(const Range& r) {
+  return "[" + std::to_string(r.lo) + "," + std::to_string(r.hi) + "]";
+}
+static std::string jbox(const Box& b, int dims) {
+  std::string s = "[";
+  for (int a = 0; a < dims; ++a) s += (a ? "," : "") + jrange(b.r[a]);
+  return s + "]";
+}
+
+std::string geometry_json(const Problem& p, int rank, int size) {
+  bool fused = false;
+  Cart cd = make_cart(p, rank, size, &fused);
+  const int dims = p.dims, R = p.radius(), B = p.border();
+  Box full = cd.compute_box(B), interior;
+  std::vector<Box> bnd;
+  cd.split_boxes(B, cd.ghost, interior, bnd);
+  std::ostringstream o;
+  int c[3] = {0, 0, 0};
+  cd.coords_of(rank, c);
+  o << "{\"rank\":" << rank << ",\"coords\":[";
+  for (int a = 0; a < dims; ++a) o << (a ? "," : "") << c[a];
+  o << "],\"ghost\":" << cd.ghost << ",\"fused\":" << (fused ? "true" : "false") << ",\"alloc\":[";
+  for (int a = 0; a < dims; ++a) o << (a ? "," : "") << cd.axis(a).alloc();
+  o << "],\"own\":[";
+  for (int a = 0; a < dims; ++a) {
+    const Slab s = cd.axis(a);
+    o << (a ? "," : "") << jrange(Range{s.ghost, s.ghost + s.count()});
+  }
+  o << "],\"full\":" << jbox(full, dims) << ",\"interior\":" << jbox(interior, dims)
+    << ",\"boundary\":[";
+  for (size_t q = 0; q < bnd.size(); ++q) o << (q ? "," : "") << jbox(bnd[q], dims);
+  o << "],\"views\":[";
+  if (fused) {  // fused launches: (box, per x/y axis: view, active, output)
+    std::vector<Box> boxes{full, interior};
+    boxes.insert(boxes.end(), bnd.begin(), bnd.end());
+    bool first = true;
+    for (const Box& bx : boxes) {
+      if (bx.empty(dims)) continue;
+      o << (first ? "" : ",") << "{\"box\":" << jbox(bx, dims) << ",\"axes\":[";
+      first = false;
+      for (int a = 1; a < dims; ++a) {
+        Range v, act, outr;
+        fused_view(cd, R, B, a, bx.r[a].lo, bx.r[a].hi, v, act, outr);
+        o << (a > 1 ? "," : "") << "[" << jrange(v) << "," << jrange(act) << "," << jrange(outr)
+          << "]";
+      }
+      o << "]}";
+    }
+  }
+  o << "],\"halo\":[";
+  const auto plan = halo_plan(cd, fused);
+  for (size_t ph = 0; ph < plan.size(); ++ph) {
+    o << (ph ? "," : "") << "[";
+    for (size_t q = 0; q < plan[ph].size(); ++q) {
+      const HaloPlanMsg& m = plan[ph][q];
+      o << (q ? "," : "") << "{\"peer\":" << m.peer << ",\"axis\":" << m.axis
+        << ",\"side\":" << m.side << ",\"send\":" << jbox(m.send, dims)
+        << ",\"recv\":" << jbox(m.recv, dims) << "}";
+    }
+    o << "]";
+  }
+  o << "]}";
+  return o.str();
+}
+
+// ------------------------------------------------------------------------------------
 // Engine: Cartesian launches and exchange
 // ------------------------------------------------------------------------------------
 void Engine::launch_box(void* in, void* aux, void* out, const Box& bx, double dt, double a,
@@ -107,16 +262,8 @@ void Engine::launch_box(void* in, void* aux, void* out, const Box& bx, double dt
   }
 }
 
-// view window, active and output bounds (view coordinates) along array axis a for a
-// fused launch on local cells [lo, hi) (solver.py _fused_view)
 void Engine::fused_view(int a, int lo, int hi, Range& view, Range& act, Range& outr) const {
-  const int R3 = 3 * p_.radius();
-  const Slab ax = cd_.axis(a);
-  view = {std::max(0, lo - R3), std::min(ax.alloc(), hi + R3)};
-  const int origin = ax.start() - ax.ghost + view.lo;
-  const int B = p_.border(), N = cd_.shape[a];
-  act = {std::max(0, B - origin), std::min(view.hi - view.lo, N - B - origin)};
-  outr = {lo - view.lo, hi - view.lo};
+  rt::fused_view(cd_, p_.radius(), p_.border(), a, lo, hi, view, act, outr);
 }
 
 void Engine::launch_fused_box(const Box& bx, double dt, bool exclusive) {
@@ -170,83 +317,33 @@ void Engine::step_fused_cart(double dt) {
   start_halo_cart(u_);
 }
 
-void* Engine::halo_buf(size_t i, size_t bytes) {
-  if (hbufs_.size() <= i) {
-    hbufs_.resize(i + 1, nullptr);
-    hcap_.resize(i + 1, 0);
-  }
-  if (hcap_[i] < bytes) {
-    if (hbufs_[i]) HIP_CHECK(hipFree(hbufs_[i]));
-    HIP_CHECK(hipMalloc(&hbufs_[i], bytes));
-    hcap_[i] = bytes;
-  }
-  return hbufs_[i];
-}
-
 void Engine::start_halo_cart(void* field) {
   HIP_CHECK(hipEventRecord(ready_, compute_));
   HIP_CHECK(hipStreamWaitEvent(comm_, ready_, 0));
-  const int dims = p_.dims, G = slab_.ghost;
-  // phases: fastest split axis first; the fused step (corners) exchanges one axis per
-  // phase, each carrying the full allocated extent of the axes exchanged before it
-  std::vector<std::vector<int>> phases;
-  std::vector<int> split;
-  for (int a = dims - 1; a >= 0; --a)
-    if (cd_.pgrid[a] > 1) split.push_back(a);
-  if (fused_)
-    for (int a : split) phases.push_back({a});
-  else if (!split.empty())
-    phases.push_back(split);
-  Range own[3];
-  for (int a = 0; a < dims; ++a) {
-    const Slab s = cd_.axis(a);
-    own[a] = {s.ghost, s.ghost + s.count()};
-  }
-  size_t slot = 0;
-  for (const auto& axes : phases) {
-    std::vector<Msg> msgs;
-    struct Unpack {
-      Box b;
-      void* buf;
-    };
-    std::vector<Unpack> unpack;
-    for (int a : axes)
-      for (int side : {-1, 1}) {
-        const int peer = cd_.neighbor(a, side);
-        if (peer < 0) continue;
-        Box sb, rb;
-        for (int q = 0; q < dims; ++q) {
-          const bool carried = fused_ && q > a;  // exchanged in an earlier phase
-          sb.r[q] = rb.r[q] = carried ? Range{0, alloc_[q]} : own[q];
-        }
-        sb.r[a] = side < 0 ? Range{own[a].lo, own[a].lo + G} : Range{own[a].hi - G, own[a].hi};
-        rb.r[a] = side < 0 ? Range{0, G} : Range{own[a].hi, own[a].hi + G};
-        // extents as (nk, nj, ni) = (z, y, x); 2-D: one "plane" of rows
-        const int nk = dims == 3 ? sb.r[0].hi - sb.r[0].lo : 1;
-        const int nj = sb.r[dims - 2].hi - sb.r[dims - 2].lo;
-        const int ni = sb.r[dims - 1].hi - sb.r[dims - 1].lo;
-        const size_t bytes = (size_t)nk * nj * ni * elem_;
-        void* sbuf = halo_buf(slot++, bytes);
-        void* rbuf = halo_buf(slot++, bytes);
-        auto origin = [&](const Box& b) {
-          return dims == 3 ? at(field, b.r[0].lo, b.r[1].lo, b.r[2].lo)
-                           : at(field, 0, b.r[0].lo, b.r[1].lo);
-        };
-        KERNEL_CHECK(advdiff_copy_box(p_.dtype, sbuf, ni, (int64_t)ni * nj, origin(sb), sy_,
-                                      dims == 3 ? sz_ : 0, ni, nj, nk, comm_));
-        msgs.push_back(Msg{peer, sbuf, rbuf, bytes});
-        unpack.push_back(Unpack{rb, rbuf});
-      }
-    tr_->exchange(msgs, comm_);
-    for (const Unpack& u : unpack) {
-      const int nk = dims == 3 ? u.b.r[0].hi - u.b.r[0].lo : 1;
-      const int nj = u.b.r[dims - 2].hi - u.b.r[dims - 2].lo;
-      const int ni = u.b.r[dims - 1].hi - u.b.r[dims - 1].lo;
-      void* dst = dims == 3 ? at(field, u.b.r[0].lo, u.b.r[1].lo, u.b.r[2].lo)
-                            : at(field, 0, u.b.r[0].lo, u.b.r[1].lo);
-      KERNEL_CHECK(advdiff_copy_box(p_.dtype, dst, sy_, dims == 3 ? sz_ : 0, u.buf, ni,
-                                    (int64_t)ni * nj, ni, nj, nk, comm_));
+  const int dims = p_.dims;
+  auto origin = [&](const Box& b) {
+    return dims == 3 ? at(field, b.r[0].lo, b.r[1].lo, b.r[2].lo)
+                     : at(field, 0, b.r[0].lo, b.r[1].lo);
+  };
+  // phases are stream-ordered on comm_: a phase's sends carry the ghosts that the phases
+  // before it received
+  for (const auto& phase : plan_) {
+    std::vector<BoxMsg> msgs;
+    for (const HaloPlanMsg& m : phase) {
+      BoxMsg b;
+      b.peer = m.peer;
+      b.dtype = p_.dtype;
+      b.send = origin(m.send);
+      b.recv = origin(m.recv);
+      b.ssy = b.rsy = sy_;
+      b.ssz = b.rsz = dims == 3 ? sz_ : 0;
+      // extents as (ni, nj, nk) = (x, y, z); 2-D: one "plane" of rows
+      b.nk = dims == 3 ? m.send.r[0].hi - m.send.r[0].lo : 1;
+      b.nj = m.send.r[dims - 2].hi - m.send.r[dims - 2].lo;
+      b.ni = m.send.r[dims - 1].hi - m.send.r[dims - 1].lo;
+      msgs.push_back(b);
     }
+    tr_->exchange_boxes(msgs, comm_);
   }
   HIP_CHECK(hipEventRecord(halo_done_, comm_));
   halo_pending_ = true;

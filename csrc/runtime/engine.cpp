@@ -49,34 +49,9 @@ static double now_s() {
 }
 
 Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_(tr), env_(env) {
-  const int R = p.radius();
-  // process grid (array order); default: slabs along the slowest axis
-  cd_.dims = p.dims;
-  cd_.rank = env.rank;
-  if (p.dims == 3) {
-    cd_.shape[0] = p.nz;
-    cd_.shape[1] = p.ny;
-    cd_.shape[2] = p.nx;
-  } else {
-    cd_.shape[0] = p.ny;
-    cd_.shape[1] = p.nx;
-  }
-  if (p.pgrid[0] > 0) {
-    for (int a = 0; a < 3; ++a) cd_.pgrid[a] = a < p.dims ? p.pgrid[a] : 1;
-  } else {
-    cd_.pgrid[0] = env.size;
-  }
-  if (cd_.size() != env.size) throw std::runtime_error("process grid does not match WORLD_SIZE");
+  // process grid (array order; default: slabs along the slowest axis) and ghost width
+  cd_ = make_cart(p, env.rank, env.size, &fused_);
   cart_ = !cd_.is_slab();
-  // fused: blocks at least 3R thick on every split axis (else per-stage, solver.py)
-  bool thick = true;
-  for (int a = 0; a < p.dims; ++a)
-    if (cd_.pgrid[a] > 1 && cd_.shape[a] / cd_.pgrid[a] < 3 * R) thick = false;
-  fused_ = p.fused && p.physics == Physics::Diffusion && p.integrator == 0 && thick;
-  cd_.ghost = fused_ ? 3 * R : R;
-  for (int a = 0; a < p.dims; ++a)
-    if (cd_.shape[a] < cd_.pgrid[a] * std::max(cd_.ghost_of_axis(a), 1))
-      throw std::runtime_error("block thinner than the ghost width: use fewer ranks");
   slab_ = cd_.axis(0);
   for (int a = 0; a < p.dims; ++a) alloc_[a] = cd_.axis(a).alloc();
   elem_ = p.dtype == ADVDIFF_F64 ? 8 : 4;
@@ -92,20 +67,28 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
     plane_bytes_ = (size_t)sx * elem_;
   }
   field_bytes_ = plane_bytes_ * (size_t)alloc_[0];
-  HIP_CHECK(hipMalloc(&u_, field_bytes_));
-  HIP_CHECK(hipMalloc(&A_, field_bytes_));
-  HIP_CHECK(hipMalloc(&B_, field_bytes_));
-  // all three zeroed: cells a step never writes (ghost edges / corners at physical faces of a
-  // Cartesian block) are packed and sent, and a reused allocation would carry stale values
-  HIP_CHECK(hipMemset(u_, 0, field_bytes_));
-  HIP_CHECK(hipMemset(A_, 0, field_bytes_));
-  HIP_CHECK(hipMemset(B_, 0, field_bytes_));
   int lo_pri = 0, hi_pri = 0;
   HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri));
   HIP_CHECK(hipStreamCreateWithPriority(&compute_, hipStreamNonBlocking, lo_pri));
   HIP_CHECK(hipStreamCreateWithPriority(&comm_, hipStreamNonBlocking, hi_pri));
   HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&halo_done_, hipEventDisableTiming));
+  // Field setup, timed like the reference's barrier-fenced HtD copy of the initial
+  // subdomain (MultiGPU/Diffusion3d_Baseline/main.c:137-148): here the IC is generated
+  // on the device, so this is the allocation + IC kernel + stage-buffer copies.
+  HIP_CHECK(hipDeviceSynchronize());
+  tr_->barrier();
+  const double ts = now_s();
+  HIP_CHECK(hipMalloc(&u_, field_bytes_));
+  HIP_CHECK(hipMalloc(&A_, field_bytes_));
+  HIP_CHECK(hipMalloc(&B_, field_bytes_));
+  // Stream-ordered fill of the whole allocation (row padding included) BEFORE the IC.  A
+  // synchronous hipMemset on the null stream is NOT ordered before work on the
+  // non-blocking compute stream: it can land after the IC kernel and zero part of it
+  // (bench/native/ipc_probe.hip: 20 of 20 trials, profiles/probe_memset_ipc_r3.log) —
+  // the cause of the intermittent 8-rank 2x2x2 Cartesian mismatch of round 2.
+  const int fill = poison_enabled() ? 0xFF : 0;
+  HIP_CHECK(hipMemsetAsync(u_, fill, field_bytes_, compute_));
   // initial condition on the device, ghosts included (they equal the neighbours' cells)
   int off[3] = {0, 0, 0};
   for (int a = 0; a < p.dims; ++a) {
@@ -127,16 +110,21 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
     KERNEL_CHECK(advdiff_init_ic_box(p.dtype, p.ic, u_, alloc_[1], alloc_[0], 1, sy_, sz_, off[1],
                                      off[0], 0, p.nx, p.ny, 1, p.dx(), p.dy(), 0.0, p.ic_p0,
                                      p.ic_p1, compute_));
+  // A (and B) start as copies of u, padding included: cells a step never writes (frozen
+  // boundary cells, unwritten ghost edges) carry the IC in every buffer
   HIP_CHECK(hipMemcpyAsync(A_, u_, field_bytes_, hipMemcpyDeviceToDevice, compute_));
   if (p.integrator == 1)
     HIP_CHECK(hipMemsetAsync(B_, 0, field_bytes_, compute_));  // du
   else
     HIP_CHECK(hipMemcpyAsync(B_, u_, field_bytes_, hipMemcpyDeviceToDevice, compute_));
   HIP_CHECK(hipStreamSynchronize(compute_));
+  tr_->barrier();
+  init_s_ = tr_->allreduce_max(now_s() - ts);
   full_ = slab_.compute_range(p.border());
   slab_.split(p.border(), slab_.ghost, interior_, blo_, bhi_);
   full_box_ = cd_.compute_box(p.border());
   cd_.split_boxes(p.border(), cd_.ghost, interior_box_, boundary_boxes_);
+  if (cart_) plan_ = halo_plan(cd_, fused_);
   const int zoff = slab_.start() - slab_.ghost;
   zact_ = {std::max(0, p.border() - zoff), std::min(slab_.alloc(), slab_.n - p.border() - zoff)};
   t_ = p.t0;
@@ -152,8 +140,6 @@ Engine::~Engine() {
   (void)hipFree(u_);
   (void)hipFree(A_);
   (void)hipFree(B_);
-  for (void* b : hbufs_)
-    if (b) (void)hipFree(b);
 }
 
 double Engine::stable_dt() const {
@@ -346,6 +332,8 @@ Stats Engine::run_iters(int iters) {
   s.seconds = tr_->allreduce_max(now_s() - t0);
   s.steps = iters;
   s.t = t_;
+  s.htod = init_s_;
+  check_transport();
   return s;
 }
 
@@ -368,6 +356,8 @@ Stats Engine::run_until(double t_end) {
   s.seconds = tr_->allreduce_max(now_s() - t0);
   s.steps = n;
   s.t = t_;
+  s.htod = init_s_;
+  check_transport();
   return s;
 }
 
@@ -443,6 +433,36 @@ std::vector<float> Engine::gather_float32() {
   std::vector<float> out(all.size() / sizeof(float));
   if (!all.empty()) std::memcpy(out.data(), all.data(), all.size());
   return out;
+}
+
+// every rank's planes with their ghost planes (slabs), concatenated in rank order
+std::vector<float> Engine::gather_float32_ghosts() {
+  HIP_CHECK(hipStreamSynchronize(comm_));
+  HIP_CHECK(hipStreamSynchronize(compute_));
+  if (cart_) throw std::runtime_error("--write-ghosts: slab decompositions only");
+  std::vector<char> raw(field_bytes_);
+  HIP_CHECK(hipMemcpy(raw.data(), u_, raw.size(), hipMemcpyDeviceToHost));
+  const int rows = p_.dims == 3 ? slab_.alloc() * p_.ny : slab_.alloc();
+  std::vector<char> packed((size_t)rows * p_.nx * sizeof(float));
+  float* dst = (float*)packed.data();
+  for (int r = 0; r < rows; ++r)
+    for (int i = 0; i < p_.nx; ++i) {
+      const size_t src = (size_t)r * sy_ + i;
+      dst[(size_t)r * p_.nx + i] = elem_ == 8 ? (float)((const double*)raw.data())[src]
+                                              : ((const float*)raw.data())[src];
+    }
+  std::vector<char> all = tr_->gather(packed);
+  std::vector<float> out(all.size() / sizeof(float));
+  if (!all.empty()) std::memcpy(out.data(), all.data(), all.size());
+  return out;
+}
+
+void Engine::check_transport() {
+  const long long e = tr_->allreduce_max((double)tr_->errors());
+  if (e > 0) {
+    std::fprintf(stderr, "transport %s: %lld halo wait timeout(s): a peer stopped\n", tr_->name(), e);
+    std::exit(5);
+  }
 }
 
 static std::string fmt(const char* f, double v) {

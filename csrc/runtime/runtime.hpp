@@ -19,6 +19,10 @@
 
 #include "advdiff/kernels.h"
 
+// sha256 prefix of the runtime + app sources the executable was built from
+// (csrc/Makefile RT_HASH; tests compare it with the tree)
+extern "C" const char* advdiff_runtime_hash(void);
+
 #define HIP_CHECK(expr)                                                                    \
   do {                                                                                     \
     hipError_t e_ = (expr);                                                                \
@@ -63,12 +67,34 @@ struct Msg {
   size_t bytes = 0;
 };
 
+// A strided box message: the ni x nj x nk box of elements at `send` (pitches ssy, ssz,
+// elements) goes to `peer`, and the peer's matching box arrives in the box at `recv`
+// (pitches rsy, rsz).  Both boxes live in the caller's fields.
+struct BoxMsg {
+  int peer = -1;
+  int dtype = ADVDIFF_F64;
+  const void* send = nullptr;
+  int64_t ssy = 0, ssz = 0;
+  void* recv = nullptr;
+  int64_t rsy = 0, rsz = 0;
+  int ni = 0, nj = 0, nk = 0;
+  size_t elem() const { return dtype == ADVDIFF_F64 ? 8 : 4; }
+  size_t bytes() const { return (size_t)ni * nj * nk * elem(); }
+  bool send_contiguous() const { return (nj == 1 || ssy == ni) && (nk == 1 || ssz == (int64_t)ni * nj); }
+  bool recv_contiguous() const { return (nj == 1 || rsy == ni) && (nk == 1 || rsz == (int64_t)ni * nj); }
+};
+
 class Transport {
  public:
-  virtual ~Transport() = default;
+  virtual ~Transport();
   virtual const char* name() const = 0;
   // Enqueue a set of messages to distinct peers on `stream` (one grouped RCCL call).
   virtual void exchange(const std::vector<Msg>& msgs, hipStream_t stream) = 0;
+  // Enqueue a set of box messages to distinct peers on `stream`.  Default: strided boxes
+  // are packed into / unpacked from device staging buffers with advdiff_copy_box around
+  // one exchange() (contiguous boxes go zero-copy); the IPC transport overrides it with
+  // direct puts into the peer's field.
+  virtual void exchange_boxes(const std::vector<BoxMsg>& msgs, hipStream_t stream);
   // Enqueue the exchange of G-plane slabs (bytes each) with the lower/upper neighbour
   // (-1 = none) on `stream`: send_lo -> lower's recv_hi, send_hi -> upper's recv_lo.
   virtual void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
@@ -78,7 +104,21 @@ class Transport {
   virtual void barrier() = 0;
   // Gather per-rank host byte blocks to rank 0 (returns the concatenation on rank 0).
   virtual std::vector<char> gather(const std::vector<char>& local) = 0;
+  // Wait timeouts or other deferred transport errors seen so far (call at a sync point).
+  virtual long long errors() { return 0; }
+
+ protected:
+  void* staging(size_t slot, size_t bytes, hipStream_t stream);  // device staging buffer
+
+ private:
+  std::vector<void*> stage_;
+  std::vector<size_t> stage_cap_;
 };
+
+// Debug: ADVDIFF_POISON=1 fills every device allocation of the runtime (fields incl. row
+// padding and ghost shells, staging buffers) and the host staging buffers with 0xFF bytes
+// (a NaN in fp32 and fp64) instead of zeros, so a read of a cell nobody wrote shows up.
+bool poison_enabled();
 
 // rank 0 <-> all TCP star used for bootstrap, scalars and gathers by every transport.
 class Star;
@@ -142,6 +182,18 @@ struct Cart {
 // "PZxPYxPX" / "PYxPX" -> pgrid (array order); throws on a mismatch with dims / world
 void parse_pgrid(const std::string& spec, int dims, int world, int* pgrid);
 
+// One message of a halo phase, in local (array-order) boxes of the block incl. ghosts.
+struct HaloPlanMsg {
+  int peer = -1, axis = 0, side = 0;
+  Box send, recv;
+};
+// Halo phases of a Cartesian block (mirror of parallel/halo.py CartesianHalo): corners =
+// false (per-stage star stencils): ONE phase with the faces of every split axis over the
+// owned extent of the other axes; corners = true (the fused step): one phase per split
+// axis, fastest first, each message spanning the FULL allocated extent of the axes
+// exchanged before it (so edge and corner ghosts arrive with the faces).
+std::vector<std::vector<HaloPlanMsg>> halo_plan(const Cart& cd, bool corners);
+
 // ------------------------------------------------------------------------------------
 // Problem + engine
 // ------------------------------------------------------------------------------------
@@ -185,6 +237,17 @@ struct Stats {
   double seconds = 0, htod = 0, dtoh = 0, t = 0;
 };
 
+// The block decomposition an Engine builds for a problem on `size` ranks (process grid,
+// ghost width; fused = the one-launch-per-step heat path is used).  Host-only.
+Cart make_cart(const Problem& p, int rank, int size, bool* fused);
+// View window, active and output bounds (view coordinates) along array axis a of a fused
+// launch on local cells [lo, hi) (solver.py _fused_view).  Host-only.
+void fused_view(const Cart& cd, int radius, int border, int a, int lo, int hi, Range& view,
+                Range& act, Range& outr);
+// Every launch box, fused-step view and halo message of `rank` as one JSON object
+// (geometry checks against the Python decomposition: tests/test_native_geometry.py).
+std::string geometry_json(const Problem& p, int rank, int size);
+
 class Engine {
  public:
   Engine(const Problem& p, Transport* tr, const ProcEnv& env);
@@ -196,6 +259,11 @@ class Engine {
   // Σ|u-e|, Σ(u-e)², max|u-e| over the owned slab vs the exact solution (sine/heat ICs)
   void error_norms(double& l1, double& l2, double& linf);
   std::vector<float> gather_float32();  // rank 0: global array (no ghosts); others empty
+  // rank 0: every rank's planes INCLUDING its ghost planes, concatenated in rank order —
+  // the reference's multi-GPU result.bin layout (each rank's Nx x Ny x (_Nz + 6) slab,
+  // SaveBinary3D(h_u, Nx, Ny, NZ), MultiGPU/Diffusion3d_Baseline/main.c:341).  Slabs only.
+  std::vector<float> gather_float32_ghosts();
+  double init_seconds() const { return init_s_; }  // barrier-fenced field setup (HtD line)
   double time() const { return t_; }
   int iteration() const { return it_; }
   const Slab& slab() const { return slab_; }
@@ -227,10 +295,10 @@ class Engine {
   void stage_cart(void* in, void* aux, void* out, double a, double b, double dt, bool ls);
   void step_fused_cart(double dt);
   void start_halo_cart(void* field);
-  void* halo_buf(size_t i, size_t bytes);
   void error_norms_cart(double& l1, double& l2, double& linf);
   std::vector<float> gather_cart();
   double exact_scale() const;  // decay factor of the exact solution at t_ (sine / heat ICs)
+  void check_transport();      // exits if the transport reported deferred errors
 
   Problem p_;
   Transport* tr_;
@@ -247,8 +315,8 @@ class Engine {
   int alloc_[3] = {1, 1, 1};  // local extents incl. ghosts (array order)
   Box full_box_, interior_box_;
   std::vector<Box> boundary_boxes_;
-  std::vector<void*> hbufs_;
-  std::vector<size_t> hcap_;
+  std::vector<std::vector<HaloPlanMsg>> plan_;  // Cartesian halo phases
+  double init_s_ = 0;                          // barrier-fenced field setup time
   hipStream_t compute_ = nullptr, comm_ = nullptr;
   hipEvent_t ready_ = nullptr, halo_done_ = nullptr;
   bool halo_pending_ = false;

@@ -11,6 +11,11 @@
 //    share ONE GPU (RCCL refuses that), so the native multi-rank path is testable on a
 //    single-GPU box; it is also the reference's own transport pattern (D2H -> send ->
 //    recv -> H2D, main.c:209-288).
+//  * IpcTransport: peer-mapped puts (kernels/ipc.hip): a rank's
+//    copy kernel writes its boundary box straight into the neighbour's ghost box (field
+//    mapped with hipIpcOpenMemHandle), then raises the neighbour's device flag; the
+//    receiving stream waits on its own flags.  No host synchronisation, no staging, no
+//    pack/unpack; across GPUs over xGMI, and between ranks sharing one GPU (tests).
 #include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/in.h>
@@ -22,7 +27,9 @@
 
 #include <chrono>
 #include <cstring>
+#include <map>
 #include <thread>
+#include <tuple>
 
 #include "runtime.hpp"
 
@@ -31,6 +38,77 @@ namespace advdiff::rt {
 static int env_int(const char* k, int def) {
   const char* v = std::getenv(k);
   return v ? std::atoi(v) : def;
+}
+
+bool poison_enabled() {
+  static const bool on = env_int("ADVDIFF_POISON", 0) != 0;
+  return on;
+}
+
+Transport::~Transport() {
+  for (void* b : stage_)
+    if (b) (void)hipFree(b);
+}
+
+void* Transport::staging(size_t slot, size_t bytes, hipStream_t stream) {
+  if (stage_.size() <= slot) {
+    stage_.resize(slot + 1, nullptr);
+    stage_cap_.resize(slot + 1, 0);
+  }
+  if (stage_cap_[slot] < bytes) {
+    if (stage_[slot]) {
+      HIP_CHECK(hipStreamSynchronize(stream));  // the old buffer may still be in use
+      HIP_CHECK(hipFree(stage_[slot]));
+    }
+    HIP_CHECK(hipMalloc(&stage_[slot], bytes));
+    if (poison_enabled()) HIP_CHECK(hipMemsetAsync(stage_[slot], 0xFF, bytes, stream));
+    stage_cap_[slot] = bytes;
+  }
+  return stage_[slot];
+}
+
+// pack strided send boxes, one exchange(), unpack strided receive boxes (stream-ordered)
+void Transport::exchange_boxes(const std::vector<BoxMsg>& msgs, hipStream_t s) {
+  std::vector<Msg> flat;
+  struct Unpack {
+    const BoxMsg* m;
+    void* buf;
+  };
+  std::vector<Unpack> unpack;
+  size_t slot = 0;
+  for (const BoxMsg& m : msgs) {
+    Msg f;
+    f.peer = m.peer;
+    f.bytes = m.bytes();
+    if (m.send_contiguous()) {
+      f.send = m.send;
+    } else {
+      void* b = staging(slot++, f.bytes, s);
+      KERNEL_CHECK(advdiff_copy_box(m.dtype, b, m.ni, (int64_t)m.ni * m.nj, m.send, m.ssy, m.ssz,
+                                    m.ni, m.nj, m.nk, s));
+      f.send = b;
+    }
+    if (m.recv_contiguous()) {
+      f.recv = m.recv;
+    } else {
+      f.recv = staging(slot++, f.bytes, s);
+      unpack.push_back(Unpack{&m, f.recv});
+    }
+    flat.push_back(f);
+  }
+  exchange(flat, s);
+  for (const Unpack& u : unpack) {
+    const BoxMsg& m = *u.m;
+    KERNEL_CHECK(advdiff_copy_box(m.dtype, m.recv, m.rsy, m.rsz, u.buf, m.ni, (int64_t)m.ni * m.nj,
+                                  m.ni, m.nj, m.nk, s));
+  }
+}
+
+static void check_distinct_peers(const std::vector<int>& peers) {
+  for (size_t i = 0; i < peers.size(); ++i)
+    for (size_t j = i + 1; j < peers.size(); ++j)
+      if (peers[i] == peers[j])
+        throw std::runtime_error("transport: two messages to one peer in one exchange");
 }
 
 ProcEnv ProcEnv::from_env() {
@@ -238,18 +316,18 @@ class RcclTransport final : public Transport {
   ncclComm_t comm_ = nullptr;
 };
 
-// ---------------------------------------------------------------- host-staged TCP
-class SocketTransport final : public Transport {
+// ---------------------------------------------------------------- TCP full mesh
+// rank j > i connects to rank i's listener (port MASTER_PORT+1+i), so any pair of ranks
+// (slab neighbours, Cartesian faces) has its own socket
+class Mesh {
  public:
-  // full mesh: rank j > i connects to rank i's listener (port MASTER_PORT+1+i), so any
-  // pair of ranks (slab neighbours, Cartesian faces) has its own socket
-  explicit SocketTransport(const ProcEnv& e) : star_(e), env_(e) {
+  Mesh(const ProcEnv& e, Star& star) {
     if (e.size == 1) return;
     fds_.assign(e.size, -1);
     const int base = e.master_port + 1;
     int lfd = -1;
     if (e.rank < e.size - 1) lfd = listen_on(base + e.rank);
-    star_.reduce(0.0, false);  // every listener is up
+    star.reduce(0.0, false);  // every listener is up
     for (int q = 0; q < e.rank; ++q) {
       fds_[q] = connect_to("127.0.0.1", base + q);
       send_all(fds_[q], &e.rank, sizeof(int));
@@ -264,9 +342,32 @@ class SocketTransport final : public Transport {
     }
     if (lfd >= 0) ::close(lfd);
   }
-  ~SocketTransport() override {
+  ~Mesh() {
     for (int fd : fds_)
       if (fd >= 0) ::close(fd);
+  }
+  int fd(int peer) const { return fds_[peer]; }
+  // send out[q] to peers[q] and receive in[q] from peers[q] (distinct peers): one sender
+  // thread per message, so a send that blocks on a full socket never stalls the receives
+  void swap(const std::vector<int>& peers, const std::vector<const void*>& out,
+            const std::vector<void*>& in, const std::vector<size_t>& bytes) {
+    check_distinct_peers(peers);
+    std::vector<std::thread> tx;
+    for (size_t q = 0; q < peers.size(); ++q)
+      tx.emplace_back([&, q] { send_all(fds_[peers[q]], out[q], bytes[q]); });
+    for (size_t q = 0; q < peers.size(); ++q) recv_all(fds_[peers[q]], in[q], bytes[q]);
+    for (auto& t : tx) t.join();
+  }
+
+ private:
+  std::vector<int> fds_;
+};
+
+// ---------------------------------------------------------------- host-staged TCP
+class SocketTransport final : public Transport {
+ public:
+  explicit SocketTransport(const ProcEnv& e) : star_(e), mesh_(e, star_), env_(e) {}
+  ~SocketTransport() override {
     if (h_send_) (void)hipHostFree(h_send_);
     if (h_recv_) (void)hipHostFree(h_recv_);
   }
@@ -280,28 +381,29 @@ class SocketTransport final : public Transport {
       if (h_recv_) (void)hipHostFree(h_recv_);
       HIP_CHECK(hipHostMalloc(&h_send_, total));
       HIP_CHECK(hipHostMalloc(&h_recv_, total));
+      if (poison_enabled()) {
+        std::memset(h_send_, 0xFF, total);
+        std::memset(h_recv_, 0xFF, total);
+      }
       cap_ = total;
     }
-    std::vector<size_t> off(msgs.size());
+    std::vector<int> peers;
+    std::vector<const void*> out;
+    std::vector<void*> in;
+    std::vector<size_t> bytes;
     size_t o = 0;
-    for (size_t q = 0; q < msgs.size(); ++q) {
-      off[q] = o;
-      HIP_CHECK(hipMemcpyAsync((char*)h_send_ + o, msgs[q].send, msgs[q].bytes,
-                               hipMemcpyDeviceToHost, s));
-      o += msgs[q].bytes;
+    for (const Msg& m : msgs) {
+      HIP_CHECK(hipMemcpyAsync((char*)h_send_ + o, m.send, m.bytes, hipMemcpyDeviceToHost, s));
+      peers.push_back(m.peer);
+      out.push_back((char*)h_send_ + o);
+      in.push_back((char*)h_recv_ + o);
+      bytes.push_back(m.bytes);
+      o += m.bytes;
     }
     HIP_CHECK(hipStreamSynchronize(s));
-    // one sender thread per message: a send that blocks on a full socket never stalls
-    // the receives below, whatever order the peers read in
-    std::vector<std::thread> tx;
+    mesh_.swap(peers, out, in, bytes);
     for (size_t q = 0; q < msgs.size(); ++q)
-      tx.emplace_back([&, q] { send_all(fds_[msgs[q].peer], (char*)h_send_ + off[q], msgs[q].bytes); });
-    for (size_t q = 0; q < msgs.size(); ++q)
-      recv_all(fds_[msgs[q].peer], (char*)h_recv_ + off[q], msgs[q].bytes);
-    for (auto& t : tx) t.join();
-    for (size_t q = 0; q < msgs.size(); ++q)
-      HIP_CHECK(hipMemcpyAsync(msgs[q].recv, (char*)h_recv_ + off[q], msgs[q].bytes,
-                               hipMemcpyHostToDevice, s));
+      HIP_CHECK(hipMemcpyAsync(msgs[q].recv, in[q], msgs[q].bytes, hipMemcpyHostToDevice, s));
     HIP_CHECK(hipStreamSynchronize(s));  // staging buffers are reused next call
   }
   void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
@@ -315,10 +417,166 @@ class SocketTransport final : public Transport {
 
  private:
   Star star_;
+  Mesh mesh_;
   ProcEnv env_;
-  std::vector<int> fds_;
   void *h_send_ = nullptr, *h_recv_ = nullptr;
   size_t cap_ = 0;
+};
+
+// ---------------------------------------------------------------- IPC peer puts
+class IpcTransport final : public Transport {
+ public:
+  explicit IpcTransport(const ProcEnv& e) : star_(e), mesh_(e, star_), env_(e) {
+    ipc_check(advdiff_ipc_create(e.size, e.rank, &ctx_), "advdiff_ipc_create");
+    advdiff_ipc_addr mine;
+    ipc_check(advdiff_ipc_flags_addr(ctx_, &mine), "advdiff_ipc_flags_addr");
+    // every rank maps every other rank's flag block (small; any pair may be neighbours)
+    std::vector<int> peers;
+    for (int q = 0; q < e.size; ++q)
+      if (q != e.rank) peers.push_back(q);
+    std::vector<advdiff_ipc_addr> theirs(peers.size());
+    std::vector<const void*> out(peers.size(), &mine);
+    std::vector<void*> in;
+    for (auto& t : theirs) in.push_back(&t);
+    mesh_.swap(peers, out, in, std::vector<size_t>(peers.size(), sizeof(advdiff_ipc_addr)));
+    for (size_t q = 0; q < peers.size(); ++q)
+      ipc_check(advdiff_ipc_set_peer(ctx_, peers[q], &theirs[q]), "advdiff_ipc_set_peer");
+    star_.reduce(0.0, false);  // all mapped before anyone signals
+  }
+  ~IpcTransport() override {
+    (void)hipDeviceSynchronize();
+    star_.reduce(0.0, false);  // nobody unmaps while a peer may still put into it
+    advdiff_ipc_destroy(ctx_);
+  }
+  const char* name() const override { return "ipc"; }
+
+  void exchange_boxes(const std::vector<BoxMsg>& msgs, hipStream_t s) override {
+    if (msgs.empty()) return;
+    std::vector<int> peers;
+    for (const BoxMsg& m : msgs) peers.push_back(m.peer);
+    check_distinct_peers(peers);
+    const std::vector<Dest> dst = resolve(msgs);
+    for (size_t q = 0; q < msgs.size(); ++q) {  // the put: my box -> the peer's ghost box
+      const BoxMsg& m = msgs[q];
+      KERNEL_CHECK(advdiff_copy_box(m.dtype, dst[q].ptr, dst[q].sy, dst[q].sz, m.send, m.ssy,
+                                    m.ssz, m.ni, m.nj, m.nk, s));
+    }
+    ipc_check(advdiff_ipc_signal(ctx_, peers.data(), (int)peers.size(), s), "advdiff_ipc_signal");
+    ipc_check(advdiff_ipc_wait(ctx_, peers.data(), (int)peers.size(), s), "advdiff_ipc_wait");
+  }
+  void exchange(const std::vector<Msg>& msgs, hipStream_t s) override {
+    std::vector<BoxMsg> b;
+    for (const Msg& m : msgs) b.push_back(flat_box(m.peer, m.send, m.recv, m.bytes));
+    exchange_boxes(b, s);
+  }
+  void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
+            size_t bytes, int lower, int upper, hipStream_t s) override {
+    exchange(neighbour_msgs(send_lo, recv_lo, send_hi, recv_hi, bytes, lower, upper), s);
+  }
+  double allreduce_max(double v) override { return star_.reduce(v, true); }
+  double allreduce_sum(double v) override { return star_.reduce(v, false); }
+  void barrier() override { star_.reduce(0.0, false); }
+  std::vector<char> gather(const std::vector<char>& local) override { return star_.gather(local); }
+  long long errors() override {
+    long long n = 0;
+    ipc_check(advdiff_ipc_errors(ctx_, &n), "advdiff_ipc_errors");
+    return n;
+  }
+
+ private:
+  struct Dest {
+    void* ptr = nullptr;
+    int64_t sy = 0, sz = 0;
+  };
+  // what a rank tells its peer about the box it receives from it
+  struct Announce {
+    advdiff_ipc_addr addr;
+    int64_t rsy, rsz;
+    int ni, nj, nk, dtype;
+    uint64_t call;  // per-pair exchange counter: both sides must be at the same call
+  };
+  static void ipc_check(int e, const char* what) {
+    if (e != 0) {
+      std::fprintf(stderr, "%s failed: %s\n", what, hipGetErrorString((hipError_t)e));
+      std::exit(2);
+    }
+  }
+  // a contiguous byte message as a box of 32-bit words (bit-exact for any dtype)
+  static BoxMsg flat_box(int peer, const void* send, void* recv, size_t bytes) {
+    if (bytes % 4) throw std::runtime_error("ipc: message size not a multiple of 4 bytes");
+    BoxMsg b;
+    b.peer = peer;
+    b.dtype = ADVDIFF_F32;
+    b.send = send;
+    b.recv = recv;
+    b.ni = (int)(bytes / 4);
+    b.nj = b.nk = 1;
+    b.ssy = b.rsy = b.ni;
+    b.ssz = b.rsz = b.ni;
+    return b;
+  }
+  // The peer's receive address of every message.  First use of a (peer, send, recv,
+  // shape) pattern: the two ranks of each pair swap Announces over the mesh (both sides
+  // hit the pattern at the same call: every rank runs the same step schedule).  Later
+  // calls are table lookups: no host communication inside the time loop.
+  std::vector<Dest> resolve(const std::vector<BoxMsg>& msgs) {
+    std::vector<Dest> out(msgs.size());
+    std::vector<size_t> miss;
+    for (size_t q = 0; q < msgs.size(); ++q) {
+      const BoxMsg& m = msgs[q];
+      ++calls_[m.peer];
+      auto it = dest_.find(key(m));
+      if (it == dest_.end())
+        miss.push_back(q);
+      else
+        out[q] = it->second;
+    }
+    if (miss.empty()) return out;
+    std::vector<int> peers;
+    std::vector<Announce> mine(miss.size()), theirs(miss.size());
+    std::vector<const void*> o;
+    std::vector<void*> in;
+    for (size_t q = 0; q < miss.size(); ++q) {
+      const BoxMsg& m = msgs[miss[q]];
+      Announce& a = mine[q];
+      std::memset(&a, 0, sizeof(a));
+      ipc_check(advdiff_ipc_describe(ctx_, m.recv, &a.addr), "advdiff_ipc_describe");
+      a.rsy = m.rsy;
+      a.rsz = m.rsz;
+      a.ni = m.ni;
+      a.nj = m.nj;
+      a.nk = m.nk;
+      a.dtype = m.dtype;
+      a.call = calls_[m.peer];
+      peers.push_back(m.peer);
+      o.push_back(&mine[q]);
+      in.push_back(&theirs[q]);
+    }
+    mesh_.swap(peers, o, in, std::vector<size_t>(miss.size(), sizeof(Announce)));
+    for (size_t q = 0; q < miss.size(); ++q) {
+      const BoxMsg& m = msgs[miss[q]];
+      const Announce& t = theirs[q];
+      if (t.ni != m.ni || t.nj != m.nj || t.nk != m.nk || t.dtype != m.dtype || t.call != mine[q].call)
+        throw std::runtime_error("ipc: rank " + std::to_string(env_.rank) + " and peer " +
+                                 std::to_string(m.peer) + " disagree on a halo message");
+      Dest d;
+      ipc_check(advdiff_ipc_map(ctx_, &t.addr, &d.ptr), "advdiff_ipc_map");
+      d.sy = t.rsy;
+      d.sz = t.rsz;
+      dest_[key(m)] = d;
+      out[miss[q]] = d;
+    }
+    return out;
+  }
+  using Key = std::tuple<int, const void*, const void*, int, int, int>;
+  static Key key(const BoxMsg& m) { return Key{m.peer, m.send, m.recv, m.ni, m.nj, m.nk}; }
+
+  Star star_;
+  Mesh mesh_;
+  ProcEnv env_;
+  advdiff_ipc* ctx_ = nullptr;
+  std::map<Key, Dest> dest_;
+  std::map<int, uint64_t> calls_;
 };
 
 // Single process: no communication at all.
@@ -336,6 +594,7 @@ class LocalTransport final : public Transport {
 std::unique_ptr<Transport> make_transport(const ProcEnv& env, const std::string& kind) {
   if (env.size == 1) return std::make_unique<LocalTransport>();
   if (kind == "socket") return std::make_unique<SocketTransport>(env);
+  if (kind == "ipc") return std::make_unique<IpcTransport>(env);
   if (kind == "rccl" || kind.empty()) return std::make_unique<RcclTransport>(env);
   throw std::runtime_error("unknown transport " + kind);
 }

@@ -73,7 +73,13 @@ def build_parser():
                     help="stencil implementation: gfx950 HIP kernels or the PyTorch reference ops")
     ap.add_argument("--decomp", default=None,
                     help="process grid: slab (default), auto, or PZxPYxPX / PYxPX")
+    ap.add_argument("--transport", choices=["rccl", "ipc", "host"], default=None,
+                    help="halo transport: rccl (nccl backend), ipc (peer-mapped device puts "
+                         "+ device flags) or host (gloo, host-staged)")
     ap.add_argument("--write", default=None, help="write float32 result.bin to this path")
+    ap.add_argument("--write-ghosts", default=None,
+                    help="write the multi-GPU result.bin layout: every rank's slab WITH its "
+                         "ghost planes, rank after rank (MultiGPU/Diffusion3d_Baseline/main.c:341)")
     ap.add_argument("--initial", default=None, help="write float32 initial.bin to this path")
     ap.add_argument("--ascii", default=None, help="write the result as ASCII (one %%g per line)")
     ap.add_argument("--print", dest="print_field", action="store_true",
@@ -147,12 +153,32 @@ def main(argv=None) -> int:
     ns = parse(argv)
     model, grid, ic, run = make_problem(ns)
     import os
-    comm = Comm.from_env(device=ns.device or os.environ.get("ADVDIFF_DEVICE"))
+    import time
+    comm = Comm.from_env(device=ns.device or os.environ.get("ADVDIFF_DEVICE"),
+                         transport=ns.transport)
     dtype = torch.float64 if ns.dtype == "fp64" else torch.float32
     t0 = 0.1 if (ic == "heat") else 0.0  # heat kernel IC is the exact solution at t0
-    solver = Solver(model, grid, comm, dtype=dtype, ic=ic, overlap=not ns.no_overlap, t0=t0,
-                    check_every=ns.check_every, decomp=ns.decomp, integrator=ns.integrator,
-                    kernel=ns.kernel)
+
+    def fenced(fn):
+        """fn() timed between barriers + device syncs, max over ranks (the reference's
+        MPI_Barrier-fenced HtD / DtH timers, MultiGPU/Diffusion3d_Baseline/main.c:137-148,
+        313-323)."""
+        sync = (lambda: torch.cuda.synchronize(comm.device)) if comm.device.type == "cuda" \
+            else (lambda: None)
+        sync()
+        comm.barrier()
+        t = time.perf_counter()
+        out = fn()
+        sync()
+        comm.barrier()
+        return out, comm.allreduce_max(time.perf_counter() - t)
+
+    # HtD: building the device fields — the IC is generated on the device (no host array
+    # is copied), so this line times the allocation + IC kernels + stage-buffer copies
+    solver, htod_s = fenced(lambda: Solver(
+        model, grid, comm, dtype=dtype, ic=ic, overlap=not ns.no_overlap, t0=t0,
+        check_every=ns.check_every, decomp=ns.decomp, integrator=ns.integrator,
+        kernel=ns.kernel))
     if ns.restart:
         solver.load_checkpoint(ns.restart)
     if ns.initial:
@@ -171,17 +197,23 @@ def main(argv=None) -> int:
     if ns.error_norms and ic in ("sine", "heat"):
         l1, l2, li = solver.error_norms()
         extra = {"L1 norm": f"{l1:e}", "L2 norm": f"{l2:e}", "Linf norm": f"{li:e}"}
+    # DtH: the final field to the host and its gather on rank 0 (the reference's timed
+    # DtH + Merge_domains)
+    g, dtoh_s = fenced(solver.gather)
+    stats.htod_s, stats.dtoh_s = htod_s, dtoh_s
     text = solver.summary(stats, style=ns.style, extra=extra)
-    if ns.write:
-        solver.save_result(ns.write)
-    if ns.ascii or ns.print_field:
-        from .utils import io as aio
-        g = solver.gather()
+    from .utils import io as aio
+    if comm.rank == 0:
+        if ns.write:
+            aio.save_binary(ns.write, g)
+        if ns.ascii:
+            aio.save_ascii(ns.ascii, g)
+        if ns.print_field:
+            print(aio.format_field(g))
+    if ns.write_ghosts:
+        gg = solver.gather_with_ghosts()
         if comm.rank == 0:
-            if ns.ascii:
-                aio.save_ascii(ns.ascii, g)
-            if ns.print_field:
-                print(aio.format_field(g))
+            aio.save_binary(ns.write_ghosts, gg)
     if ns.checkpoint:
         solver.save_checkpoint(ns.checkpoint)
     if comm.rank == 0:

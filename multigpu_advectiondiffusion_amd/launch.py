@@ -116,14 +116,14 @@ def launch(np_: int, argv: list[str], cpu: bool = False, timeout: float | None =
 # ----------------------------------------------------------------------------------
 # in-process API for tests
 # ----------------------------------------------------------------------------------
-def _spawn_entry(rank, world, port, device, backend, fn, args, queue):
+def _spawn_entry(rank, world, port, device, backend, fn, args, queue, transport=None):
     os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     try:
         import torch
         torch.set_num_threads(1)
         from .parallel.comm import Comm
-        comm = Comm.from_env(device=device, backend=backend)
+        comm = Comm.from_env(device=device, backend=backend, transport=transport)
         try:
             res = fn(comm, *args)
         finally:
@@ -134,13 +134,16 @@ def _spawn_entry(rank, world, port, device, backend, fn, args, queue):
 
 
 def spawn_local(world: int, fn, *args, device: str = "cpu", backend: str | None = None,
-                timeout: float = 300.0):
-    """Run fn(comm, *args) on `world` local ranks; return [result_rank0, ...]."""
+                timeout: float = 300.0, transport: str | None = None):
+    """Run fn(comm, *args) on `world` local ranks; return [result_rank0, ...].
+    transport: the halo transport of device fields (Comm.transport; "ipc" with
+    ADVDIFF_SHARE_GPU=1 runs all ranks on one GPU with device-side exchanges)."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_spawn_entry, args=(r, world, port, device, backend, fn, args, q))
+    procs = [ctx.Process(target=_spawn_entry,
+                         args=(r, world, port, device, backend, fn, args, q, transport))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -80,6 +80,25 @@ _SIGS = {
                          c_vp],
 }
 
+
+class IpcAddr(ctypes.Structure):
+    """advdiff_ipc_addr (kernels.h): IPC handle of an allocation + byte offset."""
+    _fields_ = [("handle", ctypes.c_ubyte * 64), ("offset", ctypes.c_uint64),
+                ("bytes", ctypes.c_uint64)]
+
+
+_IPC_SIGS = {
+    "advdiff_ipc_create": [c_int, c_int, ctypes.POINTER(c_vp)],
+    "advdiff_ipc_destroy": [c_vp],
+    "advdiff_ipc_describe": [c_vp, c_vp, ctypes.POINTER(IpcAddr)],
+    "advdiff_ipc_flags_addr": [c_vp, ctypes.POINTER(IpcAddr)],
+    "advdiff_ipc_map": [c_vp, ctypes.POINTER(IpcAddr), ctypes.POINTER(c_vp)],
+    "advdiff_ipc_set_peer": [c_vp, c_int, ctypes.POINTER(IpcAddr)],
+    "advdiff_ipc_signal": [c_vp, ctypes.POINTER(c_int), c_int, c_vp],
+    "advdiff_ipc_wait": [c_vp, ctypes.POINTER(c_int), c_int, c_vp],
+    "advdiff_ipc_errors": [c_vp, ctypes.POINTER(ctypes.c_longlong)],
+}
+
 # low-storage RK variants share the signature of the SSP stage entries
 for _k in ("advdiff_diffusion3d_stage", "advdiff_diffusion2d_stage", "advdiff_burgers3d_stage",
            "advdiff_burgers2d_stage"):
@@ -131,16 +150,14 @@ def _load():
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = c_int
-        lib.advdiff_set_step_cfg.argtypes = [c_int]
-        lib.advdiff_set_step_cfg.restype = c_int
-        lib.advdiff_set_step_persist.argtypes = [c_int]
-        lib.advdiff_set_step_persist.restype = c_int
         lib.advdiff_set_step_edge.argtypes = [c_int]
         lib.advdiff_set_step_edge.restype = c_int
         lib.advdiff_set_b3_ver.argtypes = [c_int]
         lib.advdiff_set_b3_ver.restype = c_int
-        lib.advdiff_set_b3_ty.argtypes = [c_int]
-        lib.advdiff_set_b3_ty.restype = c_int
+        for name, args in _IPC_SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = c_int
         lib.advdiff_reduce_workspace_bytes.restype = c_sz
         lib.advdiff_reduce_workspace_bytes.argtypes = []
         lib.advdiff_build_info.restype = ctypes.c_char_p

@@ -11,6 +11,10 @@ Isend/Recv gather at `main.c:327-335`).
 * Device binding: ``cuda:LOCAL_RANK`` (the reference's ``rank % ndev``; here more ranks
   than GPUs is refused rather than silently oversubscribed — RCCL forbids two ranks on
   one GPU anyway).
+* Halo transport (``transport``): "rccl" (grouped ncclSend/Recv on the comm stream, the
+  default with the nccl backend), "ipc" (peer-mapped device puts + device flags,
+  parallel/ipc.py; also runs several ranks on ONE GPU with ADVDIFF_SHARE_GPU=1) or "host"
+  (host-staged through gloo — the reference's scheme, the default with gloo).
 """
 from __future__ import annotations
 
@@ -42,7 +46,8 @@ def pg_kwargs(backend: str, dev: torch.device) -> dict:
 
 
 class Comm:
-    def __init__(self, rank=0, size=1, local_rank=0, device=None, backend=None, group=None):
+    def __init__(self, rank=0, size=1, local_rank=0, device=None, backend=None, group=None,
+                 transport=None):
         self.rank = rank
         self.size = size
         self.local_rank = local_rank
@@ -50,11 +55,33 @@ class Comm:
         self.backend = backend
         self.group = group
         self._owns_pg = False
+        self._transport = transport
+        self._ipc = None
+
+    @property
+    def transport(self) -> str:
+        """Halo transport of device fields: "ipc", "rccl" or "host" (see module doc)."""
+        if self._transport:
+            return self._transport
+        return "rccl" if self.backend == "nccl" else "host"
+
+    @transport.setter
+    def transport(self, v):
+        if v not in (None, "ipc", "rccl", "host"):
+            raise ValueError("transport must be ipc, rccl or host")
+        self._transport = v
+
+    def ipc(self):
+        """The process's IPC peer context (created on first use, collectively)."""
+        if self._ipc is None:
+            from .ipc import IpcPeers
+            self._ipc = IpcPeers(self)
+        return self._ipc
 
     # ------------------------------------------------------------------------------
     @classmethod
     def from_env(cls, device: str | None = None, backend: str | None = None,
-                 timeout_s: float | None = None) -> "Comm":
+                 timeout_s: float | None = None, transport: str | None = None) -> "Comm":
         """Create (or attach to) the default process group from torchrun env vars.
 
         device: "cuda", "cpu" or None (= cuda if available).  backend defaults to
@@ -65,6 +92,7 @@ class Comm:
         # ADVDIFF_BACKEND=gloo: host-staged device halos (rehearsing multi-rank runs with
         # several ranks on one GPU together with ADVDIFF_SHARE_GPU=1; RCCL refuses that)
         backend = backend or os.environ.get("ADVDIFF_BACKEND") or None
+        transport = transport or os.environ.get("ADVDIFF_TRANSPORT") or None
         size = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -75,15 +103,17 @@ class Comm:
             if ndev == 0:
                 raise RuntimeError("device=cuda requested but no GPU is visible")
             share = os.environ.get("ADVDIFF_SHARE_GPU", "0") == "1"
+            if share and transport == "ipc":
+                backend = backend or "gloo"  # RCCL refuses two ranks per GPU
             if size > 1 and local_rank >= ndev and not (share and backend == "gloo"):
                 raise RuntimeError(f"local rank {local_rank} >= {ndev} visible GPUs "
                                    "(one process per GPU; oversubscription is refused — "
-                                   "only gloo test runs may share with ADVDIFF_SHARE_GPU=1)")
+                                   "only gloo / ipc test runs may share with ADVDIFF_SHARE_GPU=1)")
             torch.cuda.set_device(local_rank % ndev)
             dev = torch.device("cuda", local_rank % ndev)
         else:
             dev = torch.device("cpu")
-        c = cls(rank, size, local_rank, dev)
+        c = cls(rank, size, local_rank, dev, transport=transport)
         if size > 1:
             c.backend = backend or ("nccl" if dev.type == "cuda" else "gloo")
             if not dist.is_initialized():
@@ -192,6 +222,9 @@ class Comm:
         return lst[0]
 
     def finalize(self):
+        if self._ipc is not None:
+            self._ipc.close()
+            self._ipc = None
         if self._owns_pg and dist.is_initialized():
             dist.destroy_process_group()
             self._owns_pg = False

@@ -354,3 +354,16 @@ class CartesianDecomposition:
                     boundary.append(box)
         interior = tuple(inner)
         return interior, boundary
+
+
+def fused_view(cd: CartesianDecomposition, radius: int, border: int, a: int, lo: int, hi: int):
+    """View window, active and output bounds (view coordinates) along array axis a of a
+    fused-step launch on local cells [lo, hi) of a Cartesian block: the window reaches 3R
+    beyond the box (ghosts on split axes), the active range is the global interior
+    (mirror: csrc/runtime/cart.cpp fused_view)."""
+    R3 = 3 * radius
+    ax = cd.axis(a)
+    v0, v1 = max(0, lo - R3), min(ax.alloc, hi + R3)
+    origin = ax.start - ax.ghost + v0  # global index of view cell 0
+    N = cd.shape[a]
+    return (v0, v1), (max(0, border - origin), min(v1 - v0, N - border - origin)), (lo - v0, hi - v0)

@@ -43,6 +43,23 @@ class PendingExchange:
             self.finish = None
 
 
+def _start_ipc(comm, comm_stream, phases, after_event=None) -> PendingExchange:
+    """Device puts into the peers' ghost cells (parallel/ipc.py) on the comm stream after
+    `after_event`, phases in order; the returned handle joins the current stream."""
+    cur = torch.cuda.current_stream()
+    cs = comm_stream or cur
+    if after_event is None:
+        after_event = torch.cuda.Event()
+        after_event.record(cur)
+    cs.wait_event(after_event)
+    ipc = comm.ipc()
+    for msgs in phases:
+        ipc.exchange(msgs, cs)
+    done = torch.cuda.Event()
+    done.record(cs)
+    return PendingExchange([], cs, lambda: torch.cuda.current_stream().wait_event(done))
+
+
 class SlabHalo:
     def __init__(self, comm, decomp: SlabDecomposition, comm_stream=None):
         self.comm = comm
@@ -107,6 +124,21 @@ class SlabHalo:
 
         return PendingExchange(works, cs, finish)
 
+    def _ipc_msgs(self, field):
+        d = self.d
+        msgs = []
+        for peer, s, r in ((d.lower, d.send_lower(), d.recv_lower()),
+                           (d.upper, d.send_upper(), d.recv_upper())):
+            if peer is not None:
+                msgs.append((peer, field[s[0]:s[1]], field[r[0]:r[1]]))
+        return msgs
+
+    def prepare(self, field: torch.Tensor) -> None:
+        """Collective, outside any graph capture: learn the peers' receive addresses of
+        this field's exchange (ipc transport; a no-op otherwise)."""
+        if self.comm.size > 1 and field.is_cuda and self.comm.transport == "ipc":
+            self.comm.ipc()._resolve(self._ipc_msgs(field))
+
     def start(self, field: torch.Tensor, after_event=None) -> PendingExchange | None:
         """Begin exchanging the ghost planes of `field` (axis 0).
 
@@ -114,6 +146,8 @@ class SlabHalo:
         (or after all work currently queued on the current stream)."""
         if self.comm.size == 1:
             return None
+        if field.is_cuda and self.comm.transport == "ipc":
+            return _start_ipc(self.comm, self.comm_stream, [self._ipc_msgs(field)], after_event)
         ops = self._ops(field)
         if not ops:
             return None
@@ -167,8 +201,10 @@ class CartesianHalo:
         return [sorted(split, reverse=True)] if not self.corners else \
             [[a] for a in sorted(split, reverse=True)]
 
-    def _regions(self, field, axes):
-        """[(peer, send_view, recv_view, key)] for the given axes, fixed order."""
+    def boxes(self, axes):
+        """[(peer, send_box, recv_box, (axis, side))] of one phase as local index ranges
+        ((lo, hi) per array axis) — the geometry the native runtime must reproduce
+        (csrc/runtime/cart.cpp halo_plan, tests/test_native_host.py)."""
         cd = self.cd
         own = cd.owned_box()
         out = []
@@ -179,19 +215,25 @@ class CartesianHalo:
                     continue
                 s = ax.send_lower() if side < 0 else ax.send_upper()
                 r = ax.recv_lower() if side < 0 else ax.recv_upper()
-                sl_s = []
+                sb = []
                 for b, (lo, hi) in enumerate(own):
-                    if b == a:
-                        sl_s.append(None)
-                    elif self.corners and b > a:  # already exchanged: carry its ghosts
-                        sl_s.append(slice(0, cd.axis(b).alloc))
+                    if self.corners and b > a:  # already exchanged: carry its ghosts
+                        sb.append((0, cd.axis(b).alloc))
                     else:
-                        sl_s.append(slice(lo, hi))
-                sl_r = list(sl_s)
-                sl_s[a] = slice(*s)
-                sl_r[a] = slice(*r)
-                sv, rv = field[tuple(sl_s)], field[tuple(sl_r)]
-                out.append((peer, sv, rv, (a, side)))
+                        sb.append((lo, hi))
+                rb = list(sb)
+                sb[a] = tuple(s)
+                rb[a] = tuple(r)
+                out.append((peer, tuple(sb), tuple(rb), (a, side)))
+        return out
+
+    def _regions(self, field, axes):
+        """[(peer, send_view, recv_view, key)] for the given axes, fixed order."""
+        out = []
+        for peer, sb, rb, key in self.boxes(axes):
+            sv = field[tuple(slice(lo, hi) for lo, hi in sb)]
+            rv = field[tuple(slice(lo, hi) for lo, hi in rb)]
+            out.append((peer, sv, rv, key))
         return out
 
     def _buf(self, key, like):
@@ -235,9 +277,23 @@ class CartesianHalo:
         ops += [dist.P2POp(dist.irecv, t, p) for p, t in recvs]
         return ops
 
+    def _ipc_phases(self, field):
+        return [[(p, sv, rv) for p, sv, rv, _ in self._regions(field, axes)]
+                for axes in self._phases()]
+
+    def prepare(self, field: torch.Tensor) -> None:
+        """Collective, outside any graph capture: learn the peers' receive addresses of
+        this field's exchange (ipc transport; a no-op otherwise)."""
+        if self.comm.size > 1 and field.is_cuda and self.comm.transport == "ipc":
+            ipc = self.comm.ipc()
+            for msgs in self._ipc_phases(field):
+                ipc._resolve(msgs)
+
     def start(self, field: torch.Tensor, after_event=None) -> PendingExchange | None:
         if self.comm.size == 1:
             return None
+        if field.is_cuda and self.comm.transport == "ipc":
+            return _start_ipc(self.comm, self.comm_stream, self._ipc_phases(field), after_event)
         phases = self._phases()
         if not field.is_cuda:  # gloo on the CPU: phases run to completion here
             for axes in phases:

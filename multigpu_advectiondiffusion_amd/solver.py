@@ -31,7 +31,7 @@ from .models.base import Grid, Model, RunStats
 from .models.prototypes import LSRK45_A, LSRK45_B
 from .ops import stencil
 from .parallel.comm import Comm
-from .parallel.decomposition import CartesianDecomposition, parse_proc_grid
+from .parallel.decomposition import CartesianDecomposition, fused_view, parse_proc_grid
 from .parallel.halo import CartesianHalo, SlabHalo
 from .utils import ics
 from .utils import io as aio
@@ -305,15 +305,8 @@ class Solver:
                              self.device)
 
     def _fused_view(self, a: int, lo: int, hi: int):
-        """View window, active and output bounds (view coordinates) along array axis a for
-        a fused launch on local cells [lo, hi): the window reaches 3R beyond the box
-        (ghosts on split axes), the active range is the global interior."""
-        cd, R3 = self.cd, 3 * self.model.radius
-        ax = cd.axis(a)
-        v0, v1 = max(0, lo - R3), min(ax.alloc, hi + R3)
-        origin = ax.start - ax.ghost + v0  # global index of view cell 0
-        B, N = self.model.border, cd.shape[a]
-        return (v0, v1), (max(0, B - origin), min(v1 - v0, N - B - origin)), (lo - v0, hi - v0)
+        """View window, active and output bounds along array axis a (decomposition.fused_view)."""
+        return fused_view(self.cd, self.model.radius, self.model.border, a, lo, hi)
 
     def _launch_fused_box(self, box, dt, exclusive=False):
         """Fused step of a Cartesian block box (array order) on a kernel VIEW."""
@@ -421,8 +414,22 @@ class Solver:
     GRAPH_STEPS = 8  # even: fused / LSRK paths ping-pong u/un, so buffers line up on replay
 
     def graph_capable(self) -> bool:
-        return (self.device.type == "cuda" and self.comm.size == 1 and not trace.SYNC_DEBUG
+        """Single process, or several ranks whose halos are device puts (ipc transport:
+        every exchange step is a stream-ordered kernel, so a whole multi-rank step —
+        interior, puts, flags, waits, boundary — replays as one graph)."""
+        multi_ok = self.comm.size == 1 or self.comm.transport == "ipc"
+        return (self.device.type == "cuda" and multi_ok and not trace.SYNC_DEBUG
                 and not trace.TRACE)
+
+    def _prepare_graph_halos(self):
+        """Multi-rank capture: join every in-flight exchange into the current stream (an
+        event recorded outside a capture cannot be waited on inside it) and learn the
+        peers' receive addresses of every field now (the one-time handshake is host
+        communication, which a capture must not contain)."""
+        if self.comm.size > 1:
+            self.sync_halos()
+            for f in self.fields():
+                self.halo.prepare(f)
 
     def _graph_for(self, dt: float | None, t_end: float | None = None):
         """dt=None: a graph of device-dt (adaptive CFL) steps towards t_end."""
@@ -436,6 +443,7 @@ class Solver:
             self._graphs = {}
         # state snapshot: capture executes nothing, but keep t/it bookkeeping exact
         t, it = self.t, self.it
+        self._prepare_graph_halos()
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream())
         graph = torch.cuda.CUDAGraph()
@@ -446,6 +454,8 @@ class Solver:
                         self._step_device_dt(t_end)
                     else:
                         self.step(dt)
+                if self.comm.size > 1:
+                    self.sync_halos()  # every comm-stream fork joins back into the capture
         torch.cuda.current_stream().wait_stream(side)
         self.t, self.it = t, it
         self._graphs[key] = graph
@@ -454,6 +464,8 @@ class Solver:
     def _advance(self, n: int, dt: float, use_graph: bool):
         if use_graph and n >= self.GRAPH_STEPS:
             g = self._graph_for(dt)
+            if self.comm.size > 1:
+                self.sync_halos()  # halos of eager steps: joined before the replay
             for _ in range(n // self.GRAPH_STEPS):
                 g.replay()
                 for _ in range(self.GRAPH_STEPS):  # same rounding as eager stepping
@@ -532,6 +544,8 @@ class Solver:
                   and not self.check_every and _FAULT is None)
         use_graph = (self.graph_capable() and (fixed_dt is not None or dev_dt)
                      and callback is None and not self.check_every) if graph is None else graph
+        if self.comm.size > 1 and fixed_dt is None:
+            use_graph = False  # the device-dt chunk's max|u| allreduce is not captured
         if use_graph:  # capture outside the timed region (like a warm-up)
             if fixed_dt is not None:
                 self._graph_for(fixed_dt)
@@ -623,6 +637,21 @@ class Solver:
         else:
             counts = [self.d.count_of(r) for r in range(self.comm.size)]
             g = self.comm.gather_planes(self.owned.contiguous(), counts)
+        return None if g is None else g.numpy()
+
+    def gather_with_ghosts(self) -> np.ndarray | None:
+        """Rank 0: every rank's slab INCLUDING its ghost planes, concatenated in rank
+        order — the reference's multi-GPU result.bin layout (each rank's Nx*Ny*(_Nz+6)
+        block, SaveBinary3D(h_u, Nx, Ny, NZ), MultiGPU/Diffusion3d_Baseline/main.c:341,
+        Tools.c:91-119).  Slab decompositions only."""
+        if self.cart:
+            raise ValueError("gather_with_ghosts: slab decompositions only")
+        self.sync_halos()
+        self._sync()
+        nx = self.grid.shape[0]
+        local = self.u[..., :nx].contiguous()
+        counts = [self.cd.axis(0, r).alloc for r in range(self.comm.size)]
+        g = self.comm.gather_planes(local, counts)
         return None if g is None else g.numpy()
 
     def save_result(self, path) -> None:

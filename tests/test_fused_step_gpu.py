@@ -57,21 +57,11 @@ def test_fused_step_bitwise_equals_per_stage(dtype, order, case):
 
 @pytest.mark.parametrize("order", [4, 2])
 @pytest.mark.parametrize("case", CASES + [
-    (200, 70, 130, 136, 3, 197, 3, 197, 3),   # many (tile, plane) segments per group
+    (200, 70, 130, 136, 3, 197, 3, 197, 3),   # many z chunks
 ])
-def test_fused_step_persistent_schedule_bitwise(order, case):
-    """exclusive=True (one round of persistent groups marching segments of the linearised
-    (tile, plane) space) == the grid of z chunks, bitwise; also with two plane ranges."""
-    from multigpu_advectiondiffusion_amd.ops import _lib
-    lib = _lib.require()
-    old = lib.advdiff_set_step_persist(1)
-    try:
-        _persistent_case(order, case)
-    finally:
-        lib.advdiff_set_step_persist(old)
-
-
-def _persistent_case(order, case):
+def test_fused_step_two_ranges_bitwise(order, case):
+    """Two plane ranges in one launch (a slab rank's two boundary slabs) == two launches,
+    bitwise; the placement flag (exclusive) never changes a result."""
     nz, ny, nx, sx, k0, k1, zlo, zhi, border = case
     g = torch.Generator().manual_seed(7)
     u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).cuda()
@@ -80,12 +70,14 @@ def _persistent_case(order, case):
     kw = dict(nx=nx, ny=ny, zlo=zlo, zhi=zhi, border=border, order=order, cx=c[0], cy=c[1],
               cz=c[2], dt=dt)
     mid = (k0 + k1) // 2
-    for ranges in (dict(k0=k0, k1=k1), dict(k0=k0, k1=k0 + 3, k0b=mid, k1b=k1)):
-        grid, pers = u.clone(), u.clone()
-        stencil.diffusion3d_step(u, grid, exclusive=False, **ranges, **kw)
-        stencil.diffusion3d_step(u, pers, exclusive=True, **ranges, **kw)
-        torch.cuda.synchronize()
-        assert torch.equal(grid, pers), (ranges, (grid - pers).abs().max().item())
+    one, two, excl = u.clone(), u.clone(), u.clone()
+    stencil.diffusion3d_step(u, one, k0=k0, k1=k0 + 3, k0b=mid, k1b=k1, **kw)
+    stencil.diffusion3d_step(u, two, k0=k0, k1=k0 + 3, **kw)
+    stencil.diffusion3d_step(u, two, k0=mid, k1=k1, **kw)
+    stencil.diffusion3d_step(u, excl, k0=k0, k1=k0 + 3, k0b=mid, k1b=k1, exclusive=True, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(one, two), (one - two).abs().max().item()
+    assert torch.equal(one, excl)
 
 
 def _per_stage_2d(u, nx, j0, j1, ylo, yhi, border, order, c, dt):
@@ -147,47 +139,28 @@ def test_fused_step_box_bounds_match_reference():
         assert (got.cpu() - out).abs().max().item() < 1e-12, box
 
 
-STEP_VARIANTS = [0, 1, 16, 20, 21, 22, 23, 24, 25, 27, 29, 30, 31, 32, 33]  # diffusion_fused.hip dispatch_step cfgs
-
-
-@pytest.mark.parametrize("cfg", STEP_VARIANTS)
 @pytest.mark.parametrize("order", [4, 2])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_fused_step_variants_bitwise(cfg, order, dtype):
-    """Every selectable kernel variant of the fused step (tile shape, x-neighbour source,
-    prefetch distance; grid and persistent schedules) is bit-identical to the per-stage
-    path on a sub-range with frozen planes and odd sizes."""
-    from multigpu_advectiondiffusion_amd.ops import _lib
-    lib = _lib.require()
+def test_fused_step_odd_subrange_bitwise(order, dtype):
+    """The step kernel of each order (FD4: 16 waves x 2 rows, FD2: 12 x 3) is bit-identical
+    to the per-stage path on a sub-range with frozen planes and odd sizes."""
     nz, ny, nx, sx, k0, k1, zlo, zhi, border = (77, 53, 133, 136, 5, 70, 2, 74, 2)
     g = torch.Generator().manual_seed(5)
     u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).to(dtype).cuda()
     c = (0.21, 0.17, 0.13)
     dt = 0.9 / (2 * sum(c)) if order == 2 else 0.5 / sum(c)
     exp = _per_stage(u, nx, ny, k0, k1, zlo, zhi, border, order, c, dt)
-    old = lib.advdiff_set_step_cfg(cfg)
-    oldp = lib.advdiff_set_step_persist(1)
-    try:
-        for exclusive in (False, True):
-            got = u.clone()
-            stencil.diffusion3d_step(u, got, nx=nx, ny=ny, k0=k0, k1=k1, zlo=zlo, zhi=zhi,
-                                     border=border, order=order, cx=c[0], cy=c[1], cz=c[2],
-                                     dt=dt, exclusive=exclusive)
-            torch.cuda.synchronize()
-            assert torch.equal(got, exp), (exclusive, (got - exp).abs().max().item())
-    finally:
-        lib.advdiff_set_step_cfg(old)
-        lib.advdiff_set_step_persist(oldp)
+    got = u.clone()
+    stencil.diffusion3d_step(u, got, nx=nx, ny=ny, k0=k0, k1=k1, zlo=zlo, zhi=zhi,
+                             border=border, order=order, cx=c[0], cy=c[1], cz=c[2], dt=dt)
+    torch.cuda.synchronize()
+    assert torch.equal(got, exp), (got - exp).abs().max().item()
 
 
 @pytest.mark.parametrize("order", [4, 2])
 def test_fused_step_production_size_bitwise(order):
-    """The bench's launch at production size (512^3, fp64, the default variant): the grid
-    schedule and the persistent schedule (L = tiles x planes near its int32 guard's scale,
-    per/rem split over CUs x occupancy groups) are bitwise equal to three per-stage
-    launches over the whole grid."""
-    from multigpu_advectiondiffusion_amd.ops import _lib
-    lib = _lib.require()
+    """The bench's launch at production size (512^3, fp64) is bitwise equal to three
+    per-stage launches over the whole grid."""
     n, R = 512, order // 2
     g = torch.Generator(device="cuda").manual_seed(5)
     u = torch.rand((n, n, n), generator=g, dtype=torch.float64, device="cuda")
@@ -197,16 +170,8 @@ def test_fused_step_production_size_bitwise(order):
               cy=c[1], cz=c[2], dt=dt)
     exp = _per_stage(u, n, n, R, n - R, R, n - R, R, order, c, dt)
     got = u.clone()
-    stencil.diffusion3d_step(u, got, exclusive=True, **kw)  # default: grid schedule
+    stencil.diffusion3d_step(u, got, exclusive=True, **kw)
     torch.cuda.synchronize()
-    assert torch.equal(got, exp), (got - exp).abs().max().item()
-    old = lib.advdiff_set_step_persist(1)
-    try:
-        got.copy_(u)
-        stencil.diffusion3d_step(u, got, exclusive=True, **kw)
-        torch.cuda.synchronize()
-    finally:
-        lib.advdiff_set_step_persist(old)
     assert torch.equal(got, exp), (got - exp).abs().max().item()
 
 

@@ -1,0 +1,147 @@
+"""The peer-mapped device transport (ipc: csrc/kernels/ipc.hip, parallel/ipc.py, native
+IpcTransport) with several ranks sharing the one GPU of the box: every halo is a put
+kernel straight into the neighbour's ghost cells + a device flag, no host staging, no
+host synchronisation inside a step — the production multi-GPU data path (xGMI puts)
+minus the link.  Results must equal the 1-rank run bitwise, eager and graph-replayed,
+slab and Cartesian, with and without overlap.  Reference being replaced: the host-staged
+MPI choreography of MultiGPU/Diffusion3d_Baseline/main.c:209-288."""
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from multigpu_advectiondiffusion_amd import Burgers, Diffusion, Grid, Solver
+from multigpu_advectiondiffusion_amd.launch import free_port_block, spawn_local
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _make(kind):
+    if kind == "diff3":
+        return Diffusion(K=1.0, order=4), Grid((70, 33, 41), (1.0, 1.0, 1.0)), "sine"
+    if kind == "diff3o2":
+        return Diffusion(K=1.0, order=2), Grid((67, 36, 44), (1.0, 1.0, 1.0)), "sine"
+    if kind == "burg3":
+        return Burgers(viscosity=1e-4, weno="z", cfl=0.3), Grid((66, 35, 40), (2.0, 2.0, 2.0)), "gaussian"
+    if kind == "diff2":
+        return Diffusion(K=1.0, order=4), Grid((300, 61), (1.0, 1.0)), "heat"
+    if kind == "burg2":
+        return Burgers(viscosity=0.0, weno="js", cfl=0.3), Grid((260, 57), (2.0, 2.0)), "gaussian"
+    raise KeyError(kind)
+
+
+def _reference(kind, steps):
+    model, grid, ic = _make(kind)
+    s = Solver(model, grid, dtype=torch.float64, device="cuda", ic=ic)
+    s.run(iters=steps, graph=False)
+    return s.gather()
+
+
+def _run(comm, kind, steps, overlap, decomp, graph):
+    assert comm.transport == "ipc"
+    model, grid, ic = _make(kind)
+    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, overlap=overlap, decomp=decomp)
+    assert s.graph_capable()
+    s.run(iters=steps, graph=graph)
+    g = s.gather()
+    nerr = comm.ipc().errors()
+    assert nerr == 0, f"{nerr} ipc wait timeouts"
+    return None if g is None else g.copy()
+
+
+def _spawn(world, *args):
+    return spawn_local(world, _run, *args, device="cuda", transport="ipc", timeout=240)[0]
+
+
+@pytest.mark.parametrize("kind", ["diff3", "burg3", "diff2", "burg2", "diff3o2"])
+def test_ipc_slab_bitwise(kind, monkeypatch):
+    """z/y slabs, per-stage (Burgers) and fused-step (heat) exchanges, 2 and 3 ranks,
+    overlap on/off, eager and hipGraph replay (16 steps = 2 graphs of 8) — all bitwise
+    equal to the 1-rank run."""
+    monkeypatch.setenv("ADVDIFF_SHARE_GPU", "1")
+    ref = _reference(kind, 16)
+    for world, overlap, graph in ((2, True, False), (3, True, True), (2, False, True)):
+        out = _spawn(world, kind, 16, overlap, None, graph)
+        assert np.array_equal(out, ref), (kind, world, overlap, graph, np.abs(out - ref).max())
+
+
+@pytest.mark.parametrize("kind,world,decomp", [
+    ("diff3", 4, (1, 2, 2)), ("diff3", 8, (2, 2, 2)), ("burg3", 4, (2, 1, 2)),
+    ("diff2", 4, (2, 2)), ("burg2", 2, (1, 2)),
+])
+def test_ipc_cartesian_bitwise(kind, world, decomp, monkeypatch):
+    """Cartesian blocks: strided boxes put straight into the neighbours' ghost boxes (no
+    pack/unpack), the fused step's phased corner exchange ordered on the device by the
+    flags — eager and graph-replayed, bitwise equal to the 1-rank run."""
+    monkeypatch.setenv("ADVDIFF_SHARE_GPU", "1")
+    ref = _reference(kind, 16)
+    for overlap, graph in ((True, True), (False, False)):
+        out = _spawn(world, kind, 16, overlap, decomp, graph)
+        assert np.array_equal(out, ref), (kind, decomp, overlap, graph, np.abs(out - ref).max())
+
+
+# ------------------------------------------------------------------------------------
+# native executables (csrc/runtime/transport.cpp IpcTransport)
+# ------------------------------------------------------------------------------------
+def _native(app, args, out, world=1, extra=(), env_extra=None):
+    exe = ROOT / "bin" / app
+    assert exe.exists(), f"{exe} not built (make -C csrc apps)"
+    port = free_port_block(world + 1)
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ADVDIFF_PORT=str(port),
+                   **(env_extra or {}))
+        cmd = [str(exe)] + [str(a) for a in args] + ["--write", str(out)] + list(extra)
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        so, _ = p.communicate(timeout=240)
+        outs.append(so)
+        assert p.returncode == 0, so
+    return outs[0]
+
+
+NATIVE_CASES = [
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 50, 44, 46, 9], (46, 44, 50), 8, "2x2x2",
+     ["--ic", "sine", "--no-overlap"]),              # the round-2 intermittent case
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 50, 44, 46, 9], (46, 44, 50), 8, "2x2x2",
+     ["--ic", "sine"]),
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 66, 40, 45, 12], (45, 40, 66), 3, "slab",
+     ["--ic", "sine"]),
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 66, 40, 45, 12], (45, 40, 66), 4, "2x2x1",
+     ["--ic", "sine", "--no-fused"]),
+    ("burgers3d", [0.03, 0.3, 2.0, 2.0, 2.0, 40, 36, 41], (41, 36, 40), 4, "2x1x2", []),
+    ("burgers3d", [0.03, 0.3, 2.0, 2.0, 2.0, 40, 36, 41], (41, 36, 40), 2, "slab", []),
+    ("diffusion2d", [1.0, 1.0, 1.0, 130, 90, 30], (90, 130), 4, "2x2", ["--ic", "disc"]),
+]
+
+
+@pytest.mark.parametrize("app,args,shape,world,decomp,extra", NATIVE_CASES)
+@pytest.mark.parametrize("transport", ["ipc", "socket"])
+def test_native_poisoned_multirank_bitwise(tmp_path, app, args, shape, world, decomp, extra,
+                                           transport):
+    """ADVDIFF_POISON=1: every device allocation (fields with row padding and ghost
+    shells, staging buffers) starts as NaN instead of zero, so a cell read before anybody
+    wrote it shows up in the result.  The P-rank run over the ipc (device puts) and the
+    socket (host-staged) transports must still equal the 1-rank run bitwise."""
+    one, many = tmp_path / "one.bin", tmp_path / "many.bin"
+    poison = {"ADVDIFF_POISON": "1"}
+    _native(app, args, one, extra=extra, env_extra=poison)
+    dec = [] if decomp == "slab" else ["--decomp", decomp]
+    txt = _native(app, args, many, world=world, extra=extra + ["--transport", transport] + dec,
+                  env_extra=poison)
+    assert f"transport={transport}" in txt, txt
+    a = np.fromfile(one, dtype=np.float32).reshape(shape)
+    b = np.fromfile(many, dtype=np.float32).reshape(shape)
+    assert np.isfinite(a).all()
+    if not np.array_equal(a, b):
+        bad = np.argwhere(a != b)
+        pytest.fail(f"{len(bad)} cells differ, max {np.nanmax(np.abs(a - b))}, box "
+                    f"{bad.min(axis=0)}..{bad.max(axis=0)} of {shape}\n{txt[-2000:]}")

@@ -35,7 +35,18 @@ def _run(app, args, out, world=1, extra=()):
         so, _ = p.communicate(timeout=240)
         outs.append(so)
         assert p.returncode == 0, so
+    _check_banner(outs[0])
     return outs[0]
+
+
+def _check_banner(txt):
+    """The executable was built from this tree's runtime and kernel sources."""
+    from multigpu_advectiondiffusion_amd.ops import _lib
+    from tests.test_native_host import runtime_tree_hash
+    line = [l for l in txt.splitlines() if l.startswith("advdiff native build:")]
+    assert line, txt[-1000:]
+    assert f"runtime {runtime_tree_hash()}" in line[0], (line[0], runtime_tree_hash())
+    assert f"kernels {_lib.source_hash()}" in line[0], (line[0], _lib.source_hash())
 
 
 def _py(model, grid, ic, integrator="ssprk3", **run):

@@ -39,3 +39,106 @@ def test_library_matches_tree():
         assert "stale" not in err, err
         pytest.skip(f"library not loadable here: {err}")
     assert _lib.library_hash() == _lib.source_hash()
+
+
+def _tree_hash(paths):
+    import hashlib
+    h = hashlib.sha256()
+    for p in sorted(paths):
+        h.update((CSRC / p).read_bytes())
+    return h.hexdigest()[:16]
+
+
+def runtime_tree_hash():
+    """Hash of the native runtime + app sources (csrc/Makefile RT_HASH)."""
+    rel = [f"runtime/{p.name}" for p in (CSRC / "runtime").iterdir() if p.suffix in (".cpp", ".hpp")]
+    rel += [f"apps/{p.name}" for p in (CSRC / "apps").iterdir() if p.suffix == ".cpp"]
+    return _tree_hash(rel)
+
+
+def test_native_binaries_match_tree():
+    """bin/* embed the hash of the runtime/app sources they were built from
+    (advdiff_runtime_hash); it must equal the tree's, so a stale bin/ fails here (and its
+    banner is checked again by the GPU tests)."""
+    r = subprocess.run(["make", "-s", "-C", str(CSRC), "rthash"], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == runtime_tree_hash()
+    bins = [CSRC.parent / "bin" / a for a in ("diffusion2d", "diffusion3d", "burgers2d", "burgers3d")]
+    if not all(b.exists() for b in bins):
+        pytest.skip("bin/ not built")
+    for b in bins:
+        assert runtime_tree_hash().encode() in b.read_bytes(), f"{b} is stale (make -C csrc apps)"
+
+
+GEOMETRY_CASES = [
+    # app, positional args, world, decomp, extra
+    ("diffusion3d", [1, 1, 1, 1, 50, 44, 46, 9], 8, "2x2x2", []),
+    ("diffusion3d", [1, 1, 1, 1, 66, 40, 45, 12], 4, "1x2x2", []),
+    ("diffusion3d", [1, 1, 1, 1, 66, 40, 45, 12], 4, "2x2x1", ["--no-fused"]),
+    ("diffusion3d", [1, 1, 1, 1, 66, 40, 45, 12], 3, "slab", []),
+    ("burgers3d", [0.03, 0.3, 2, 2, 2, 40, 36, 41], 4, "2x1x2", []),
+    ("diffusion2d", [1, 1, 1, 130, 90, 30], 4, "2x2", []),
+    ("burgers2d", [0.1, 0.4, 2, 2, 140, 100], 2, "1x2", ["--weno", "js"]),
+]
+
+
+@pytest.mark.parametrize("app,args,world,decomp,extra", GEOMETRY_CASES)
+def test_native_geometry_matches_python(app, args, world, decomp, extra):
+    """Every rank's launch boxes, fused-step views and halo messages of the native runtime
+    (bin/<app> --geometry, csrc/runtime/cart.cpp) equal the Python decomposition's
+    (CartesianDecomposition, CartesianHalo.boxes, decomposition.fused_view)."""
+    import json
+    import os
+
+    from multigpu_advectiondiffusion_amd.models import Burgers, Diffusion
+    from multigpu_advectiondiffusion_amd.parallel.decomposition import (
+        CartesianDecomposition, fused_view, parse_proc_grid)
+    from multigpu_advectiondiffusion_amd.parallel.halo import CartesianHalo
+    exe = CSRC.parent / "bin" / app
+    if not exe.exists():
+        pytest.skip("bin/ not built")
+    env = dict(os.environ, RANK="0", WORLD_SIZE=str(world))
+    cmd = [str(exe)] + [str(a) for a in args] + ["--decomp", decomp, "--geometry"] + extra
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0, r.stderr
+    native = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert len(native) == world
+    three = app.endswith("3d")
+    if app.startswith("diffusion"):
+        model = Diffusion(K=1.0, order=4)
+        shape = tuple(reversed(args[4:7] if three else args[3:5]))
+    else:
+        model = Burgers(viscosity=1e-5, weno="js" if "js" in extra else "z", cfl=0.3)
+        shape = tuple(reversed(args[5:8] if three else args[4:6]))
+    R, B = model.radius, model.border
+    pgrid = parse_proc_grid(None if decomp == "slab" else decomp, world, shape, R)
+    fused = model.supports_fused and "--no-fused" not in extra and not any(
+        n // p < 3 * R for n, p in zip(shape, pgrid) if p > 1)
+    G = 3 * R if fused else R
+    lst = lambda box: [list(x) for x in box]  # noqa: E731
+    for rank in range(world):
+        cd = CartesianDecomposition(shape, pgrid, rank, G)
+        nat = native[rank]
+        assert nat["fused"] == fused and nat["ghost"] == G
+        assert nat["coords"] == list(cd.coords)
+        assert nat["alloc"] == list(cd.alloc)
+        assert nat["own"] == lst(cd.owned_box())
+        assert nat["full"] == lst(cd.compute_box(B))
+        interior, boundary = cd.split_boxes(B, G)
+        assert nat["interior"] == lst(interior)
+        assert nat["boundary"] == [lst(b) for b in boundary]
+        if fused:
+            boxes = [cd.compute_box(B), interior] + list(boundary)
+            boxes = [b for b in boxes if all(hi > lo for lo, hi in b)]
+            assert len(nat["views"]) == len(boxes)
+            for v, box in zip(nat["views"], boxes):
+                assert v["box"] == lst(box)
+                for a in range(1, len(shape)):
+                    want = [list(x) for x in fused_view(cd, R, B, a, *box[a])]
+                    assert v["axes"][a - 1] == want, (rank, box, a)
+        if cd.size > 1 and not cd.is_slab:
+            halo = CartesianHalo(None, cd, corners=fused)
+            py = [[{"peer": p, "axis": k[0], "side": k[1], "send": lst(s), "recv": lst(rr)}
+                   for p, s, rr, k in halo.boxes(axes)] for axes in halo._phases()]
+            assert nat["halo"] == py, rank
