@@ -21,6 +21,8 @@ CASES = [
     ("burgers2d_js_400x406", lambda: Burgers(viscosity=0.0, weno="js", cfl=0.4), (400, 406), "gaussian", 400),
     ("burgers2d_js_1001x1001", lambda: Burgers(viscosity=0.0, weno="js", cfl=0.4), (1001, 1001), "gaussian", 200),
     ("burgers2d_z_visc_2048x2048", lambda: Burgers(viscosity=1e-5, weno="z", cfl=0.3), (2048, 2048), "gaussian", 100),
+    ("burgers2d_js_4096x4096", lambda: Burgers(viscosity=0.0, weno="js", cfl=0.4), (4096, 4096), "gaussian", 50),
+    ("burgers2d_js_16384x16384", lambda: Burgers(viscosity=0.0, weno="js", cfl=0.4), (16384, 16384), "gaussian", 10),
     ("heat2d_fd4_400x406", lambda: Diffusion(K=1.0, order=4, safety=0.8), (400, 406), "disc", 2000),
     ("heat2d_fd4_1001x1001", lambda: Diffusion(K=1.0, order=4), (1001, 1001), "heat", 2000),
 ]
@@ -28,7 +30,10 @@ CASES = [
 
 def main():
     out = {"knobs": {k: v for k, v in os.environ.items() if k.startswith("ADVDIFF_")}}
+    only = sys.argv[1:]  # optional name filters
     for name, mk, shape, ic, steps in CASES:
+        if only and not any(o in name for o in only):
+            continue
         m = mk()
         g = Grid(shape, (2.0,) * len(shape))
         m.bind(g)

@@ -732,6 +732,173 @@ __global__ __launch_bounds__(TX) void burgers2d_stage_kernel(
 }
 
 // ------------------------------------------------------------------------------
+// WENO5 2-D stage, v2 (default for WENO5-JS/Z in 2-D): every wave is independent — no
+// __syncthreads at all.  A wave owns a 64-column strip (lane 0 supplies the left face of
+// the strip only, lanes 1..63 are output cells: 63-cell strips anchored at the active
+// region, as the 3-D v9 x tiles) and marches along y:
+//   * y faces from the lane's own register column (rings of f+, f-, u and the scaled
+//     curvatures, two of three curvatures per side carried from the previous row; the
+//     march is unrolled by the ring length, so the rings rotate by renaming);
+//   * x faces: the row's split fluxes (and u for the viscous term) go to a WAVE-PRIVATE
+//     LDS row of 64 + 5 halo cells (5 lanes also stage one halo column each); a lane reads
+//     f+(x-2..x+2) / f-(x-1..x+3) and computes the face to the right of its cell with the
+//     v9 x-face form (w5_side_h, 37 fp64 ops per side, one reciprocal per face); the face
+//     to its left arrives from lane l-1 by one DPP shift (the old kernel: 3 barriers per
+//     row, the left face of the 256-lane tile computed by a single lane, two full
+//     divisions per face);
+//   * LDS writes and reads of one wave are executed in order, and a compiler fence keeps
+//     them in program order, so the row needs no barrier (and, written after the previous
+//     row's reads were issued, no second buffer);
+//   * global loads: u(j+3) of the own column and the halo lane's column of row j+1, one
+//     row ahead; plane-free 32-bit byte offsets through a buffer descriptor per launch.
+// Per interior cell and stage ~170 fp64 lane-ops inviscid: the 3-D v9 stage's cost per
+// direction (tests: bitwise P-rank == 1-rank, fp64 reference to rounding).
+// ------------------------------------------------------------------------------
+template <typename T, bool WZ, bool VISC, int MODE>
+__global__ __launch_bounds__(256) void burgers2d_w5_kernel(
+    const T* __restrict__ in, T* aux, T* out, int nx, int64_t sy, int j0, int j1, int ychunk,
+    int border, T rdx3, T rdy6, T vx, T vy, T dt, T a, T b, const double* __restrict__ dtp) {
+  constexpr int R = 3, NR = 5, TXO = 63, NW = 4;
+  constexpr int LW = 64 + 5;  // x = ib-2 .. ib+66
+  constexpr int NARR = VISC ? 3 : 2;
+  __shared__ T lds[NW][NARR][LW];
+  const W5Sgpr<T> kk;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int ib = border - 1 + ((int)blockIdx.x * NW + w) * TXO;  // x of lane 0
+  if (ib + 1 >= nx - border) return;  // a strip past the active region: wave-uniform exit
+  const int jc0 = j0 + (int)blockIdx.y * ychunk;
+  const int jc1 = min(jc0 + ychunk, j1);
+  const int jlast = jc1 - 1;
+  const int i = ib + lane;
+  const bool active = lane >= 1 && i < nx - border;
+  const int E = (int)sizeof(T);
+  const uint32_t goff = (uint32_t)min(i, nx - 1) * (uint32_t)E;
+  // halo lanes 0..4 also stage x = ib-2, ib-1, ib+64, ib+65, ib+66
+  const bool hl = lane < 5;
+  const int hx = lane < 2 ? ib - 2 + lane : ib + 62 + lane;
+  const int hslot = lane < 2 ? lane : 64 + lane;
+  const uint32_t hoff = (uint32_t)clampi(hx, 0, nx - 1) * (uint32_t)E;
+  const int64_t syb = sy * E;
+  auto row = [&](const T* base, int j) { return plane_rsrc((const char*)base + (int64_t)j * syb); };
+  if (dtp != nullptr && !device_dt(dtp, dt)) {  // adaptive run at t_end: out = in
+    if (active)
+      for (int j = jc0; j < jc1; ++j) gst<T>(row(out, j), goff, gld<T>(row(in, j), goff));
+    return;
+  }
+  T* sp = lds[w][0];
+  T* sm = lds[w][1];
+  T* su = VISC ? lds[w][NARR - 1] : nullptr;
+
+  // ---- rings: row p lives in slot (p - jc0 + 2 NR) % NR ----
+  T rp[NR], rm[NR], ru[NR], cp[NR], cm[NR], fy[NR];  // f+, f-, u, C(f+), C(f-), 6 x y face
+  {
+    T uy[2 * R], fp[2 * R], fm[2 * R];  // rows jc0-3 .. jc0+2
+#pragma unroll
+    for (int q = 0; q < 2 * R; ++q) {
+      uy[q] = gld<T>(row(in, jc0 - R + q), goff);
+      lf_split(uy[q], fp[q], fm[q]);
+    }
+    auto sl = [](int p) { return (p + 2 * NR) % NR; };
+    {  // face jc0-½: the march's y-face arithmetic (bit-identical to it)
+      T n1, S1, n2, S2;
+      w5_side<T, WZ>(fp[0], fp[1], fp[2], fp[3], fp[4], w5_curv(fp[0], fp[1], fp[2], kk),
+                     w5_curv(fp[1], fp[2], fp[3], kk), w5_curv(fp[2], fp[3], fp[4], kk), n1, S1, kk);
+      w5_side<T, WZ>(fm[5], fm[4], fm[3], fm[2], fm[1], w5_curv(fm[5], fm[4], fm[3], kk),
+                     w5_curv(fm[4], fm[3], fm[2], kk), w5_curv(fm[3], fm[2], fm[1], kk), n2, S2, kk);
+      fy[sl(-1)] = w5_combine6(n1, S1, n2, S2);
+    }
+    cp[sl(-1)] = w5_curv(fp[1], fp[2], fp[3], kk);
+    cp[sl(0)] = w5_curv(fp[2], fp[3], fp[4], kk);
+    cm[sl(0)] = w5_curv(fm[2], fm[3], fm[4], kk);
+    cm[sl(1)] = w5_curv(fm[3], fm[4], fm[5], kk);
+#pragma unroll
+    for (int q = 1; q < 2 * R; ++q) {  // rows jc0-2 .. jc0+2
+      rp[sl(q - R)] = fp[q];
+      ru[sl(q - R)] = uy[q];
+    }
+#pragma unroll
+    for (int q = 2; q < 2 * R; ++q) rm[sl(q - R)] = fm[q];  // jc0-1 .. jc0+2
+  }
+  T un = gld<T>(row(in, jc0 + R), goff);  // u(j+3) of the current row
+  T hv = gld<T>(row(in, jc0), hoff);       // the halo column of the current row
+  T ax = T(0);
+  if constexpr (reads_aux<MODE>()) ax = gld<T>(row(aux, jc0), goff);
+
+  auto body = [&]<int PH>(int j) {
+    auto sl = [](int d) { return (PH + d + 2 * NR) % NR; };  // slot of row j + d
+    // new row j+3 of the own column: f-(j+3) now; f+(j+3) and u(j+3) after their use
+    T pn, mn;
+    lf_split(un, pn, mn);
+    rm[sl(3)] = mn;
+    const T unew = un;
+    const T hcur = hv;
+    const int jn = min(j + 1, jlast);
+    un = gld<T>(row(in, jn + R), goff);
+    hv = gld<T>(row(in, jn), hoff);
+    T axk = ax;
+    if constexpr (reads_aux<MODE>()) ax = gld<T>(row(aux, jn), goff);
+
+    // the row j into the wave's LDS row (own cell + one halo cell on lanes 0..4)
+    const T ctr = ru[sl(0)];
+    sp[lane + 2] = rp[sl(0)];
+    sm[lane + 2] = rm[sl(0)];
+    if constexpr (VISC) su[lane + 2] = ctr;
+    if (hl) {
+      T hp, hm;
+      lf_split(hcur, hp, hm);
+      sp[hslot] = hp;
+      sm[hslot] = hm;
+      if constexpr (VISC) su[hslot] = hcur;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // stores before the reads
+    T pv[5], mv[5];
+#pragma unroll
+    for (int d = 0; d < 5; ++d) {
+      pv[d] = sp[lane + d];      // f+(x-2 .. x+2)
+      mv[d] = sm[lane + 1 + d];  // f-(x-1 .. x+3)
+    }
+    T d2x = T(0), d2y = T(0);
+    if constexpr (VISC) {
+      d2x = fd4_d2k(su[lane], su[lane + 1], ctr, su[lane + 3], su[lane + 4], kk);
+      d2y = fd4_d2k(ru[sl(-2)], ru[sl(-1)], ctr, ru[sl(1)], ru[sl(2)], kk);
+    }
+    T fx;
+    {
+      T n1, S1, n2, S2;
+      w5_face3_sides<T, WZ>(pv, mv, n1, S1, n2, S2, kk);
+      fx = w5_combine6(n1, S1, n2, S2);  // 3 x flux at x+½
+    }
+    cp[sl(1)] = w5_curv(rp[sl(0)], rp[sl(1)], rp[sl(2)], kk);
+    cm[sl(2)] = w5_curv(rm[sl(1)], rm[sl(2)], rm[sl(3)], kk);
+    {
+      T n1, S1, n2, S2;
+      w5_side<T, WZ>(rp[sl(-2)], rp[sl(-1)], rp[sl(0)], rp[sl(1)], rp[sl(2)], cp[sl(-1)],
+                     cp[sl(0)], cp[sl(1)], n1, S1, kk);
+      w5_side<T, WZ>(rm[sl(3)], rm[sl(2)], rm[sl(1)], rm[sl(0)], rm[sl(-1)], cm[sl(2)],
+                     cm[sl(1)], cm[sl(0)], n2, S2, kk);
+      fy[sl(0)] = w5_combine6(n1, S1, n2, S2);  // 6 x flux at j+½
+    }
+    const T fxl = wave_shr1(fx);  // face x-½ from lane l-1 (lane 0: unused)
+    T L = -((fx - fxl) * rdx3 + (fy[sl(0)] - fy[sl(-1)]) * rdy6);
+    if constexpr (VISC) L += vx * d2x + vy * d2y;
+    T dnew = T(0);
+    const T v = stage_value<T, MODE>(axk, ctr, L, dt, a, b, dnew);
+    if (active) {
+      gst<T>(row(out, j), goff, v);
+      if constexpr (MODE == kLs1 || MODE == kLs) gst<T>(row(aux, j), goff, dnew);
+    }
+    rp[sl(3)] = pn;  // f+(j+3), u(j+3) replace f+(j-2), u(j-2)
+    ru[sl(3)] = unew;
+  };
+  for (int jb = jc0; jb < jc1; jb += NR) {
+    [&]<int... P>(std::integer_sequence<int, P...>) {
+      (void)((jb + P < jc1 ? (body.template operator()<P>(jb + P), true) : false) && ...);
+    }(std::make_integer_sequence<int, NR>{});
+  }
+}
+
+// ------------------------------------------------------------------------------
 // Host launchers
 // ------------------------------------------------------------------------------
 constexpr int kBTX3 = 64, kBTY3 = 8;
@@ -829,8 +996,37 @@ static hipError_t launch_b3(const BArgs& p) {
   }
 }
 
+// 2-D WENO5 kernel version (ADVDIFF_B2_VER / advdiff_set_b2_ver): 2 (default) = the
+// barrier-free wave-strip kernel (burgers2d_w5_kernel), 1 = the generic row-tile kernel
+// (three barriers per row; WENO7 always runs it).
+static int g_b2_ver = -1;
+static int b2_ver() {
+  if (g_b2_ver < 0) g_b2_ver = knob("B2_VER", 2);
+  return g_b2_ver;
+}
+
+template <typename T, bool WZ, bool VISC, int MODE>
+static hipError_t launch_b2_w5(const BArgs& p) {
+  const int strips = div_up(std::max(p.nx - 2 * p.border, 1), 63);
+  const int gx = div_up(strips, 4);
+  static const int minc = std::max(knob("B2_MINC", 1), 1);
+  const int yc = pick_chunk(p.hi - p.lo, gx, minc, 256);
+  const int gy = div_up(p.hi - p.lo, yc);
+  const double s = 1.0 / 12.0;
+  hipLaunchKernelGGL((burgers2d_w5_kernel<T, WZ, VISC, MODE>), dim3(gx, gy, 1), dim3(256, 1, 1),
+                     0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx, p.sy, p.lo, p.hi, yc,
+                     p.border, T(p.rdx / 3.0), T(p.rdy / 6.0), T(p.vx * s), T(p.vy * s), T(p.dt),
+                     T(p.a), T(p.b), p.dtp);
+  return hipGetLastError();
+}
+
 template <typename T, int W, bool WZ, bool VISC, int MODE>
 static hipError_t launch_b2(const BArgs& p) {
+  if constexpr (W == 5) {
+    // rows are addressed with 32-bit byte offsets inside a row (sy elements)
+    if (b2_ver() == 2 && (int64_t)p.sy * (int64_t)sizeof(T) < (int64_t(1) << 31))
+      return launch_b2_w5<T, WZ, VISC, MODE>(p);
+  }
   const int gx = div_up(p.nx, kBTX2);
   // fewest rows per y chunk: 1 — small grids (the reference's 400x406 rows) are latency-
   // bound, and a wave walking fewer rows in sequence wins there (400x406 WENO5-JS step
@@ -913,6 +1109,12 @@ static hipError_t run_b(int dtype, bool three_d, int scheme, bool ls, const BArg
 }
 
 }  // namespace advdiff
+
+extern "C" int advdiff_set_b2_ver(int v) {
+  const int old = advdiff::b2_ver();
+  advdiff::g_b2_ver = v;
+  return old;
+}
 
 extern "C" int advdiff_set_b3_ver(int v) {
   const int old = advdiff::b3_ver();

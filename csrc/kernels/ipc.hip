@@ -63,19 +63,24 @@ struct IpcWaitArgs {
 __global__ void ipc_signal_kernel(IpcSignalArgs a) {
   const int q = threadIdx.x;
   if (q >= a.n) return;
-  const uint64_t v = a.sent[q][0] + 1;
-  a.sent[q][0] = v;
+  // the counters are touched by one lane of one kernel at a time (stream order), but the
+  // kernels may run on different XCDs: device-scope atomics, never a stale L2 line
+  const uint64_t v = __hip_atomic_load(a.sent[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __hip_atomic_store(a.sent[q], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(a.remote[q], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // lane q: expect[q] += 1, then spin (acquire loads, s_sleep) until recv[q] reaches it.
 // Bounded: after timeout_ticks the lane records a timeout and leaves, so the grid always
 // drains even if a peer died (the host checks advdiff_ipc_errors at its sync points).
+// Ranks SHARING one GPU (tests) need every queue of every rank mapped by the hardware
+// scheduler: a spinning wait on a mapped queue can starve a producer whose queue is not
+// (oversubscribed HWS) — run them with few hardware queues (GPU_MAX_HW_QUEUES=1).
 __global__ void ipc_wait_kernel(IpcWaitArgs a) {
   const int q = threadIdx.x;
   if (q >= a.n) return;
-  const uint64_t e = a.expect[q][0] + 1;
-  a.expect[q][0] = e;
+  const uint64_t e = __hip_atomic_load(a.expect[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __hip_atomic_store(a.expect[q], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (__hip_atomic_load(a.flag[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
     __builtin_amdgcn_s_sleep(4);

@@ -147,3 +147,34 @@ def test_torch_kernel_switch_cpu_equivalence():
     assert np.array_equal(a.gather(), b.gather())
     with pytest.raises(ValueError):
         Solver(m, g, dtype=torch.float64, device="cpu", kernel="triton")
+
+
+def test_write_ghosts_layout(tmp_path):
+    """--write-ghosts: the reference's multi-GPU result.bin (every rank's slab WITH its
+    ghost planes, rank after rank: SaveBinary3D(h_u, Nx, Ny, _Nz + 6),
+    MultiGPU/Diffusion3d_Baseline/main.c:341).  Each block's owned planes equal the
+    global result, its inner ghost planes equal the neighbour's boundary planes, and the
+    summary block carries timed HtD/DtH lines."""
+    out, gh = tmp_path / "res.bin", tmp_path / "ghosts.bin"
+    nx, ny, nz, iters = 16, 14, 20, 3
+    rc = subprocess.run([sys.executable, "-m", "multigpu_advectiondiffusion_amd.launch", "-np", "2",
+                         "--cpu", "--timeout", "200", "diffusion3d", "1", "1", "1", "1", str(nx),
+                         str(ny), str(nz), str(iters), "--ic", "sine", "--write", str(out),
+                         "--write-ghosts", str(gh)],
+                        capture_output=True, text=True, timeout=300)
+    assert rc.returncode == 0, rc.stderr[-2000:]
+    glob = aio.load_binary(out, (nz, ny, nx))
+    raw = np.fromfile(gh, dtype=np.float32)
+    G = 6  # fused FD4 step: 3R ghost planes
+    counts = [10, 10]
+    assert raw.size == sum(c + 2 * G for c in counts) * ny * nx
+    blocks = np.split(raw, [(counts[0] + 2 * G) * ny * nx])
+    b0 = blocks[0].reshape(counts[0] + 2 * G, ny, nx)
+    b1 = blocks[1].reshape(counts[1] + 2 * G, ny, nx)
+    assert np.array_equal(b0[G:G + 10], glob[0:10]) and np.array_equal(b1[G:G + 10], glob[10:20])
+    assert np.array_equal(b0[G + 10:], glob[10:10 + G])   # rank 0's upper ghosts
+    assert np.array_equal(b1[:G], glob[10 - G:10])         # rank 1's lower ghosts
+    txt = rc.stdout
+    htod = float([l for l in txt.splitlines() if "Data transfer(s) HtD" in l][0].split(":")[1].split()[0])
+    dtoh = float([l for l in txt.splitlines() if "Data transfer(s) DtH" in l][0].split(":")[1].split()[0])
+    assert htod > 0.0 and dtoh > 0.0

@@ -58,6 +58,17 @@ def _spawn(world, *args):
     return spawn_local(world, _run, *args, device="cuda", transport="ipc", timeout=240)[0]
 
 
+@pytest.fixture(autouse=True)
+def _shared_gpu_env(monkeypatch):
+    """All ranks share the box's one GPU: one hardware queue per rank keeps every rank's
+    queue mapped by the hardware scheduler (with 4 per rank, 8 ranks + the test process
+    oversubscribe it, and a spinning device wait can starve a producer whose queue is
+    unmapped).  Real runs have one rank per GPU and are not affected."""
+    monkeypatch.setenv("ADVDIFF_SHARE_GPU", "1")
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "1")
+    monkeypatch.setenv("ADVDIFF_IPC_TIMEOUT_S", os.environ.get("ADVDIFF_IPC_TIMEOUT_S", "60"))
+
+
 @pytest.mark.parametrize("kind", ["diff3", "burg3", "diff2", "burg2", "diff3o2"])
 def test_ipc_slab_bitwise(kind, monkeypatch):
     """z/y slabs, per-stage (Burgers) and fused-step (heat) exchanges, 2 and 3 ranks,

@@ -140,6 +140,50 @@ def test_burgers2d_stage(dtype, weno_z, visc):
     assert err < (1e-11 if dtype == torch.float64 else 5e-4), err
 
 
+@pytest.mark.parametrize("ver", [2, 1])
+@pytest.mark.parametrize("mode", ["ssp1", "ssp", "ls"])
+@pytest.mark.parametrize("weno_z,visc", [(False, 0.0), (True, 0.01)])
+@pytest.mark.parametrize("rows", [(3, 4), (3, 9), (5, 44), (3, 130)])
+def test_burgers2d_stage_versions(ver, mode, weno_z, visc, rows):
+    """Both 2-D WENO5 kernels (v2: barrier-free wave strips, the default; v1: the generic
+    row tile) in every stage epilogue, on row ranges shorter than, equal to and not a
+    multiple of v2's 5-row unroll, a width with a partial last strip and an idle wave
+    (nx = 203: 197 active columns = 3 strips + 8), against the fp64 reference; cells
+    outside the updated box must be untouched."""
+    from multigpu_advectiondiffusion_amd.ops import _lib
+    lib = _lib.require()
+    j0, j1 = rows
+    ny, nx, sx = 136, 203, 208
+    f = _smooth3(1, ny, sx, 14, torch.float64)[0]
+    u0 = _smooth3(1, ny, sx, 15, torch.float64)[0]
+    aux = _smooth3(1, ny, sx, 16, torch.float64)[0]
+    rd = (1 / 0.01, 1 / 0.02)
+    vv = tuple(visc * r * r for r in rd)
+    a, b = {"ssp1": (0.0, 1.0), "ssp": (0.75, 0.25), "ls": (-0.4, 0.3)}[mode]
+    ls = mode == "ls"
+    exp_out, exp_aux = u0.clone(), aux.clone()
+    if ls:
+        ref.burgers2d_stage(f, exp_aux, exp_out, nx, j0, j1, 3, weno_z, *rd, *vv, 1e-3, a, b,
+                            ls=True)
+    else:
+        ref.burgers2d_stage(f, u0, exp_out, nx, j0, j1, 3, weno_z, *rd, *vv, 1e-3, a, b)
+    old = lib.advdiff_set_b2_ver(ver)
+    try:
+        gout, gaux = u0.to(DEV), aux.to(DEV)
+        kw = dict(nx=nx, j0=j0, j1=j1, border=3, weno_z=weno_z, rdx=rd[0], rdy=rd[1],
+                  vx=vv[0], vy=vv[1], dt=1e-3, a=a, b=b)
+        if ls:
+            stencil.burgers2d_stage(f.to(DEV), gaux, gout, ls=True, **kw)
+        else:
+            stencil.burgers2d_stage(f.to(DEV), gout.clone(), gout, **kw)
+        torch.cuda.synchronize()
+    finally:
+        lib.advdiff_set_b2_ver(old)
+    assert (gout.cpu() - exp_out).abs().max().item() < 1e-11
+    if ls:
+        assert (gaux.cpu() - exp_aux).abs().max().item() < 1e-11
+
+
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_norms(dtype):
     x = _rand3(13, 17, 40, dtype, 7) - 0.5

@@ -177,3 +177,24 @@ def test_native_cartesian_error_norms(tmp_path):
     pick = lambda t, k: float([l for l in t.splitlines() if l.startswith(k)][0].split(":")[1])  # noqa
     for k in ("L1 norm", "L2 norm", "Linf norm"):
         assert abs(pick(t1, k) - pick(t4, k)) <= 1e-12 * max(abs(pick(t1, k)), 1e-30), k
+
+
+def test_native_write_ghosts(tmp_path):
+    """--write-ghosts (native): every rank's slab with its ghost planes, rank after rank —
+    the reference's multi-GPU result.bin (MultiGPU/Diffusion3d_Baseline/main.c:341); the
+    owned planes equal --write's, the inner ghosts equal the neighbour's boundary planes;
+    the summary's HtD/DtH lines are timed (non-zero)."""
+    nx, ny, nz = 40, 36, 30
+    res, gh = tmp_path / "r.bin", tmp_path / "g.bin"
+    txt = _run("diffusion3d", [1.0, 1.0, 1.0, 1.0, nx, ny, nz, 5], res, world=2,
+               extra=["--ic", "sine", "--transport", "socket", "--write-ghosts", str(gh)])
+    glob = np.fromfile(res, dtype=np.float32).reshape(nz, ny, nx)
+    raw = np.fromfile(gh, dtype=np.float32)
+    G, c = 6, nz // 2
+    assert raw.size == 2 * (c + 2 * G) * ny * nx
+    b0, b1 = (x.reshape(c + 2 * G, ny, nx) for x in np.split(raw, 2))
+    assert np.array_equal(b0[G:G + c], glob[:c]) and np.array_equal(b1[G:G + c], glob[c:])
+    assert np.array_equal(b0[G + c:], glob[c:c + G]) and np.array_equal(b1[:G], glob[c - G:c])
+    for key in ("Data transfer(s) HtD", "Data transfer(s) DtH"):
+        v = float([l for l in txt.splitlines() if key in l][0].split(":")[1].split()[0])
+        assert v > 0.0, key
