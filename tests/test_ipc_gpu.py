@@ -60,12 +60,12 @@ def _spawn(world, *args):
 
 @pytest.fixture(autouse=True)
 def _shared_gpu_env(monkeypatch):
-    """All ranks share the box's one GPU: one hardware queue per rank keeps every rank's
+    """All ranks share the box's one GPU: few hardware queues per rank keep every rank's
     queue mapped by the hardware scheduler (with 4 per rank, 8 ranks + the test process
     oversubscribe it, and a spinning device wait can starve a producer whose queue is
     unmapped).  Real runs have one rank per GPU and are not affected."""
     monkeypatch.setenv("ADVDIFF_SHARE_GPU", "1")
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "1")
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", os.environ.get("ADVDIFF_TEST_HW_QUEUES", "2"))
     monkeypatch.setenv("ADVDIFF_IPC_TIMEOUT_S", os.environ.get("ADVDIFF_IPC_TIMEOUT_S", "60"))
 
 
