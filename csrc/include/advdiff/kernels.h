@@ -192,6 +192,10 @@ int advdiff_debug_print(int dtype, const void* u, int64_t sy, int64_t sz, int i0
 int advdiff_device_info(int dev, int64_t* out, int n);
 // Peer topology: can_access (hipDeviceCanAccessPeer), HSA link type (4 = xGMI), hop count.
 int advdiff_peer_info(int a, int b, int* can_access, int* link_type, int* hops);
+// fused 3-D step: phase-overlap variant (-1 = the per-order default; 0 plain, 3 graded wave
+// priority, 7 graded priority + the second wave half deferring its stage 3; bit-identical)
+// — A/B knob, returns the previous value
+int advdiff_set_step_var(int v);
 // v3 fused step: boundary-anchored edge tiles (1, default) or the plain partition (0)
 int advdiff_set_step_edge(int on);
 // 3-D WENO5 stage kernel version (9 = default, 3 = the v3 fallback used for planes of
@@ -200,6 +204,7 @@ int advdiff_set_b3_ver(int v);
 // 2-D WENO5 stage kernel version (2 = the barrier-free wave-strip kernel, default; 1 = the
 // generic row-tile kernel); returns the previous value.
 int advdiff_set_b2_ver(int v);
+
 // ---------------------------------------------------------------------------------
 // Peer transport of one node (ipc.hip): hipIpc-mapped device memory + device flags.  A
 // rank puts boundary cells straight into a neighbour's ghost cells (advdiff_copy_box with

@@ -967,6 +967,9 @@ static hipError_t launch_b3_v9(const BArgs& p) {
   return hipGetLastError();
 }
 
+// (Round-3 A/B, rejected: the wave computing a plane's extra bottom faces raising its
+// s_setprio for that plane — 233.9 vs 217.2 us per 256^3 stage, profiles/burgers_ab_r3.log.)
+
 // v9 addresses a plane with 32-bit byte offsets
 template <typename T>
 static bool v9_fits(const BArgs& p) {

@@ -151,6 +151,23 @@ __device__ __forceinline__ T fd4_axis(T acc, T k, T m2, T m1, T p1, T p2) {
 #pragma clang fp contract(off)
   return fma(k, fma(T(16), m1 + p1, -(m2 + p2)), acc);
 }
+// the same split in two: the axis sum S = 16 (m1+p1) - (m2+p2) (FD4) / m1+p1 (FD2), then
+// acc + K S — fd4_axis(acc, k, ...) == fd_apply(acc, k, fd4_sum(...)) bit for bit
+template <typename T>
+__device__ __forceinline__ T fd4_sum(T m2, T m1, T p1, T p2) {
+#pragma clang fp contract(off)
+  return fma(T(16), m1 + p1, -(m2 + p2));
+}
+template <typename T>
+__device__ __forceinline__ T fd2_sum(T m1, T p1) {
+#pragma clang fp contract(off)
+  return m1 + p1;
+}
+template <typename T>
+__device__ __forceinline__ T fd_apply(T acc, T k, T s) {
+#pragma clang fp contract(off)
+  return fma(k, s, acc);
+}
 // one FD2 axis: acc + K (m1+p1)
 template <typename T>
 __device__ __forceinline__ T fd2_axis(T acc, T k, T m1, T p1) {

@@ -142,7 +142,17 @@ struct V3Geom {
   static constexpr int TOTAL = OFF_B + 2 * ASET;
 };
 
-template <typename T, int ORDER, int NW, int RPW, int XS, int PF, bool SEP>
+// VAR = PRIO + 4 DEFER (round 3 A/B of the barrier-synchronised phases).  PRIO: which
+// waves run at a raised s_setprio (0 none, 1 the second half, 2 the "busy" waves whose
+// rows all carry three stages, 3 graded by the wave's row-stage count: the busiest at 2,
+// one row-stage less at 1).  DEFER: which waves DEFER the arithmetic and the store of their
+// stage 3 by one plane (0 none, 1 the second half, 2 the non-busy waves): such a wave
+// reads the stage's LDS neighbours (as their y-axis sum) before the next barrier and
+// computes right after it, while the others start the plane with their stage-1 LDS reads
+// — LDS traffic and VALU work of the two groups overlap instead of alternating in lockstep
+// (MI355X_MICROARCH.md "Two waves per SIMD", items 4 and 9).  Same arithmetic, bit-
+// identical results.
+template <typename T, int ORDER, int NW, int RPW, int XS, int PF, bool SEP, int VAR = 0>
 __device__ __forceinline__ void v3_march(
     T* lds, int tx, int ty, int gx, int gy, int edge, int kc0, int kc1,
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
@@ -164,6 +174,27 @@ __device__ __forceinline__ void v3_march(
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
   const int tid = w * 64 + lane;
   static_assert(TX > 0, "tile too narrow");
+  constexpr int PRIO = VAR % 4, DMODE = VAR / 4;
+  constexpr bool DEFER = DMODE != 0;
+  // row-stages of the wave (rows w + q NW: 1 + in S2 + in S3 each); busy: all in S3
+  int nst = 0;
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const int row = w + q * NW;
+    nst += 1 + (row >= R && row < S1R - R) + (row >= 2 * R && row < S1R - 2 * R);
+  }
+  const bool busy = nst == 3 * RPW;
+  const bool late = DMODE == 1 ? w >= NW / 2 : (DMODE == 2 ? !busy : false);  // scalar
+  if constexpr (PRIO == 1) {
+    if (w >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  } else if constexpr (PRIO == 2) {
+    if (busy) __builtin_amdgcn_s_setprio(1);
+  } else if constexpr (PRIO == 3) {
+    if (busy)
+      __builtin_amdgcn_s_setprio(2);
+    else if (nst == 3 * RPW - 1)
+      __builtin_amdgcn_s_setprio(1);
+  }
   const AxisTile atx = axis_tile(tx, gx, W, R, bx.xa0, bx.xa1, bx.xo0, bx.xo1, nx, edge);
   const AxisTile aty = axis_tile(ty, gy, S1R, R, bx.ya0, bx.ya1, bx.yo0, bx.yo1, ny, edge);
   const int x = atx.org + lane;
@@ -262,36 +293,89 @@ __device__ __forceinline__ void v3_march(
   }
   const T third = T(1.0 / 3.0);
 
-  // PH in [0, 2 NR): ring slots and the LDS buffer set (PH & 1) are compile-time
+  // stage 3 of plane kp from its ingredients: centre, z, x (DPP) and the y-axis sum ys,
+  // which comes from LDS (the normal path and the deferred one share it; the chain order
+  // centre, z, x, y is the per-stage kernels', so results stay bit-identical)
+  static_assert(XS, "stage 3 takes its x neighbours by DPP");
+  auto s3_finish = [&](int q, int kp, T c, T uo, T zm2, T zm1, T zp1, T zp2, T ys) {
+    T acc = fd_ctr(q3.kc, c, third * uo);
+    if constexpr (R == 2) {
+      acc = fd4_axis(acc, q3.k[2], zm2, zm1, zp1, zp2);
+      const T xm1 = wave_shr1(c), xp1 = wave_shl1(c);
+      const T xm2 = wave_shr1(xm1), xp2 = wave_shl1(xp1);
+      acc = fd4_axis(acc, q3.k[0], xm2, xm1, xp1, xp2);
+    } else {
+      acc = fd2_axis(acc, q3.k[2], zm1, zp1);
+      acc = fd2_axis(acc, q3.k[0], wave_shr1(c), wave_shl1(c));
+    }
+    acc = fd_apply(acc, q3.k[1], ys);
+    acc = pin(acc);
+    if (m3[q]) gst<T>(plane_rsrc((char*)uout + (int64_t)kp * szb), goff[q], acc);
+  };
+  // the y-axis sum of stage 3 from the B plane of buffer set AO (LDS)
+  auto s3_ysum = [&](int q, int AO) {
+    const int b = ar[q] + AO + ABB;
+    if constexpr (R == 2)
+      return fd4_sum(ld(b + 0 * W * E), ld(b + 1 * W * E), ld(b + 3 * W * E), ld(b + 4 * W * E));
+    else
+      return fd2_sum(ld(b + 0 * E), ld(b + 2 * W * E));
+  };
+  // deferred stage 3 (late waves, DEFER): the y sum and u^n of the plane, kept in registers
+  // across the barrier
+  T dys[RPW], duo[RPW];
+  (void)dys;
+  (void)duo;
+
+  // PH in [0, 2 NR): ring slots and the LDS buffer set (PH & 1) are compile-time.
+  // k == kc1 (DEFER only): a pseudo iteration without a top and a barrier that completes
+  // the late waves' last deferred stage 3.
   auto body = [&]<int PH>(int k) {
     auto sl = [](int d) { return (PH + d + 4 * NR) % NR; };
     constexpr int UIN = (PH + 3 * R) % NR;
     constexpr int SET = PH & 1;
     constexpr int UO = SET * USETB, AO = SET * ASETB;
-    // ---- top: new u plane enters the ring; LDS planes u(k+2R), A(k+R), B(k) ----
-    // the prefetch ring (PF slots) and the delay line (R slots) rotate by renaming:
-    // iteration PH consumes prefetch slot PF0 and refills it with plane k+PF
     constexpr int PF0 = PH % PF;
+    const bool real = !DEFER || k < kc1;  // scalar
+    if (real) {
+      // ---- top: new u plane enters the ring; LDS planes u(k+2R), A(k+R), B(k) ----
+      // the prefetch ring (PF slots) and the delay line (R slots) rotate by renaming:
+      // iteration PH consumes prefetch slot PF0 and refills it with plane k+PF
 #pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-      dl[q][(PH + R - 1) % R] = ru[q][UIN];
-      ru[q][UIN] = un[PF0][q];
-      lds_st<T>(lb, ub[q] + UO + (R * UW + R) * E, ru[q][sl(2 * R)]);
-      lds_st<T>(lb, aw[q] + AO, ra[q][sl(R)]);
-      lds_st<T>(lb, aw[q] + AO + ABB, rb[q][sl(0)]);
+      for (int q = 0; q < RPW; ++q) {
+        dl[q][(PH + R - 1) % R] = ru[q][UIN];
+        ru[q][UIN] = un[PF0][q];
+        lds_st<T>(lb, ub[q] + UO + (R * UW + R) * E, ru[q][sl(2 * R)]);
+        lds_st<T>(lb, aw[q] + AO, ra[q][sl(R)]);
+        lds_st<T>(lb, aw[q] + AO + ABB, rb[q][sl(0)]);
+      }
+#pragma unroll
+      for (int h = 0; h < NH; ++h)  // the rim of u(k+2R)
+        if (hl[h] >= 0) lds_st<T>(lb, hl[h] + UO, hv[PF0][h]);
+      {
+        const auto p2 = plane(k + PF + 2 * R);
+        const auto p3 = plane(k + PF + 3 * R);
+#pragma unroll
+        for (int h = 0; h < NH; ++h) hv[PF0][h] = gld<T>(p2, hoff[h]);
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) un[PF0][q] = gld<T>(p3, goff[q]);
+      }
+      __syncthreads();
     }
+    if constexpr (DEFER) {
+      // the late half opens the plane with the previous plane's stage-3 arithmetic (no
+      // LDS): B(k-1) and its z neighbours are still in the ring (stage 2 of this plane
+      // overwrites them only below)
+      if (late && k - 1 >= kc0) {
 #pragma unroll
-    for (int h = 0; h < NH; ++h)  // the rim of u(k+2R)
-      if (hl[h] >= 0) lds_st<T>(lb, hl[h] + UO, hv[PF0][h]);
-    {
-      const auto p2 = plane(k + PF + 2 * R);
-      const auto p3 = plane(k + PF + 3 * R);
-#pragma unroll
-      for (int h = 0; h < NH; ++h) hv[PF0][h] = gld<T>(p2, hoff[h]);
-#pragma unroll
-      for (int q = 0; q < RPW; ++q) un[PF0][q] = gld<T>(p3, goff[q]);
+        for (int q = 0; q < RPW; ++q) {
+          const int row = w + q * NW;
+          if (row < aty.lo || row >= aty.hi) continue;  // scalar branch
+          s3_finish(q, k - 1, rb[q][sl(-1)], duo[q], rb[q][sl(-3)], rb[q][sl(-2)],
+                    rb[q][sl(0)], rb[q][sl(1)], dys[q]);
+        }
+      }
+      if (!real) return;
     }
-    __syncthreads();
     // ---- stage 1: A(k+2R) on S1 ----
     const int pz1 = k + 2 * R;
     const bool z1 = pz1 >= zlo && pz1 < zhi;
@@ -370,60 +454,29 @@ __device__ __forceinline__ void v3_march(
         rb[q][sl(R)] = (z2 && m2[q]) ? acc : uo;
       }
     }
-    // ---- stage 3: u^{n+1}(k) on S3 ----
+    // ---- stage 3: u^{n+1}(k) on S3 (late waves: LDS reads now, arithmetic next plane) ----
     if (k >= kc0) {
-      const auto po = plane_rsrc((char*)uout + (int64_t)k * szb);
 #pragma unroll
       for (int q = 0; q < RPW; ++q) {
         const int row = w + q * NW;
         if (row < aty.lo || row >= aty.hi) continue;  // scalar branch
-        const int b = ar[q] + AO + ABB;
-        const T c = rb[q][sl(0)];
-        T acc = fd_ctr(q3.kc, c, third * dl[q][PH % R]);
-        constexpr int XC = XS ? 0 : R;
-        if constexpr (R == 2) {
-          acc = fd4_axis(acc, q3.k[2], rb[q][sl(-2)], rb[q][sl(-1)], rb[q][sl(1)], rb[q][sl(2)]);
-          T xm2, xm1, xp1, xp2;
-          if constexpr (XS) {
-            xm1 = wave_shr1(c);
-            xp1 = wave_shl1(c);
-            xm2 = wave_shr1(xm1);
-            xp2 = wave_shl1(xp1);
-          } else {
-            xm2 = ld(b + (2 * W + 0) * E);
-            xm1 = ld(b + (2 * W + 1) * E);
-            xp1 = ld(b + (2 * W + 3) * E);
-            xp2 = ld(b + (2 * W + 4) * E);
-          }
-          acc = fd4_axis(acc, q3.k[0], xm2, xm1, xp1, xp2);
-          acc = fd4_axis(acc, q3.k[1], ld(b + (0 * W + XC) * E),
-                         ld(b + (1 * W + XC) * E), ld(b + (3 * W + XC) * E),
-                         ld(b + (4 * W + XC) * E));
+        if (DEFER && late) {
+          dys[q] = s3_ysum(q, AO);
+          duo[q] = dl[q][PH % R];
         } else {
-          acc = fd2_axis(acc, q3.k[2], rb[q][sl(-1)], rb[q][sl(1)]);
-          T xm1, xp1;
-          if constexpr (XS) {
-            xm1 = wave_shr1(c);
-            xp1 = wave_shl1(c);
-          } else {
-            xm1 = ld(b + (W + 0) * E);
-            xp1 = ld(b + (W + 2) * E);
-          }
-          acc = fd2_axis(acc, q3.k[0], xm1, xp1);
-          acc = fd2_axis(acc, q3.k[1], ld(b + XC * E),
-                         ld(b + (2 * W + XC) * E));
+          s3_finish(q, k, rb[q][sl(0)], dl[q][PH % R], rb[q][sl(-2)], rb[q][sl(-1)],
+                    rb[q][sl(1)], rb[q][sl(2)], s3_ysum(q, AO));
         }
-        acc = pin(acc);
-        if (m3[q]) gst<T>(po, goff[q], acc);
       }
     }
   };
   static_assert((2 * NR) % PF == 0 && (2 * NR) % R == 0, "ring phases must repeat");
 
   // the LDS set of iteration k is (k - kst) & 1: unroll 2 NR so it is static
-  for (int kb = kst; kb < kc1; kb += 2 * NR) {
+  const int kend = kc1 + (DEFER ? 1 : 0);
+  for (int kb = kst; kb < kend; kb += 2 * NR) {
     [&]<int... P>(std::integer_sequence<int, P...>) {
-      (void)((kb + P < kc1 ? (body.template operator()<P>(kb + P), true) : false) && ...);
+      (void)((kb + P < kend ? (body.template operator()<P>(kb + P), true) : false) && ...);
     }(std::make_integer_sequence<int, 2 * NR>{});
   }
 }
@@ -442,7 +495,7 @@ constexpr int step_min_waves() {
 // The march variant: DPP x neighbours in stages 2/3 (XS = 1), prefetch distance 2,
 // unmerged LDS reads (SEP).  The other (XS, PF, SEP) combinations measured 1-9 % slower
 // at 512^3 (profiles/step_variants_r2.log, step_cfgs_edge_r2.log) and were removed.
-template <typename T, int ORDER, int NW, int RPW>
+template <typename T, int ORDER, int NW, int RPW, int VAR>
 __global__ __launch_bounds__(64 * NW) __attribute__((
     amdgpu_waves_per_eu(step_min_waves<T, ORDER, NW, RPW>()))) void diffusion3d_step_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
@@ -454,7 +507,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((
   const bool second = tile.z >= sc.gza;
   const int kc0 = second ? k0b + (tile.z - sc.gza) * sc.zchunk : k0 + tile.z * sc.zchunk;
   const int kc1 = min(kc0 + sc.zchunk, second ? k1b : k1);
-  v3_march<T, ORDER, NW, RPW, 1, 2, true>(lds, tile.x, tile.y, sc.gx, sc.gy, sc.edge, kc0, kc1,
+  v3_march<T, ORDER, NW, RPW, 1, 2, true, VAR>(lds, tile.x, tile.y, sc.gx, sc.gy, sc.edge, kc0, kc1,
                                            uin, uout, nx, ny, sy, sz, nz_alloc, zlo, zhi, bx,
                                            q1, q2, q3);
 }
@@ -478,7 +531,7 @@ struct SArgs {
   hipStream_t st;
 };
 
-template <typename T, int ORDER, int NW, int RPW>
+template <typename T, int ORDER, int NW, int RPW, int VAR>
 static hipError_t launch_step(const SArgs& a) {
   constexpr int R = ORDER / 2;
   const int edge = step_edge();
@@ -488,7 +541,7 @@ static hipError_t launch_step(const SArgs& a) {
   // resident workgroups = CUs x occupancy of this instance (LDS / VGPR bound: 1-2 per CU)
   static const int per_cu = [] {
     int nb = 0;
-    const void* fn = (const void*)diffusion3d_step_kernel<T, ORDER, NW, RPW>;
+    const void* fn = (const void*)diffusion3d_step_kernel<T, ORDER, NW, RPW, VAR>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * NW, 0) != hipSuccess || nb < 1)
       nb = 1;
     return nb;
@@ -508,7 +561,7 @@ static hipError_t launch_step(const SArgs& a) {
   const FdCoef<T> q1 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 1.0, true);
   const FdCoef<T> q2 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 0.25, true);
   const FdCoef<T> q3 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 2.0 / 3.0, true);
-  hipLaunchKernelGGL((diffusion3d_step_kernel<T, ORDER, NW, RPW>), grid, dim3(64, NW, 1), 0,
+  hipLaunchKernelGGL((diffusion3d_step_kernel<T, ORDER, NW, RPW, VAR>), grid, dim3(64, NW, 1), 0,
                      a.st, (const T*)a.uin, (T*)a.uout, a.nx, a.ny, a.sy, a.sz, a.nz_alloc,
                      a.k0, a.k1, a.k0b, a.k1b, sc, a.zlo, a.zhi, a.bx, q1, q2, q3);
   return hipGetLastError();
@@ -518,15 +571,50 @@ static hipError_t launch_step(const SArgs& a) {
 // FD4 16 waves x 2 rows (32 stage-1 rows) 662 us vs 715 us for 12 x 3; FD2 12 x 3 rows
 // 535 us vs 549 us for 16 x 2 (profiles/step_cfgs_edge_r2.log).  48 rows overflow the
 // 16-bit DS offsets, 10 x 4 spills at 168 VGPRs.
+// Phase-overlap variant (v3_march VAR) per order, from the round-3 interleaved A/B at
+// 512^3 fp64 (bench/step_ab.py, profiles/step_ab_r3.log; medians of 7 rounds x 10):
+//   FD4 (16 x 2): graded priority (VAR 3) 655.5 us vs 691.9 plain (-5.3 %); deferring
+//                 stage 3 as well: 669.8 (priority alone wins);
+//   FD2 (12 x 3): second half defers stage 3 + graded priority (VAR 7) 549.3 vs 560.7
+//                 (-2.0 %); priority alone: 562.6 (no gain).
+// ADVDIFF_STEP_VAR / advdiff_set_step_var selects 0 (plain), 3 or 7 for A/B (-1: default).
+static int g_step_var = -2;
+static int step_var() {
+  if (g_step_var == -2) g_step_var = knob("STEP_VAR", -1);
+  return g_step_var;
+}
+
+template <typename T, int ORDER, int NW, int RPW>
+static hipError_t launch_step_var(const SArgs& a) {
+  constexpr int DEF = ORDER == 4 ? 3 : 7;
+  const int v = step_var() < 0 ? DEF : step_var();
+  switch (v) {
+    case 0: return launch_step<T, ORDER, NW, RPW, 0>(a);
+    case 3: return launch_step<T, ORDER, NW, RPW, 3>(a);
+    case 7: return launch_step<T, ORDER, NW, RPW, 7>(a);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// Tile shape per order.  With the edge tiles (axis_tile), interleaved medians at 512^3:
+// FD4 16 waves x 2 rows (32 stage-1 rows) 662 us vs 715 us for 12 x 3; FD2 12 x 3 rows
+// 535 us vs 549 us for 16 x 2 (profiles/step_cfgs_edge_r2.log).  48 rows overflow the
+// 16-bit DS offsets, 10 x 4 spills at 168 VGPRs.
 template <typename T, int ORDER>
 static hipError_t dispatch_step(const SArgs& a) {
   if constexpr (ORDER == 4)
-    return launch_step<T, ORDER, 16, 2>(a);
+    return launch_step_var<T, ORDER, 16, 2>(a);
   else
-    return launch_step<T, ORDER, 12, 3>(a);
+    return launch_step_var<T, ORDER, 12, 3>(a);
 }
 
 }  // namespace advdiff
+
+extern "C" int advdiff_set_step_var(int v) {
+  const int old = advdiff::step_var();
+  advdiff::g_step_var = v;
+  return old;
+}
 
 extern "C" int advdiff_set_step_edge(int on) {
   const int old = advdiff::step_edge();
@@ -596,5 +684,5 @@ extern "C" int advdiff_diffusion3d_step(int dtype, const void* uin, void* uout, 
 extern "C" int advdiff_preload_diffusion_fused(void) {
   hipFuncAttributes a;
   return hipFuncGetAttributes(
-      &a, (const void*)advdiff::diffusion3d_step_kernel<double, 4, 16, 2>);
+      &a, (const void*)advdiff::diffusion3d_step_kernel<double, 4, 16, 2, 3>);
 }

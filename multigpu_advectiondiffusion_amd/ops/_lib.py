@@ -150,6 +150,8 @@ def _load():
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = c_int
+        lib.advdiff_set_step_var.argtypes = [c_int]
+        lib.advdiff_set_step_var.restype = c_int
         lib.advdiff_set_step_edge.argtypes = [c_int]
         lib.advdiff_set_step_edge.restype = c_int
         lib.advdiff_set_b3_ver.argtypes = [c_int]

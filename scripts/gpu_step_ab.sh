@@ -1,12 +1,12 @@
 #!/bin/bash
-# Fused-step A/B on one GPU: bitwise tests of the fused step, edge tiles on/off timing,
-# then the bench (scripts/gpu_step_ab.sh; results under gpurun_out/).
-set -o pipefail
-export TMPDIR=/tmp
+# Fused-step phase-overlap variants: bitwise tests, interleaved kernel A/B, bench per variant.
+cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_fused_step_gpu.py > gpurun_out/t_step.log 2>&1 || { echo TESTFAIL; tail -30 gpurun_out/t_step.log; exit 1; }
-tail -2 gpurun_out/t_step.log
-timeout -k 10 300 python -u bench/step_variants.py --cfgs 0 --edges 1,0 --schedules grid,persist --rounds 5 --reps 10 > gpurun_out/step_ab.log 2>&1 || { echo ABFAIL; tail -20 gpurun_out/step_ab.log; exit 1; }
-grep -v "^{" gpurun_out/step_ab.log
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || { echo BENCHFAIL; tail -5 gpurun_out/bench.log; exit 1; }
-tail -1 gpurun_out/bench.log | cut -c1-300
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_fused_step_gpu.py > gpurun_out/pytest_step.log 2>&1 || { echo "STEP TESTS FAILED"; tail -30 gpurun_out/pytest_step.log; exit 1; }
+tail -1 gpurun_out/pytest_step.log
+timeout -k 10 400 python -u bench/step_ab.py --rounds 7 --reps 10 > gpurun_out/step_ab.log 2>&1 || { echo "STEP AB FAILED"; tail -20 gpurun_out/step_ab.log; exit 1; }
+cat gpurun_out/step_ab.log | grep '^{'
+for v in ${BENCH_VARS:-0 2 3}; do
+  ADVDIFF_STEP_VAR=$v timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_var$v.log 2>&1 || { echo "BENCH var $v FAILED"; tail -20 gpurun_out/bench_var$v.log; exit 1; }
+  python3 -c "import json,sys; d=json.loads([l for l in open('gpurun_out/bench_var$v.log') if l.startswith('{')][-1]); print('var $v', d['value'], d['ms_per_step'], 'sustained', d['sustained']['value'], 'fd2', d['fd2_7pt']['value'])"
+done

@@ -139,22 +139,35 @@ def test_fused_step_box_bounds_match_reference():
         assert (got.cpu() - out).abs().max().item() < 1e-12, box
 
 
+@pytest.mark.parametrize("var", [-1, 0, 3, 7])
 @pytest.mark.parametrize("order", [4, 2])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_fused_step_odd_subrange_bitwise(order, dtype):
-    """The step kernel of each order (FD4: 16 waves x 2 rows, FD2: 12 x 3) is bit-identical
-    to the per-stage path on a sub-range with frozen planes and odd sizes."""
+def test_fused_step_odd_subrange_bitwise(var, order, dtype):
+    """The step kernel of each order (FD4: 16 waves x 2 rows, FD2: 12 x 3) in every
+    phase-overlap variant (advdiff_set_step_var: priority / deferred stage 3 of the second
+    wave half) is bit-identical to the per-stage path on a sub-range with frozen planes,
+    odd sizes and chunk lengths that are not a multiple of the march unroll."""
+    from multigpu_advectiondiffusion_amd.ops import _lib
+    lib = _lib.require()
     nz, ny, nx, sx, k0, k1, zlo, zhi, border = (77, 53, 133, 136, 5, 70, 2, 74, 2)
     g = torch.Generator().manual_seed(5)
     u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).to(dtype).cuda()
     c = (0.21, 0.17, 0.13)
     dt = 0.9 / (2 * sum(c)) if order == 2 else 0.5 / sum(c)
     exp = _per_stage(u, nx, ny, k0, k1, zlo, zhi, border, order, c, dt)
-    got = u.clone()
-    stencil.diffusion3d_step(u, got, nx=nx, ny=ny, k0=k0, k1=k1, zlo=zlo, zhi=zhi,
-                             border=border, order=order, cx=c[0], cy=c[1], cz=c[2], dt=dt)
-    torch.cuda.synchronize()
-    assert torch.equal(got, exp), (got - exp).abs().max().item()
+    old = lib.advdiff_set_step_var(var)
+    try:
+        for kk in ((k0, k1), (k0, k0 + 1), (k0, k0 + 11), (k0 + 3, k1)):
+            got = u.clone()
+            stencil.diffusion3d_step(u, got, nx=nx, ny=ny, k0=kk[0], k1=kk[1], zlo=zlo, zhi=zhi,
+                                     border=border, order=order, cx=c[0], cy=c[1], cz=c[2],
+                                     dt=dt)
+            torch.cuda.synchronize()
+            want = u.clone()
+            want[kk[0]:kk[1]] = exp[kk[0]:kk[1]]
+            assert torch.equal(got, want), (kk, (got - want).abs().max().item())
+    finally:
+        lib.advdiff_set_step_var(old)
 
 
 @pytest.mark.parametrize("order", [4, 2])
