@@ -154,7 +154,8 @@ def halo_diag(s, reps=5, dt=None):
     s.comm.barrier()
     ms = s.comm.allreduce_max((_t.perf_counter() - t0) / reps * 1e3)
     link = halo_link_bytes(s.cd.shape, s.pgrid, s.ghost, s.u.element_size(),
-                           corners=s.cart and s.fused)
+                           corners=s.cart and s.fused,
+                           direct=getattr(s.halo, "direct", True))
     # the same steps with the exchange switched off (ghosts go stale — run LAST, after
     # the validation): the compute-only step time; the timed ms/step minus this is the
     # part of the exchange the overlap did not hide

@@ -42,7 +42,7 @@ struct advdiff_ipc {
 
 namespace advdiff {
 
-constexpr int kIpcMaxPeers = 16;
+constexpr int kIpcMaxPeers = 32;  // 3^3 - 1 = 26 neighbours of a direct exchange
 
 struct IpcSignalArgs {
   uint64_t* remote[kIpcMaxPeers];  // peer's recv[rank]

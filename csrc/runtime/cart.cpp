@@ -13,6 +13,7 @@
 // The reference has no counterpart (its only split is z-slabs).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <sstream>
 
 #include "runtime.hpp"
@@ -133,23 +134,75 @@ void fused_view(const Cart& cd, int radius, int border, int a, int lo, int hi, R
   outr = {lo - view.lo, hi - view.lo};
 }
 
-std::vector<std::vector<HaloPlanMsg>> halo_plan(const Cart& cd, bool corners) {
+bool halo_direct_default() {
+  const char* v = std::getenv("ADVDIFF_CORNERS");
+  return !(v && std::string(v) == "phased");
+}
+
+static void check_distinct(const std::vector<HaloPlanMsg>& ph) {
+  for (size_t i = 0; i < ph.size(); ++i)  // distinct peers per phase (one message each)
+    for (size_t j = i + 1; j < ph.size(); ++j)
+      if (ph[i].peer == ph[j].peer)
+        throw std::runtime_error("halo phase with two messages to one peer");
+}
+
+std::vector<std::vector<HaloPlanMsg>> halo_plan(const Cart& cd, bool corners, bool direct) {
   const int dims = cd.dims, G = cd.ghost;
-  std::vector<std::vector<int>> phases;
   std::vector<int> split;
   for (int a = dims - 1; a >= 0; --a)
     if (cd.pgrid[a] > 1) split.push_back(a);
-  if (corners)
-    for (int a : split) phases.push_back({a});
-  else if (!split.empty())
-    phases.push_back(split);
+  std::vector<std::vector<HaloPlanMsg>> out;
+  if (split.empty()) return out;
   Range own[3], alloc[3];
   for (int a = 0; a < dims; ++a) {
     const Slab s = cd.axis(a);
     own[a] = {s.ghost, s.ghost + s.count()};
     alloc[a] = {0, s.alloc()};
   }
-  std::vector<std::vector<HaloPlanMsg>> out;
+  if (corners && direct) {
+    // every offset d in {-1,0,1}^dims \ {0} (0 on unsplit axes), last axis fastest
+    int c[3] = {0, 0, 0};
+    cd.coords_of(cd.rank, c);
+    std::vector<HaloPlanMsg> ph;
+    int lim[3];
+    for (int a = 0; a < 3; ++a) lim[a] = (a < dims && cd.pgrid[a] > 1) ? 1 : 0;
+    for (int d0 = -lim[0]; d0 <= lim[0]; ++d0)
+      for (int d1 = -lim[1]; d1 <= lim[1]; ++d1)
+        for (int d2 = -lim[2]; d2 <= lim[2]; ++d2) {
+          const int d[3] = {d0, d1, d2};
+          if (!d0 && !d1 && !d2) continue;
+          int nc[3] = {0, 0, 0};
+          bool inside = true;
+          for (int a = 0; a < dims; ++a) {
+            nc[a] = c[a] + d[a];
+            if (nc[a] < 0 || nc[a] >= cd.pgrid[a]) inside = false;
+          }
+          if (!inside) continue;
+          HaloPlanMsg m;
+          m.peer = cd.rank_of(nc);
+          for (int a = 0; a < dims; ++a) {
+            m.off[a] = d[a];
+            if (d[a] < 0) {
+              m.send.r[a] = {own[a].lo, own[a].lo + G};
+              m.recv.r[a] = {0, G};
+            } else if (d[a] > 0) {
+              m.send.r[a] = {own[a].hi - G, own[a].hi};
+              m.recv.r[a] = {own[a].hi, own[a].hi + G};
+            } else {
+              m.send.r[a] = m.recv.r[a] = own[a];
+            }
+          }
+          ph.push_back(m);
+        }
+    check_distinct(ph);
+    out.push_back(ph);
+    return out;
+  }
+  std::vector<std::vector<int>> phases;
+  if (corners)
+    for (int a : split) phases.push_back({a});
+  else
+    phases.push_back(split);
   for (const auto& axes : phases) {
     std::vector<HaloPlanMsg> ph;
     for (int a : axes)
@@ -158,8 +211,7 @@ std::vector<std::vector<HaloPlanMsg>> halo_plan(const Cart& cd, bool corners) {
         if (peer < 0) continue;
         HaloPlanMsg m;
         m.peer = peer;
-        m.axis = a;
-        m.side = side;
+        m.off[a] = side;
         for (int q = 0; q < dims; ++q) {
           const bool carried = corners && q > a;  // exchanged in an earlier phase
           m.send.r[q] = m.recv.r[q] = carried ? alloc[q] : own[q];
@@ -168,10 +220,7 @@ std::vector<std::vector<HaloPlanMsg>> halo_plan(const Cart& cd, bool corners) {
         m.recv.r[a] = side < 0 ? Range{0, G} : Range{own[a].hi, own[a].hi + G};
         ph.push_back(m);
       }
-    for (size_t i = 0; i < ph.size(); ++i)  // distinct peers per phase (one message each)
-      for (size_t j = i + 1; j < ph.size(); ++j)
-        if (ph[i].peer == ph[j].peer)
-          throw std::runtime_error("halo phase with two messages to one peer (a process-grid axis of 2 with periodic wrap?)");
+    check_distinct(ph);
     out.push_back(ph);
   }
   return out;
@@ -232,8 +281,9 @@ std::string geometry_json(const Problem& p, int rank, int size) {
     o << (ph ? "," : "") << "[";
     for (size_t q = 0; q < plan[ph].size(); ++q) {
       const HaloPlanMsg& m = plan[ph][q];
-      o << (q ? "," : "") << "{\"peer\":" << m.peer << ",\"axis\":" << m.axis
-        << ",\"side\":" << m.side << ",\"send\":" << jbox(m.send, dims)
+      o << (q ? "," : "") << "{\"peer\":" << m.peer << ",\"off\":[";
+      for (int a = 0; a < dims; ++a) o << (a ? "," : "") << m.off[a];
+      o << "],\"send\":" << jbox(m.send, dims)
         << ",\"recv\":" << jbox(m.recv, dims) << "}";
     }
     o << "]";

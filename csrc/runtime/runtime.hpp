@@ -182,17 +182,23 @@ struct Cart {
 // "PZxPYxPX" / "PYxPX" -> pgrid (array order); throws on a mismatch with dims / world
 void parse_pgrid(const std::string& spec, int dims, int world, int* pgrid);
 
-// One message of a halo phase, in local (array-order) boxes of the block incl. ghosts.
+// One message of a halo phase, in local (array-order) boxes of the block incl. ghosts;
+// off = the peer's process-grid offset (array order).
 struct HaloPlanMsg {
-  int peer = -1, axis = 0, side = 0;
+  int peer = -1;
+  int off[3] = {0, 0, 0};
   Box send, recv;
 };
 // Halo phases of a Cartesian block (mirror of parallel/halo.py CartesianHalo): corners =
 // false (per-stage star stencils): ONE phase with the faces of every split axis over the
-// owned extent of the other axes; corners = true (the fused step): one phase per split
-// axis, fastest first, each message spanning the FULL allocated extent of the axes
-// exchanged before it (so edge and corner ghosts arrive with the faces).
-std::vector<std::vector<HaloPlanMsg>> halo_plan(const Cart& cd, bool corners);
+// owned extent of the other axes.  corners = true (the fused step), direct (default,
+// ADVDIFF_CORNERS != "phased"): ONE phase with a message to every neighbour offset in
+// {-1,0,1}^dims (faces, edges and corners from the neighbours that own them — one xGMI
+// hop each on a fully connected node); phased: one phase per split axis, fastest first,
+// each message spanning the FULL allocated extent of the axes exchanged before it.
+bool halo_direct_default();
+std::vector<std::vector<HaloPlanMsg>> halo_plan(const Cart& cd, bool corners,
+                                               bool direct = halo_direct_default());
 
 // ------------------------------------------------------------------------------------
 // Problem + engine

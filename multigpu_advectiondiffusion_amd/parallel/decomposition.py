@@ -186,15 +186,26 @@ def parse_proc_grid(spec, world: int, shape_array: tuple, ghost: int) -> tuple:
 
 
 def halo_link_bytes(shape_array: tuple, pgrid: tuple, ghost: int, elem: int,
-                    corners: bool) -> float:
+                    corners: bool, direct: bool = True) -> float:
     """Bytes one rank moves over its busiest xGMI link per exchange (upper bound over
-    ranks).  Every neighbour pair has its own point-to-point link, so messages to
-    different neighbours overlap; with corners (the fused step's phased exchange: axis by
-    axis, fastest first, each phase carrying the ghosts of the axes before it) the
-    phases run one after another, so their per-phase maxima add up."""
+    ranks).  Every GPU pair of an 8-GPU node has its own point-to-point link, so messages
+    to different neighbours overlap.  corners (the fused step) with direct = True: one
+    phase, edges and corners straight from the diagonal neighbours, so the busiest link
+    carries the largest face; direct = False (the phased exchange: axis by axis, fastest
+    first, each phase carrying the ghosts of the axes before it): the phases run one after
+    another, so their per-phase maxima add up."""
     dims = len(shape_array)
     local = [-(-n // p) for n, p in zip(shape_array, pgrid)]  # largest block
     split = [a for a in range(dims) if pgrid[a] > 1]
+    if corners and direct:
+        faces = [0.0]
+        for a in split:
+            face = ghost
+            for b in range(dims):
+                if b != a:
+                    face *= local[b]
+            faces.append(face * elem)
+        return float(max(faces))
     done = set()
     per_phase = []
     for a in sorted(split, reverse=True):
@@ -211,7 +222,7 @@ def halo_link_bytes(shape_array: tuple, pgrid: tuple, ghost: int, elem: int,
 
 
 def candidate_proc_grids(world: int, shape_array: tuple, ghost: int, elem: int = 8,
-                         corners: bool = False, keep: int = 3) -> list:
+                         corners: bool = False, keep: int = 3, direct: bool = True) -> list:
     """Process grids worth trying on an xGMI node, best first by `halo_link_bytes`: the
     slab, plus grids that split only the two slowest axes (a split of the contiguous x
     axis makes the strided x faces AND boundary boxes a few cells wide, which waste
@@ -228,8 +239,8 @@ def candidate_proc_grids(world: int, shape_array: tuple, ghost: int, elem: int =
             continue
         if any(n // q < max(ghost, 1) for n, q in zip(shape_array, p)):
             continue
-        scored.append((halo_link_bytes(shape_array, p, ghost, elem, corners), p))
-    base = halo_link_bytes(shape_array, slab, ghost, elem, corners)
+        scored.append((halo_link_bytes(shape_array, p, ghost, elem, corners, direct), p))
+    base = halo_link_bytes(shape_array, slab, ghost, elem, corners, direct)
     for b, p in sorted(scored):
         if b < 0.9 * base and len(out) < keep:
             out.append(p)

@@ -179,35 +179,82 @@ class CartesianHalo:
     message of G layers over the owned extent of the other axes; all messages of a rank
     form ONE grouped RCCL call.
     corners=True (the fused full-step kernel: three stacked star stencils reach diagonal
-    neighbours): axis by axis, fastest first (x, then y, then z); each phase's message
-    spans the FULL allocated extent of the axes already exchanged, so edge and corner
-    ghosts arrive with the faces — three dependent phases, ordered on the comm stream
-    (no host blocking).
+    neighbours), two ways to fill the edge and corner ghosts:
+      direct (default, ADVDIFF_CORNERS=direct): ONE phase with a message to every
+        neighbour in the 3^d - 1 offsets of the process grid — faces to the face
+        neighbours, edges and corners straight from the diagonal neighbours.  An 8-GPU
+        MI355X node is fully connected by xGMI (7 links per GPU), so a diagonal neighbour
+        is one hop away and every message of the phase has a link of its own: a 2x2x2
+        grid uses all 7 links at once, and no phase waits for another;
+      phased (ADVDIFF_CORNERS=phased): axis by axis, fastest first (x, then y, then z);
+        each phase's message spans the FULL allocated extent of the axes already
+        exchanged, so edge and corner ghosts arrive with the faces — three dependent
+        phases, ordered on the comm stream (no host blocking).
+    Both fill every ghost cell with the owner's value: bitwise the same results.
     Axis-0 messages with full x/y extent are whole planes (contiguous, zero-copy); other
     messages are strided and go through pack/unpack with the native ``advdiff_copy_box``
     kernel on the comm stream.  Reference: none (the reference only splits z, §2.5).
     """
 
-    def __init__(self, comm, decomp, comm_stream=None, corners: bool = False):
+    def __init__(self, comm, decomp, comm_stream=None, corners: bool = False,
+                 direct: bool | None = None):
+        import os
         self.comm = comm
         self.cd = decomp
         self.comm_stream = comm_stream
         self.corners = corners
+        if direct is None:
+            direct = os.environ.get("ADVDIFF_CORNERS", "direct") != "phased"
+        self.direct = bool(corners and direct)
         self._bufs = {}
 
     def _phases(self):
-        """Axis groups exchanged together: all at once (faces) or fastest axis first."""
+        """Axis groups exchanged together: all at once (faces), fastest axis first
+        (phased corners), or None = one phase over every neighbour offset (direct)."""
         split = [a for a in range(self.cd.dims) if self.cd.pgrid[a] > 1]
+        if not split:
+            return []
+        if self.direct:
+            return [None]
         return [sorted(split, reverse=True)] if not self.corners else \
             [[a] for a in sorted(split, reverse=True)]
 
+    def _offsets(self):
+        """Neighbour offsets of the direct exchange (fastest axis varying fastest, as the
+        native halo_plan): every d in {-1,0,1}^dims, d != 0, zero on unsplit axes."""
+        import itertools
+        cd = self.cd
+        rng = [(-1, 0, 1) if cd.pgrid[a] > 1 else (0,) for a in range(cd.dims)]
+        return [d for d in itertools.product(*rng) if any(d)]
+
     def boxes(self, axes):
-        """[(peer, send_box, recv_box, (axis, side))] of one phase as local index ranges
-        ((lo, hi) per array axis) — the geometry the native runtime must reproduce
-        (csrc/runtime/cart.cpp halo_plan, tests/test_native_host.py)."""
+        """[(peer, send_box, recv_box, offset)] of one phase as local index ranges
+        ((lo, hi) per array axis; offset = the neighbour's coordinate offset) — the
+        geometry the native runtime must reproduce (csrc/runtime/cart.cpp halo_plan,
+        tests/test_native_host.py)."""
         cd = self.cd
         own = cd.owned_box()
         out = []
+        if axes is None:  # direct: one message per neighbour offset
+            G = cd.ghost
+            coords = cd.coords
+            for d in self._offsets():
+                c = [x + dx for x, dx in zip(coords, d)]
+                if not all(0 <= c[a] < cd.pgrid[a] for a in range(cd.dims)):
+                    continue
+                sb, rb = [], []
+                for a, (lo, hi) in enumerate(own):
+                    if d[a] < 0:
+                        sb.append((lo, lo + G))
+                        rb.append((0, G))
+                    elif d[a] > 0:
+                        sb.append((hi - G, hi))
+                        rb.append((hi, hi + G))
+                    else:
+                        sb.append((lo, hi))
+                        rb.append((lo, hi))
+                out.append((cd.rank_of(c), tuple(sb), tuple(rb), tuple(d)))
+            return out
         for a in axes:
             ax = cd.axis(a)
             for side, peer in ((-1, cd.neighbor(a, -1)), (1, cd.neighbor(a, 1))):
@@ -224,7 +271,8 @@ class CartesianHalo:
                 rb = list(sb)
                 sb[a] = tuple(s)
                 rb[a] = tuple(r)
-                out.append((peer, tuple(sb), tuple(rb), (a, side)))
+                off = tuple(side if b == a else 0 for b in range(cd.dims))
+                out.append((peer, tuple(sb), tuple(rb), off))
         return out
 
     def _regions(self, field, axes):

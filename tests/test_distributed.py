@@ -203,28 +203,38 @@ def _run_cart_fused(comm, kind, steps, decomp, fused):
     ("diff3", 4, (1, 2, 2)), ("diff3", 2, (1, 1, 2)), ("diff3o2", 4, (2, 2, 1)),
     ("diff2", 2, (1, 2)), ("diff2", 4, (2, 2)),
 ])
-def test_cartesian_fused_step_bitwise(kind, world, decomp):
+@pytest.mark.parametrize("corners", ["direct", "phased"])
+def test_cartesian_fused_step_bitwise(kind, world, decomp, corners, monkeypatch):
     """Cartesian blocks with the fused full-step kernel (3R ghosts on every split axis,
-    launches on views with explicit active/output bounds) == 1 rank, bitwise."""
+    launches on views with explicit active/output bounds) == 1 rank, bitwise — with the
+    one-phase diagonal-neighbour corner exchange and with the phased one."""
+    monkeypatch.setenv("ADVDIFF_CORNERS", corners)
     ref = _serial(kind, 3)
     out = spawn_local(world, _run_cart_fused, kind, 3, decomp, True)[0]
     assert np.array_equal(out, ref), np.abs(out - ref).max()
 
 
 def test_candidate_proc_grids_xgmi_model():
-    """Busiest-link bytes of the fused heat exchange (3R = 6 ghosts, phased corners) at
-    the weak-scaling grids: the slab moves 50 MB per link at N = 8, the z/y grids 38 MB;
-    x is never split; at N = 2 / 4 the slab is the only candidate."""
+    """Busiest-link bytes of the fused heat exchange (3R = 6 ghosts) at the weak-scaling
+    grids: the slab moves 50 MB per link at N = 8; the z/y grids 38 MB with the phased
+    corner exchange and 25 MB with the direct one (edges and corners from the diagonal
+    neighbours over their own links); x is never split; at N = 2 the slab is the only
+    candidate."""
     from multigpu_advectiondiffusion_amd.parallel.decomposition import (
         candidate_proc_grids, halo_link_bytes)
     g8 = (1024, 1024, 1024)
     assert round(halo_link_bytes(g8, (8, 1, 1), 6, 8, True) / 1e6, 1) == 50.3
-    assert round(halo_link_bytes(g8, (2, 4, 1), 6, 8, True) / 1e6, 1) == 38.3
+    assert round(halo_link_bytes(g8, (2, 4, 1), 6, 8, True, direct=False) / 1e6, 1) == 38.3
+    assert round(halo_link_bytes(g8, (2, 4, 1), 6, 8, True) / 1e6, 1) == 25.2
+    assert round(halo_link_bytes(g8, (2, 2, 2), 6, 8, True) / 1e6, 1) == 12.6
     c8 = candidate_proc_grids(8, g8, 6, 8, corners=True)
     assert c8[0] == (8, 1, 1) and set(c8[1:]) == {(2, 4, 1), (4, 2, 1)}
     assert all(p[2] == 1 for p in c8)
     assert candidate_proc_grids(2, (1024, 512, 512), 6, 8, corners=True) == [(2, 1, 1)]
-    assert candidate_proc_grids(4, (1024, 1024, 512), 6, 8, corners=True) == [(4, 1, 1)]
+    # N = 4, direct: the (2, 2, 1) faces are half the slab's
+    assert candidate_proc_grids(4, (1024, 1024, 512), 6, 8, corners=True) == [(4, 1, 1), (2, 2, 1)]
+    assert candidate_proc_grids(4, (1024, 1024, 512), 6, 8, corners=True,
+                                direct=False) == [(4, 1, 1)]
     assert candidate_proc_grids(1, g8, 6) == [(1, 1, 1)]
     # faces only (per-stage WENO exchange): messages to different neighbours overlap
     assert halo_link_bytes((512,) * 3, (2, 2, 2), 3, 8, False) == 3 * 256 * 256 * 8

@@ -81,15 +81,18 @@ def test_ipc_slab_bitwise(kind, monkeypatch):
         assert np.array_equal(out, ref), (kind, world, overlap, graph, np.abs(out - ref).max())
 
 
-@pytest.mark.parametrize("kind,world,decomp", [
-    ("diff3", 4, (1, 2, 2)), ("diff3", 8, (2, 2, 2)), ("burg3", 4, (2, 1, 2)),
-    ("diff2", 4, (2, 2)), ("burg2", 2, (1, 2)),
+@pytest.mark.parametrize("kind,world,decomp,corners", [
+    ("diff3", 4, (1, 2, 2), "direct"), ("diff3", 8, (2, 2, 2), "direct"),
+    ("diff3", 8, (2, 2, 2), "phased"), ("burg3", 4, (2, 1, 2), "direct"),
+    ("diff2", 4, (2, 2), "direct"), ("diff2", 4, (2, 2), "phased"), ("burg2", 2, (1, 2), "direct"),
 ])
-def test_ipc_cartesian_bitwise(kind, world, decomp, monkeypatch):
+def test_ipc_cartesian_bitwise(kind, world, decomp, corners, monkeypatch):
     """Cartesian blocks: strided boxes put straight into the neighbours' ghost boxes (no
-    pack/unpack), the fused step's phased corner exchange ordered on the device by the
-    flags — eager and graph-replayed, bitwise equal to the 1-rank run."""
+    pack/unpack); the fused step's corner exchange one phase over all 3^d - 1 neighbour
+    offsets (direct) or axis by axis ordered on the device by the flags (phased) — eager
+    and graph-replayed, bitwise equal to the 1-rank run."""
     monkeypatch.setenv("ADVDIFF_SHARE_GPU", "1")
+    monkeypatch.setenv("ADVDIFF_CORNERS", corners)
     ref = _reference(kind, 16)
     for overlap, graph in ((True, True), (False, False)):
         out = _spawn(world, kind, 16, overlap, decomp, graph)
@@ -124,6 +127,8 @@ NATIVE_CASES = [
      ["--ic", "sine", "--no-overlap"]),              # the round-2 intermittent case
     ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 50, 44, 46, 9], (46, 44, 50), 8, "2x2x2",
      ["--ic", "sine"]),
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 50, 44, 46, 9], (46, 44, 50), 8, "2x2x2",
+     ["--ic", "sine", "ADVDIFF_CORNERS=phased"]),  # the axis-by-axis corner exchange
     ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 66, 40, 45, 12], (45, 40, 66), 3, "slab",
      ["--ic", "sine"]),
     ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 66, 40, 45, 12], (45, 40, 66), 4, "2x2x1",
@@ -144,6 +149,8 @@ def test_native_poisoned_multirank_bitwise(tmp_path, app, args, shape, world, de
     socket (host-staged) transports must still equal the 1-rank run bitwise."""
     one, many = tmp_path / "one.bin", tmp_path / "many.bin"
     poison = {"ADVDIFF_POISON": "1"}
+    poison.update(e.split("=", 1) for e in extra if e.startswith("ADVDIFF_"))
+    extra = [e for e in extra if not e.startswith("ADVDIFF_")]
     _native(app, args, one, extra=extra, env_extra=poison)
     dec = [] if decomp == "slab" else ["--decomp", decomp]
     txt = _native(app, args, many, world=world, extra=extra + ["--transport", transport] + dec,

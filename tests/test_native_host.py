@@ -83,8 +83,9 @@ GEOMETRY_CASES = [
 ]
 
 
+@pytest.mark.parametrize("corners", ["direct", "phased"])
 @pytest.mark.parametrize("app,args,world,decomp,extra", GEOMETRY_CASES)
-def test_native_geometry_matches_python(app, args, world, decomp, extra):
+def test_native_geometry_matches_python(app, args, world, decomp, extra, corners):
     """Every rank's launch boxes, fused-step views and halo messages of the native runtime
     (bin/<app> --geometry, csrc/runtime/cart.cpp) equal the Python decomposition's
     (CartesianDecomposition, CartesianHalo.boxes, decomposition.fused_view)."""
@@ -98,7 +99,7 @@ def test_native_geometry_matches_python(app, args, world, decomp, extra):
     exe = CSRC.parent / "bin" / app
     if not exe.exists():
         pytest.skip("bin/ not built")
-    env = dict(os.environ, RANK="0", WORLD_SIZE=str(world))
+    env = dict(os.environ, RANK="0", WORLD_SIZE=str(world), ADVDIFF_CORNERS=corners)
     cmd = [str(exe)] + [str(a) for a in args] + ["--decomp", decomp, "--geometry"] + extra
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=60, env=env)
     assert r.returncode == 0, r.stderr
@@ -138,7 +139,7 @@ def test_native_geometry_matches_python(app, args, world, decomp, extra):
                     want = [list(x) for x in fused_view(cd, R, B, a, *box[a])]
                     assert v["axes"][a - 1] == want, (rank, box, a)
         if cd.size > 1 and not cd.is_slab:
-            halo = CartesianHalo(None, cd, corners=fused)
-            py = [[{"peer": p, "axis": k[0], "side": k[1], "send": lst(s), "recv": lst(rr)}
+            halo = CartesianHalo(None, cd, corners=fused, direct=corners == "direct")
+            py = [[{"peer": p, "off": list(k), "send": lst(s), "recv": lst(rr)}
                    for p, s, rr, k in halo.boxes(axes)] for axes in halo._phases()]
             assert nat["halo"] == py, rank
