@@ -3,7 +3,7 @@
 # counter group per rocprofv3 run (--pmc with kernel trace only), plus the counter list.
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
-out=gpurun_out/pmc_r3
+out=${PMC_OUT:-gpurun_out/pmc_r3}
 mkdir -p $out
 timeout -s KILL 60 rocprofv3 -L > $out/counters_list.txt 2>&1 || echo "counter list rc=$?"
 SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES"
