@@ -13,7 +13,8 @@
 //   ghost planes, MultiGPU/Diffusion3d_Baseline/main.c:341)  --error-norms
 //   --decomp slab|PZxPYxPX|PYxPX (process grid in array order: Cartesian blocks, cart.cpp;
 //   default z-slabs as the reference)  --geometry (print every rank's launch / halo
-//   geometry as JSON lines and exit; no GPU work)
+//   geometry as JSON lines and exit; no GPU work)  --graph / --no-graph (hipGraph
+//   stepping, Engine::steps; default: on for the single-rank and ipc transports)
 // Launch one process per GPU with torchrun-style env vars (RANK/WORLD_SIZE/LOCAL_RANK/
 // MASTER_ADDR/MASTER_PORT), e.g. via `python -m multigpu_advectiondiffusion_amd.launch`.
 #include <chrono>
@@ -42,7 +43,8 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
     std::string a = argv[q];
     if (a.rfind("--", 0) == 0) {
       const bool flag = a == "--fp32" || a == "--no-overlap" || a == "--error-norms" ||
-                        a == "--no-fused" || a == "--geometry";
+                        a == "--no-fused" || a == "--geometry" || a == "--graph" ||
+                        a == "--no-graph";
       if (flag || q + 1 >= argc) {
         opt[a] = "1";
       } else {
@@ -60,7 +62,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
                        : (dims == 3 ? " tEnd CFL L W H Nx Ny Nz [bx by bz]" : " tEnd CFL L W Nx Ny [bx by]"))
               << " [--ic NAME] [--order 2|4] [--weno js|z|js7] [--integrator ssprk3|lsrk45] [--no-fused] [--visc C] [--fp32] [--no-overlap]"
                  " [--transport rccl|ipc|socket] [--decomp slab|PZxPYxPX|PYxPX] [--write FILE]"
-                 " [--write-ghosts FILE] [--error-norms] [--geometry]\n";
+                 " [--write-ghosts FILE] [--error-norms] [--geometry] [--graph|--no-graph]\n";
     return 1;
   }
   Problem p;
@@ -98,6 +100,8 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   if (opt.count("--visc")) p.C = std::stod(opt["--visc"]);
   if (opt.count("--fp32")) p.dtype = ADVDIFF_F32;
   if (opt.count("--no-overlap")) p.overlap = false;
+  if (opt.count("--graph")) p.graph = 1;
+  if (opt.count("--no-graph")) p.graph = 0;
   const std::string decomp = opt.count("--decomp") ? opt["--decomp"] : "slab";
   std::string ic = opt.count("--ic") ? opt["--ic"] : (diff ? "heat" : "gaussian");
   p.ic = ic_code(ic);
@@ -132,7 +136,8 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   std::string title =
       std::string(diff ? "Diffusion-" : "Burgers-") + (dims == 3 ? "3D" : "2D") +
       (diff ? (p.order == 4 ? " MI355X-FD4" : " MI355X-FD2") : (p.weno == 1 ? " MI355X-WENO5Z" : p.weno == 0 ? " MI355X-WENO5JS" : " MI355X-WENO7JS"));
-  std::string optname = std::string("Fused LDS z-march + RK3 (gfx950), transport=") + tr->name();
+  std::string optname = std::string("Fused LDS z-march + RK3 (gfx950), transport=") + tr->name() +
+                        (eng.graphs() ? ", hipGraph steps" : "");
   if (eng.cartesian()) {
     optname += ", decomp=" + std::to_string(eng.cart().pgrid[0]) + "x" +
                std::to_string(eng.cart().pgrid[1]);

@@ -128,11 +128,18 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   const int zoff = slab_.start() - slab_.ghost;
   zact_ = {std::max(0, p.border() - zoff), std::min(slab_.alloc(), slab_.n - p.border() - zoff)};
   t_ = p.t0;
+  // hipGraph stepping: on by default where every exchange is stream-ordered device work
+  const char* ge = std::getenv("ADVDIFF_GRAPH");
+  const int want = ge ? std::atoi(ge) : p.graph;
+  graph_ = want < 0 ? tr_->graph_safe() : want != 0;
+  if (graph_ && std::string(tr_->name()) == "socket")
+    throw std::runtime_error("--graph: the socket transport synchronises the host inside a step");
 }
 
 Engine::~Engine() {
   (void)hipStreamSynchronize(compute_);
   (void)hipStreamSynchronize(comm_);
+  for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   (void)hipEventDestroy(ready_);
   (void)hipEventDestroy(halo_done_);
   (void)hipStreamDestroy(compute_);
@@ -319,12 +326,63 @@ void Engine::step(double dt) {
   ++it_;
 }
 
+// Capture kGraphSteps steps of `dt` from the current state (u_ parity) into an executable
+// graph.  The comm stream joins the capture through the ready_ event of the first halo
+// start; the last exchange is joined back into compute_ before the capture ends, so a
+// replay leaves no exchange pending.  Capturing runs no work: the host state the steps
+// advance (t_, it_, buffer roles) is restored afterwards.
+hipGraphExec_t Engine::graph_for(double dt) {
+  const GraphKey key{dt, u_};
+  auto it = graphs_.find(key);
+  if (it != graphs_.end()) return it->second;
+  const double t = t_;
+  const int itn = it_;
+  void *u = u_, *a = A_, *b = B_;
+  HIP_CHECK(hipStreamBeginCapture(compute_, hipStreamCaptureModeThreadLocal));
+  for (int q = 0; q < kGraphSteps; ++q) step(dt);
+  if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
+  halo_pending_ = false;
+  hipGraph_t g = nullptr;
+  HIP_CHECK(hipStreamEndCapture(compute_, &g));
+  hipGraphExec_t ex = nullptr;
+  HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+  HIP_CHECK(hipGraphDestroy(g));
+  if (u_ != u || A_ != a || B_ != b)
+    throw std::runtime_error("graph capture: buffer roles did not return to their start");
+  t_ = t;
+  it_ = itn;
+  graphs_.emplace(key, ex);
+  return ex;
+}
+
+void Engine::steps(int n, double dt) {
+  if (!graph_) {
+    for (int q = 0; q < n; ++q) step(dt);
+    return;
+  }
+  // eager steps first: the transport's one-time handshakes (host communication) must not
+  // fall inside a capture, and the u/A ping-pong visits both parities in two steps
+  for (; warm_ < 2 && n > 0; ++warm_, --n) step(dt);
+  if (n >= kGraphSteps && halo_pending_) {  // an event recorded outside a capture cannot
+    HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));  // be waited on inside it
+    halo_pending_ = false;
+  }
+  for (; n >= kGraphSteps; n -= kGraphSteps) {
+    HIP_CHECK(hipGraphLaunch(graph_for(dt), compute_));
+    for (int q = 0; q < kGraphSteps; ++q) {  // the same additions as kGraphSteps eager steps
+      t_ += dt;
+      ++it_;
+    }
+  }
+  for (; n > 0; --n) step(dt);
+}
+
 Stats Engine::run_iters(int iters) {
   const double dt = stable_dt();
   HIP_CHECK(hipDeviceSynchronize());
   tr_->barrier();
   const double t0 = now_s();
-  for (int q = 0; q < iters; ++q) step(dt);
+  steps(iters, dt);
   HIP_CHECK(hipStreamSynchronize(compute_));
   HIP_CHECK(hipStreamSynchronize(comm_));
   tr_->barrier();
@@ -342,7 +400,16 @@ Stats Engine::run_until(double t_end) {
   HIP_CHECK(hipDeviceSynchronize());
   tr_->barrier();
   const double t0 = now_s();
+  // the steps of the full dt0 (graph-replayable), counted with the loop's own arithmetic
   int n = 0;
+  {
+    double t = t_;
+    while (t < t_end * (1 - 1e-14) && !(t + dt0 > t_end)) {
+      t += dt0;
+      ++n;
+    }
+  }
+  steps(n, dt0);
   while (t_ < t_end * (1 - 1e-14)) {
     double dt = dt0;
     if (t_ + dt > t_end) dt = t_end - t_;

@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -106,6 +107,10 @@ class Transport {
   virtual std::vector<char> gather(const std::vector<char>& local) = 0;
   // Wait timeouts or other deferred transport errors seen so far (call at a sync point).
   virtual long long errors() { return 0; }
+  // every exchange step is stream-ordered device work with no host synchronisation, so a
+  // step can be captured into a hipGraph (local, ipc: yes; socket: host-staged, no; rccl:
+  // capturable, but never run multi-rank on the 1-GPU test box -> opt-in with --graph)
+  virtual bool graph_safe() const { return false; }
 
  protected:
   void* staging(size_t slot, size_t bytes, hipStream_t stream);  // device staging buffer
@@ -227,6 +232,7 @@ struct Problem {
   bool overlap = true;
   int integrator = 0;              // 0 SSP-RK3, 1 low-storage RK4(5)
   bool fused = true;               // 3-D heat + SSP-RK3: one launch per step (3R ghosts)
+  int graph = -1;                  // hipGraph stepping: -1 auto (graph-safe transports), 0, 1
   int radius() const {
     return physics == Physics::Diffusion ? order / 2 : (weno == 2 ? 4 : 3);
   }
@@ -260,6 +266,11 @@ class Engine {
   ~Engine();
   double stable_dt() const;
   void step(double dt);
+  // n steps of constant dt: through hipGraphs of kGraphSteps steps when enabled (after two
+  // eager steps that run the transport's one-time handshakes for both buffer parities)
+  void steps(int n, double dt);
+  bool graphs() const { return graph_; }
+  static constexpr int kGraphSteps = 8;  // even: the u/A ping-pong returns to its start
   Stats run_iters(int iters);
   Stats run_until(double t_end);
   // Σ|u-e|, Σ(u-e)², max|u-e| over the owned slab vs the exact solution (sine/heat ICs)
@@ -329,6 +340,16 @@ class Engine {
   Range full_, interior_, blo_, bhi_;
   double t_ = 0;
   int it_ = 0;
+  // hipGraph stepping: one executable graph per (dt, u_ parity) of kGraphSteps steps
+  bool graph_ = false;
+  int warm_ = 0;  // eager steps run so far (handshakes)
+  struct GraphKey {
+    double dt;
+    void* u;
+    bool operator<(const GraphKey& o) const { return dt < o.dt || (dt == o.dt && u < o.u); }
+  };
+  std::map<GraphKey, hipGraphExec_t> graphs_;
+  hipGraphExec_t graph_for(double dt);
 };
 
 // Reference summary blocks (MultiGPU/Diffusion3d_Baseline/Tools.c:255-270)

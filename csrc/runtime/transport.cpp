@@ -449,6 +449,7 @@ class IpcTransport final : public Transport {
     advdiff_ipc_destroy(ctx_);
   }
   const char* name() const override { return "ipc"; }
+  bool graph_safe() const override { return true; }
 
   void exchange_boxes(const std::vector<BoxMsg>& msgs, hipStream_t s) override {
     if (msgs.empty()) return;
@@ -583,6 +584,7 @@ class IpcTransport final : public Transport {
 class LocalTransport final : public Transport {
  public:
   const char* name() const override { return "local"; }
+  bool graph_safe() const override { return true; }
   void exchange(const std::vector<Msg>&, hipStream_t) override {}
   void halo(const void*, void*, const void*, void*, size_t, int, int, hipStream_t) override {}
   double allreduce_max(double v) override { return v; }

@@ -198,3 +198,49 @@ def test_native_write_ghosts(tmp_path):
     for key in ("Data transfer(s) HtD", "Data transfer(s) DtH"):
         v = float([l for l in txt.splitlines() if key in l][0].split(":")[1].split()[0])
         assert v > 0.0, key
+
+
+@pytest.mark.parametrize("app,args,shape,extra", [
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 70, 60, 56, 21], (56, 60, 70), ["--ic", "sine"]),
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 70, 60, 56, 19], (56, 60, 70),
+     ["--ic", "sine", "--no-fused"]),
+    ("burgers3d", [0.05, 0.3, 2.0, 2.0, 2.0, 48, 44, 40], (40, 44, 48),
+     ["--weno", "js7", "--integrator", "lsrk45"]),
+    ("diffusion2d", [1.0, 1.0, 1.0, 130, 90, 30], (90, 130), ["--ic", "disc"]),
+    ("burgers2d", [0.1, 0.4, 2.0, 2.0, 140, 100], (100, 140), ["--weno", "js"]),
+])
+def test_native_graph_steps_bitwise(tmp_path, app, args, shape, extra):
+    """hipGraph stepping of the native engine (Engine::steps: 2 eager steps, then graphs of
+    8 steps, eager remainder) == eager stepping, bitwise; the banner says which ran."""
+    a, b = tmp_path / "graph.bin", tmp_path / "eager.bin"
+    txt = _run(app, args, a, extra=extra + ["--graph"])
+    assert "hipGraph steps" in txt, txt[-800:]
+    txt = _run(app, args, b, extra=extra + ["--no-graph"])
+    assert "hipGraph steps" not in txt
+    ga = np.fromfile(a, dtype=np.float32).reshape(shape)
+    gb = np.fromfile(b, dtype=np.float32).reshape(shape)
+    assert np.isfinite(ga).all() and np.array_equal(ga, gb), np.abs(ga - gb).max()
+
+
+@pytest.mark.parametrize("world,decomp,extra", [
+    (2, "slab", []), (4, "2x2x1", []), (8, "2x2x2", []), (4, "2x1x2", ["--no-fused"]),
+])
+def test_native_ipc_graph_steps_bitwise(tmp_path, world, decomp, extra):
+    """Multi-rank hipGraph replay over the ipc transport (puts, signal and wait kernels
+    captured with the stencil launches; ranks share the one GPU) == the 1-rank eager run."""
+    args = [1.0, 1.0, 1.0, 1.0, 50, 44, 46, 21]
+    one, many = tmp_path / "one.bin", tmp_path / "many.bin"
+    _run("diffusion3d", args, one, extra=["--ic", "sine", "--no-graph"] + extra)
+    dec = [] if decomp == "slab" else ["--decomp", decomp]
+    env = dict(os.environ)
+    os.environ.update(ADVDIFF_SHARE_GPU="1", GPU_MAX_HW_QUEUES="2", ADVDIFF_IPC_TIMEOUT_S="60")
+    try:
+        txt = _run("diffusion3d", args, many, world=world,
+                   extra=["--ic", "sine", "--transport", "ipc"] + dec + extra)
+    finally:
+        os.environ.clear()
+        os.environ.update(env)
+    assert "hipGraph steps" in txt, txt[-800:]
+    a = np.fromfile(one, dtype=np.float32).reshape(46, 44, 50)
+    b = np.fromfile(many, dtype=np.float32).reshape(46, 44, 50)
+    assert np.array_equal(a, b), np.abs(a - b).max()
