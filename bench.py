@@ -238,7 +238,8 @@ def main():
     if not linf <= bound:
         raise SystemExit(f"bench validation failed: L_inf vs exact = {linf:.3e} > {bound:.3e}")
 
-    link = "RCCL" if comm.backend == "nccl" else str(comm.backend)
+    link = ("ipc device puts" if comm.transport == "ipc" and n > 1 else
+            "RCCL" if comm.backend == "nccl" else str(comm.backend))
     result = {
         "metric": METRIC,
         "value": round(mlups, 1),

@@ -217,6 +217,36 @@ extern "C" int advdiff_ipc_wait(advdiff_ipc* c, const int* peers, int n, void* s
   return hipGetLastError();
 }
 
+// Forget every mapping and exported handle (call with no put in flight, collectively): a
+// freed-and-reallocated field may come back at the same address, where a cached handle or
+// mapping would still name the old allocation.  The flag blocks stay mapped.
+extern "C" int advdiff_ipc_reset(advdiff_ipc* c) {
+  if (c == nullptr) return hipErrorInvalidValue;
+  hipError_t e = hipDeviceSynchronize();
+  std::lock_guard<std::mutex> g(c->mu);
+  for (auto it = c->opened.begin(); it != c->opened.end();) {
+    bool flags = false;  // a peer's flag block: keep it (the counters live there)
+    for (uint64_t* cell : c->peer_cell)
+      if (cell && (char*)cell >= (char*)it->second && (char*)cell < (char*)it->second + 4096)
+        flags = true;
+    if (flags) {
+      ++it;
+      continue;
+    }
+    const hipError_t ec = hipIpcCloseMemHandle(it->second);
+    if (e == hipSuccess) e = ec;
+    it = c->opened.erase(it);
+  }
+  for (auto it = c->exported.begin(); it != c->exported.end();) {
+    if (it->first == (uintptr_t)c->block) {
+      ++it;
+    } else {
+      it = c->exported.erase(it);
+    }
+  }
+  return e;
+}
+
 // wait timeouts so far (synchronous read: call at a sync point)
 extern "C" int advdiff_ipc_errors(advdiff_ipc* c, long long* timeouts) {
   if (c == nullptr || timeouts == nullptr) return hipErrorInvalidValue;

@@ -97,6 +97,7 @@ _IPC_SIGS = {
     "advdiff_ipc_signal": [c_vp, ctypes.POINTER(c_int), c_int, c_vp],
     "advdiff_ipc_wait": [c_vp, ctypes.POINTER(c_int), c_int, c_vp],
     "advdiff_ipc_errors": [c_vp, ctypes.POINTER(ctypes.c_longlong)],
+    "advdiff_ipc_reset": [c_vp],
 }
 
 # low-storage RK variants share the signature of the SSP stage entries

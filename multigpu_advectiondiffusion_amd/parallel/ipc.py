@@ -68,6 +68,21 @@ class IpcPeers:
         comm.barrier()  # every flag block mapped before anyone signals
         self._dest = {}
         self._calls = {}
+        self.epoch = 0  # bumped by reset(): graphs captured before it hold stale pointers
+
+    def reset(self) -> None:
+        """Collective: forget every learned receive address, peer mapping and exported
+        handle (the flag blocks and their counters stay).  Called when a solver allocates
+        its fields: a field freed and reallocated (another solver, the allocator's cache
+        emptied) can come back at an address the cache still keys, while the peer's new
+        receive box lives elsewhere — puts through the stale entry would miss it."""
+        torch.cuda.synchronize(self.comm.device)
+        self.comm.barrier()  # nobody has a put in flight into a mapping being closed
+        _lib.check(self.lib.advdiff_ipc_reset(self.ctx), "advdiff_ipc_reset")
+        self._dest.clear()
+        self._calls.clear()
+        self.epoch += 1
+        self.comm.barrier()
 
     # ------------------------------------------------------------------------------
     def _swap(self, peers, payloads):

@@ -157,6 +157,15 @@ class Solver:
         if device_dt is None:
             device_dt = self.device.type == "cuda" and kernel == "native"
         self.device_dt = bool(device_dt) and model.needs_umax
+        if self._ipc_multi():
+            comm.ipc().reset()  # new fields: no cached peer address may survive (ipc.py)
+
+    def _ipc_multi(self) -> bool:
+        return (self.device.type == "cuda" and self.comm.size > 1
+                and self.comm.transport == "ipc")
+
+    def _ipc_epoch(self) -> int:
+        return self.comm.ipc().epoch if self._ipc_multi() else 0
 
     def _initial_field(self, ic, params):
         """IC of the local slab incl. ghosts (ghosts = the neighbours' planes at t0).
@@ -435,12 +444,16 @@ class Solver:
         """dt=None: a graph of device-dt (adaptive CFL) steps towards t_end."""
         # A graph bakes in the buffer addresses: the fused / LSRK paths ping-pong u <-> un,
         # so after an odd number of eager steps the other parity needs its own graph.
-        key = (None if dt is None else float(dt), t_end, self.GRAPH_STEPS, self.u.data_ptr())
+        # multi-rank ipc: the graph also bakes in the peers' receive addresses, valid for the
+        # IpcPeers epoch it was captured in
+        ep = self._ipc_epoch()
+        key = (None if dt is None else float(dt), t_end, self.GRAPH_STEPS, self.u.data_ptr(), ep)
         g = getattr(self, "_graphs", {}).get(key)
         if g is not None:
             return g
         if not hasattr(self, "_graphs"):
             self._graphs = {}
+        self._graphs = {k: v for k, v in self._graphs.items() if k[-1] == ep}
         # state snapshot: capture executes nothing, but keep t/it bookkeeping exact
         t, it = self.t, self.it
         self._prepare_graph_halos()
