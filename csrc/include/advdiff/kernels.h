@@ -226,8 +226,8 @@ int advdiff_ipc_map(advdiff_ipc* c, const advdiff_ipc_addr* a, void** ptr);
 int advdiff_ipc_set_peer(advdiff_ipc* c, int peer, const advdiff_ipc_addr* peer_flags);
 int advdiff_ipc_signal(advdiff_ipc* c, const int* peers, int n, void* stream);
 int advdiff_ipc_wait(advdiff_ipc* c, const int* peers, int n, void* stream);
-// close every peer mapping and exported handle except the flag blocks (collective, no
-// put in flight): after fields were freed and reallocated
+// close every peer mapping except the flag blocks (collective, no put in flight): after
+// fields were freed and reallocated
 int advdiff_ipc_reset(advdiff_ipc* c);
 int advdiff_ipc_errors(advdiff_ipc* c, long long* timeouts);
 

@@ -139,7 +139,7 @@ struct V3Geom {
   static constexpr int ASET = S1R * W + 2 * R;      // A/B plane buffer (+R pad each side)
   static constexpr int OFF_A = 2 * USET;            // element offset of A0 in the block
   static constexpr int OFF_B = OFF_A + 2 * ASET;    // B0
-  static constexpr int TOTAL = OFF_B + 2 * ASET;
+  static constexpr int TOTAL = OFF_B + 2 * ASET + R * W;  // + pad: PAIR reads past B1
 };
 
 // VAR = PRIO + 4 DEFER (round 3 A/B of the barrier-synchronised phases).  PRIO: which
@@ -174,13 +174,18 @@ __device__ __forceinline__ void v3_march(
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
   const int tid = w * 64 + lane;
   static_assert(TX > 0, "tile too narrow");
-  constexpr int PRIO = VAR % 4, DMODE = VAR / 4;
+  constexpr int PRIO = VAR % 4, DMODE = (VAR / 4) % 4;
   constexpr bool DEFER = DMODE != 0;
-  // row-stages of the wave (rows w + q NW: 1 + in S2 + in S3 each); busy: all in S3
+  // PAIR: the wave owns RPW ADJACENT rows (w RPW + q) instead of rows w + q NW, so the y
+  // neighbours its rows share are read from LDS once and its own rows come from registers
+  // (FD4 16 x 2: 8 -> 4 LDS reads per stage and wave; FD2 12 x 3: 6 -> 2)
+  constexpr bool PAIR = VAR / 16 != 0;
+  auto row_of = [&](int q) { return PAIR ? w * RPW + q : w + q * NW; };
+  // row-stages of the wave (1 + in S2 + in S3 per row); busy: all in S3
   int nst = 0;
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
-    const int row = w + q * NW;
+    const int row = row_of(q);
     nst += 1 + (row >= R && row < S1R - R) + (row >= 2 * R && row < S1R - 2 * R);
   }
   const bool busy = nst == 3 * RPW;
@@ -221,7 +226,7 @@ __device__ __forceinline__ void v3_march(
   bool m1[RPW], m2[RPW], m3[RPW];
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
-    const int row = w + q * NW;
+    const int row = row_of(q);
     const int y = aty.org + row;
     const bool inxy = xin && y >= bx.ya0 && y < bx.ya1;
     m1[q] = inxy;
@@ -233,6 +238,11 @@ __device__ __forceinline__ void v3_march(
     const int rc = clampi(row, R, S1R - R - 1);                 // in-bounds for masked rows
     ar[q] = (G::OFF_A + R + (rc - R) * W + lane - (XS ? 0 : R)) * E;
   }
+  // PAIR: the wave's first row and its A/B-plane LDS base at row row0 - R (the lowest
+  // row any of its y reads touches: immediates stay non-negative)
+  const int row0 = w * RPW;
+  const int apb = (G::OFF_A + R + (row0 - R) * W + lane) * E;
+  (void)apb;
   uint32_t hoff[NH];
   int hl[NH];
 #pragma unroll
@@ -320,6 +330,32 @@ __device__ __forceinline__ void v3_march(
     else
       return fd2_sum(ld(b + 0 * E), ld(b + 2 * W * E));
   };
+  // PAIR: the column of one plane over rows row0-R .. row0+RPW-1+R — the R rows on each
+  // side from LDS (base + immediates; rows beyond the region read the U sets / the pad and
+  // are used by no computed row), the wave's own rows from registers
+  constexpr int NY = RPW + 2 * R;
+  auto ywin = [&](T (&y)[NY], int base, int stride, const T* own) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      y[j] = ld(base + j * stride);
+      y[R + RPW + j] = ld(base + (R + RPW + j) * stride);
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) y[R + q] = own[q];
+  };
+  // y-axis sum / axis term of row q from such a window (the same operands, the same order)
+  auto ysum_w = [&](const T (&y)[NY], int q) {
+    if constexpr (R == 2)
+      return fd4_sum(y[q], y[q + 1], y[q + 3], y[q + 4]);
+    else
+      return fd2_sum(y[q], y[q + 2]);
+  };
+  auto yaxis_w = [&](T acc, T k, const T (&y)[NY], int q) {
+    if constexpr (R == 2)
+      return fd4_axis(acc, k, y[q], y[q + 1], y[q + 3], y[q + 4]);
+    else
+      return fd2_axis(acc, k, y[q], y[q + 2]);
+  };
   // deferred stage 3 (late waves, DEFER): the y sum and u^n of the plane, kept in registers
   // across the barrier
   T dys[RPW], duo[RPW];
@@ -368,7 +404,7 @@ __device__ __forceinline__ void v3_march(
       if (late && k - 1 >= kc0) {
 #pragma unroll
         for (int q = 0; q < RPW; ++q) {
-          const int row = w + q * NW;
+          const int row = row_of(q);
           if (row < aty.lo || row >= aty.hi) continue;  // scalar branch
           s3_finish(q, k - 1, rb[q][sl(-1)], duo[q], rb[q][sl(-3)], rb[q][sl(-2)],
                     rb[q][sl(0)], rb[q][sl(1)], dys[q]);
@@ -379,6 +415,13 @@ __device__ __forceinline__ void v3_march(
     // ---- stage 1: A(k+2R) on S1 ----
     const int pz1 = k + 2 * R;
     const bool z1 = pz1 >= zlo && pz1 < zhi;
+    T yu[NY];
+    if constexpr (PAIR) {
+      T own[RPW];
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) own[q] = ru[q][sl(2 * R)];
+      ywin(yu, ub[0] + UO + R * E, UW * E, own);
+    }
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
       const int b = ub[q] + UO;
@@ -390,14 +433,20 @@ __device__ __forceinline__ void v3_march(
         acc = fd4_axis(acc, q1.k[0], ld(b + (2 * UW + 0) * E),
                        ld(b + (2 * UW + 1) * E), ld(b + (2 * UW + 3) * E),
                        ld(b + (2 * UW + 4) * E));
-        acc = fd4_axis(acc, q1.k[1], ld(b + (0 * UW + 2) * E),
-                       ld(b + (1 * UW + 2) * E), ld(b + (3 * UW + 2) * E),
-                       ld(b + (4 * UW + 2) * E));
+        if constexpr (PAIR)
+          acc = yaxis_w(acc, q1.k[1], yu, q);
+        else
+          acc = fd4_axis(acc, q1.k[1], ld(b + (0 * UW + 2) * E),
+                         ld(b + (1 * UW + 2) * E), ld(b + (3 * UW + 2) * E),
+                         ld(b + (4 * UW + 2) * E));
       } else {
         acc = fd2_axis(acc, q1.k[2], ru[q][sl(R)], ru[q][sl(3 * R)]);
         acc = fd2_axis(acc, q1.k[0], ld(b + (UW + 0) * E),
                        ld(b + (UW + 2) * E));
-        acc = fd2_axis(acc, q1.k[1], ld(b + 1 * E), ld(b + (2 * UW + 1) * E));
+        if constexpr (PAIR)
+          acc = yaxis_w(acc, q1.k[1], yu, q);
+        else
+          acc = fd2_axis(acc, q1.k[1], ld(b + 1 * E), ld(b + (2 * UW + 1) * E));
       }
       acc = pin(acc);
       ra[q][sl(2 * R)] = (z1 && m1[q]) ? acc : c;
@@ -406,9 +455,18 @@ __device__ __forceinline__ void v3_march(
     if (k >= kc0 - 2 * R) {
       const int pz2 = k + R;
       const bool z2 = pz2 >= zlo && pz2 < zhi;
+      T ya[NY];
+      if constexpr (PAIR) {
+        if (row0 + RPW > R && row0 < S1R - R) {  // scalar: a row of the wave is in S2
+          T own[RPW];
+#pragma unroll
+          for (int q = 0; q < RPW; ++q) own[q] = ra[q][sl(R)];
+          ywin(ya, apb + AO, W * E, own);
+        }
+      }
 #pragma unroll
       for (int q = 0; q < RPW; ++q) {
-        const int row = w + q * NW;
+        const int row = row_of(q);
         const T uo = ru[q][sl(R)];
         if (row < R || row >= S1R - R) {  // scalar branch
           rb[q][sl(R)] = uo;
@@ -433,9 +491,12 @@ __device__ __forceinline__ void v3_march(
             xp2 = ld(b + (2 * W + 4) * E);
           }
           acc = fd4_axis(acc, q2.k[0], xm2, xm1, xp1, xp2);
-          acc = fd4_axis(acc, q2.k[1], ld(b + (0 * W + XC) * E),
-                         ld(b + (1 * W + XC) * E), ld(b + (3 * W + XC) * E),
-                         ld(b + (4 * W + XC) * E));
+          if constexpr (PAIR)
+            acc = yaxis_w(acc, q2.k[1], ya, q);
+          else
+            acc = fd4_axis(acc, q2.k[1], ld(b + (0 * W + XC) * E),
+                           ld(b + (1 * W + XC) * E), ld(b + (3 * W + XC) * E),
+                           ld(b + (4 * W + XC) * E));
         } else {
           acc = fd2_axis(acc, q2.k[2], ra[q][sl(0)], ra[q][sl(2)]);
           T xm1, xp1;
@@ -447,8 +508,11 @@ __device__ __forceinline__ void v3_march(
             xp1 = ld(b + (W + 2) * E);
           }
           acc = fd2_axis(acc, q2.k[0], xm1, xp1);
-          acc = fd2_axis(acc, q2.k[1], ld(b + XC * E),
-                         ld(b + (2 * W + XC) * E));
+          if constexpr (PAIR)
+            acc = yaxis_w(acc, q2.k[1], ya, q);
+          else
+            acc = fd2_axis(acc, q2.k[1], ld(b + XC * E),
+                           ld(b + (2 * W + XC) * E));
         }
         acc = pin(acc);
         rb[q][sl(R)] = (z2 && m2[q]) ? acc : uo;
@@ -456,16 +520,30 @@ __device__ __forceinline__ void v3_march(
     }
     // ---- stage 3: u^{n+1}(k) on S3 (late waves: LDS reads now, arithmetic next plane) ----
     if (k >= kc0) {
+      T yb[NY];
+      if constexpr (PAIR) {
+        if (row0 + RPW > aty.lo && row0 < aty.hi) {  // scalar: a row of the wave is in S3
+          T own[RPW];
+#pragma unroll
+          for (int q = 0; q < RPW; ++q) own[q] = rb[q][sl(0)];
+          ywin(yb, apb + AO + ABB, W * E, own);
+        }
+      }
 #pragma unroll
       for (int q = 0; q < RPW; ++q) {
-        const int row = w + q * NW;
+        const int row = row_of(q);
         if (row < aty.lo || row >= aty.hi) continue;  // scalar branch
+        T ys;
+        if constexpr (PAIR)
+          ys = ysum_w(yb, q);
+        else
+          ys = s3_ysum(q, AO);
         if (DEFER && late) {
-          dys[q] = s3_ysum(q, AO);
+          dys[q] = ys;
           duo[q] = dl[q][PH % R];
         } else {
           s3_finish(q, k, rb[q][sl(0)], dl[q][PH % R], rb[q][sl(-2)], rb[q][sl(-1)],
-                    rb[q][sl(1)], rb[q][sl(2)], s3_ysum(q, AO));
+                    rb[q][sl(1)], rb[q][sl(2)], ys);
         }
       }
     }
@@ -592,6 +670,9 @@ static hipError_t launch_step_var(const SArgs& a) {
     case 0: return launch_step<T, ORDER, NW, RPW, 0>(a);
     case 3: return launch_step<T, ORDER, NW, RPW, 3>(a);
     case 7: return launch_step<T, ORDER, NW, RPW, 7>(a);
+    case 16: return launch_step<T, ORDER, NW, RPW, 16>(a);
+    case 19: return launch_step<T, ORDER, NW, RPW, 19>(a);
+    case 23: return launch_step<T, ORDER, NW, RPW, 23>(a);
     default: return hipErrorInvalidValue;
   }
 }

@@ -137,12 +137,20 @@ extern "C" int advdiff_ipc_describe(advdiff_ipc* c, const void* ptr, advdiff_ipc
   hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr);
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> g(c->mu);
+  // Export first: it succeeds for an allocation not exported yet (new, or one reallocated
+  // at a freed base — whose cached handle is stale) and fails for a live allocation
+  // exported before, whose cached handle is then still the right one.
+  hipIpcMemHandle_t h;
+  e = hipIpcGetMemHandle(&h, base);
   auto it = c->exported.find((uintptr_t)base);
-  if (it == c->exported.end()) {
-    hipIpcMemHandle_t h;
-    e = hipIpcGetMemHandle(&h, base);
-    if (e != hipSuccess) return e;
-    it = c->exported.emplace((uintptr_t)base, h).first;
+  if (e == hipSuccess) {
+    if (it == c->exported.end())
+      it = c->exported.emplace((uintptr_t)base, h).first;
+    else
+      it->second = h;
+  } else {
+    (void)hipGetLastError();  // not a launch error: keep KERNEL_CHECK's last-error clean
+    if (it == c->exported.end()) return e;
   }
   static_assert(sizeof(hipIpcMemHandle_t) <= sizeof(out->handle), "IPC handle size");
   std::memset(out, 0, sizeof(*out));
@@ -217,9 +225,9 @@ extern "C" int advdiff_ipc_wait(advdiff_ipc* c, const int* peers, int n, void* s
   return hipGetLastError();
 }
 
-// Forget every mapping and exported handle (call with no put in flight, collectively): a
-// freed-and-reallocated field may come back at the same address, where a cached handle or
-// mapping would still name the old allocation.  The flag blocks stay mapped.
+// Close every peer mapping except the flag blocks (call with no put in flight,
+// collectively): a peer's field freed and reallocated may come back under a handle whose
+// cached mapping still names the old allocation.
 extern "C" int advdiff_ipc_reset(advdiff_ipc* c) {
   if (c == nullptr) return hipErrorInvalidValue;
   hipError_t e = hipDeviceSynchronize();
@@ -237,13 +245,8 @@ extern "C" int advdiff_ipc_reset(advdiff_ipc* c) {
     if (e == hipSuccess) e = ec;
     it = c->opened.erase(it);
   }
-  for (auto it = c->exported.begin(); it != c->exported.end();) {
-    if (it->first == (uintptr_t)c->block) {
-      ++it;
-    } else {
-      it = c->exported.erase(it);
-    }
-  }
+  // (the exported handles stay: a live allocation cannot be exported twice, and
+  // advdiff_ipc_describe replaces the handle of a reallocated one)
   return e;
 }
 

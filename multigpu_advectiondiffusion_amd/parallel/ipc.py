@@ -71,8 +71,8 @@ class IpcPeers:
         self.epoch = 0  # bumped by reset(): graphs captured before it hold stale pointers
 
     def reset(self) -> None:
-        """Collective: forget every learned receive address, peer mapping and exported
-        handle (the flag blocks and their counters stay).  Called when a solver allocates
+        """Collective: forget every learned receive address and peer mapping (the flag
+        blocks and their counters stay).  Called when a solver allocates
         its fields: a field freed and reallocated (another solver, the allocator's cache
         emptied) can come back at an address the cache still keys, while the peer's new
         receive box lives elsewhere — puts through the stale entry would miss it."""

@@ -99,7 +99,7 @@ def test_ipc_cartesian_bitwise(kind, world, decomp, corners, monkeypatch):
         assert np.array_equal(out, ref), (kind, decomp, overlap, graph, np.abs(out - ref).max())
 
 
-def _run_rebuilt(comm, kind, steps, decomps, final):
+def _run_rebuilt(comm, kind, steps, decomps, final, empty=True):
     """bench.py's decomposition tuning: solvers of several grids alive and stepping
     interleaved, all freed (allocator cache emptied), then a new solver of `final`: its
     fields may come back at addresses the first solvers' exchanges were keyed on."""
@@ -112,7 +112,8 @@ def _run_rebuilt(comm, kind, steps, decomps, final):
         s.run(iters=steps)  # graphs of the trial solvers too
     del tries, s
     torch.cuda.synchronize()
-    torch.cuda.empty_cache()
+    if empty:  # fresh allocations; else the new fields reuse the cached (exported) blocks
+        torch.cuda.empty_cache()
     s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, decomp=final)
     s.run(iters=steps)
     g = s.gather()
@@ -120,17 +121,18 @@ def _run_rebuilt(comm, kind, steps, decomps, final):
     return None if g is None else g.copy()
 
 
-@pytest.mark.parametrize("kind,world,decomps,final", [
-    ("diff3", 4, [None, (2, 2, 1)], (2, 2, 1)), ("diff3", 4, [(2, 2, 1), None], None),
-    ("burg3", 4, [None, (2, 2, 1)], (2, 2, 1)),
+@pytest.mark.parametrize("kind,world,decomps,final,empty", [
+    ("diff3", 4, [None, (2, 2, 1)], (2, 2, 1), True), ("diff3", 4, [(2, 2, 1), None], None, True),
+    ("burg3", 4, [None, (2, 2, 1)], (2, 2, 1), True), ("diff3", 2, [None], None, False),
+    ("diff3o2", 4, [None, (2, 2, 1)], None, False),
 ])
-def test_ipc_solver_rebuilt_after_free(kind, world, decomps, final, monkeypatch):
+def test_ipc_solver_rebuilt_after_free(kind, world, decomps, final, empty, monkeypatch):
     """Regression (round-3 bench rehearsal, 4 ipc ranks: L_inf 4.9e-5 after tuning): the
     peers' receive addresses learned by freed solvers must not be reused by a new one
     (IpcPeers.reset at solver construction, graphs keyed by its epoch)."""
     monkeypatch.setenv("ADVDIFF_SHARE_GPU", "1")
     ref = _reference(kind, 16)
-    out = spawn_local(world, _run_rebuilt, kind, 16, decomps, final, device="cuda",
+    out = spawn_local(world, _run_rebuilt, kind, 16, decomps, final, empty, device="cuda",
                       transport="ipc", timeout=240)[0]
     assert np.array_equal(out, ref), np.abs(out - ref).max()
 
