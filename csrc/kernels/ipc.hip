@@ -19,6 +19,7 @@
 // expect[world] (messages consumed from q, local), err (wait timeouts).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -135,7 +136,11 @@ extern "C" int advdiff_ipc_describe(advdiff_ipc* c, const void* ptr, advdiff_ipc
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
   hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr);
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess) {
+    std::fprintf(stderr, "advdiff_ipc_describe: hipMemGetAddressRange(%p): %s\n", ptr,
+                 hipGetErrorString(e));
+    return e;
+  }
   std::lock_guard<std::mutex> g(c->mu);
   // Export first: it succeeds for an allocation not exported yet (new, or one reallocated
   // at a freed base — whose cached handle is stale) and fails for a live allocation
@@ -150,7 +155,11 @@ extern "C" int advdiff_ipc_describe(advdiff_ipc* c, const void* ptr, advdiff_ipc
       it->second = h;
   } else {
     (void)hipGetLastError();  // not a launch error: keep KERNEL_CHECK's last-error clean
-    if (it == c->exported.end()) return e;
+    if (it == c->exported.end()) {
+      std::fprintf(stderr, "advdiff_ipc_describe: hipIpcGetMemHandle(base %p, %zu B, ptr %p): %s\n",
+                   (void*)base, size, ptr, hipGetErrorString(e));
+      return e;
+    }
   }
   static_assert(sizeof(hipIpcMemHandle_t) <= sizeof(out->handle), "IPC handle size");
   std::memset(out, 0, sizeof(*out));

@@ -119,6 +119,11 @@ class Solver:
         ax = self.cd.alloc[-1]
         self.sx = _row_pitch(ax, elem) if pad_rows else ax
         self.ic_name, self.ic_params = ic, ic_params
+        if self._ipc_multi():
+            # BEFORE allocating: the peers close their mappings of any field freed since
+            # (a new allocation made while a peer still maps freed memory cannot be
+            # exported: bench/ipc_realloc_probe.py), and no cached address survives
+            comm.ipc().reset()
         self.u = self._initial_field(ic, ic_params)
         self.du = None
         if self.fused:
@@ -157,8 +162,6 @@ class Solver:
         if device_dt is None:
             device_dt = self.device.type == "cuda" and kernel == "native"
         self.device_dt = bool(device_dt) and model.needs_umax
-        if self._ipc_multi():
-            comm.ipc().reset()  # new fields: no cached peer address may survive (ipc.py)
 
     def _ipc_multi(self) -> bool:
         return (self.device.type == "cuda" and self.comm.size > 1
