@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--vars", default="0,3,7")
+    ap.add_argument("--vars", default="0,3,7,23")
     a = ap.parse_args()
     lib = _lib.require()
     variants = [int(v) for v in a.vars.split(",")]

@@ -142,7 +142,8 @@ struct V3Geom {
   static constexpr int TOTAL = OFF_B + 2 * ASET + R * W;  // + pad: PAIR reads past B1
 };
 
-// VAR = PRIO + 4 DEFER (round 3 A/B of the barrier-synchronised phases).  PRIO: which
+// VAR = PRIO + 4 DEFER + 16 PAIR (round 3 A/B of the barrier-synchronised phases; PAIR:
+// each wave owns RPW adjacent rows, see row_of).  PRIO: which
 // waves run at a raised s_setprio (0 none, 1 the second half, 2 the "busy" waves whose
 // rows all carry three stages, 3 graded by the wave's row-stage count: the busiest at 2,
 // one row-stage less at 1).  DEFER: which waves DEFER the arithmetic and the store of their
@@ -654,8 +655,14 @@ static hipError_t launch_step(const SArgs& a) {
 //   FD4 (16 x 2): graded priority (VAR 3) 655.5 us vs 691.9 plain (-5.3 %); deferring
 //                 stage 3 as well: 669.8 (priority alone wins);
 //   FD2 (12 x 3): second half defers stage 3 + graded priority (VAR 7) 549.3 vs 560.7
-//                 (-2.0 %); priority alone: 562.6 (no gain).
-// ADVDIFF_STEP_VAR / advdiff_set_step_var selects 0 (plain), 3 or 7 for A/B (-1: default).
+//                 (-2.0 %); priority alone: 562.6 (no gain);
+//   adjacent rows per wave (PAIR, VAR + 16; profiles/step_ab_pair_r3.log, two runs):
+//                 FD2 VAR 23 539.1 / 544.1 us vs VAR 7 550.3 / 551.3 (-1.3..2.0 %) -> the
+//                 FD2 default; FD4 VAR 19 660.6 vs 644.8 (VAR 3), VAR 23 ties VAR 3 and
+//                 VAR 16 (no priority) 658.8 — FD4 keeps VAR 3 (its LDS reads are not
+//                 the limit: -37 % of them bought nothing).
+// ADVDIFF_STEP_VAR / advdiff_set_step_var selects 0 (plain), 3, 7 or 23 for A/B (-1:
+// default).
 static int g_step_var = -2;
 static int step_var() {
   if (g_step_var == -2) g_step_var = knob("STEP_VAR", -1);
@@ -664,14 +671,12 @@ static int step_var() {
 
 template <typename T, int ORDER, int NW, int RPW>
 static hipError_t launch_step_var(const SArgs& a) {
-  constexpr int DEF = ORDER == 4 ? 3 : 7;
+  constexpr int DEF = ORDER == 4 ? 3 : 23;
   const int v = step_var() < 0 ? DEF : step_var();
   switch (v) {
     case 0: return launch_step<T, ORDER, NW, RPW, 0>(a);
     case 3: return launch_step<T, ORDER, NW, RPW, 3>(a);
     case 7: return launch_step<T, ORDER, NW, RPW, 7>(a);
-    case 16: return launch_step<T, ORDER, NW, RPW, 16>(a);
-    case 19: return launch_step<T, ORDER, NW, RPW, 19>(a);
     case 23: return launch_step<T, ORDER, NW, RPW, 23>(a);
     default: return hipErrorInvalidValue;
   }

@@ -139,7 +139,7 @@ def test_fused_step_box_bounds_match_reference():
         assert (got.cpu() - out).abs().max().item() < 1e-12, box
 
 
-@pytest.mark.parametrize("var", [-1, 0, 3, 7, 16, 19, 23])
+@pytest.mark.parametrize("var", [-1, 0, 3, 7, 23])
 @pytest.mark.parametrize("order", [4, 2])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_fused_step_odd_subrange_bitwise(var, order, dtype):
