@@ -4,9 +4,11 @@
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out
 export ADVDIFF_IPC_TIMEOUT_S=${ADVDIFF_IPC_TIMEOUT_S:-30}
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-  tests/test_ipc_gpu.py > gpurun_out/pytest_ipc.log 2>&1 || { echo "IPC TESTS FAILED"; tail -60 gpurun_out/pytest_ipc.log; exit 1; }
-tail -3 gpurun_out/pytest_ipc.log
+if [ "${IPC:-1}" = "1" ]; then
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+    tests/test_ipc_gpu.py > gpurun_out/pytest_ipc.log 2>&1 || { echo "IPC TESTS FAILED"; tail -60 gpurun_out/pytest_ipc.log; exit 1; }
+  tail -3 gpurun_out/pytest_ipc.log
+fi
 if [ "${FULL:-1}" = "1" ]; then
   timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
     tests/ > gpurun_out/pytest_gpu.log 2>&1 || { echo "GPU SUITE FAILED"; tail -60 gpurun_out/pytest_gpu.log; exit 1; }
