@@ -202,6 +202,7 @@ def _run_cart_fused(comm, kind, steps, decomp, fused):
 @pytest.mark.parametrize("kind,world,decomp", [
     ("diff3", 4, (1, 2, 2)), ("diff3", 2, (1, 1, 2)), ("diff3o2", 4, (2, 2, 1)),
     ("diff2", 2, (1, 2)), ("diff2", 4, (2, 2)),
+    ("diff3", 9, (3, 3, 1)),  # the centre block exchanges with all 8 neighbours
 ])
 @pytest.mark.parametrize("corners", ["direct", "phased"])
 def test_cartesian_fused_step_bitwise(kind, world, decomp, corners, monkeypatch):
