@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--vars", default="0,3,7,23")
+    ap.add_argument("--orders", default="4,2")
     a = ap.parse_args()
     lib = _lib.require()
     variants = [int(v) for v in a.vars.split(",")]
@@ -31,7 +32,7 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(3)
     u = torch.rand((n, n, n), dtype=torch.float64, device="cuda", generator=g)
     out = {}
-    for order in (4, 2):
+    for order in [int(o) for o in a.orders.split(",")]:
         R = order // 2
         kw = dict(nx=n, ny=n, k0=R, k1=n - R, zlo=R, zhi=n - R, border=R, order=order,
                   cx=0.21, cy=0.17, cz=0.13, dt=0.9 / (2 * 0.51) if order == 2 else 0.5 / 0.51)

@@ -181,6 +181,9 @@ __device__ __forceinline__ void v3_march(
   // neighbours its rows share are read from LDS once and its own rows come from registers
   // (FD4 16 x 2: 8 -> 4 LDS reads per stage and wave; FD2 12 x 3: 6 -> 2)
   constexpr bool PAIR = VAR / 16 != 0;
+  // (Round 3, rejected: issuing every LDS read of the plane right after the barrier,
+  // before any stage's arithmetic — FD2 542.6 vs 537.8 us, FD4 spills at 128 VGPRs;
+  // profiles/step_ab_hoist_r3.log.)
   auto row_of = [&](int q) { return PAIR ? w * RPW + q : w + q * NW; };
   // row-stages of the wave (1 + in S2 + in S3 per row); busy: all in S3
   int nst = 0;
@@ -416,7 +419,9 @@ __device__ __forceinline__ void v3_march(
     // ---- stage 1: A(k+2R) on S1 ----
     const int pz1 = k + 2 * R;
     const bool z1 = pz1 >= zlo && pz1 < zhi;
-    T yu[NY];
+    T yu[NY], ya[NY], yb[NY];
+    const bool ws2 = row0 + RPW > R && row0 < S1R - R;         // scalar: a row in S2
+    const bool ws3 = k >= kc0 && row0 + RPW > aty.lo && row0 < aty.hi;  // a row in S3
     if constexpr (PAIR) {
       T own[RPW];
 #pragma unroll
@@ -456,9 +461,8 @@ __device__ __forceinline__ void v3_march(
     if (k >= kc0 - 2 * R) {
       const int pz2 = k + R;
       const bool z2 = pz2 >= zlo && pz2 < zhi;
-      T ya[NY];
       if constexpr (PAIR) {
-        if (row0 + RPW > R && row0 < S1R - R) {  // scalar: a row of the wave is in S2
+        if (ws2) {  // scalar: a row of the wave is in S2
           T own[RPW];
 #pragma unroll
           for (int q = 0; q < RPW; ++q) own[q] = ra[q][sl(R)];
@@ -521,9 +525,8 @@ __device__ __forceinline__ void v3_march(
     }
     // ---- stage 3: u^{n+1}(k) on S3 (late waves: LDS reads now, arithmetic next plane) ----
     if (k >= kc0) {
-      T yb[NY];
       if constexpr (PAIR) {
-        if (row0 + RPW > aty.lo && row0 < aty.hi) {  // scalar: a row of the wave is in S3
+        if (ws3) {  // scalar: a row of the wave is in S3
           T own[RPW];
 #pragma unroll
           for (int q = 0; q < RPW; ++q) own[q] = rb[q][sl(0)];
@@ -678,8 +681,9 @@ static hipError_t launch_step_var(const SArgs& a) {
     case 3: return launch_step<T, ORDER, NW, RPW, 3>(a);
     case 7: return launch_step<T, ORDER, NW, RPW, 7>(a);
     case 23: return launch_step<T, ORDER, NW, RPW, 23>(a);
-    default: return hipErrorInvalidValue;
+    default: break;
   }
+  return hipErrorInvalidValue;
 }
 
 // Tile shape per order.  With the edge tiles (axis_tile), interleaved medians at 512^3:

@@ -111,6 +111,10 @@ class Transport {
   // step can be captured into a hipGraph (local, ipc: yes; socket: host-staged, no; rccl:
   // capturable, but never run multi-rank on the 1-GPU test box -> opt-in with --graph)
   virtual bool graph_safe() const { return false; }
+  // one-time host handshakes per message pattern (ipc): dry mode runs them without any
+  // device work, so an engine can settle them before it captures a graph
+  virtual bool needs_handshake() const { return false; }
+  virtual void set_dry(bool) {}
 
  protected:
   void* staging(size_t slot, size_t bytes, hipStream_t stream);  // device staging buffer
@@ -269,6 +273,9 @@ class Engine {
   // n steps of constant dt: through hipGraphs of kGraphSteps steps when enabled (after two
   // eager steps that run the transport's one-time handshakes for both buffer parities)
   void steps(int n, double dt);
+  // settle the transport's handshakes (dry exchanges of every field) and capture the
+  // graph of the current buffer parity, OUTSIDE the timed loop (captures run no work)
+  void prepare_graphs(double dt);
   bool graphs() const { return graph_; }
   static constexpr int kGraphSteps = 8;  // even: the u/A ping-pong returns to its start
   Stats run_iters(int iters);

@@ -450,6 +450,8 @@ class IpcTransport final : public Transport {
   }
   const char* name() const override { return "ipc"; }
   bool graph_safe() const override { return true; }
+  bool needs_handshake() const override { return true; }
+  void set_dry(bool on) override { dry_ = on; }
 
   void exchange_boxes(const std::vector<BoxMsg>& msgs, hipStream_t s) override {
     if (msgs.empty()) return;
@@ -457,6 +459,7 @@ class IpcTransport final : public Transport {
     for (const BoxMsg& m : msgs) peers.push_back(m.peer);
     check_distinct_peers(peers);
     const std::vector<Dest> dst = resolve(msgs);
+    if (dry_) return;  // handshake only
     for (size_t q = 0; q < msgs.size(); ++q) {  // the put: my box -> the peer's ghost box
       const BoxMsg& m = msgs[q];
       KERNEL_CHECK(advdiff_copy_box(m.dtype, dst[q].ptr, dst[q].sy, dst[q].sz, m.send, m.ssy,
@@ -578,6 +581,7 @@ class IpcTransport final : public Transport {
   advdiff_ipc* ctx_ = nullptr;
   std::map<Key, Dest> dest_;
   std::map<int, uint64_t> calls_;
+  bool dry_ = false;
 };
 
 // Single process: no communication at all.

@@ -152,11 +152,9 @@ def _native(app, args, out, world=1, extra=(), env_extra=None):
         cmd = [str(exe)] + [str(a) for a in args] + ["--write", str(out)] + list(extra)
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))
-    outs = []
-    for p in procs:
-        so, _ = p.communicate(timeout=240)
-        outs.append(so)
-        assert p.returncode == 0, so
+    outs = [p.communicate(timeout=240)[0] for p in procs]
+    bad = [(r, p.returncode, o) for r, (p, o) in enumerate(zip(procs, outs)) if p.returncode]
+    assert not bad, "\n".join(f"rank {r} exit {c}:\n{o[-1500:]}" for r, c, o in bad)
     return outs[0]
 
 
