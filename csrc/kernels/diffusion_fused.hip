@@ -664,6 +664,10 @@ static hipError_t launch_step(const SArgs& a) {
 //                 FD2 default; FD4 VAR 19 660.6 vs 644.8 (VAR 3), VAR 23 ties VAR 3 and
 //                 VAR 16 (no priority) 658.8 — FD4 keeps VAR 3 (its LDS reads are not
 //                 the limit: -37 % of them bought nothing).
+// Also rejected in round 3 (profiles/step_ab_xs_cfg_r3.log): stage-2/3 x neighbours from
+// LDS instead of DPP (-23 % VALU instructions, FD4 643.9 -> 651.8 us) and a 16 x 3 FD2 tile
+// (amplification 1.20 -> 1.16: 540.7 -> 543.5 us) — the step moves 77 % (FD4) / 85 % (FD2)
+// of the copy rate once its halo re-reads are counted.
 // ADVDIFF_STEP_VAR / advdiff_set_step_var selects 0 (plain), 3, 7 or 23 for A/B (-1:
 // default).
 static int g_step_var = -2;
