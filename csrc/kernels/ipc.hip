@@ -110,7 +110,11 @@ extern "C" int advdiff_ipc_create(int world, int rank, advdiff_ipc** out) {
   c->rank = rank;
   c->peer_cell.assign(world, nullptr);
   const size_t bytes = (3 * (size_t)world + 1) * sizeof(uint64_t);
-  hipError_t e = hipMalloc(&c->block, bytes < 4096 ? 4096 : bytes);
+  // Uncached device memory: a peer GPU's release store lands in this block WHILE the wait
+  // kernel spins on it, and only fine-grained / uncached memory promises cross-device
+  // coherence inside a dispatch (coarse-grained memory only at dispatch boundaries).
+  hipError_t e = hipExtMallocWithFlags((void**)&c->block, bytes < 4096 ? 4096 : bytes,
+                                       hipDeviceMallocUncached);
   if (e == hipSuccess) e = hipMemset(c->block, 0, bytes);
   if (e == hipSuccess) e = hipDeviceSynchronize();  // setup only: zeroed before any peer maps it
   if (e != hipSuccess) {
