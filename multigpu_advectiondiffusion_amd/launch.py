@@ -36,7 +36,9 @@ def free_port_block(n: int, tries: int = 64) -> int:
     so a lone free port is not enough on a busy host."""
     import random
     for _ in range(tries):
-        b = random.randint(20000, 60000 - n - 1)
+        # below Linux's ephemeral range (32768+): an outgoing connection of another
+        # process (or of an earlier rank) cannot take a port of the block meanwhile
+        b = random.randint(20000, 32000 - n - 1)
         socks = []
         try:
             for q in range(b, b + n + 1):
