@@ -71,6 +71,9 @@ def build_parser():
     ap.add_argument("--no-overlap", action="store_true", help="disable halo/compute overlap")
     ap.add_argument("--kernel", choices=["native", "torch"], default="native",
                     help="stencil implementation: gfx950 HIP kernels or the PyTorch reference ops")
+    ap.add_argument("--exchange", choices=["u", "lu"], default="u",
+                    help="halo payload: u (stage output) or lu (the reference's RHS exchange "
+                         "with redundant ghost-plane updates; slab, PyTorch ops)")
     ap.add_argument("--decomp", default=None,
                     help="process grid: slab (default), auto, or PZxPYxPX / PYxPX")
     ap.add_argument("--transport", choices=["rccl", "ipc", "host"], default=None,
@@ -178,7 +181,7 @@ def main(argv=None) -> int:
     solver, htod_s = fenced(lambda: Solver(
         model, grid, comm, dtype=dtype, ic=ic, overlap=not ns.no_overlap, t0=t0,
         check_every=ns.check_every, decomp=ns.decomp, integrator=ns.integrator,
-        kernel=ns.kernel))
+        kernel=ns.kernel, exchange=ns.exchange))
     if ns.restart:
         solver.load_checkpoint(ns.restart)
     if ns.initial:

@@ -77,6 +77,29 @@ class Model:
     def stable_dt(self, umax: float | None = None) -> float:  # pragma: no cover
         raise NotImplementedError
 
+    # -- RHS-exchange stages (Solver(exchange="lu"), the reference's MultiGPU scheme) --
+    def rhs(self, inp, L, lo, hi) -> None:  # pragma: no cover
+        """L[lo:hi] = the spatial operator of `inp` on planes [lo, hi) (active x/y cells;
+        PyTorch ops)."""
+        raise NotImplementedError
+
+    def _active(self, t, lo, hi):
+        """View of planes [lo, hi), x/y cells inside the frozen border."""
+        B = self.border
+        if self.grid.dims == 3:
+            return t[lo:hi, B:self.grid.ny - B, B:self.grid.nx - B]
+        return t[lo:hi, B:self.grid.nx - B]
+
+    def rk_update(self, inp, u0, out, L, lo, hi, dt, a, b, ls=False) -> None:
+        """out = a·u0 + b·(inp + dt·L) on planes [lo, hi) — the combine of the fused stage
+        (ops/reference.py::_combine), bit for bit."""
+        if hi <= lo:
+            return
+        from ..ops import reference as ref
+        v = self._active
+        ref._combine(v(out, lo, hi), v(u0, lo, hi) if (a != 0 or ls) else None,
+                     v(inp, lo, hi), v(L, lo, hi), dt, a, b, ls)
+
     def describe(self) -> dict:
         return {"model": self.name, "radius": self.radius, "border": self.border}
 

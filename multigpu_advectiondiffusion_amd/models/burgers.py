@@ -97,6 +97,19 @@ class Burgers(Model):
                                             vx=self.visc[0], vy=self.visc[1], dt=dt, a=a, b=b,
                                             stream=stream, ls=ls, dt_dev=dt_dev)
 
+    def rhs(self, inp, L, lo, hi):
+        if hi <= lo:
+            return
+        from ..ops import reference as ref
+        g = self.grid
+        if self.dims == 3:
+            f = ref.burgers_rhs_3d(inp, g.nx, g.ny, lo, hi, self.border, self.weno, *self.rd,
+                                   *self.visc)
+        else:
+            f = ref.burgers_rhs_2d(inp, g.nx, lo, hi, self.border, self.weno, *self.rd,
+                                   *self.visc)
+        self._active(L, lo, hi).copy_(f)
+
     def describe(self):
         d = super().describe()
         d.update({"viscosity": self.C, "weno": self.weno, "cfl": self.cfl,

@@ -95,6 +95,18 @@ class Diffusion(Model):
                                       order=self.order, cx=self.coef[0], cy=self.coef[1],
                                       dt=dt, a=a, b=b, stream=stream, ls=ls)
 
+    def rhs(self, inp, L, lo, hi):
+        if hi <= lo:
+            return
+        from ..ops import reference as ref
+        g = self.grid
+        if self.dims == 3:
+            lap = ref.diffusion3d_rhs(inp, g.nx, g.ny, lo, hi, self.border, self.order,
+                                      *self.coef)
+        else:
+            lap = ref.diffusion2d_rhs(inp, g.nx, lo, hi, self.border, self.order, *self.coef)
+        self._active(L, lo, hi).copy_(lap)
+
     def describe(self):
         d = super().describe()
         d.update({"K": self.K, "order": self.order, "safety": self.safety,

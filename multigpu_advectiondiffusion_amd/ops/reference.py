@@ -160,10 +160,8 @@ def _combine(out_view, u0_view, c, L, dt, a, b, ls=False):
 # ---------------------------------------------------------------------------------
 # heat equation stages
 # ---------------------------------------------------------------------------------
-def diffusion3d_stage(inp, u0, out, nx, ny, k0, k1, border, order, cx, cy, cz, dt, a, b,
-                      ls=False):
-    if k1 <= k0 or nx - 2 * border <= 0 or ny - 2 * border <= 0:
-        return
+def diffusion3d_rhs(inp, nx, ny, k0, k1, border, order, cx, cy, cz):
+    """K∇²u on the box k in [k0,k1), j,i in [border, n-border) (cx = K/dx² ...)."""
     B = border
     s = 1.0 / 12.0 if order == 4 else 1.0
     cx, cy, cz = cx * s, cy * s, cz * s
@@ -181,8 +179,18 @@ def diffusion3d_stage(inp, u0, out, nx, ny, k0, k1, border, order, cx, cy, cz, d
                + cz * d2_fd2(sh(-1, 0, 0), c, sh(1, 0, 0)))
     else:
         raise ValueError(f"order {order}")
+    return lap
+
+
+def diffusion3d_stage(inp, u0, out, nx, ny, k0, k1, border, order, cx, cy, cz, dt, a, b,
+                      ls=False):
+    if k1 <= k0 or nx - 2 * border <= 0 or ny - 2 * border <= 0:
+        return
+    B = border
+    lap = diffusion3d_rhs(inp, nx, ny, k0, k1, B, order, cx, cy, cz)
     _combine(out[k0:k1, B:ny - B, B:nx - B],
-             u0[k0:k1, B:ny - B, B:nx - B] if (a != 0 or ls) else None, c, lap, dt, a, b, ls)
+             u0[k0:k1, B:ny - B, B:nx - B] if (a != 0 or ls) else None,
+             inp[k0:k1, B:ny - B, B:nx - B], lap, dt, a, b, ls)
 
 
 def diffusion3d_step(uin, uout, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy, cz, dt):
@@ -277,9 +285,7 @@ def diffusion2d_step(uin, uout, nx, j0, j1, ylo, yhi, border, order, cx, cy, dt)
     diffusion2d_stage(B, uin, uout, nx, j0, j1, border, order, cx, cy, dt, 1.0 / 3.0, 2.0 / 3.0)
 
 
-def diffusion2d_stage(inp, u0, out, nx, j0, j1, border, order, cx, cy, dt, a, b, ls=False):
-    if j1 <= j0 or nx - 2 * border <= 0:
-        return
+def diffusion2d_rhs(inp, nx, j0, j1, border, order, cx, cy):
     B = border
     s = 1.0 / 12.0 if order == 4 else 1.0
     cx, cy = cx * s, cy * s
@@ -293,8 +299,16 @@ def diffusion2d_stage(inp, u0, out, nx, j0, j1, border, order, cx, cy, dt, a, b,
                + cy * d2_fd4(sh(-2, 0), sh(-1, 0), c, sh(1, 0), sh(2, 0)))
     else:
         lap = cx * d2_fd2(sh(0, -1), c, sh(0, 1)) + cy * d2_fd2(sh(-1, 0), c, sh(1, 0))
-    _combine(out[j0:j1, B:nx - B], u0[j0:j1, B:nx - B] if (a != 0 or ls) else None, c, lap, dt,
-             a, b, ls)
+    return lap
+
+
+def diffusion2d_stage(inp, u0, out, nx, j0, j1, border, order, cx, cy, dt, a, b, ls=False):
+    if j1 <= j0 or nx - 2 * border <= 0:
+        return
+    B = border
+    lap = diffusion2d_rhs(inp, nx, j0, j1, B, order, cx, cy)
+    _combine(out[j0:j1, B:nx - B], u0[j0:j1, B:nx - B] if (a != 0 or ls) else None,
+             inp[j0:j1, B:nx - B], lap, dt, a, b, ls)
 
 
 # ---------------------------------------------------------------------------------

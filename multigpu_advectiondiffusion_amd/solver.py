@@ -69,7 +69,7 @@ class Solver:
                  overlap: bool = True, pad_rows: bool = True, t0: float = 0.0,
                  check_every: int = 0, fused: bool | None = None, decomp=None,
                  integrator: str = "ssprk3", kernel: str = "native",
-                 device_dt: bool | None = None):
+                 device_dt: bool | None = None, exchange: str = "u"):
         """decomp: process grid — None/"slab" (split the slowest axis only, the
         reference's layout), "auto" (smallest halo surface) or "PZxPYxPX" / a tuple in
         array axis order ((pz, py, px) in 3-D, (py, px) in 2-D).
@@ -79,10 +79,19 @@ class Solver:
         the same device — the naive A/B baseline; same launch ranges and schedule).
         device_dt: adaptive-CFL models compute dt on the device (no per-step host sync;
         graph-replayable); None = on for the native GPU path, False = the host-driven
-        loop (bitwise the same step sequence, tests/test_adaptive_dt.py)."""
+        loop (bitwise the same step sequence, tests/test_adaptive_dt.py).
+        exchange: "u" (default: exchange the stage OUTPUT's ghost planes) or "lu" (the
+        reference's MultiGPU scheme, `MultiGPU/Diffusion3d_Baseline/main.c:209-288,300`:
+        exchange the boundary planes of the RHS L(u) and advance the ghost planes
+        redundantly with the RK update).  "lu" is a slab, per-stage, PyTorch-ops mode kept
+        for semantic parity; its results equal the "u" mode's bit for bit
+        (tests/test_lu_exchange.py)."""
         if kernel not in ("native", "torch"):
             raise ValueError("kernel must be 'native' or 'torch'")
+        if exchange not in ("u", "lu"):
+            raise ValueError("exchange must be 'u' or 'lu'")
         self.kernel = kernel
+        self.exchange = exchange
         if integrator not in INTEGRATORS:
             raise ValueError(f"integrator must be one of {INTEGRATORS}")
         self.integrator = integrator
@@ -107,7 +116,12 @@ class Solver:
         ashape = tuple(reversed(grid.shape))  # array axis order: (z, y, x) / (y, x)
         self.pgrid = parse_proc_grid(decomp, comm.size, ashape, model.radius)
         self.cart = any(p > 1 for p in self.pgrid[1:])
+        if exchange == "lu" and self.cart:
+            raise ValueError("exchange='lu' is the reference's slab scheme: use a slab "
+                             "decomposition")
         self.fused = model.supports_fused if fused is None else (fused and model.supports_fused)
+        if exchange == "lu":
+            self.fused = False  # the RHS exchange is a per-stage scheme
         thin = any(n // p < 3 * model.radius for n, p in zip(ashape, self.pgrid) if p > 1)
         if self.fused and (integrator != "ssprk3" or thin):
             self.fused = False  # LSRK, or blocks thinner than the wide (3R) halo
@@ -136,6 +150,8 @@ class Solver:
         else:
             self.A = self.u.clone()
             self.B = self.u.clone()
+        # exchange="lu": the RHS of the current stage (ghost planes = the neighbours' L)
+        self.L = torch.zeros_like(self.u) if exchange == "lu" else None
         self.t = float(t0)
         self.it = 0
         self.comm_stream = None
@@ -161,7 +177,7 @@ class Solver:
         self._dts = None     # device [t, dt, steps] of the adaptive loop
         if device_dt is None:
             device_dt = self.device.type == "cuda" and kernel == "native"
-        self.device_dt = bool(device_dt) and model.needs_umax
+        self.device_dt = bool(device_dt) and model.needs_umax and exchange == "u"
 
     def _ipc_multi(self) -> bool:
         return (self.device.type == "cuda" and self.comm.size > 1
@@ -230,7 +246,8 @@ class Solver:
 
     def memory_bytes(self) -> int:
         """Device bytes of the resident fields (see utils/sizing.py)."""
-        n = sum(f.numel() for f in self.fields()) + (self.du.numel() if self.du is not None else 0)
+        n = sum(f.numel() for f in self.fields()) + sum(
+            t.numel() for t in (self.du, self.L) if t is not None)
         return n * self.u.element_size()
 
     def fields(self):
@@ -301,6 +318,39 @@ class Solver:
             self._launch(inp, u0, out, self.full, dt, a, b, ls)
         with trace.range_("halo_start"):
             self._pending[id(out)] = self.halo.start(out)
+
+    def _stage_lu(self, inp, u0, out, a, b, dt, ls=False):
+        """One RK stage with the reference's RHS exchange (main.c:209-288, 300): L(inp) on
+        the owned planes, L's boundary planes to the neighbours' ghost planes, then the RK
+        update of every active plane, the ghost planes included — each rank advances its
+        ghost planes with the same formula as their owner, so no u exchange is needed.
+        Overlapped like the reference: boundary L first, its exchange beside the interior
+        L and the owned-plane update."""
+        m, L = self.model, self.L
+        lo, hi = self.full
+        z0, z1 = self.zact
+        if self.comm.size == 1:
+            m.rhs(inp, L, lo, hi)
+        elif self.overlap:
+            with trace.range_("boundary"):
+                for rng in self.boundary:
+                    m.rhs(inp, L, *rng)
+            with trace.range_("halo_start"):
+                pend = self.halo.start(L)
+            with trace.range_("interior"):
+                m.rhs(inp, L, *self.interior)
+                m.rk_update(inp, u0, out, L, lo, hi, dt, a, b, ls)
+            with trace.range_("halo_wait"):
+                if pend is not None:
+                    pend.wait()
+            m.rk_update(inp, u0, out, L, z0, lo, dt, a, b, ls)
+            m.rk_update(inp, u0, out, L, hi, z1, dt, a, b, ls)
+            return
+        else:
+            m.rhs(inp, L, lo, hi)
+            with trace.range_("halo"):
+                self.halo.exchange(L)
+        m.rk_update(inp, u0, out, L, z0, z1, dt, a, b, ls)
 
     def _launch_fused(self, rng, dt, rng2=(0, 0), exclusive=False):
         """exclusive: nothing else (RCCL copy kernels) runs beside this launch — a single
@@ -378,16 +428,17 @@ class Solver:
         if self.fused:
             self._step_fused(dt)
             return
+        stage = self._stage_lu if self.exchange == "lu" else self._stage
         if self.du is not None:
             for A, Bc in zip(LSRK45_A, LSRK45_B):
-                self._stage(self.u, self.du, self.un, A, Bc, dt, ls=True)
+                stage(self.u, self.du, self.un, A, Bc, dt, ls=True)
                 self.u, self.un = self.un, self.u
         else:
             u, A, B = self.u, self.A, self.B
             (a1, b1), (a2, b2), (a3, b3) = RK3
-            self._stage(u, None, A, a1, b1, dt)
-            self._stage(A, u, B, a2, b2, dt)
-            self._stage(B, u, u, a3, b3, dt)
+            stage(u, None, A, a1, b1, dt)
+            stage(A, u, B, a2, b2, dt)
+            stage(B, u, u, a3, b3, dt)
         if self._dt_dev is None:  # device-dt steps keep t / it on the device
             self.t += dt
             self.it += 1
@@ -430,7 +481,8 @@ class Solver:
         every exchange step is a stream-ordered kernel, so a whole multi-rank step —
         interior, puts, flags, waits, boundary — replays as one graph)."""
         multi_ok = self.comm.size == 1 or self.comm.transport == "ipc"
-        return (self.device.type == "cuda" and multi_ok and not trace.SYNC_DEBUG
+        return (self.device.type == "cuda" and multi_ok and self.exchange == "u"
+                and not trace.SYNC_DEBUG
                 and not trace.TRACE)
 
     def _prepare_graph_halos(self):
@@ -713,16 +765,23 @@ class Solver:
                                       times3=(style == "multigpu" or self.model.name == "burgers"))
         ml = metrics.mlups(stats.compute_s, stats.steps, cells)
         # LSRK stage: read u, du; write du, u (stage 1 skips the du read)
-        bpc = 5 * 32.0 - 8.0 if self.du is not None else self.model.bytes_per_cell_step
+        # (per-stage launches of a fusable model — LSRK, thin slabs, --exchange lu — move
+        # the per-stage 64 B, not the fused step's 16 B)
+        bpc = (5 * 32.0 - 8.0 if self.du is not None
+               else self.model.bytes_per_cell_step if self.fused else 64.0)
         bw = bpc * cells * stats.steps / max(stats.compute_s, 1e-30)
         ex = {("MLUPS (cells x RK steps / s)" if self.du is not None
                else "MLUPS (cells x RK3 steps / s)"): f"{ml:.1f}",
               "Stage-MLUPS": f"{(5 if self.du is not None else 3) * ml:.1f}",
               "Effective HBM bandwidth (GB/s, est.)": f"{bw / 1e9:.1f}",
               "Processes / devices": f"{self.comm.size} x {self.device.type}"}
+        if self.exchange == "lu":
+            ex["Halo payload"] = "RHS L(u) boundary planes, redundant ghost update"
         if extra:
             ex.update(extra)
         opt = "Fused LDS z-march + RK3 (gfx950)" if self.device.type == "cuda" else "PyTorch CPU"
+        if self.device.type == "cuda" and (self.kernel == "torch" or self.exchange == "lu"):
+            opt = "PyTorch reference ops (GPU)"
         if style == "multigpu":
             return metrics.summary_multigpu(self.model.title, opt, stats.compute_s, stats.htod_s,
                                             stats.dtoh_s, gf, stats.steps, g.shape, ex,
