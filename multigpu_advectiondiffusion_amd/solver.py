@@ -150,8 +150,13 @@ class Solver:
         else:
             self.A = self.u.clone()
             self.B = self.u.clone()
-        # exchange="lu": the RHS of the current stage (ghost planes = the neighbours' L)
+        # exchange="lu": the RHS of a stage (ghost planes = the neighbours' L).  Two buffers
+        # alternate: the ipc transport's puts carry no receiver acknowledgement, so a buffer
+        # may only be written again by a peer after an exchange that orders this rank's
+        # reads of it (as u/A/B rotate in the default mode) — with ONE buffer a peer's
+        # next-stage put can land before this rank's ghost update has read the last one
         self.L = torch.zeros_like(self.u) if exchange == "lu" else None
+        self._L2 = torch.zeros_like(self.u) if exchange == "lu" else None
         self.t = float(t0)
         self.it = 0
         self.comm_stream = None
@@ -247,7 +252,7 @@ class Solver:
     def memory_bytes(self) -> int:
         """Device bytes of the resident fields (see utils/sizing.py)."""
         n = sum(f.numel() for f in self.fields()) + sum(
-            t.numel() for t in (self.du, self.L) if t is not None)
+            t.numel() for t in (self.du, self.L, self._L2) if t is not None)
         return n * self.u.element_size()
 
     def fields(self):
@@ -327,6 +332,7 @@ class Solver:
         Overlapped like the reference: boundary L first, its exchange beside the interior
         L and the owned-plane update."""
         m, L = self.model, self.L
+        self.L, self._L2 = self._L2, self.L
         lo, hi = self.full
         z0, z1 = self.zact
         if self.comm.size == 1:
