@@ -6,6 +6,7 @@ import shutil
 import subprocess
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 CSRC = Path(__file__).resolve().parent.parent / "csrc"
@@ -89,6 +90,53 @@ def test_native_geometry_matches_python(app, args, world, decomp, extra, corners
     """Every rank's launch boxes, fused-step views and halo messages of the native runtime
     (bin/<app> --geometry, csrc/runtime/cart.cpp) equal the Python decomposition's
     (CartesianDecomposition, CartesianHalo.boxes, decomposition.fused_view)."""
+    _check_native_geometry(app, args, world, decomp, extra, corners)
+
+
+def _native_layouts():
+    from hypothesis import strategies as st
+
+    @st.composite
+    def draw_layout(draw):
+        app = draw(st.sampled_from(["diffusion3d", "diffusion2d", "burgers3d"]))
+        dims = 2 if app.endswith("2d") else 3
+        pgrid = [draw(st.integers(1, 3)) for _ in range(dims)]
+        if all(p == 1 for p in pgrid):
+            pgrid[0] = 2
+        # array-order extents: >= R cells per block; thin blocks fall back to per-stage
+        shape = [p * 3 + draw(st.integers(1, 24)) for p in pgrid]
+        if app == "burgers3d":
+            shape = [max(n, 7) for n in shape]
+        ext = list(reversed(shape))  # Nx Ny [Nz]
+        if app == "diffusion3d":
+            args = [1, 1, 1, 1] + ext + [2]
+        elif app == "diffusion2d":
+            args = [1, 1, 1] + ext + [2]
+        else:
+            args = [0.01, 0.3, 2, 2, 2] + ext
+        extra = draw(st.sampled_from([[], ["--no-fused"]])) if app.startswith("diff") else []
+        corners = draw(st.sampled_from(["direct", "phased"]))
+        decomp = "x".join(str(p) for p in pgrid)
+        return app, args, int(np.prod(pgrid)), decomp, extra, corners
+    return draw_layout()
+
+
+def test_native_geometry_matches_python_random():
+    """The same comparison over random layouts (hypothesis): process grids up to 3 per
+    axis, uneven blocks, thin blocks that fall back to per-stage launches, both corner
+    modes."""
+    hyp = pytest.importorskip("hypothesis")
+    if not (CSRC.parent / "bin" / "diffusion3d").exists():
+        pytest.skip("bin/ not built")
+
+    @hyp.settings(max_examples=60, deadline=None, derandomize=True)
+    @hyp.given(_native_layouts())
+    def run(layout):
+        _check_native_geometry(*layout)
+    run()
+
+
+def _check_native_geometry(app, args, world, decomp, extra, corners):
     import json
     import os
 
@@ -102,9 +150,6 @@ def test_native_geometry_matches_python(app, args, world, decomp, extra, corners
     env = dict(os.environ, RANK="0", WORLD_SIZE=str(world), ADVDIFF_CORNERS=corners)
     cmd = [str(exe)] + [str(a) for a in args] + ["--decomp", decomp, "--geometry"] + extra
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=60, env=env)
-    assert r.returncode == 0, r.stderr
-    native = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
-    assert len(native) == world
     three = app.endswith("3d")
     if app.startswith("diffusion"):
         model = Diffusion(K=1.0, order=4)
@@ -117,6 +162,14 @@ def test_native_geometry_matches_python(app, args, world, decomp, extra, corners
     fused = model.supports_fused and "--no-fused" not in extra and not any(
         n // p < 3 * R for n, p in zip(shape, pgrid) if p > 1)
     G = 3 * R if fused else R
+    if r.returncode != 0 and "thinner than the ghost width" in r.stderr:
+        # a layout both sides refuse (a block, or an unsplit axis 0, thinner than G)
+        with pytest.raises(ValueError):
+            CartesianDecomposition(shape, pgrid, 0, G)
+        return
+    assert r.returncode == 0, r.stderr
+    native = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert len(native) == world
     lst = lambda box: [list(x) for x in box]  # noqa: E731
     for rank in range(world):
         cd = CartesianDecomposition(shape, pgrid, rank, G)
