@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Interleaved A/B of the fused 3-D heat step's phase-overlap variants (advdiff_set_step_var:
-0 base, 1 second wave half at s_setprio 1, 2 second half defers its stage 3 by one plane,
-3 both), 512^3 fp64, FD4 and FD2.  Rounds x variants x reps launches timed with HIP events,
-medians per variant; every variant's output must equal variant 0's bit for bit.
+0 plain, 3 graded wave priority, 7 + the second half defers its stage 3 by one plane,
+23 + adjacent rows per wave; -1 = the order's default), 512^3 fp64, FD4 and FD2.  Rounds x
+variants x reps launches timed with HIP events, medians per variant; every variant's
+output must equal the first one's bit for bit.
 
-    python bench/step_ab.py [--n 512] [--rounds 5] [--reps 10] [--vars 0,1,2,3]
+    python bench/step_ab.py [--n 512] [--rounds 5] [--reps 10] [--vars 0,3,7,23]
 """
 import argparse
 import json
