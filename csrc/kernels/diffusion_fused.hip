@@ -667,7 +667,10 @@ static hipError_t launch_step(const SArgs& a) {
 // Also rejected in round 3 (profiles/step_ab_xs_cfg_r3.log): stage-2/3 x neighbours from
 // LDS instead of DPP (-23 % VALU instructions, FD4 643.9 -> 651.8 us) and a 16 x 3 FD2 tile
 // (amplification 1.20 -> 1.16: 540.7 -> 543.5 us) — the step moves 77 % (FD4) / 85 % (FD2)
-// of the copy rate once its halo re-reads are counted.
+// of the copy rate once its halo re-reads are counted (67 / 78 % by a later direct count).
+// Also rejected: prefetching NR planes ahead instead of 2 (FD4 equal, FD2 +1.6 %,
+// profiles/prefetch_ab_r3.log) and pacing the workgroups of an XCD so co-XCD tiles read
+// their shared halo rows together (no gain, profiles/pace_ab_r3.log).
 // ADVDIFF_STEP_VAR / advdiff_set_step_var selects 0 (plain), 3, 7 or 23 for A/B (-1:
 // default).
 static int g_step_var = -2;
