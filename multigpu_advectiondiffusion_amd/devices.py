@@ -70,5 +70,10 @@ def _native_details(out: dict) -> None:
         out["peer_topology"] = topo
 
 
-if __name__ == "__main__":
+def main(argv=None) -> int:
     print(json.dumps(scan(), indent=1))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
