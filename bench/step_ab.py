@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
-"""Interleaved A/B of the fused 3-D heat step's phase-overlap variants (advdiff_set_step_var:
-0 plain, 3 graded wave priority, 7 + the second half defers its stage 3 by one plane,
-23 + adjacent rows per wave; -1 = the order's default), 512^3 fp64, FD4 and FD2.  Rounds x
-variants x reps launches timed with HIP events, medians per variant; every variant's
-output must equal the first one's bit for bit.
+"""Interleaved A/B of the fused 3-D heat step's built variants (advdiff_set_step_var: 0 the
+plain kernel, -1 the order's phase-overlap default — FD4 graded wave priority (VAR 3), FD2
+adjacent rows + deferred stage 3 + priority (VAR 23); a new VAR needs its instance in
+csrc/kernels/diffusion_fused.hip), 512^3 fp64, FD4 and FD2.  Rounds x variants x reps
+launches timed with HIP events, medians per variant; every variant's output must equal the
+first one's bit for bit.
 
-    python bench/step_ab.py [--n 512] [--rounds 5] [--reps 10] [--vars 0,3,7,23]
+    python bench/step_ab.py [--n 512] [--rounds 5] [--reps 10] [--vars 0,-1]
 """
 import argparse
 import json
@@ -24,7 +25,7 @@ def main():
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--vars", default="0,3,7,23")
+    ap.add_argument("--vars", default="0,-1")
     ap.add_argument("--orders", default="4,2")
     a = ap.parse_args()
     lib = _lib.require()

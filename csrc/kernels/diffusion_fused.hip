@@ -671,8 +671,10 @@ static hipError_t launch_step(const SArgs& a) {
 // Also rejected: prefetching NR planes ahead instead of 2 (FD4 equal, FD2 +1.6 %,
 // profiles/prefetch_ab_r3.log) and pacing the workgroups of an XCD so co-XCD tiles read
 // their shared halo rows together (no gain, profiles/pace_ab_r3.log).
-// ADVDIFF_STEP_VAR / advdiff_set_step_var selects 0 (plain), 3, 7 or 23 for A/B (-1:
-// default).
+// Built instances: the order's default (FD4 VAR 3, FD2 VAR 23) and the plain kernel
+// (VAR 0) as the fallback; ADVDIFF_STEP_VAR / advdiff_set_step_var picks -1 (default) or 0.
+// VAR 7 and the cross-order variants (FD4 23, FD2 3) were removed after their A/Bs; the
+// template still takes any VAR for a new experiment.
 static int g_step_var = -2;
 static int step_var() {
   if (g_step_var == -2) g_step_var = knob("STEP_VAR", -1);
@@ -682,14 +684,9 @@ static int step_var() {
 template <typename T, int ORDER, int NW, int RPW>
 static hipError_t launch_step_var(const SArgs& a) {
   constexpr int DEF = ORDER == 4 ? 3 : 23;
-  const int v = step_var() < 0 ? DEF : step_var();
-  switch (v) {
-    case 0: return launch_step<T, ORDER, NW, RPW, 0>(a);
-    case 3: return launch_step<T, ORDER, NW, RPW, 3>(a);
-    case 7: return launch_step<T, ORDER, NW, RPW, 7>(a);
-    case 23: return launch_step<T, ORDER, NW, RPW, 23>(a);
-    default: break;
-  }
+  const int v = step_var();
+  if (v < 0 || v == DEF) return launch_step<T, ORDER, NW, RPW, DEF>(a);
+  if (v == 0) return launch_step<T, ORDER, NW, RPW, 0>(a);
   return hipErrorInvalidValue;
 }
 

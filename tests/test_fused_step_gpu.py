@@ -139,13 +139,13 @@ def test_fused_step_box_bounds_match_reference():
         assert (got.cpu() - out).abs().max().item() < 1e-12, box
 
 
-@pytest.mark.parametrize("var", [-1, 0, 3, 7, 23])
+@pytest.mark.parametrize("var", [-1, 0])
 @pytest.mark.parametrize("order", [4, 2])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_fused_step_odd_subrange_bitwise(var, order, dtype):
-    """The step kernel of each order (FD4: 16 waves x 2 rows, FD2: 12 x 3) in every
-    phase-overlap variant (advdiff_set_step_var: priority / deferred stage 3 of the second
-    wave half) is bit-identical to the per-stage path on a sub-range with frozen planes,
+    """The step kernel of each order (FD4: 16 waves x 2 rows, FD2: 12 x 3), both built
+    variants (advdiff_set_step_var: -1 the order's phase-overlap default, 0 the plain
+    kernel), is bit-identical to the per-stage path on a sub-range with frozen planes,
     odd sizes and chunk lengths that are not a multiple of the march unroll."""
     from multigpu_advectiondiffusion_amd.ops import _lib
     lib = _lib.require()
