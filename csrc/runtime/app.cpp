@@ -15,6 +15,9 @@
 //   default z-slabs as the reference)  --geometry (print every rank's launch / halo
 //   geometry as JSON lines and exit; no GPU work)  --graph / --no-graph (hipGraph
 //   stepping, Engine::steps; default: on for the single-rank and ipc transports)
+//   --restart PREFIX (start from fp64 checkpoint shards of any layout, Python or native:
+//   diffusion runs `iters` more steps, Burgers continues to tEnd)  --checkpoint PREFIX
+//   (write this run's shards at the end; checkpoint.cpp, the format of utils/io.py)
 // Launch one process per GPU with torchrun-style env vars (RANK/WORLD_SIZE/LOCAL_RANK/
 // MASTER_ADDR/MASTER_PORT), e.g. via `python -m multigpu_advectiondiffusion_amd.launch`.
 #include <chrono>
@@ -62,7 +65,8 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
                        : (dims == 3 ? " tEnd CFL L W H Nx Ny Nz [bx by bz]" : " tEnd CFL L W Nx Ny [bx by]"))
               << " [--ic NAME] [--order 2|4] [--weno js|z|js7] [--integrator ssprk3|lsrk45] [--no-fused] [--visc C] [--fp32] [--no-overlap]"
                  " [--transport rccl|ipc|socket] [--decomp slab|PZxPYxPX|PYxPX] [--write FILE]"
-                 " [--write-ghosts FILE] [--error-norms] [--geometry] [--graph|--no-graph]\n";
+                 " [--write-ghosts FILE] [--error-norms] [--geometry] [--graph|--no-graph]"
+                 " [--restart PREFIX] [--checkpoint PREFIX]\n";
     return 1;
   }
   Problem p;
@@ -132,7 +136,9 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   if (decomp != "slab") parse_pgrid(decomp, dims, env.size, p.pgrid);
   auto tr = make_transport(env, tk);
   Engine eng(p, tr.get(), env);
+  if (opt.count("--restart")) eng.load_checkpoint(opt["--restart"]);
   Stats st = diff ? eng.run_iters(iters) : eng.run_until(tEnd + p.t0);
+  if (opt.count("--checkpoint")) eng.save_checkpoint(opt["--checkpoint"], ic);
   std::string title =
       std::string(diff ? "Diffusion-" : "Burgers-") + (dims == 3 ? "3D" : "2D") +
       (diff ? (p.order == 4 ? " MI355X-FD4" : " MI355X-FD2") : (p.weno == 1 ? " MI355X-WENO5Z" : p.weno == 0 ? " MI355X-WENO5JS" : " MI355X-WENO7JS"));

@@ -214,6 +214,22 @@ std::vector<std::vector<HaloPlanMsg>> halo_plan(const Cart& cd, bool corners,
 // ------------------------------------------------------------------------------------
 enum class Physics { Diffusion, Burgers };
 
+// ------------------------------------------------------------------------------------
+// Checkpoint shards (checkpoint.cpp; the format of utils/io.py): host-only helpers
+// ------------------------------------------------------------------------------------
+struct ShardInfo {
+  std::vector<int64_t> shape, box0, grid;  // shard box (array order), global grid (x first)
+  std::string dtype;                       // "float64" (both writers) or "float32"
+  double t = 0;
+  long long it = 0;
+  size_t offset = 0;  // byte offset of the payload
+};
+std::string shard_path(const std::string& prefix, int rank);  // PREFIX.rankNNNNN.ckpt
+std::vector<std::string> list_shards(const std::string& prefix);
+ShardInfo read_shard_info(const std::string& path);
+// raw text of a top-level key of a JSON object (nested objects skipped)
+bool json_top_value(const std::string& js, const std::string& key, std::string& raw);
+
 struct Problem {
   Physics physics = Physics::Diffusion;
   int pgrid[3] = {0, 0, 0};        // process grid (array order); 0 = slab (P, 1, 1)
@@ -287,6 +303,11 @@ class Engine {
   // the reference's multi-GPU result.bin layout (each rank's Nx x Ny x (_Nz + 6) slab,
   // SaveBinary3D(h_u, Nx, Ny, NZ), MultiGPU/Diffusion3d_Baseline/main.c:341).  Slabs only.
   std::vector<float> gather_float32_ghosts();
+  // fp64 shard of the owned cells (utils/io.py format; collective: returns when every
+  // rank's shard is written) / restart from the shards of ANY layout (owned + in-domain
+  // ghost cells, then the stage buffers as after the IC; sets t and it)
+  void save_checkpoint(const std::string& prefix, const std::string& ic_name);
+  void load_checkpoint(const std::string& prefix);
   double init_seconds() const { return init_s_; }  // barrier-fenced field setup (HtD line)
   double time() const { return t_; }
   int iteration() const { return it_; }
@@ -308,6 +329,11 @@ class Engine {
   void step_fused(double dt);
   void start_halo(void* field);
   void* plane(void* base, int l) const { return (char*)base + (size_t)l * plane_bytes_; }
+  // checkpoint views: array order padded to three axes (2-D: axis 0 is a unit axis whose
+  // one "plane" is the whole field)
+  void own_box(int lo[3], int g0[3], int n[3]) const;
+  size_t plane_span() const { return p_.dims == 3 ? plane_bytes_ : field_bytes_; }
+  void* plane3(void* base, int k) const { return p_.dims == 3 ? plane(base, k) : base; }
   // ---- Cartesian blocks (cart_): kernels on views, phased / face halo exchange ----
   void* at(void* base, int z, int y, int x) const {
     return (char*)base + ((size_t)z * sz_ + (size_t)y * sy_ + (size_t)x) * elem_;

@@ -1,11 +1,12 @@
 // Host-only unit test of the native runtime (no GPU needed; built with ASan + UBSan by
 // `make check`): slab decomposition invariants, the TCP star transport's collectives
-// across forked ranks, and the reference summary block.
+// across forked ranks, the reference summary block and the checkpoint shard header.
 #include <sys/wait.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <cassert>
+#include <fstream>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -181,7 +182,43 @@ static void test_cart_partition() {
   EXPECT(threw);
 }
 
+// a shard as utils/io.py writes it (json.dumps(sort_keys=True): a nested "model" object
+// whose keys must not shadow the top-level ones; payload 64-B aligned)
+static void test_checkpoint_header() {
+  const std::string js =
+      "{\"box0\": [8, 0, 0], \"dtype\": \"float64\", \"grid\": [5, 3, 20], \"ic\": \"sine\", "
+      "\"integrator\": \"ssprk3\", \"it\": 12, \"lengths\": [1.0, 1.0, 1.0], \"model\": "
+      "{\"K\": 1.0, \"it\": 99, \"model\": \"diffusion\", \"shape\": [1], \"t\": 7.5}, "
+      "\"nplanes\": 4, \"pgrid\": [2, 1, 1], \"plane0\": 8, \"rank\": 1, \"shape\": [4, 3, 5], "
+      "\"t\": 0.0012500000000000002, \"world\": 2}";
+  std::string raw;
+  EXPECT(json_top_value(js, "it", raw) && raw == "12");
+  EXPECT(json_top_value(js, "t", raw) && raw == "0.0012500000000000002");
+  EXPECT(json_top_value(js, "shape", raw) && raw == "[4, 3, 5]");
+  EXPECT(!json_top_value(js, "K", raw));  // nested only
+  char tmpl[] = "/tmp/advdiff_ckpt_XXXXXX";
+  const int fd = mkstemp(tmpl);
+  EXPECT(fd >= 0);
+  close(fd);
+  {
+    std::ofstream f(tmpl, std::ios::binary);
+    const uint64_t n = js.size();
+    f.write("ADVDIFF1", 8);
+    f.write((const char*)&n, 8);
+    f.write(js.data(), (std::streamsize)js.size());
+  }
+  const ShardInfo h = read_shard_info(tmpl);
+  EXPECT((h.shape == std::vector<int64_t>{4, 3, 5}));
+  EXPECT((h.box0 == std::vector<int64_t>{8, 0, 0}));
+  EXPECT((h.grid == std::vector<int64_t>{5, 3, 20}));
+  EXPECT(h.dtype == "float64" && h.it == 12 && h.t == 0.0012500000000000002);
+  EXPECT(h.offset % 64 == 0 && h.offset >= 16 + js.size() && h.offset < 16 + js.size() + 64);
+  std::remove(tmpl);
+  EXPECT(shard_path("out/ck", 3) == "out/ck.rank00003.ckpt");
+}
+
 int main() {
+  test_checkpoint_header();
   test_slab_partition();
   test_cart_partition();
   test_star_collectives();

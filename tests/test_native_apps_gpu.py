@@ -244,3 +244,81 @@ def test_native_ipc_graph_steps_bitwise(tmp_path, world, decomp, extra):
     a = np.fromfile(one, dtype=np.float32).reshape(46, 44, 50)
     b = np.fromfile(many, dtype=np.float32).reshape(46, 44, 50)
     assert np.array_equal(a, b), np.abs(a - b).max()
+
+
+# ---- checkpoint / restart of the native engine (csrc/runtime/checkpoint.cpp) ----------
+def _ckpt(prefix, shape):
+    """(fp64 global array, header) of a shard set, read with the Python loader."""
+    from multigpu_advectiondiffusion_amd.utils import io as aio
+    arr, meta = aio.load_checkpoint_box(prefix, [0] * len(shape), list(shape))
+    return arr, meta
+
+
+@pytest.mark.parametrize("world,extra", [
+    (1, []),
+    (2, ["--transport", "socket"]),                         # slab restart on 2 ranks
+    (2, ["--transport", "socket", "--decomp", "1x2x1"]),    # Cartesian blocks
+])
+def test_native_checkpoint_restart_bitwise(tmp_path, world, extra):
+    """20 steps in one run == 10 steps, fp64 shards, restart (any layout) + 10 steps, bit
+    for bit (the shards are fp64: the comparison is on the solver's own precision)."""
+    nx, ny, nz = 54, 46, 40
+    args = lambda it: [1.0, 1.0, 1.0, 1.0, nx, ny, nz, it]
+    ic = ["--ic", "sine"]
+    _run("diffusion3d", args(20), tmp_path / "a.bin", extra=ic + ["--checkpoint", str(tmp_path / "a")])
+    _run("diffusion3d", args(10), tmp_path / "b.bin", extra=ic + ["--checkpoint", str(tmp_path / "b")])
+    txt = _run("diffusion3d", args(10), tmp_path / "c.bin", world=world,
+               extra=ic + ["--restart", str(tmp_path / "b"), "--checkpoint", str(tmp_path / "c")] + extra)
+    a, ma = _ckpt(tmp_path / "a", (nz, ny, nx))
+    c, mc = _ckpt(tmp_path / "c", (nz, ny, nx))
+    assert np.array_equal(a, c), np.abs(a - c).max()
+    assert (ma["it"], mc["it"]) == (20, 20) and ma["t"] == mc["t"], (ma, mc)
+    assert mc["world"] == world and mc["model"]["writer"] == "native"
+    assert np.array_equal(np.fromfile(tmp_path / "a.bin", dtype=np.float32),
+                          np.fromfile(tmp_path / "c.bin", dtype=np.float32)), txt[-500:]
+
+
+def test_native_python_checkpoint_interop(tmp_path):
+    """Python shards restart the native engine and native shards restart the Python solver:
+    Python 8 steps -> native 6 -> Python 6 equals 20 Python steps bit for bit (3-D heat,
+    and 2-D heat restarted on 2 ranks)."""
+    for dims in (3, 2):
+        if dims == 3:
+            shape, lens, app = (50, 44, 38), (1.0, 1.0, 1.0), "diffusion3d"
+            args = lambda it: [1.0, *lens, *shape, it]
+            ic, extra = "sine", ["--ic", "sine"]
+        else:
+            shape, lens, app = (120, 84), (1.0, 1.0), "diffusion2d"
+            args = lambda it: [1.0, *lens, *shape, it]
+            ic, extra = "disc", ["--ic", "disc", "--decomp", "2x1"]
+        mk = lambda: Solver(Diffusion(K=1.0, order=4), Grid(shape, lens), dtype=torch.float64,
+                            device="cuda", ic=ic)
+        ref = mk()
+        ref.run(iters=20)
+        full = ref.gather()
+        s = mk()
+        s.run(iters=8)
+        s.save_checkpoint(tmp_path / f"p{dims}")
+        world = 2 if dims == 2 else 1
+        _run(app, args(6), tmp_path / f"n{dims}.bin", world=world,
+             extra=extra + (["--transport", "socket"] if world > 1 else [])
+             + ["--restart", str(tmp_path / f"p{dims}"), "--checkpoint", str(tmp_path / f"n{dims}")])
+        s2 = mk()
+        meta = s2.load_checkpoint(tmp_path / f"n{dims}")
+        assert meta["it"] == 14 and meta["model"]["writer"] == "native", meta
+        s2.run(iters=6)
+        got = s2.gather()
+        assert s2.it == 20 and s2.t == ref.t
+        assert np.array_equal(got, full), (dims, np.abs(got - full).max())
+
+
+def test_native_burgers_restart_continues(tmp_path):
+    """A Burgers restart continues from the checkpoint's t to tEnd (3-D, WENO5-Z)."""
+    base = [0.3, 2.0, 2.0, 2.0, 40, 36, 32]
+    _run("burgers3d", [0.02] + base, tmp_path / "a.bin", extra=["--checkpoint", str(tmp_path / "a")])
+    _run("burgers3d", [0.04] + base, tmp_path / "b.bin",
+         extra=["--restart", str(tmp_path / "a"), "--checkpoint", str(tmp_path / "b")])
+    a, ma = _ckpt(tmp_path / "a", (32, 36, 40))
+    b, mb = _ckpt(tmp_path / "b", (32, 36, 40))
+    assert abs(ma["t"] - 0.02) < 1e-12 and abs(mb["t"] - 0.04) < 1e-12, (ma["t"], mb["t"])
+    assert mb["it"] > ma["it"] and np.isfinite(b).all() and not np.array_equal(a, b)
