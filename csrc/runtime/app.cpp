@@ -18,6 +18,8 @@
 //   --restart PREFIX (start from fp64 checkpoint shards of any layout, Python or native:
 //   diffusion runs `iters` more steps, Burgers continues to tEnd)  --checkpoint PREFIX
 //   (write this run's shards at the end; checkpoint.cpp, the format of utils/io.py)
+//   --check-every N (NaN/Inf watchdog every N steps: a non-finite field stops every rank
+//   with an error instead of running on; eager stepping)
 // Launch one process per GPU with torchrun-style env vars (RANK/WORLD_SIZE/LOCAL_RANK/
 // MASTER_ADDR/MASTER_PORT), e.g. via `python -m multigpu_advectiondiffusion_amd.launch`.
 #include <chrono>
@@ -66,7 +68,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
               << " [--ic NAME] [--order 2|4] [--weno js|z|js7] [--integrator ssprk3|lsrk45] [--no-fused] [--visc C] [--fp32] [--no-overlap]"
                  " [--transport rccl|ipc|socket] [--decomp slab|PZxPYxPX|PYxPX] [--write FILE]"
                  " [--write-ghosts FILE] [--error-norms] [--geometry] [--graph|--no-graph]"
-                 " [--restart PREFIX] [--checkpoint PREFIX]\n";
+                 " [--restart PREFIX] [--checkpoint PREFIX] [--check-every N]\n";
     return 1;
   }
   Problem p;
@@ -106,6 +108,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   if (opt.count("--no-overlap")) p.overlap = false;
   if (opt.count("--graph")) p.graph = 1;
   if (opt.count("--no-graph")) p.graph = 0;
+  if (opt.count("--check-every")) p.check_every = std::stoi(opt["--check-every"]);
   const std::string decomp = opt.count("--decomp") ? opt["--decomp"] : "slab";
   std::string ic = opt.count("--ic") ? opt["--ic"] : (diff ? "heat" : "gaussian");
   p.ic = ic_code(ic);

@@ -132,6 +132,7 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   const char* ge = std::getenv("ADVDIFF_GRAPH");
   const int want = ge ? std::atoi(ge) : p.graph;
   graph_ = want < 0 ? tr_->graph_safe() : want != 0;
+  if (sync_debug_enabled() || p.check_every > 0) graph_ = false;  // per-launch / per-step host checks
   if (graph_ && std::string(tr_->name()) == "socket")
     throw std::runtime_error("--graph: the socket transport synchronises the host inside a step");
 }
@@ -147,6 +148,8 @@ Engine::~Engine() {
   (void)hipFree(u_);
   (void)hipFree(A_);
   (void)hipFree(B_);
+  (void)hipFree(red_ws_);
+  (void)hipFree(red_);
 }
 
 double Engine::stable_dt() const {
@@ -381,7 +384,10 @@ void Engine::prepare_graphs(double dt) {
 
 void Engine::steps(int n, double dt) {
   if (!graph_) {
-    for (int q = 0; q < n; ++q) step(dt);
+    for (int q = 0; q < n; ++q) {
+      step(dt);
+      watchdog();
+    }
     return;
   }
   // eager steps first: the transport's one-time handshakes (host communication) must not
@@ -440,6 +446,7 @@ Stats Engine::run_until(double t_end) {
     double dt = dt0;
     if (t_ + dt > t_end) dt = t_end - t_;
     step(dt);
+    watchdog();
     ++n;
   }
   HIP_CHECK(hipStreamSynchronize(compute_));
@@ -452,6 +459,38 @@ Stats Engine::run_until(double t_end) {
   s.htod = init_s_;
   check_transport();
   return s;
+}
+
+bool sync_debug_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("ADVDIFF_SYNC_DEBUG");
+    return v != nullptr && *v != '\0' && std::string(v) != "0";
+  }();
+  return on;
+}
+
+double Engine::check_finite() {
+  if (red_ws_ == nullptr) {
+    HIP_CHECK(hipMalloc(&red_ws_, advdiff_reduce_workspace_bytes()));
+    HIP_CHECK(hipMalloc((void**)&red_, 3 * sizeof(double)));
+  }
+  int lo[3], g0[3], n[3];
+  own_box(lo, g0, n);
+  const int64_t pz = p_.dims == 3 ? sz_ : sz_ * alloc_[0];
+  KERNEL_CHECK(advdiff_reduce_norms(p_.dtype, u_, nullptr, sy_, pz, lo[2], lo[2] + n[2], lo[1],
+                                    lo[1] + n[1], lo[0], lo[0] + n[0], red_ws_, red_, compute_));
+  double h[3] = {0, 0, 0};
+  HIP_CHECK(hipMemcpyAsync(h, red_, sizeof h, hipMemcpyDeviceToHost, compute_));
+  HIP_CHECK(hipStreamSynchronize(compute_));
+  // a NaN can hide from a max (fmax drops it) but not from the sum; agree on a flag, since
+  // NaN comparisons inside a MAX allreduce are not reliable either
+  const bool bad = !std::isfinite(h[0]) || !std::isfinite(h[2]);
+  if (tr_->allreduce_max(bad ? 1.0 : 0.0) > 0.0) {
+    char msg[128];
+    std::snprintf(msg, sizeof msg, "non-finite solution at step %d, t=%g", it_, t_);
+    throw std::runtime_error(msg);
+  }
+  return tr_->allreduce_max(h[2]);
 }
 
 void Engine::error_norms(double& l1, double& l2, double& linf) {

@@ -34,9 +34,16 @@ extern "C" const char* advdiff_runtime_hash(void);
     }                                                                                      \
   } while (0)
 
+// ADVDIFF_SYNC_DEBUG=1: synchronise the device after every launch and report the first
+// failing one by its call site (the reference's CUDA_ERROR_CHECK,
+// MultiGPU/Diffusion2d_Baseline/Kernels.cu:12,34-57; hipGraph stepping is off then)
 #define KERNEL_CHECK(expr)                                                                \
   do {                                                                                    \
     int e_ = (expr);                                                                      \
+    if (e_ == 0 && advdiff::rt::sync_debug_enabled()) {                                   \
+      e_ = (int)hipDeviceSynchronize();                                                   \
+      if (e_ == 0) e_ = (int)hipGetLastError();                                           \
+    }                                                                                     \
     if (e_ != 0) {                                                                        \
       std::fprintf(stderr, "kernel launch failed (%d) at %s:%d: %s\n", e_, __FILE__,      \
                    __LINE__, #expr);                                                      \
@@ -45,6 +52,8 @@ extern "C" const char* advdiff_runtime_hash(void);
   } while (0)
 
 namespace advdiff::rt {
+
+bool sync_debug_enabled();  // ADVDIFF_SYNC_DEBUG (see KERNEL_CHECK)
 
 // ------------------------------------------------------------------------------------
 // Process environment (torchrun-compatible: RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*)
@@ -253,6 +262,7 @@ struct Problem {
   int integrator = 0;              // 0 SSP-RK3, 1 low-storage RK4(5)
   bool fused = true;               // 3-D heat + SSP-RK3: one launch per step (3R ghosts)
   int graph = -1;                  // hipGraph stepping: -1 auto (graph-safe transports), 0, 1
+  int check_every = 0;             // NaN/Inf watchdog every N steps (0: off; eager stepping)
   int radius() const {
     return physics == Physics::Diffusion ? order / 2 : (weno == 2 ? 4 : 3);
   }
@@ -308,6 +318,9 @@ class Engine {
   // ghost cells, then the stage buffers as after the IC; sets t and it)
   void save_checkpoint(const std::string& prefix, const std::string& ic_name);
   void load_checkpoint(const std::string& prefix);
+  // NaN/Inf watchdog: Σ|u| and max|u| of the owned cells on every rank; throws
+  // "non-finite solution at step N" on every rank if any rank's are not finite
+  double check_finite();
   double init_seconds() const { return init_s_; }  // barrier-fenced field setup (HtD line)
   double time() const { return t_; }
   int iteration() const { return it_; }
@@ -373,6 +386,11 @@ class Engine {
   Range full_, interior_, blo_, bhi_;
   double t_ = 0;
   int it_ = 0;
+  void* red_ws_ = nullptr;  // watchdog reduction workspace / device result (lazy)
+  double* red_ = nullptr;
+  void watchdog() {
+    if (p_.check_every > 0 && it_ % p_.check_every == 0) check_finite();
+  }
   // hipGraph stepping: one executable graph per (dt, u_ parity) of kGraphSteps steps
   bool graph_ = false;
   int warm_ = 0;  // eager steps run so far (handshakes)

@@ -322,3 +322,46 @@ def test_native_burgers_restart_continues(tmp_path):
     b, mb = _ckpt(tmp_path / "b", (32, 36, 40))
     assert abs(ma["t"] - 0.02) < 1e-12 and abs(mb["t"] - 0.04) < 1e-12, (ma["t"], mb["t"])
     assert mb["it"] > ma["it"] and np.isfinite(b).all() and not np.array_equal(a, b)
+
+
+# ---- failure detection of the native engine ------------------------------------------
+def _run_expect_fail(app, args, world, extra=(), env_extra=None):
+    exe = BIN / app
+    port = free_port_block(world + 1)
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ADVDIFF_PORT=str(port),
+                   **(env_extra or {}))
+        procs.append(subprocess.Popen([str(exe)] + [str(a) for a in args] + list(extra),
+                                      env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    return [(p.communicate(timeout=240)[0], p.returncode) for p in procs]
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_native_watchdog_stops_unstable_run(world):
+    """--check-every: a run made unstable (dt 4x the FD4 limit) stops on EVERY rank with a
+    'non-finite solution' error instead of running on (SURVEY §5 failure detection)."""
+    res = _run_expect_fail("diffusion3d", [1.0, 1.0, 1.0, 1.0, 40, 36, 34, 600], world,
+                           extra=["--ic", "sine", "--safety", "4", "--check-every", "10"]
+                           + (["--transport", "socket"] if world > 1 else []))
+    for out, rc in res:
+        assert rc != 0 and "non-finite solution at step" in out, out[-800:]
+
+
+def test_native_watchdog_and_sync_debug_keep_results(tmp_path):
+    """A stable run with the watchdog, and one with ADVDIFF_SYNC_DEBUG=1 (device sync +
+    error check after every launch), give the same bits as the plain run."""
+    args = [1.0, 1.0, 1.0, 1.0, 44, 40, 36, 12]
+    _run("diffusion3d", args, tmp_path / "a.bin", extra=["--ic", "sine"])
+    _run("diffusion3d", args, tmp_path / "b.bin", extra=["--ic", "sine", "--check-every", "3"])
+    os.environ["ADVDIFF_SYNC_DEBUG"] = "1"
+    try:
+        _run("diffusion3d", args, tmp_path / "c.bin", world=2,
+             extra=["--ic", "sine", "--transport", "socket"])
+    finally:
+        del os.environ["ADVDIFF_SYNC_DEBUG"]
+    a = np.fromfile(tmp_path / "a.bin", dtype=np.float32)
+    for f in ("b.bin", "c.bin"):
+        assert np.array_equal(a, np.fromfile(tmp_path / f, dtype=np.float32)), f
