@@ -66,11 +66,12 @@ bool json_top_value(const std::string& js, const std::string& key, std::string& 
         if (v == std::string::npos) return false;
         ++v;
         while (v < js.size() && js[v] == ' ') ++v;
+        if (v >= js.size()) return false;
         size_t end = v;
-        if (js[v] == '[') {
-          end = js.find(']', v) + 1;
-        } else if (js[v] == '"') {
-          end = js.find('"', v + 1) + 1;
+        if (js[v] == '[' || js[v] == '"') {
+          end = js.find(js[v] == '[' ? ']' : '"', v + 1);
+          if (end == std::string::npos) return false;
+          ++end;
         } else {
           while (end < js.size() && js[end] != ',' && js[end] != '}') ++end;
         }
@@ -243,7 +244,12 @@ void Engine::load_checkpoint(const std::string& prefix) {
   for (const std::string& path : list_shards(prefix)) {
     ShardInfo h = read_shard_info(path);
     if (h.grid != want) throw std::runtime_error(path + ": checkpoint grid differs from the run's");
-    if (first) t = h.t, it = h.it, first = false;
+    if (first) {
+      t = h.t, it = h.it, first = false;
+    } else if (h.t != t || h.it != it) {  // e.g. stale shards of an earlier, wider run
+      throw std::runtime_error(path + ": shard of another checkpoint (it " + std::to_string(h.it) +
+                               " vs " + std::to_string(it) + ") under the same prefix");
+    }
     Src s;
     for (int a = 0; a < 3; ++a) s.g0[a] = 0, s.n[a] = 1;
     for (int a = 0; a < p_.dims; ++a) s.g0[off + a] = (int)h.box0[a], s.n[off + a] = (int)h.shape[a];

@@ -196,6 +196,11 @@ static void test_checkpoint_header() {
   EXPECT(json_top_value(js, "t", raw) && raw == "0.0012500000000000002");
   EXPECT(json_top_value(js, "shape", raw) && raw == "[4, 3, 5]");
   EXPECT(!json_top_value(js, "K", raw));  // nested only
+  // truncated headers: refused, and no out-of-range access (ASan)
+  EXPECT(!json_top_value("{\"it\":", "it", raw));
+  EXPECT(!json_top_value("{\"shape\": [1, 2", "shape", raw));
+  EXPECT(!json_top_value("{\"dtype\": \"float", "dtype", raw));
+  EXPECT(!json_top_value("{\"it", "it", raw));
   char tmpl[] = "/tmp/advdiff_ckpt_XXXXXX";
   const int fd = mkstemp(tmpl);
   EXPECT(fd >= 0);

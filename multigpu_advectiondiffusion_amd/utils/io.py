@@ -113,6 +113,10 @@ def load_checkpoint_box(prefix, box0, extents):
         h, off = read_header(path)
         if meta is None:
             meta = h
+        elif (h.get("it"), h.get("t")) != (meta.get("it"), meta.get("t")):
+            # e.g. stale shards of an earlier run on more ranks under the same prefix
+            raise ValueError(f"{path}: shard of another checkpoint (it {h.get('it')} vs "
+                             f"{meta.get('it')}) under the prefix {prefix}")
         dt = np.dtype(h["dtype"]).newbyteorder("<")
         shape = tuple(h["shape"])
         sb = h.get("box0", [h["plane0"]] + [0] * (len(shape) - 1))

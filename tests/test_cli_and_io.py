@@ -74,6 +74,19 @@ def test_checkpoint_roundtrip_single(tmp_path):
         Solver(Burgers(), Grid((16, 14, 19), (2.0, 2.0, 2.0)), device="cpu").load_checkpoint(tmp_path / "ck")
 
 
+def test_checkpoint_rejects_mixed_shards(tmp_path):
+    """Stale shards of another checkpoint under the same prefix (an earlier run on more
+    ranks) are refused instead of being mixed into the restart."""
+    from multigpu_advectiondiffusion_amd.utils import io as aio
+    s = Solver(Diffusion(K=1.0), Grid((12, 10, 9), (1.0, 1.0, 1.0)), device="cpu", ic="sine")
+    s.run(iters=2)
+    s.save_checkpoint(tmp_path / "ck")
+    stale = dict(s.meta(), it=7)
+    aio.save_checkpoint(tmp_path / "ck", 1, np.zeros((1, 10, 12)), 8, stale)
+    with pytest.raises(ValueError, match="another checkpoint"):
+        s.load_checkpoint(tmp_path / "ck")
+
+
 def test_nan_watchdog():
     s = Solver(Diffusion(K=1.0, safety=50.0, fused=False), Grid((16, 16, 16), (1.0, 1.0, 1.0)),
                device="cpu", ic="square", check_every=5)
