@@ -25,11 +25,7 @@
 #include "launch.hpp"
 #include "advdiff/kernels.h"
 
-#include <algorithm>
-#include <array>
-#include <map>
 #include <utility>
-#include <vector>
 
 namespace advdiff {
 
@@ -50,16 +46,8 @@ struct Box2 {
 struct StepSched {
   int gx, gy;       // tiles along x / y
   int gza, zchunk;  // chunks of the first range, planes per chunk
+  int per, rem;     // unused (ABI of the kernel argument block)
   int edge;         // v3: boundary-anchored edge tiles (axis_tile)
-  // XCD-balanced uneven z chunks (nch > 0; one plane range only): a 1-D grid of nch x
-  // gx gy blocks in chunk-major order; block b runs on XCD b & 7 (the dispatcher's round-
-  // robin, bench/native/xcc_probe.hip), so every XCD gets an equal share of every chunk,
-  // and within a chunk an XCD's blocks take CONTIGUOUS tiles (y-neighbours share halo
-  // rows in its L2, as xcd_tile).  Chunk c covers planes k0 + off[c] .. k0 + off[c+1];
-  // long chunks first let the short late ones fill the CUs that a uniform chunking would
-  // leave idle in its last round (schedule_split below).
-  int nch;
-  int off[5];
 };
 
 // Tile placement along one axis of the v3 march (span W = 64 lanes in x, S1R rows in y;
@@ -589,19 +577,6 @@ constexpr int step_min_waves() {
 // The march variant: DPP x neighbours in stages 2/3 (XS = 1), prefetch distance 2,
 // unmerged LDS reads (SEP).  The other (XS, PF, SEP) combinations measured 1-9 % slower
 // at 512^3 (profiles/step_variants_r2.log, step_cfgs_edge_r2.log) and were removed.
-// Tile of block b among the blocks [base, base + T2) of one chunk: the blocks of XCD x
-// (b % 8 == x) take the contiguous tiles after those of XCDs 0 .. x-1.  Host and device.
-__host__ __device__ inline int chunk_xcd_tile(int b, int base, int T2, int xcd) {
-  auto first = [&](int x) { return base + (((x - base) % 8) + 8) % 8; };
-  auto count = [&](int x) {
-    const int f = first(x);
-    return f < base + T2 ? (base + T2 - 1 - f) / 8 + 1 : 0;
-  };
-  int start = 0;
-  for (int x = 0; x < xcd; ++x) start += count(x);
-  return start + (b - first(xcd)) / 8;
-}
-
 template <typename T, int ORDER, int NW, int RPW, int VAR>
 __global__ __launch_bounds__(64 * NW) __attribute__((
     amdgpu_waves_per_eu(step_min_waves<T, ORDER, NW, RPW>()))) void diffusion3d_step_kernel(
@@ -609,22 +584,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((
     int nz_alloc, int k0, int k1, int k0b, int k1b, StepSched sc, int zlo, int zhi,
     Box2 bx, FdCoef<T> q1, FdCoef<T> q2, FdCoef<T> q3) {
   __shared__ T lds[V3Geom<T, ORDER, NW, RPW>::TOTAL];
-  Tile3 tile;
-  int kc0, kc1;
-  if (sc.nch > 0) {  // XCD-balanced chunks (StepSched)
-    const int b = blockIdx.x, xcd = b & 7, T2 = sc.gx * sc.gy;
-    const int c = b / T2, base = c * T2;
-    const int t = chunk_xcd_tile(b, base, T2, xcd);
-    tile = Tile3{t % sc.gx, t / sc.gx, c};
-    kc0 = k0 + sc.off[c];
-    kc1 = min(k0 + sc.off[c + 1], k1);
-  } else {
-    tile = xcd_tile();
-    // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
-    const bool second = tile.z >= sc.gza;
-    kc0 = second ? k0b + (tile.z - sc.gza) * sc.zchunk : k0 + tile.z * sc.zchunk;
-    kc1 = min(kc0 + sc.zchunk, second ? k1b : k1);
-  }
+  const Tile3 tile = xcd_tile();
+  // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
+  const bool second = tile.z >= sc.gza;
+  const int kc0 = second ? k0b + (tile.z - sc.gza) * sc.zchunk : k0 + tile.z * sc.zchunk;
+  const int kc1 = min(kc0 + sc.zchunk, second ? k1b : k1);
   v3_march<T, ORDER, NW, RPW, 1, 2, true, VAR>(lds, tile.x, tile.y, sc.gx, sc.gy, sc.edge, kc0, kc1,
                                            uin, uout, nx, ny, sy, sz, nz_alloc, zlo, zhi, bx,
                                            q1, q2, q3);
@@ -634,71 +598,6 @@ static int g_step_edge = -1;
 static int step_edge() {  // v3 edge tiles (axis_tile): ADVDIFF_STEP_EDGE / advdiff_set_step_edge
   if (g_step_edge < 0) g_step_edge = knob("STEP_EDGE", 1);
   return g_step_edge;
-}
-
-// Uneven z chunks: list-schedule every XCD's jobs (the blocks b % 8 == x of the chunk-
-// major grid, each len + warm planes) on its `cus` resident slots; the cost is the slowest
-// XCD's makespan.  schedule_split searches 2-3 chunks (the first at least as long as the
-// second) on a grid of >= 2 planes and returns the best plan if it beats the uniform
-// chunking, scored the same way.
-static long long split_makespan(const int* len, int nch, int tiles, int cus, int warm) {
-  long long worst = 0;
-  std::vector<long long> free_at((size_t)std::max(cus, 1));
-  for (int x = 0; x < 8; ++x) {
-    std::fill(free_at.begin(), free_at.end(), 0);
-    for (long long b = x; b < (long long)tiles * nch; b += 8) {
-      auto it = std::min_element(free_at.begin(), free_at.end());
-      *it += len[b / tiles] + warm;
-    }
-    worst = std::max(worst, *std::max_element(free_at.begin(), free_at.end()));
-  }
-  return worst;
-}
-
-struct SplitPlan {
-  int nch = 0;
-  int off[5] = {0, 0, 0, 0, 0};
-  long long cost = 0;
-};
-
-static SplitPlan schedule_split(int n, int tiles, long long slots, int warm, int minc) {
-  SplitPlan best;
-  const int cus = (int)(slots / 8);
-  if (n < 2 * minc || cus < 1) return best;
-  {  // the uniform chunking it must beat (pick_chunk_rounds' choice)
-    const int len = pick_chunk_rounds(n, tiles, slots, warm, minc);
-    const int nch = (n + len - 1) / len;
-    if (nch > 64) return best;
-    std::vector<int> l((size_t)nch, len);
-    l.back() = n - len * (nch - 1);
-    best.cost = split_makespan(l.data(), nch, tiles, cus, warm);
-  }
-  const long long uniform = best.cost;
-  int len[4];
-  auto consider = [&](int nch) {
-    const long long m = split_makespan(len, nch, tiles, cus, warm);
-    if (m < best.cost) {
-      best.cost = m;
-      best.nch = nch;
-      best.off[0] = 0;
-      for (int c = 0; c < nch; ++c) best.off[c + 1] = best.off[c] + len[c];
-    }
-  };
-  const int step = std::max(2, (n / 96) & ~1);  // ~10^3-10^4 candidates at any size
-  for (int a = minc; a <= n - minc; a += step) {  // two chunks
-    len[0] = a;
-    len[1] = n - a;
-    consider(2);
-  }
-  for (int a = minc; a <= n - 2 * minc; a += step)  // three chunks
-    for (int b = minc; b <= std::min(a, n - a - minc); b += step) {
-      len[0] = a;
-      len[1] = b;
-      len[2] = n - a - b;
-      consider(3);
-    }
-  if (best.nch == 0 || best.cost >= uniform) return SplitPlan{};
-  return best;
 }
 
 struct SArgs {
@@ -735,36 +634,11 @@ static hipError_t launch_step(const SArgs& a) {
   static const int minc = knob("STEP_MIN_CHUNK", 16);
   const int na = std::max(a.k1 - a.k0, 0), nb = std::max(a.k1b - a.k0b, 0);
   const long long slots = (long long)device_cus() * per_cu;
-  StepSched sc{};
-  sc.gx = gx;
-  sc.gy = gy;
-  sc.edge = edge;
-  dim3 grid;
-  // XCD-balanced uneven chunks (ADVDIFF_STEP_SPLIT=0: uniform chunks only)
-  static const int split_on = knob("STEP_SPLIT", 1);
-  SplitPlan plan;
-  // FD4 only, by measurement (profiles/split_ab_r3.log, 6 alternations): FD4 +1.2 % in
-  // the 20-step window, +1.4 % sustained; the FD2 step (half the VALU work, at 85 % of the copy
-  // rate) LOST 11-13 % with every plan the slot model picked — its idle last-round slots
-  // cost little in a bandwidth-bound launch, and the uneven chunks cost L2 reuse (open).
-  if (split_on && nb == 0 && ORDER == 4) {
-    static std::map<std::array<long long, 3>, SplitPlan> cache;
-    const std::array<long long, 3> key{na, (long long)gx * gy, slots};
-    auto it = cache.find(key);
-    if (it == cache.end())
-      it = cache.emplace(key, schedule_split(na, gx * gy, slots, 4 * R + 2, minc)).first;
-    plan = it->second;
-  }
-  if (plan.nch > 0) {
-    sc.nch = plan.nch;
-    for (int c = 0; c <= plan.nch; ++c) sc.off[c] = plan.off[c];
-    grid = dim3(gx * gy * plan.nch, 1, 1);
-  } else {
-    const int zc = pick_chunk_rounds(na + nb, (long long)gx * gy, slots, 4 * R, minc);
-    sc.gza = na > 0 ? div_up(na, zc) : 0;
-    sc.zchunk = zc;
-    grid = dim3(gx, gy, sc.gza + (nb > 0 ? div_up(nb, zc) : 0));
-  }
+  StepSched sc{gx, gy, 0, 0, 0, 0, edge};
+  const int zc = pick_chunk_rounds(na + nb, (long long)gx * gy, slots, 4 * R, minc);
+  sc.gza = na > 0 ? div_up(na, zc) : 0;
+  sc.zchunk = zc;
+  const dim3 grid(gx, gy, sc.gza + (nb > 0 ? div_up(nb, zc) : 0));
   // SSP-RK3 stage coefficients b = 1, 1/4, 2/3: exactly the per-stage path's (FdCoef)
   const FdCoef<T> q1 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 1.0, true);
   const FdCoef<T> q2 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 0.25, true);
