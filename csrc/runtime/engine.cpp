@@ -132,7 +132,11 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   const char* ge = std::getenv("ADVDIFF_GRAPH");
   const int want = ge ? std::atoi(ge) : p.graph;
   graph_ = want < 0 ? tr_->graph_safe() : want != 0;
-  if (sync_debug_enabled() || p.check_every > 0) graph_ = false;  // per-launch / per-step host checks
+  if (const char* f = std::getenv("ADVDIFF_FAULT")) {  // "RANK:STEP"
+    if (std::sscanf(f, "%d:%d", &fault_rank_, &fault_step_) != 2) fault_rank_ = fault_step_ = -1;
+  }
+  if (sync_debug_enabled() || p.check_every > 0 || fault_rank_ >= 0)
+    graph_ = false;  // per-launch / per-step host checks
   if (graph_ && std::string(tr_->name()) == "socket")
     throw std::runtime_error("--graph: the socket transport synchronises the host inside a step");
 }

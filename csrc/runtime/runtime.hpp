@@ -263,6 +263,8 @@ struct Problem {
   bool fused = true;               // 3-D heat + SSP-RK3: one launch per step (3R ghosts)
   int graph = -1;                  // hipGraph stepping: -1 auto (graph-safe transports), 0, 1
   int check_every = 0;             // NaN/Inf watchdog every N steps (0: off; eager stepping)
+  // (ADVDIFF_FAULT="RANK:STEP" makes RANK throw after STEP, like the Python solver's fault
+  // injection: the launcher must then stop every other rank; eager stepping)
   int radius() const {
     return physics == Physics::Diffusion ? order / 2 : (weno == 2 ? 4 : 3);
   }
@@ -388,8 +390,12 @@ class Engine {
   int it_ = 0;
   void* red_ws_ = nullptr;  // watchdog reduction workspace / device result (lazy)
   double* red_ = nullptr;
+  int fault_rank_ = -1, fault_step_ = -1;  // ADVDIFF_FAULT="RANK:STEP" (failure tests)
   void watchdog() {
     if (p_.check_every > 0 && it_ % p_.check_every == 0) check_finite();
+    if (fault_rank_ == env_.rank && fault_step_ == it_)
+      throw std::runtime_error("injected fault on rank " + std::to_string(env_.rank) +
+                               " at step " + std::to_string(it_));
   }
   // hipGraph stepping: one executable graph per (dt, u_ parity) of kGraphSteps steps
   bool graph_ = false;

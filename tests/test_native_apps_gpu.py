@@ -365,3 +365,19 @@ def test_native_watchdog_and_sync_debug_keep_results(tmp_path):
     a = np.fromfile(tmp_path / "a.bin", dtype=np.float32)
     for f in ("b.bin", "c.bin"):
         assert np.array_equal(a, np.fromfile(tmp_path / f, dtype=np.float32)), f
+
+
+def test_native_launcher_fail_fast_on_injected_fault():
+    """ADVDIFF_FAULT=1:3 makes native rank 1 fail after step 3; the launcher stops rank 0
+    (blocked in its next halo exchange) instead of letting it hang, and reports the error."""
+    import time
+    from multigpu_advectiondiffusion_amd.launch import launch
+    os.environ["ADVDIFF_FAULT"] = "1:3"
+    try:
+        t0 = time.monotonic()
+        rc = launch(2, ["diffusion3d", "1", "1", "1", "1", "48", "40", "36", "200", "--ic", "sine",
+                        "--transport", "socket"], native=True, timeout=120)
+    finally:
+        del os.environ["ADVDIFF_FAULT"]
+    assert rc not in (0, 124), rc
+    assert time.monotonic() - t0 < 100
