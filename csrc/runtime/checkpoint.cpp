@@ -262,8 +262,7 @@ void Engine::load_checkpoint(const std::string& prefix) {
     srcs.push_back(std::move(s));
   }
   const size_t span = plane_span();
-  std::vector<char> pl(span);
-  std::vector<double> seg;
+  std::vector<char> pl(span), raw;
   long long covered = 0;
   for (int k = 0; k < bn[0]; ++k) {
     char* dev = (char*)plane3(u_, blo[0] + k);
@@ -275,22 +274,29 @@ void Engine::load_checkpoint(const std::string& prefix) {
       const int i0 = std::max(s.g0[2], bg0[2]), i1 = std::min(s.g0[2] + s.n[2], bg0[2] + bn[2]);
       if (j1 <= j0 || i1 <= i0) continue;
       const size_t es = s.h.dtype == "float64" ? 8 : 4;
-      seg.resize((size_t)(i1 - i0));
-      std::vector<char> raw((size_t)(i1 - i0) * es);
-      for (int gj = j0; gj < j1; ++gj) {
+      const int ni = i1 - i0;
+      // rows of the shard that span its full x extent are contiguous: one read per plane
+      // (slab shards always); otherwise one read per row
+      const bool whole = ni == s.n[2];
+      const int rows_per_read = whole ? j1 - j0 : 1;
+      raw.resize((size_t)rows_per_read * ni * es);
+      for (int gj = j0; gj < j1; gj += rows_per_read) {
         const size_t idx = ((size_t)(gk - s.g0[0]) * s.n[1] + (gj - s.g0[1])) * s.n[2] + (i0 - s.g0[2]);
         s.f.seekg((std::streamoff)(s.h.offset + idx * es));
         s.f.read(raw.data(), (std::streamsize)raw.size());
         if (!s.f) throw std::runtime_error("checkpoint: truncated shard");
-        const size_t base = (size_t)(blo[1] + gj - bg0[1]) * sy_ + blo[2] + (i0 - bg0[2]);
-        for (int i = 0; i < i1 - i0; ++i) {
-          const double v = es == 8 ? ((const double*)raw.data())[i] : ((const float*)raw.data())[i];
-          if (elem_ == 8)
-            ((double*)pl.data())[base + i] = v;
-          else
-            ((float*)pl.data())[base + i] = (float)v;
+        for (int r = 0; r < rows_per_read; ++r) {
+          const size_t base = (size_t)(blo[1] + gj + r - bg0[1]) * sy_ + blo[2] + (i0 - bg0[2]);
+          const char* src = raw.data() + (size_t)r * ni * es;
+          for (int i = 0; i < ni; ++i) {
+            const double v = es == 8 ? ((const double*)src)[i] : ((const float*)src)[i];
+            if (elem_ == 8)
+              ((double*)pl.data())[base + i] = v;
+            else
+              ((float*)pl.data())[base + i] = (float)v;
+          }
         }
-        covered += i1 - i0;
+        covered += (long long)rows_per_read * ni;
       }
     }
     HIP_CHECK(hipMemcpy(dev, pl.data(), span, hipMemcpyHostToDevice));
