@@ -42,11 +42,12 @@ struct Box2 {
 // z >= gza belong to the second plane range), as many rounds of resident groups as the
 // grid needs — the dispatcher balances the load dynamically.  (A persistent schedule —
 // one round of groups each marching an equal share of the linearised (tile, plane) space
-// — measured 9-11 % slower at 512^3 and was removed: profiles/step_variants_r2.log.)
+// — measured 9-11 % slower at 512^3 and was removed: profiles/step_variants_r2.log.  Uneven
+// XCD-balanced chunk lengths gained 1.4 % at 512^3 but lost 6-13 % at other sizes and for
+// FD2: profiles/split_ab_r3.log, split_sizes_r3.log.)
 struct StepSched {
   int gx, gy;       // tiles along x / y
   int gza, zchunk;  // chunks of the first range, planes per chunk
-  int per, rem;     // unused (ABI of the kernel argument block)
   int edge;         // v3: boundary-anchored edge tiles (axis_tile)
 };
 
@@ -634,7 +635,7 @@ static hipError_t launch_step(const SArgs& a) {
   static const int minc = knob("STEP_MIN_CHUNK", 16);
   const int na = std::max(a.k1 - a.k0, 0), nb = std::max(a.k1b - a.k0b, 0);
   const long long slots = (long long)device_cus() * per_cu;
-  StepSched sc{gx, gy, 0, 0, 0, 0, edge};
+  StepSched sc{gx, gy, 0, 0, edge};
   const int zc = pick_chunk_rounds(na + nb, (long long)gx * gy, slots, 4 * R, minc);
   sc.gza = na > 0 ? div_up(na, zc) : 0;
   sc.zchunk = zc;
