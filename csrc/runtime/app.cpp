@@ -18,6 +18,8 @@
 //   --restart PREFIX (start from fp64 checkpoint shards of any layout, Python or native:
 //   diffusion runs `iters` more steps, Burgers continues to tEnd)  --checkpoint PREFIX
 //   (write this run's shards at the end; checkpoint.cpp, the format of utils/io.py)
+//   --ascii FILE (the result as one %g per line, fp64 values: the reference's Save3D, Tools.c:
+//   66-86)  --print (the field as rows of %8.2f, a blank line between planes: Print3D)
 //   --check-every N (NaN/Inf watchdog every N steps: a non-finite field stops every rank
 //   with an error instead of running on; eager stepping)
 // Launch one process per GPU with torchrun-style env vars (RANK/WORLD_SIZE/LOCAL_RANK/
@@ -49,7 +51,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
     if (a.rfind("--", 0) == 0) {
       const bool flag = a == "--fp32" || a == "--no-overlap" || a == "--error-norms" ||
                         a == "--no-fused" || a == "--geometry" || a == "--graph" ||
-                        a == "--no-graph";
+                        a == "--no-graph" || a == "--print";
       if (flag || q + 1 >= argc) {
         opt[a] = "1";
       } else {
@@ -68,7 +70,8 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
               << " [--ic NAME] [--order 2|4] [--weno js|z|js7] [--integrator ssprk3|lsrk45] [--no-fused] [--visc C] [--fp32] [--no-overlap]"
                  " [--transport rccl|ipc|socket] [--decomp slab|PZxPYxPX|PYxPX] [--write FILE]"
                  " [--write-ghosts FILE] [--error-norms] [--geometry] [--graph|--no-graph]"
-                 " [--restart PREFIX] [--checkpoint PREFIX] [--check-every N]\n";
+                 " [--restart PREFIX] [--checkpoint PREFIX] [--check-every N] [--ascii FILE]"
+                 " [--print]\n";
     return 1;
   }
   Problem p;
@@ -167,6 +170,8 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   st.dtoh = tr->allreduce_max(wall() - tw);
   std::vector<float> gg;
   if (opt.count("--write-ghosts")) gg = eng.gather_float32_ghosts();
+  std::vector<double> gd;  // fp64 text output, formatted as utils/io.py does
+  if (opt.count("--ascii") || opt.count("--print")) gd = eng.gather_float64();
   if (env.rank == 0) {
     std::cout << "advdiff native build: runtime " << advdiff_runtime_hash() << ", kernels "
               << advdiff_source_hash() << "\n";
@@ -179,6 +184,29 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
     }
     if (opt.count("--write")) write_binary(opt["--write"], g);
     if (opt.count("--write-ghosts")) write_binary(opt["--write-ghosts"], gg);
+    if (opt.count("--ascii")) {
+      FILE* f = std::fopen(opt["--ascii"].c_str(), "w");
+      if (f == nullptr) throw std::runtime_error("cannot write " + opt["--ascii"]);
+      for (double v : gd) std::fprintf(f, "%g\n", v);
+      std::fclose(f);
+    }
+    if (opt.count("--print")) {
+      const int nx = p.nx, ny = p.ny;  // 3-D: nz planes of ny rows; 2-D: one plane
+      const size_t plane = (size_t)nx * ny;
+      std::string txt;
+      char cell[64];
+      for (size_t k = 0; k * plane < gd.size(); ++k) {
+        for (int j = 0; j < ny; ++j) {
+          for (int i = 0; i < nx; ++i) {
+            std::snprintf(cell, sizeof cell, "%8.2f", gd[k * plane + (size_t)j * nx + i]);
+            txt += cell;
+          }
+          txt += "\n";
+        }
+        txt += "\n";
+      }
+      std::cout << txt << "\n";
+    }
     std::cout.flush();
   }
   tr->barrier();

@@ -445,7 +445,8 @@ void Engine::error_norms_cart(double& l1, double& l2, double& linf) {
 }
 
 // owned block of every rank as float32 [z][y][x], assembled on rank 0
-std::vector<float> Engine::gather_cart() {
+template <typename V>
+std::vector<V> Engine::gather_cart() {
   const int dims = p_.dims;
   std::vector<char> raw(field_bytes_);
   HIP_CHECK(hipMemcpy(raw.data(), u_, raw.size(), hipMemcpyDeviceToHost));
@@ -456,21 +457,21 @@ std::vector<float> Engine::gather_cart() {
   }
   const Range z = dims == 3 ? own[0] : Range{0, 1};
   const Range y = own[dims - 2], x = own[dims - 1];
-  std::vector<char> packed((size_t)(z.hi - z.lo) * (y.hi - y.lo) * (x.hi - x.lo) * sizeof(float));
-  float* dst = (float*)packed.data();
+  std::vector<char> packed((size_t)(z.hi - z.lo) * (y.hi - y.lo) * (x.hi - x.lo) * sizeof(V));
+  V* dst = (V*)packed.data();
   size_t q = 0;
   for (int k = z.lo; k < z.hi; ++k)
     for (int j = y.lo; j < y.hi; ++j)
       for (int i = x.lo; i < x.hi; ++i) {
         const size_t src = (size_t)k * (dims == 3 ? sz_ : 0) + (size_t)j * sy_ + i;
-        dst[q++] = elem_ == 8 ? (float)((const double*)raw.data())[src]
-                              : ((const float*)raw.data())[src];
+        dst[q++] = elem_ == 8 ? (V)((const double*)raw.data())[src]
+                              : (V)((const float*)raw.data())[src];
       }
   std::vector<char> all = tr_->gather(packed);
   if (all.empty()) return {};
   const int NZ = dims == 3 ? cd_.shape[0] : 1, NY = cd_.shape[dims - 2], NX = cd_.shape[dims - 1];
-  std::vector<float> out((size_t)NZ * NY * NX);
-  const float* src = (const float*)all.data();
+  std::vector<V> out((size_t)NZ * NY * NX);
+  const V* src = (const V*)all.data();
   for (int r = 0; r < cd_.size(); ++r) {
     int st[3] = {0, 0, 0}, ct[3] = {1, 1, 1};
     for (int a = 0; a < dims; ++a) {
@@ -480,12 +481,14 @@ std::vector<float> Engine::gather_cart() {
     }
     for (int k = 0; k < ct[0]; ++k)
       for (int j = 0; j < ct[1]; ++j) {
-        float* row = out.data() + ((size_t)(st[0] + k) * NY + st[1] + j) * NX + st[2];
+        V* row = out.data() + ((size_t)(st[0] + k) * NY + st[1] + j) * NX + st[2];
         std::copy(src, src + ct[2], row);
         src += ct[2];
       }
   }
   return out;
 }
+template std::vector<float> Engine::gather_cart<float>();
+template std::vector<double> Engine::gather_cart<double>();
 
 }  // namespace advdiff::rt

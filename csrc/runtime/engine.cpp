@@ -549,27 +549,30 @@ double Engine::exact_scale() const {
   return 1.0;
 }
 
-std::vector<float> Engine::gather_float32() {
+template <typename V>
+std::vector<V> Engine::gather_as() {
   HIP_CHECK(hipStreamSynchronize(comm_));
   HIP_CHECK(hipStreamSynchronize(compute_));
-  if (cart_) return gather_cart();
+  if (cart_) return gather_cart<V>();
   const int G = slab_.ghost, c = slab_.count();
   std::vector<char> raw(plane_bytes_ * c);
   HIP_CHECK(hipMemcpy(raw.data(), plane(u_, G), raw.size(), hipMemcpyDeviceToHost));
   const int rows = p_.dims == 3 ? c * p_.ny : c;
-  std::vector<char> packed((size_t)rows * p_.nx * sizeof(float));
-  float* dst = (float*)packed.data();
+  std::vector<char> packed((size_t)rows * p_.nx * sizeof(V));
+  V* dst = (V*)packed.data();
   for (int r = 0; r < rows; ++r)
     for (int i = 0; i < p_.nx; ++i) {
       const size_t src = (size_t)r * sy_ + i;
-      dst[(size_t)r * p_.nx + i] = elem_ == 8 ? (float)((const double*)raw.data())[src]
-                                              : ((const float*)raw.data())[src];
+      dst[(size_t)r * p_.nx + i] = elem_ == 8 ? (V)((const double*)raw.data())[src]
+                                              : (V)((const float*)raw.data())[src];
     }
   std::vector<char> all = tr_->gather(packed);
-  std::vector<float> out(all.size() / sizeof(float));
+  std::vector<V> out(all.size() / sizeof(V));
   if (!all.empty()) std::memcpy(out.data(), all.data(), all.size());
   return out;
 }
+template std::vector<float> Engine::gather_as<float>();
+template std::vector<double> Engine::gather_as<double>();
 
 // every rank's planes with their ghost planes (slabs), concatenated in rank order
 std::vector<float> Engine::gather_float32_ghosts() {

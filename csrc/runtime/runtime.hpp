@@ -310,7 +310,12 @@ class Engine {
   Stats run_until(double t_end);
   // Σ|u-e|, Σ(u-e)², max|u-e| over the owned slab vs the exact solution (sine/heat ICs)
   void error_norms(double& l1, double& l2, double& linf);
-  std::vector<float> gather_float32();  // rank 0: global array (no ghosts); others empty
+  // rank 0: global array (no ghosts), as float (result.bin) or double (--ascii, --print);
+  // others empty
+  std::vector<float> gather_float32() { return gather_as<float>(); }
+  std::vector<double> gather_float64() { return gather_as<double>(); }
+  template <typename V>
+  std::vector<V> gather_as();
   // rank 0: every rank's planes INCLUDING its ghost planes, concatenated in rank order —
   // the reference's multi-GPU result.bin layout (each rank's Nx x Ny x (_Nz + 6) slab,
   // SaveBinary3D(h_u, Nx, Ny, NZ), MultiGPU/Diffusion3d_Baseline/main.c:341).  Slabs only.
@@ -361,7 +366,8 @@ class Engine {
   void step_fused_cart(double dt);
   void start_halo_cart(void* field);
   void error_norms_cart(double& l1, double& l2, double& linf);
-  std::vector<float> gather_cart();
+  template <typename V>
+  std::vector<V> gather_cart();
   double exact_scale() const;  // decay factor of the exact solution at t_ (sine / heat ICs)
   void check_transport();      // exits if the transport reported deferred errors
 

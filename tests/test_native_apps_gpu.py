@@ -381,3 +381,19 @@ def test_native_launcher_fail_fast_on_injected_fault():
         del os.environ["ADVDIFF_FAULT"]
     assert rc not in (0, 124), rc
     assert time.monotonic() - t0 < 100
+
+
+def test_native_ascii_and_print_match_python(tmp_path):
+    """--ascii (one %g per line, fp64) and --print (rows of %8.2f) of the native apps give
+    the same text as the Python front end (the reference's Save3D / Print3D)."""
+    import sys
+    args = ["1", "1", "1", "1", "12", "10", "8", "5", "--ic", "sine"]
+    py = subprocess.run([sys.executable, "-m", "multigpu_advectiondiffusion_amd", "diffusion3d",
+                         *args, "--ascii", str(tmp_path / "py.txt"), "--print"],
+                        capture_output=True, text=True, check=True, cwd=ROOT).stdout
+    nat = _run("diffusion3d", args, tmp_path / "n.bin",
+               extra=["--ascii", str(tmp_path / "n.txt"), "--print"])
+    a, b = (tmp_path / "py.txt").read_text(), (tmp_path / "n.txt").read_text()
+    assert a == b and len(a.splitlines()) == 12 * 10 * 8
+    block = py[:py.index("\n\n\n") + 3]  # Python prints the field before its summary
+    assert block.count("\n") > 80 and block in nat
