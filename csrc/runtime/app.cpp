@@ -18,16 +18,21 @@
 //   --restart PREFIX (start from fp64 checkpoint shards of any layout, Python or native:
 //   diffusion runs `iters` more steps, Burgers continues to tEnd)  --checkpoint PREFIX
 //   (write this run's shards at the end; checkpoint.cpp, the format of utils/io.py)
+//   --config FILE.json (the keys of the Python front end's config files; see apply_config)
 //   --ascii FILE (the result as one %g per line, fp64 values: the reference's Save3D, Tools.c:
 //   66-86)  --print (the field as rows of %8.2f, a blank line between planes: Print3D)
 //   --check-every N (NaN/Inf watchdog every N steps: a non-finite field stops every rank
 //   with an error instead of running on; eager stepping)
 // Launch one process per GPU with torchrun-style env vars (RANK/WORLD_SIZE/LOCAL_RANK/
 // MASTER_ADDR/MASTER_PORT), e.g. via `python -m multigpu_advectiondiffusion_amd.launch`.
+#include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <cstring>
+#include <fstream>
 #include <iostream>
 #include <map>
+#include <sstream>
 #include <string>
 
 #include "runtime.hpp"
@@ -41,6 +46,66 @@ static int ic_code(const std::string& s) {
   auto it = m.find(s);
   if (it == m.end()) throw std::runtime_error("unknown IC " + s);
   return it->second;
+}
+
+// --config FILE.json: a flat object, laid out like the Python front end's config files
+// (cli.py _load_config): "args" = the positional list, every other key one of THESE
+// options ("write-ghosts" or "write_ghosts"; true = a flag, false = absent).  Entries
+// override the command line, as in cli.py.  TOML / YAML configs are the Python side's.
+static void apply_config(const std::string& path, std::vector<std::string>& pos,
+                         std::map<std::string, std::string>& opt) {
+  if (path.size() < 5 || path.compare(path.size() - 5, 5, ".json") != 0)
+    throw std::runtime_error("--config: the native apps read JSON configs (" + path + ")");
+  std::ifstream f(path);
+  if (!f) throw std::runtime_error("--config: cannot read " + path);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  const std::string js = ss.str();
+  size_t q = js.find('{');
+  auto skip = [&] {
+    while (q < js.size() && (std::isspace((unsigned char)js[q]) || js[q] == ',')) ++q;
+  };
+  auto string_at = [&]() {  // js[q] == '"'
+    const size_t e = js.find('"', q + 1);
+    if (e == std::string::npos) throw std::runtime_error("--config: bad JSON string");
+    std::string v = js.substr(q + 1, e - q - 1);
+    q = e + 1;
+    return v;
+  };
+  auto scalar_at = [&]() {  // a string, number, true or false
+    skip();
+    if (q < js.size() && js[q] == '"') return string_at();
+    const size_t b = q;
+    while (q < js.size() && js[q] != ',' && js[q] != '}' && js[q] != ']' &&
+           !std::isspace((unsigned char)js[q]))
+      ++q;
+    return js.substr(b, q - b);
+  };
+  if (q == std::string::npos) throw std::runtime_error("--config: not a JSON object");
+  ++q;
+  for (skip(); q < js.size() && js[q] != '}'; skip()) {
+    if (js[q] != '"') throw std::runtime_error("--config: expected a key");
+    std::string key = string_at();
+    q = js.find(':', q);
+    if (q == std::string::npos) throw std::runtime_error("--config: expected ':'");
+    ++q;
+    skip();
+    if (key == "args") {
+      if (js[q] != '[') throw std::runtime_error("--config: \"args\" must be a list");
+      ++q;
+      pos.clear();
+      for (skip(); q < js.size() && js[q] != ']'; skip()) pos.push_back(scalar_at());
+      ++q;
+      continue;
+    }
+    if (js[q] == '[' || js[q] == '{') throw std::runtime_error("--config: " + key + " must be a scalar");
+    const std::string v = scalar_at();
+    std::replace(key.begin(), key.end(), '_', '-');
+    if (v == "false")
+      opt.erase("--" + key);
+    else
+      opt["--" + key] = v == "true" ? "1" : v;
+  }
 }
 
 int run_app(int argc, char** argv, Physics phys, int dims) {
@@ -61,6 +126,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
       pos.push_back(a);
     }
   }
+  if (opt.count("--config")) apply_config(opt["--config"], pos, opt);
   const bool diff = phys == Physics::Diffusion;
   const size_t need = diff ? (dims == 3 ? 8 : 6) : (dims == 3 ? 8 : 6);
   if (pos.size() < need) {
@@ -71,7 +137,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
                  " [--transport rccl|ipc|socket] [--decomp slab|PZxPYxPX|PYxPX] [--write FILE]"
                  " [--write-ghosts FILE] [--error-norms] [--geometry] [--graph|--no-graph]"
                  " [--restart PREFIX] [--checkpoint PREFIX] [--check-every N] [--ascii FILE]"
-                 " [--print]\n";
+                 " [--print] [--config FILE.json]\n";
     return 1;
   }
   Problem p;

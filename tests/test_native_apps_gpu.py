@@ -397,3 +397,19 @@ def test_native_ascii_and_print_match_python(tmp_path):
     assert a == b and len(a.splitlines()) == 12 * 10 * 8
     block = py[:py.index("\n\n\n") + 3]  # Python prints the field before its summary
     assert block.count("\n") > 80 and block in nat
+
+
+def test_native_config_file(tmp_path):
+    """--config FILE.json (positional "args" + options, overriding the command line) runs
+    the same problem as the equivalent command line, bit for bit."""
+    import json
+    cfg = tmp_path / "run.json"
+    cfg.write_text(json.dumps({"args": [1.0, 1.0, 1.0, 1.0, 30, 28, 26, 6], "ic": "sine",
+                               "order": 2, "no_fused": True, "error-norms": False}))
+    _run("diffusion3d", [1.0, 1.0, 1.0, 1.0, 30, 28, 26, 6], tmp_path / "a.bin",
+         extra=["--ic", "sine", "--order", "2", "--no-fused"])
+    txt = _run("diffusion3d", [], tmp_path / "b.bin",
+               extra=["--config", str(cfg), "--ic", "heat", "--error-norms"])
+    assert "L1 norm" not in txt  # "error-norms": false in the file wins
+    assert np.array_equal(np.fromfile(tmp_path / "a.bin", dtype=np.float32),
+                          np.fromfile(tmp_path / "b.bin", dtype=np.float32))
