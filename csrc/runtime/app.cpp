@@ -18,6 +18,8 @@
 //   --restart PREFIX (start from fp64 checkpoint shards of any layout, Python or native:
 //   diffusion runs `iters` more steps, Burgers continues to tEnd)  --checkpoint PREFIX
 //   (write this run's shards at the end; checkpoint.cpp, the format of utils/io.py)
+//   --style multigpu|singlegpu (summary block of the multi-GPU apps, default, or of the
+//   single-GPU apps: no HtD/DtH lines, Final Time, SG GFLOPs convention)
 //   --config FILE.json (the keys of the Python front end's config files; see apply_config)
 //   --ascii FILE (the result as one %g per line, fp64 values: the reference's Save3D, Tools.c:
 //   66-86)  --print (the field as rows of %8.2f, a blank line between planes: Print3D)
@@ -137,7 +139,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
                  " [--transport rccl|ipc|socket] [--decomp slab|PZxPYxPX|PYxPX] [--write FILE]"
                  " [--write-ghosts FILE] [--error-norms] [--geometry] [--graph|--no-graph]"
                  " [--restart PREFIX] [--checkpoint PREFIX] [--check-every N] [--ascii FILE]"
-                 " [--print] [--config FILE.json]\n";
+                 " [--print] [--config FILE.json] [--style multigpu|singlegpu]\n";
     return 1;
   }
   Problem p;
@@ -242,11 +244,31 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
     std::cout << "advdiff native build: runtime " << advdiff_runtime_hash() << ", kernels "
               << advdiff_source_hash() << "\n";
     if (pos.size() > need) std::cout << "(block sizes ignored: gfx950 tiles are fixed)\n";
-    std::cout << summary_multigpu(title, optname, st, p, env.size);
-    if (norms) {
-      std::printf("L1 norm                                       :  %e\n", l1);
-      std::printf("L2 norm                                       :  %e\n", l2);
-      std::printf("Linf norm                                     :  %e\n", li);
+    const std::string style = opt.count("--style") ? opt["--style"] : "multigpu";
+    if (style == "singlegpu") {  // the single-GPU apps' block, norms inside it (cli.py)
+      auto f = [](const char* spec, double v) {
+        char b[64];
+        std::snprintf(b, sizeof b, spec, v);
+        return std::string(b);
+      };
+      const double ml = st.seconds > 0 ? p.cells() * (double)st.steps / st.seconds / 1e6 : 0;
+      std::vector<std::pair<std::string, std::string>> ex = {
+          {"MLUPS (cells x RK3 steps / s)", f("%.1f", ml)},
+          {"Stage-MLUPS", f("%.1f", 3 * ml)},
+          {"Processes / devices", std::to_string(env.size) + " x gfx950"}};
+      if (norms) {
+        ex.push_back({"L1 norm", f("%e", l1)});
+        ex.push_back({"L2 norm", f("%e", l2)});
+        ex.push_back({"Linf norm", f("%e", li)});
+      }
+      std::cout << summary_singlegpu(title, optname, st, p, ex);
+    } else {
+      std::cout << summary_multigpu(title, optname, st, p, env.size);
+      if (norms) {
+        std::printf("L1 norm                                       :  %e\n", l1);
+        std::printf("L2 norm                                       :  %e\n", l2);
+        std::printf("Linf norm                                     :  %e\n", li);
+      }
     }
     if (opt.count("--write")) write_binary(opt["--write"], g);
     if (opt.count("--write-ghosts")) write_binary(opt["--write-ghosts"], gg);

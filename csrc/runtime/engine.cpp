@@ -638,6 +638,38 @@ std::string summary_multigpu(const std::string& title, const std::string& opt, c
   return o.str();
 }
 
+// The single-GPU apps' block (SingleGPU/*/tools.cpp PrintSummary; the labels and layout of
+// utils/metrics.py summary_singlegpu): GFLOPs without the x3 for diffusion (quirk of the
+// reference's SG heat apps), with it for Burgers.
+std::string summary_singlegpu(const std::string& title, const std::string& opt, const Stats& s,
+                              const Problem& p, const std::vector<std::pair<std::string, std::string>>& extra) {
+  const std::string sep(67, '=');
+  const double k = p.physics == Physics::Burgers ? 3.0 : 1.0;
+  const double gflops = s.seconds > 0 ? k * s.steps * p.cells() * 1e-9 * 8.0 / s.seconds : 0;
+  std::ostringstream o;
+  o << "=========================== " << title << " =======================\n";
+  o << "Optimization                                 :  " << opt << "\n";
+  o << "Kernel time ex. data transfers               :  " << fmt("%f", s.seconds) << " seconds\n";
+  o << sep << "\n";
+  o << "Total effective GFLOPs                       :  " << fmt("%f", gflops) << "\n";
+  o << sep << "\n";
+  if (p.dims == 3)
+    o << "3D Grid Size                                 :  " << p.nx << " x " << p.ny << " x "
+      << p.nz << " \n";
+  else
+    o << "2D Grid Size                                 :  " << p.nx << " x " << p.ny << " \n";
+  o << "Iterations                                   :  " << s.steps << "\n";
+  o << "Final Time                                   :  " << fmt("%g", s.t) << "\n";
+  o << sep << "\n";
+  for (const auto& kv : extra) {
+    std::string key = kv.first;
+    if (key.size() < 45) key.resize(45, ' ');
+    o << key << ":  " << kv.second << "\n";
+  }
+  if (!extra.empty()) o << sep << "\n";
+  return o.str();
+}
+
 void write_binary(const std::string& path, const std::vector<float>& data) {
   FILE* f = std::fopen(path.c_str(), "wb");
   if (!f) {

@@ -418,6 +418,10 @@ class Engine {
 // Reference summary blocks (MultiGPU/Diffusion3d_Baseline/Tools.c:255-270)
 std::string summary_multigpu(const std::string& title, const std::string& opt, const Stats& s,
                              const Problem& p, int nprocs);
+// the single-GPU apps' summary block (utils/metrics.py summary_singlegpu)
+std::string summary_singlegpu(const std::string& title, const std::string& opt, const Stats& s,
+                              const Problem& p,
+                              const std::vector<std::pair<std::string, std::string>>& extra);
 void write_binary(const std::string& path, const std::vector<float>& data);
 
 }  // namespace advdiff::rt

@@ -106,6 +106,15 @@ static void test_summary_block() {
          std::string::npos);
   EXPECT(txt.find("Iterations                                   :  5 x 3 RK steps") !=
          std::string::npos);
+  // single-GPU block: the SG heat GFLOPs has no x3 (5 x 1320 x 8e-9 / 0.5 s), Burgers has
+  s.t = 0.25;
+  const std::string sg = summary_singlegpu("Diffusion-3D", "opt", s, p, {{"MLUPS", "1.0"}});
+  EXPECT(sg.find("Total effective GFLOPs                       :  0.000106\n") != std::string::npos);
+  EXPECT(sg.find("3D Grid Size                                 :  10 x 11 x 12 \n") != std::string::npos);
+  EXPECT(sg.find("Final Time                                   :  0.25\n") != std::string::npos);
+  EXPECT(sg.find("MLUPS                                        :  1.0\n") != std::string::npos);
+  p.physics = Physics::Burgers;
+  EXPECT(summary_singlegpu("B", "o", s, p, {}).find(":  0.000317\n") != std::string::npos);
 }
 
 // Cartesian blocks: over all ranks, interior + boundary boxes cover every non-frozen

@@ -413,3 +413,14 @@ def test_native_config_file(tmp_path):
     assert "L1 norm" not in txt  # "error-norms": false in the file wins
     assert np.array_equal(np.fromfile(tmp_path / "a.bin", dtype=np.float32),
                           np.fromfile(tmp_path / "b.bin", dtype=np.float32))
+
+
+def test_native_singlegpu_summary_style(tmp_path):
+    """--style singlegpu prints the single-GPU apps' block (Final Time, no HtD/DtH lines,
+    norms inside it) with the labels of the Python front end's."""
+    txt = _run("diffusion3d", [1.0, 1.0, 1.0, 1.0, 24, 22, 20, 4], tmp_path / "a.bin",
+               extra=["--ic", "sine", "--style", "singlegpu", "--error-norms"])
+    assert "Final Time                                   :  " in txt
+    assert "Data transfer(s) HtD" not in txt
+    assert "3D Grid Size                                 :  24 x 22 x 20 \n" in txt
+    assert "Linf norm                                    :  " in txt
