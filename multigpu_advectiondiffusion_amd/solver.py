@@ -669,11 +669,15 @@ class Solver:
     # diagnostics
     # ------------------------------------------------------------------------------
     def check_finite(self):
-        """NaN/Inf watchdog (absent in the reference)."""
-        mx = self.global_max_abs()
-        if not np.isfinite(mx):
+        """NaN/Inf watchdog (absent in the reference).  Σ|u| as well as
+        max|u|: the device reduction takes its max with fmax, which drops NaN operands, so
+        an isolated NaN cell shows only in the sum; the ranks agree on a flag (NaN
+        comparisons inside a MAX allreduce are not reliable either)."""
+        s1, _, mx = self.reducer()(self.u, None, self._owned_xyz_box())
+        bad = 0.0 if (np.isfinite(s1) and np.isfinite(mx)) else 1.0
+        if self.comm.allreduce_max(bad) > 0.0:
             raise FloatingPointError(f"non-finite solution at step {self.it}, t={self.t:g}")
-        return mx
+        return self.comm.allreduce_max(mx)
 
     def error_norms(self, exact: torch.Tensor | None = None, K: float | None = None,
                     t_exact: float | None = None):

@@ -94,6 +94,15 @@ def test_nan_watchdog():
         s.run(iters=400)
 
 
+def test_watchdog_catches_an_isolated_nan():
+    """One NaN cell among finite ones (max|u| alone can miss it) stops the run."""
+    s = Solver(Diffusion(K=1.0), Grid((14, 12, 10), (1.0, 1.0, 1.0)), device="cpu", ic="sine")
+    s.check_finite()
+    s.owned[3, 4, 5] = float("nan")
+    with pytest.raises(FloatingPointError):
+        s.check_finite()
+
+
 def test_fp32_cpu_path():
     s = Solver(Diffusion(K=1.0), Grid((20, 20, 20), (1.0, 1.0, 1.0)), device="cpu",
                dtype=torch.float32, ic="sine")

@@ -351,3 +351,15 @@ def test_burgers3d_production_size_vs_reference():
                         0.25)
     torch.cuda.synchronize()
     assert (out - exp).abs().max().item() < 1e-11
+
+
+def test_watchdog_catches_an_isolated_nan_gpu():
+    """The device reduction's max uses fmax (drops NaN): the watchdog also checks the sum,
+    so one NaN cell among finite ones stops the run on the GPU path too."""
+    from multigpu_advectiondiffusion_amd import Diffusion, Grid, Solver
+    s = Solver(Diffusion(K=1.0), Grid((70, 33, 41), (1.0, 1.0, 1.0)), dtype=torch.float64,
+               device="cuda", ic="sine")
+    s.check_finite()
+    s.owned[7, 9, 11] = float("nan")
+    with pytest.raises(FloatingPointError):
+        s.check_finite()
