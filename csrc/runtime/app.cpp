@@ -20,6 +20,8 @@
 //   (write this run's shards at the end; checkpoint.cpp, the format of utils/io.py)
 //   --style multigpu|singlegpu (summary block of the multi-GPU apps, default, or of the
 //   single-GPU apps: no HtD/DtH lines, Final Time, SG GFLOPs convention)
+//   --initial FILE (the starting field, float32 like result.bin: the reference's initial.bin)
+//   --json (one metrics line with the keys of the Python front end's --json)
 //   --config FILE.json (the keys of the Python front end's config files; see apply_config)
 //   --ascii FILE (the result as one %g per line, fp64 values: the reference's Save3D, Tools.c:
 //   66-86)  --print (the field as rows of %8.2f, a blank line between planes: Print3D)
@@ -118,7 +120,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
     if (a.rfind("--", 0) == 0) {
       const bool flag = a == "--fp32" || a == "--no-overlap" || a == "--error-norms" ||
                         a == "--no-fused" || a == "--geometry" || a == "--graph" ||
-                        a == "--no-graph" || a == "--print";
+                        a == "--no-graph" || a == "--print" || a == "--json";
       if (flag || q + 1 >= argc) {
         opt[a] = "1";
       } else {
@@ -139,7 +141,8 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
                  " [--transport rccl|ipc|socket] [--decomp slab|PZxPYxPX|PYxPX] [--write FILE]"
                  " [--write-ghosts FILE] [--error-norms] [--geometry] [--graph|--no-graph]"
                  " [--restart PREFIX] [--checkpoint PREFIX] [--check-every N] [--ascii FILE]"
-                 " [--print] [--config FILE.json] [--style multigpu|singlegpu]\n";
+                 " [--print] [--config FILE.json] [--style multigpu|singlegpu] [--initial FILE]"
+                 " [--json]\n";
     return 1;
   }
   Problem p;
@@ -211,6 +214,10 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   auto tr = make_transport(env, tk);
   Engine eng(p, tr.get(), env);
   if (opt.count("--restart")) eng.load_checkpoint(opt["--restart"]);
+  if (opt.count("--initial")) {  // the starting field (IC or restart), float32 like result.bin
+    const std::vector<float> g0 = eng.gather_float32();
+    if (env.rank == 0) write_binary(opt["--initial"], g0);
+  }
   Stats st = diff ? eng.run_iters(iters) : eng.run_until(tEnd + p.t0);
   if (opt.count("--checkpoint")) eng.save_checkpoint(opt["--checkpoint"], ic);
   std::string title =
@@ -294,6 +301,19 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
         txt += "\n";
       }
       std::cout << txt << "\n";
+    }
+    if (opt.count("--json")) {  // one metrics line, the keys of cli.py --json
+      const double ml = st.seconds > 0 ? p.cells() * (double)st.steps / st.seconds / 1e6 : 0;
+      char line[512];
+      const std::string grid = "[" + std::to_string(p.nx) + ", " + std::to_string(p.ny) +
+                               (dims == 3 ? ", " + std::to_string(p.nz) : std::string()) + "]";
+      std::snprintf(line, sizeof line,
+                    "{\"app\": \"%s\", \"grid\": %s, \"steps\": %d, \"seconds\": %.17g, "
+                    "\"mlups\": %.17g, \"n_procs\": %d, \"dtype\": \"%s\", \"t\": %.17g}",
+                    (std::string(diff ? "diffusion" : "burgers") + (dims == 3 ? "3d" : "2d")).c_str(),
+                    grid.c_str(), st.steps, st.seconds, ml, env.size,
+                    p.dtype == ADVDIFF_F64 ? "fp64" : "fp32", st.t);
+      std::cout << line << "\n";
     }
     std::cout.flush();
   }

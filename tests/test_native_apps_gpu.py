@@ -424,3 +424,21 @@ def test_native_singlegpu_summary_style(tmp_path):
     assert "Data transfer(s) HtD" not in txt
     assert "3D Grid Size                                 :  24 x 22 x 20 \n" in txt
     assert "Linf norm                                    :  " in txt
+
+
+def test_native_initial_and_json(tmp_path):
+    """--initial writes the starting field (as the Python front end's --initial) and
+    --json prints one metrics line with the Python front end's keys."""
+    import json
+    import sys
+    args = ["1", "1", "1", "1", "20", "18", "16", "4", "--ic", "sine"]
+    subprocess.run([sys.executable, "-m", "multigpu_advectiondiffusion_amd", "diffusion3d", *args,
+                    "--initial", str(tmp_path / "py0.bin")], check=True, cwd=ROOT,
+                   capture_output=True)
+    txt = _run("diffusion3d", args, tmp_path / "n.bin",
+               extra=["--initial", str(tmp_path / "n0.bin"), "--json"])
+    a = np.fromfile(tmp_path / "py0.bin", dtype=np.float32)
+    assert np.array_equal(a, np.fromfile(tmp_path / "n0.bin", dtype=np.float32)) and a.size == 20 * 18 * 16
+    line = json.loads([l for l in txt.splitlines() if l.startswith("{")][-1])
+    assert line["app"] == "diffusion3d" and line["grid"] == [20, 18, 16] and line["steps"] == 4
+    assert line["n_procs"] == 1 and line["dtype"] == "fp64" and line["mlups"] > 0
