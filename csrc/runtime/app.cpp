@@ -22,6 +22,7 @@
 //   single-GPU apps: no HtD/DtH lines, Final Time, SG GFLOPs convention)
 //   --initial FILE (the starting field, float32 like result.bin: the reference's initial.bin)
 //   --json (one metrics line with the keys of the Python front end's --json)
+//   --warmup N (N untimed steps first, then the state as before them: Engine::warmup)
 //   --config FILE.json (the keys of the Python front end's config files; see apply_config)
 //   --ascii FILE (the result as one %g per line, fp64 values: the reference's Save3D, Tools.c:
 //   66-86)  --print (the field as rows of %8.2f, a blank line between planes: Print3D)
@@ -142,7 +143,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
                  " [--write-ghosts FILE] [--error-norms] [--geometry] [--graph|--no-graph]"
                  " [--restart PREFIX] [--checkpoint PREFIX] [--check-every N] [--ascii FILE]"
                  " [--print] [--config FILE.json] [--style multigpu|singlegpu] [--initial FILE]"
-                 " [--json]\n";
+                 " [--json] [--warmup N]\n";
     return 1;
   }
   Problem p;
@@ -218,6 +219,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
     const std::vector<float> g0 = eng.gather_float32();
     if (env.rank == 0) write_binary(opt["--initial"], g0);
   }
+  if (opt.count("--warmup")) eng.warmup(std::stoi(opt["--warmup"]));
   Stats st = diff ? eng.run_iters(iters) : eng.run_until(tEnd + p.t0);
   if (opt.count("--checkpoint")) eng.save_checkpoint(opt["--checkpoint"], ic);
   std::string title =

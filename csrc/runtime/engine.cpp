@@ -430,6 +430,41 @@ Stats Engine::run_iters(int iters) {
   return s;
 }
 
+void Engine::warmup(int n) {
+  if (n <= 0) return;
+  HIP_CHECK(hipStreamSynchronize(comm_));
+  HIP_CHECK(hipStreamSynchronize(compute_));
+  void* const roles[3] = {u_, A_, B_};
+  void* saved[3] = {nullptr, nullptr, nullptr};
+  for (int q = 0; q < 3; ++q) {
+    HIP_CHECK(hipMalloc(&saved[q], field_bytes_));
+    HIP_CHECK(hipMemcpyAsync(saved[q], roles[q], field_bytes_, hipMemcpyDeviceToDevice, compute_));
+  }
+  const double t = t_;
+  const int it = it_;
+  const double dt = stable_dt();
+  if (n >= kGraphSteps) prepare_graphs(dt);
+  steps(n, dt);
+  if (halo_pending_) {
+    HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
+    halo_pending_ = false;
+  }
+  HIP_CHECK(hipStreamSynchronize(comm_));
+  HIP_CHECK(hipStreamSynchronize(compute_));
+  tr_->barrier();  // no peer still puts into a ghost box being restored
+  u_ = roles[0];
+  A_ = roles[1];
+  B_ = roles[2];
+  for (int q = 0; q < 3; ++q) {
+    HIP_CHECK(hipMemcpyAsync(roles[q], saved[q], field_bytes_, hipMemcpyDeviceToDevice, compute_));
+  }
+  HIP_CHECK(hipStreamSynchronize(compute_));
+  for (void* b : saved) HIP_CHECK(hipFree(b));
+  t_ = t;
+  it_ = it;
+  tr_->barrier();
+}
+
 Stats Engine::run_until(double t_end) {
   const double dt0 = stable_dt();
   prepare_graphs(dt0);

@@ -307,6 +307,9 @@ class Engine {
   bool graphs() const { return graph_; }
   static constexpr int kGraphSteps = 8;  // even: the u/A ping-pong returns to its start
   Stats run_iters(int iters);
+  // n untimed steps, then the state exactly as before them (fields, buffer roles, t, it):
+  // clocks, code objects, graphs and transport handshakes are warm (cli.py --warmup)
+  void warmup(int n);
   Stats run_until(double t_end);
   // Σ|u-e|, Σ(u-e)², max|u-e| over the owned slab vs the exact solution (sine/heat ICs)
   void error_norms(double& l1, double& l2, double& linf);

@@ -442,3 +442,24 @@ def test_native_initial_and_json(tmp_path):
     line = json.loads([l for l in txt.splitlines() if l.startswith("{")][-1])
     assert line["app"] == "diffusion3d" and line["grid"] == [20, 18, 16] and line["steps"] == 4
     assert line["n_procs"] == 1 and line["dtype"] == "fp64" and line["mlups"] > 0
+
+
+@pytest.mark.parametrize("app,args,world,extra", [
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 40, 36, 34, 10], 1, ["--ic", "sine"]),
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 40, 36, 34, 10], 2, ["--ic", "sine", "--transport", "ipc"]),
+    ("burgers3d", [0.02, 0.3, 2.0, 2.0, 2.0, 36, 32, 30], 1, []),
+])
+def test_native_warmup_keeps_the_result(tmp_path, app, args, world, extra):
+    """--warmup N runs N untimed steps (graphs, handshakes and clocks warm) and restores the
+    state: the result equals the run without warm-up bit for bit."""
+    env = dict(os.environ)
+    if world > 1:
+        os.environ.update(ADVDIFF_SHARE_GPU="1", GPU_MAX_HW_QUEUES="2", ADVDIFF_IPC_TIMEOUT_S="60")
+    try:
+        _run(app, args, tmp_path / "a.bin", world=world, extra=extra)
+        txt = _run(app, args, tmp_path / "b.bin", world=world, extra=extra + ["--warmup", "9"])
+    finally:
+        os.environ.clear()
+        os.environ.update(env)
+    assert np.array_equal(np.fromfile(tmp_path / "a.bin", dtype=np.float32),
+                          np.fromfile(tmp_path / "b.bin", dtype=np.float32)), txt[-400:]
