@@ -96,6 +96,14 @@ def build_parser():
     ap.add_argument("--check-every", type=int, default=0, help="NaN/Inf watchdog period (steps)")
     ap.add_argument("--json", action="store_true", help="also print one JSON metrics line")
     ap.add_argument("--warmup", type=int, default=0, help="untimed warm-up steps")
+    g = ap.add_mutually_exclusive_group()
+    g.add_argument("--graph", dest="graph", action="store_const", const=True, default=None,
+                   help="replay hipGraphs of the steps (default: wherever they are safe)")
+    g.add_argument("--no-graph", dest="graph", action="store_const", const=False,
+                   help="launch every step eagerly (the native apps' --no-graph)")
+    ap.add_argument("--geometry", action="store_true",
+                    help="print this rank's decomposition (owned box, halo messages) as "
+                         "JSON and exit, like the native apps' --geometry")
     return ap
 
 
@@ -182,6 +190,26 @@ def main(argv=None) -> int:
         model, grid, comm, dtype=dtype, ic=ic, overlap=not ns.no_overlap, t0=t0,
         check_every=ns.check_every, decomp=ns.decomp, integrator=ns.integrator,
         kernel=ns.kernel, exchange=ns.exchange))
+    if ns.geometry:  # decomposition only (no steps), one JSON line per rank in rank order
+        geo = {"rank": comm.rank, "world": comm.size, "pgrid": list(solver.pgrid),
+               "global_box": [list(b) for b in solver.cd.global_box()],
+               "owned_box": [list(b) for b in solver.cd.owned_box()],
+               "ghost": solver.cd.ghost}
+        if solver.cart:
+            geo["halo_phases"] = [
+                [{"peer": p, "send": [list(b) for b in sb], "recv": [list(b) for b in rb],
+                  "offset": list(off)} for p, sb, rb, off in solver.halo.boxes(axes)]
+                for axes in solver.halo._phases()]
+        allg = [geo]
+        if comm.size > 1:
+            import torch.distributed as dist
+            allg = [None] * comm.size
+            dist.all_gather_object(allg, geo)
+        if comm.rank == 0:
+            for g in allg:
+                print(json.dumps(g), flush=True)
+        comm.finalize()
+        return 0
     if ns.restart:
         solver.load_checkpoint(ns.restart)
     if ns.initial:
@@ -189,13 +217,13 @@ def main(argv=None) -> int:
     if ns.warmup:
         wt, wi = solver.t, solver.it
         saved = [f.clone() for f in solver.fields()]
-        solver.run(iters=ns.warmup)
+        solver.run(iters=ns.warmup, graph=ns.graph)
         for f, s in zip(solver.fields(), saved):
             f.copy_(s)
         solver.t, solver.it = wt, wi
     if "t_end" in run:
         run = {"t_end": run["t_end"] + (t0 if ic == "heat" else 0.0)}
-    stats = solver.run(**run)
+    stats = solver.run(**run, graph=ns.graph)
     extra = {}
     if ns.error_norms and ic in ("sine", "heat"):
         l1, l2, li = solver.error_norms()

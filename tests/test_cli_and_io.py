@@ -103,6 +103,30 @@ def test_watchdog_catches_an_isolated_nan():
         s.check_finite()
 
 
+def test_cli_geometry_and_graph_flags():
+    """--geometry prints every rank's decomposition as JSON and runs no steps (2 gloo ranks,
+    Cartesian blocks: the halo phases too); --no-graph runs eagerly with the same result."""
+    from multigpu_advectiondiffusion_amd.launch import free_port
+    import os
+    port = free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(
+            [sys.executable, "-m", "multigpu_advectiondiffusion_amd", "diffusion3d", "1", "1", "1",
+             "1", "20", "18", "16", "5", "--device", "cpu", "--decomp", "1x2x1", "--geometry"],
+            env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    lines = [json.loads(l) for l in outs[0].splitlines() if l.startswith("{")]
+    assert [g["rank"] for g in lines] == [0, 1] and lines[0]["pgrid"] == [1, 2, 1]
+    assert lines[0]["halo_phases"] and lines[0]["halo_phases"][0][0]["peer"] == 1
+    assert "Total effective GFLOPs" not in outs[0]
+    assert cli.main(["diffusion3d", "1", "1", "1", "1", "12", "10", "8", "3", "--device", "cpu",
+                     "--no-graph"]) == 0
+
+
 def test_fp32_cpu_path():
     s = Solver(Diffusion(K=1.0), Grid((20, 20, 20), (1.0, 1.0, 1.0)), device="cpu",
                dtype=torch.float32, ic="sine")
