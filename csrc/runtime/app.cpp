@@ -99,12 +99,18 @@ static void apply_config(const std::string& path, std::vector<std::string>& pos,
       if (js[q] != '[') throw std::runtime_error("--config: \"args\" must be a list");
       ++q;
       pos.clear();
-      for (skip(); q < js.size() && js[q] != ']'; skip()) pos.push_back(scalar_at());
+      for (skip(); q < js.size() && js[q] != ']'; skip()) {
+        const size_t q0 = q;
+        pos.push_back(scalar_at());
+        if (q == q0) throw std::runtime_error("--config: bad \"args\" list");
+      }
       ++q;
       continue;
     }
     if (js[q] == '[' || js[q] == '{') throw std::runtime_error("--config: " + key + " must be a scalar");
+    const size_t q0 = q;
     const std::string v = scalar_at();
+    if (q == q0) throw std::runtime_error("--config: bad value of " + key);
     std::replace(key.begin(), key.end(), '_', '-');
     if (v == "false")
       opt.erase("--" + key);

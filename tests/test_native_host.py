@@ -196,3 +196,31 @@ def _check_native_geometry(app, args, world, decomp, extra, corners):
             py = [[{"peer": p, "off": list(k), "send": lst(s), "recv": lst(rr)}
                    for p, s, rr, k in halo.boxes(axes)] for axes in halo._phases()]
             assert nat["halo"] == py, rank
+
+
+def test_native_config_file_host(tmp_path):
+    """bin/* --config FILE.json on the CPU (the file is applied before any device work):
+    a config that carries the positional args and the decomposition gives the same
+    --geometry output as the command line; malformed files fail with a message."""
+    import json
+    import os
+    exe = CSRC.parent / "bin" / "diffusion3d"
+    if not exe.exists():
+        pytest.skip("bin/ not built")
+    env = dict(os.environ, RANK="0", WORLD_SIZE="4")
+    args = ["1", "1", "1", "1", "40", "36", "32", "5"]
+    a = subprocess.run([str(exe), *args, "--decomp", "2x2x1", "--geometry"], env=env,
+                       capture_output=True, text=True, timeout=60)
+    cfg = tmp_path / "c.json"
+    cfg.write_text(json.dumps({"args": [1, 1, 1, 1, 40, 36, 32, 5], "decomp": "2x2x1",
+                               "geometry": True}))
+    b = subprocess.run([str(exe), "--config", str(cfg)], env=env, capture_output=True,
+                       text=True, timeout=60)
+    assert a.returncode == 0 and b.returncode == 0, (a.stdout + a.stderr, b.stdout + b.stderr)
+    assert a.stdout == b.stdout and a.stdout.count("\n") == 4
+    for bad, msg in (('{"args": [1, 2}', 'bad "args" list'), ('{"ic": }', "bad value of ic"),
+                     ('[1, 2]', "not a JSON object"), ('{1: 2}', "expected a key")):
+        cfg.write_text(bad)
+        r = subprocess.run([str(exe), "--config", str(cfg)], env=env, capture_output=True,
+                           text=True, timeout=30)
+        assert r.returncode != 0 and msg in r.stderr, (bad, r.stderr)
