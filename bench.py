@@ -37,10 +37,8 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-from multigpu_advectiondiffusion_amd import Burgers, Diffusion, Grid, Solver  # noqa: E402
-from multigpu_advectiondiffusion_amd.parallel import Comm, weak_scaling_grid  # noqa: E402
-from multigpu_advectiondiffusion_amd.parallel.decomposition import candidate_proc_grids  # noqa: E402
+# (the package is imported inside run(): a self-launching parent, --gpus N without
+# WORLD_SIZE, never touches the GPU)
 
 METRIC = "MLUPS (whole node), 3D diffusion 512^3 + Burgers3D WENO5, 1/2/4/8 MI355X"
 BASE_DIFFUSION = 927.2   # best published 3-D heat MLUPS (SingleGPU/Diffusion3d_Blocking/Run.m:3-12)
@@ -66,14 +64,14 @@ def linf_bound(grid, K: float, t: float, order: int) -> float:
     return 2.0 * frozen + trunc
 
 
-def timed(solver: Solver, steps: int, warmup: int, dt: float) -> float:
+def timed(solver, steps: int, warmup: int, dt: float) -> float:
     if warmup:
         solver.run(iters=warmup, dt=dt)
     st = solver.run(iters=steps, dt=dt)  # barrier + sync on both sides, max over ranks
     return st.compute_s
 
 
-def sustained(solver: Solver, steps: int, dt: float, cells: int) -> dict | None:
+def sustained(solver, steps: int, dt: float, cells: int) -> dict | None:
     """Informational settled-clock rate: `steps` more steps right after the headline
     window, timed the same way (barrier + sync both sides, max over ranks)."""
     if steps <= 0:
@@ -97,20 +95,24 @@ def _fingerprint(s):
     return (s.comm.allreduce_sum(a), s.comm.allreduce_sum(b), s.comm.allreduce_max(c))
 
 
-def tune_decomp(make, cands, dt, dev, trial_steps=3, rounds=3):
-    """Process-grid autotuning (N > 1, outside the timed region): every candidate of
-    parallel.decomposition.candidate_proc_grids (the slab + grids that move fewer bytes
-    over the busiest xGMI link) is built, warmed up by 2 steps, then timed over `rounds`
-    interleaved rounds of `trial_steps` steps (A B C A B C ..., so the chip's power-
-    management clock dip cannot favour whichever grid happens to run first); a grid's
-    time is its best round (max over ranks, so every rank picks the same).  The fastest
-    grid whose solution matches the slab's (global Σ|u|, Σu², max|u| to 1e-10 relative)
-    is used for the timed run.  Returns (grid, {grid: ms/step or a rejection note})."""
+def tune(make, cands, dt, dev, trial_steps=8, rounds=3):
+    """Autotuning of the (process grid, halo transport) pair, N > 1, outside the timed
+    region.  cands = [(pgrid, transport)]: the slab + grids of
+    parallel.decomposition.candidate_proc_grids (fewer bytes over the busiest xGMI link)
+    times the transports that passed their preflight (rccl: grouped RCCL send/recv,
+    stepped eagerly; ipc: device puts, hipGraph-replayed).  Every candidate is built,
+    warmed up by 2 steps, then timed over `rounds` interleaved rounds of `trial_steps`
+    steps (A B C A B C ..., so the chip's power-management clock dip cannot favour
+    whichever runs first; trial_steps = one graph's worth, so graph-replayed candidates
+    are timed as the run will use them); a candidate's time is its best round (max over
+    ranks, so every rank picks the same).  The fastest candidate whose solution matches
+    the first's (global Σ|u|, Σu², max|u| to 1e-10 relative) wins.
+    Returns ((pgrid, transport), {"ZxYxX/transport": ms/step or a rejection note})."""
     if len(cands) == 1:
         return cands[0], {}
     solvers = []
-    for p in cands:
-        s = make(p)
+    for p, t in cands:
+        s = make(p, t)
         s.run(iters=2, dt=dt)
         solvers.append(s)
     best_ms = [float("inf")] * len(cands)
@@ -119,20 +121,68 @@ def tune_decomp(make, cands, dt, dev, trial_steps=3, rounds=3):
             ms = s.run(iters=trial_steps, dt=dt).compute_s / trial_steps * 1e3
             best_ms[i] = min(best_ms[i], ms)
     trials, best, ref = {}, None, None
-    for p, s, ms in zip(cands, solvers, best_ms):
+    for (p, t), s, ms in zip(cands, solvers, best_ms):
         fp = _fingerprint(s)
-        key = "x".join(map(str, p))
+        key = "x".join(map(str, p)) + "/" + t
         if ref is None:
             ref = fp
         elif any(abs(x - y) > 1e-10 * max(abs(y), 1e-300) for x, y in zip(fp, ref)):
-            trials[key] = f"rejected: solution differs from the slab's ({fp} vs {ref})"
+            trials[key] = f"rejected: solution differs from the first candidate's ({fp} vs {ref})"
             continue
         trials[key] = round(ms, 4)
         if best is None or ms < best[0]:
-            best = (ms, p)
+            best = (ms, (p, t))
     del solvers, s
     _free(dev)
     return best[1], trials
+
+
+def transports_for(comm, want: str):
+    """Halo transports to consider (N > 1 on GPUs) and the ipc preflight record.
+    want: "tune" (every transport of this Comm whose preflight passes), or one name."""
+    if comm.size == 1 or comm.device.type != "cuda":
+        return [comm.transport], None
+    names = comm.transports() if want == "tune" else [want]
+    pre = None
+    if "ipc" in names:
+        try:
+            pre = comm.ipc().preflight()
+        except Exception as e:  # noqa: BLE001 - any failure rejects the transport
+            pre = f"failed: {type(e).__name__}: {e}"
+            if comm.rank == 0:
+                print(f"bench: ipc transport rejected ({pre})", file=sys.stderr, flush=True)
+            names = [t for t in names if t != "ipc"]
+            if not names:
+                raise SystemExit(f"bench: the requested ipc transport failed its preflight: {pre}")
+    return names, pre
+
+
+def bitwise_vs_1gpu(make_n, make_1, steps, dt, comm, dev):
+    """N > 1: the timed configuration (fresh solver, same process grid and transport —
+    graph replay included for ipc) and ONE GPU (rank 0's, a single-process solver of the
+    same global grid) run the same `steps` steps; their bit_hash()es (order-independent
+    64-bit hash of every cell's bit pattern with its global index) must agree.  The
+    kernels are bitwise decomposition-invariant, so any difference is a halo or transport
+    error (a stale ghost plane, a lost put) — which a tolerance check against the exact
+    solution could miss.  Returns (equal, {"hash_n", "hash_1"})."""
+    s = make_n()
+    s.run(iters=steps, dt=dt)
+    hn = s.bit_hash()
+    ipc = s._ipc_multi()
+    del s
+    _free(dev)
+    if ipc:
+        comm.ipc().reset()  # the peers unmap the freed fields before rank 0 reallocates
+    h1 = None
+    if comm.rank == 0:
+        s1 = make_1()
+        s1.run(iters=steps, dt=dt)
+        h1 = s1.bit_hash()
+        del s1
+        _free(dev)
+    h1 = comm.broadcast_object(h1)
+    return hn == h1, {"steps": steps, "hash_n": f"{hn & (2**64 - 1):016x}",
+                      "hash_1": f"{h1 & (2**64 - 1):016x}"}
 
 
 def halo_diag(s, reps=5, dt=None):
@@ -173,7 +223,7 @@ def halo_diag(s, reps=5, dt=None):
             "step_ms_without_exchange": round(nohalo, 4)}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -188,6 +238,10 @@ def main():
                     help="process grid: 'tune' (default: the fastest of the candidate grids "
                          "measured over a few steps; the slab on 1 GPU), 'slab', 'auto' or "
                          "PZxPYxPX")
+    ap.add_argument("--transport", default="tune",
+                    help="halo transport for N > 1: 'tune' (default: every transport that "
+                         "passes its preflight, the fastest measured), 'rccl', 'ipc' or "
+                         "'host'")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: base^3 cells per GPU (default); strong: the 8-GPU grid "
                          "(2*base)^3 on any N")
@@ -195,13 +249,57 @@ def main():
     ap.add_argument("--sustained-steps", type=int, default=200,
                     help="extra steps timed after the headline window (informational "
                          "'sustained' fields; 0 = off)")
-    args = ap.parse_args()
+    ap.add_argument("--check-steps", type=int, default=10,
+                    help="N > 1: steps of the bitwise N-rank vs 1-GPU check (0 = off)")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="self-launch (--gpus N > 1 without WORLD_SIZE): wall-clock limit "
+                         "of the N ranks, seconds")
+    return ap.parse_args(argv)
+
+
+def self_launch(args) -> int:
+    """--gpus N > 1 without a launcher: start N ranks of this script ourselves (fresh
+    subprocesses with the torchrun environment, before this process touches the GPU;
+    never an exec) and return the first failing rank's exit code.  Rank 0 prints the
+    JSON line."""
+    from multigpu_advectiondiffusion_amd.launch import launch_cmd
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    rc = launch_cmd(args.gpus, cmd, timeout=args.launch_timeout)
+    if rc != 0:
+        print(f"bench: {args.gpus}-rank run failed (exit {rc})", file=sys.stderr, flush=True)
+    return rc
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    # a dead peer must end an ipc wait well before the driver's clock does
+    os.environ.setdefault("ADVDIFF_IPC_TIMEOUT_S", "60")
+    world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if world == 0 and args.gpus > 1:
+        return self_launch(args)
+    if world and world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+              f"{world}-rank run as {args.gpus} GPUs", file=sys.stderr, flush=True)
+        return 2
+    run(args)
+    return 0
+
+
+def run(args):
+    from multigpu_advectiondiffusion_amd import Burgers, Diffusion, Grid, Solver
+    from multigpu_advectiondiffusion_amd.parallel import Comm, weak_scaling_grid
+    from multigpu_advectiondiffusion_amd.parallel.decomposition import candidate_proc_grids
 
     comm = Comm.from_env(device=args.device)
     n = comm.size
-    if args.gpus != n and comm.rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={n}; using {n}", file=sys.stderr)
+    if n != args.gpus:
+        raise SystemExit(f"bench: world {n} != --gpus {args.gpus}")
     dev = comm.device
+    single = Comm(device=str(dev)) if dev.type == "cuda" else Comm(device="cpu")
+    transports, preflight = transports_for(comm, args.transport)
+
+    def cands_of(grids):
+        return [(p, t) for p in grids for t in transports]
 
     # ---- headline: 3-D heat, FD4, fp64, sine IC -------------------------------------
     grid_of = ((lambda b: weak_scaling_grid(b, n)) if args.scaling == "weak"
@@ -212,17 +310,17 @@ def main():
     model.bind(grid)
     dt = model.stable_dt()
 
-    def make_heat(p):
-        return Solver(model, grid, comm, dtype=torch.float64, ic="sine",
-                      overlap=not args.no_overlap, decomp=p)
+    def make_heat(p, t, m=model, c=comm):
+        return Solver(m, grid, c, dtype=torch.float64, ic="sine",
+                      overlap=not args.no_overlap, decomp=p, transport=t)
 
     ashape = tuple(reversed(shape))
     if args.decomp == "tune":
-        cands = candidate_proc_grids(n, ashape, 3 * model.radius, 8, corners=True)
-        decomp, trials = tune_decomp(make_heat, cands, dt, dev)
+        grids = candidate_proc_grids(n, ashape, 3 * model.radius, 8, corners=True)
     else:
-        decomp, trials = (None if args.decomp == "slab" else args.decomp), {}
-    solver = make_heat(decomp)
+        grids = [None if args.decomp == "slab" else args.decomp]
+    (decomp, transport), trials = tune(make_heat, cands_of(grids), dt, dev)
+    solver = make_heat(decomp, transport)
     secs = timed(solver, args.steps, args.warmup, dt)
     mlups = grid.cells * args.steps / secs / 1e6
     sust = sustained(solver, args.sustained_steps, dt, grid.cells)
@@ -237,9 +335,18 @@ def main():
     bound = linf_bound(grid, model.K, t_end, 4)
     if not linf <= bound:
         raise SystemExit(f"bench validation failed: L_inf vs exact = {linf:.3e} > {bound:.3e}")
+    checks = {}
+    if n > 1 and args.check_steps > 0:
+        ok, rec = bitwise_vs_1gpu(lambda: make_heat(decomp, transport),
+                                  lambda: make_heat(None, None, c=single),
+                                  args.check_steps, dt, comm, dev)
+        checks["heat"] = {"bitwise": ok, **rec}
+        if not ok:
+            raise SystemExit(f"bench validation failed: {n}-rank heat solution differs from "
+                             f"the 1-GPU solution ({rec})")
 
-    link = ("ipc device puts" if comm.transport == "ipc" and n > 1 else
-            "RCCL" if comm.backend == "nccl" else str(comm.backend))
+    link = {"ipc": "ipc device puts", "rccl": "RCCL", "host": "host-staged"}.get(transport,
+                                                                                 transport)
     result = {
         "metric": METRIC,
         "value": round(mlups, 1),
@@ -264,24 +371,26 @@ def main():
         "linf_vs_exact": float(f"{linf:.3e}"),
         "linf_bound": float(f"{bound:.3e}"),
         "t_end": t_end,
-        "rccl_world": n,
-        "decomp_trials_ms_per_step": trials,
+        "halo_transport": transport if n > 1 else None,
+        "rccl_world": comm.rccl_world,
+        "transport_trials_ms_per_step": trials,
+        **({"ipc_preflight": preflight} if preflight is not None else {}),
         **diag,
         "comm_backend": comm.backend or "none (single process)",
         "device_ids": comm.device_ids(),
     }
+    if n > 1:
+        result["bitwise_vs_1gpu"] = {"heat": checks.get("heat", {}).get("bitwise")}
 
     # ---- the 7-point (FD2) Laplacian named by BASELINE.json, same grid ----------------
     if not args.no_fd2:
         m2 = Diffusion(K=1.0, order=2)
-        s2 = Solver(m2, grid, comm, dtype=torch.float64, ic="sine",
-                    overlap=not args.no_overlap, decomp=decomp)
+        s2 = make_heat(decomp, transport, m=m2)
         secs2 = timed(s2, args.steps, args.warmup, m2.stable_dt())
         _, _, linf2 = s2.error_norms()
         bound2 = linf_bound(grid, m2.K, s2.t, 2)
         del s2
-        if dev.type == "cuda":
-            torch.cuda.empty_cache()
+        _free(dev)
         if not linf2 <= bound2:
             raise SystemExit(f"bench validation failed: FD2 L_inf vs exact = {linf2:.3e} "
                              f"> {bound2:.3e}")
@@ -300,28 +409,40 @@ def main():
         bmodel.bind(bgrid)
         bdt = bmodel.stable_dt()
 
-        def make_burgers(p):
-            return Solver(bmodel, bgrid, comm, dtype=torch.float64, ic="gaussian",
-                          overlap=not args.no_overlap, decomp=p)
+        def make_burgers(p, t, c=comm):
+            return Solver(bmodel, bgrid, c, dtype=torch.float64, ic="gaussian",
+                          overlap=not args.no_overlap, decomp=p, transport=t)
         if args.decomp == "tune":
-            bc = candidate_proc_grids(n, tuple(reversed(bshape)), bmodel.radius, 8)
-            bdecomp, btrials = tune_decomp(make_burgers, bc, bdt, dev)
+            bgrids = candidate_proc_grids(n, tuple(reversed(bshape)), bmodel.radius, 8)
         else:
-            bdecomp, btrials = (None if args.decomp == "slab" else args.decomp), {}
-        bsolver = make_burgers(bdecomp)
+            bgrids = [None if args.decomp == "slab" else args.decomp]
+        (bdecomp, btransport), btrials = tune(make_burgers, cands_of(bgrids), bdt, dev)
+        bsolver = make_burgers(bdecomp, btransport)
         bsteps = args.burgers_steps or args.steps
-        bsecs = timed(bsolver, bsteps, args.warmup, bmodel.stable_dt())
+        bsecs = timed(bsolver, bsteps, args.warmup, bdt)
         bml = bgrid.cells * bsteps / bsecs / 1e6
-        bsust = sustained(bsolver, args.sustained_steps, bmodel.stable_dt(), bgrid.cells)
+        bsust = sustained(bsolver, args.sustained_steps, bdt, bgrid.cells)
         bsolver.check_finite()
+        bpg = list(bsolver.pgrid)
+        del bsolver
+        _free(dev)
         result["burgers3d"] = {"value": round(bml, 1), "unit": "MLUPS", "grid": list(bshape),
                                "steps": bsteps, "ms_per_step": round(bsecs / bsteps * 1e3, 4),
                                "vs_baseline": round(bml / BASE_BURGERS, 2),
                                "model": "burgers3d WENO5-Z + FD4 viscous (C=1e-5) + SSP-RK3",
-                               "pgrid": list(bsolver.pgrid),
-                               "decomp_trials_ms_per_step": btrials,
+                               "pgrid": bpg,
+                               "halo_transport": btransport if n > 1 else None,
+                               "transport_trials_ms_per_step": btrials,
                                **({"sustained": bsust} if bsust else {})}
-        del bsolver
+        if n > 1 and args.check_steps > 0:
+            ok, rec = bitwise_vs_1gpu(lambda: make_burgers(bdecomp, btransport),
+                                      lambda: make_burgers(None, None, c=single),
+                                      args.check_steps, bdt, comm, dev)
+            result["burgers3d"]["bitwise_check"] = rec
+            result["bitwise_vs_1gpu"]["burgers3d"] = ok
+            if not ok:
+                raise SystemExit(f"bench validation failed: {n}-rank Burgers solution "
+                                 f"differs from the 1-GPU solution ({rec})")
 
     if comm.rank == 0:
         print(json.dumps(result), flush=True)
@@ -329,4 +450,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

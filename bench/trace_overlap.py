@@ -1,17 +1,36 @@
 #!/usr/bin/env python3
-"""Overlap of the halo puts with the stencil launches, per rank, from a rocprofv3 kernel
-trace (`--kernel-trace --output-format csv`) of a multi-rank native run (ranks told apart
-by the launching thread): for every put kernel (`advdiff_copy_box` into a neighbour's
-ghost box) of a rank, how much of it ran while the SAME rank's step kernel was running.
-The wait kernels are left out: their duration is the time spent waiting for the peer.
+"""Overlap of the halo puts with the stencil launches, per rank, from rocprofv3 kernel
+traces (`--kernel-trace --output-format csv`) of a multi-rank run: for every put kernel
+(`ipc_put_kernel` / `advdiff_copy_box` into a neighbour's ghost box) of a rank, how much of
+it ran while the SAME rank's step (or stage) kernel was running.  The wait kernels are
+left out: their duration is the time spent waiting for the peer.
 
-    python bench/trace_overlap.py <dir with *kernel_trace.csv> [--md out.md]
+Ranks are told apart by their per-rank trace directory (`launch.py --profile DIR` writes
+DIR/rank<r>/..., like the reference's `nvprof -o X.%q{OMPI_COMM_WORLD_RANK}.nvprof`,
+`MultiGPU/Diffusion3d_Baseline/run.sh:2`), or — one trace of the whole launcher — by the
+launching thread.
+
+    python bench/trace_overlap.py <dir with */*kernel_trace.csv> [--md out.md]
 """
 import argparse
 import csv
 import glob
 import os
+import re
 from collections import defaultdict
+
+
+def _rank_of(path, row):
+    m = re.search(r"[/\\]rank(\d+)[/\\]", path)
+    return f"rank {m.group(1)}" if m else f"thread {row['Thread_Id']}"
+
+
+def _is_put(name):
+    return "ipc_put" in name or "copy_box" in name
+
+
+def _is_step(name):
+    return ("step_kernel" in name or "stage" in name or "_step" in name) and not _is_put(name)
 
 
 def main():
@@ -19,18 +38,16 @@ def main():
     ap.add_argument("root")
     ap.add_argument("--md", default=None)
     a = ap.parse_args()
-    rows = []
-    for f in glob.glob(os.path.join(a.root, "**", "*kernel_trace.csv"), recursive=True):
-        rows += list(csv.DictReader(open(f)))
     by_rank = defaultdict(list)
-    for r in rows:
-        by_rank[r["Thread_Id"]].append(
-            (int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
-    out = ["| rank (thread) | step launches | mean step µs | put kernels | put µs | of which beside the rank's own step launch |",
+    for f in glob.glob(os.path.join(a.root, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            by_rank[_rank_of(f, r)].append(
+                (int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    out = ["| rank | step launches | mean step µs | put kernels | put µs | of which beside the rank's own step launch |",
            "|---|---|---|---|---|---|"]
     for tid, ks in sorted(by_rank.items()):
-        steps = [(s, e) for s, e, n in ks if "step_kernel" in n]
-        puts = [(s, e) for s, e, n in ks if "copy_box" in n]
+        steps = [(s, e) for s, e, n in ks if _is_step(n)]
+        puts = [(s, e) for s, e, n in ks if _is_put(n)]
         if not steps or not puts:
             continue
         tot = sum(e - s for s, e in puts)

@@ -207,8 +207,8 @@ int advdiff_set_b2_ver(int v);
 
 // ---------------------------------------------------------------------------------
 // Peer transport of one node (ipc.hip): hipIpc-mapped device memory + device flags.  A
-// rank puts boundary cells straight into a neighbour's ghost cells (advdiff_copy_box with
-// a mapped destination), raises the neighbour's flag (advdiff_ipc_signal) and makes its
+// rank puts boundary cells straight into a neighbour's ghost cells (advdiff_ipc_put: a box
+// copy with system-scope stores into a mapped destination), raises the neighbour's flag (advdiff_ipc_signal) and makes its
 // stream wait for its own flags (advdiff_ipc_wait).  All stream-ordered kernels: no host
 // synchronisation, hipGraph-capturable.  Works across the GPUs of a node (xGMI) and
 // between several processes on one GPU.
@@ -224,6 +224,8 @@ int advdiff_ipc_describe(advdiff_ipc* c, const void* ptr, advdiff_ipc_addr* out)
 int advdiff_ipc_flags_addr(advdiff_ipc* c, advdiff_ipc_addr* out);
 int advdiff_ipc_map(advdiff_ipc* c, const advdiff_ipc_addr* a, void** ptr);
 int advdiff_ipc_set_peer(advdiff_ipc* c, int peer, const advdiff_ipc_addr* peer_flags);
+int advdiff_ipc_put(int dtype, void* dst, int64_t dsy, int64_t dsz, const void* src,
+                    int64_t ssy, int64_t ssz, int ni, int nj, int nk, void* stream);
 int advdiff_ipc_signal(advdiff_ipc* c, const int* peers, int n, void* stream);
 int advdiff_ipc_wait(advdiff_ipc* c, const int* peers, int n, void* stream);
 // close every peer mapping except the flag blocks (collective, no put in flight): after

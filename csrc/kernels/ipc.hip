@@ -1,6 +1,6 @@
 // Peer-to-peer transport primitives of one node: hipIpc-mapped device memory + device-side
 // flags.  This is the P2PComm of SURVEY.md §7.1 ("peer-mapped xGMI puts"): a rank writes
-// its boundary cells STRAIGHT INTO the neighbour's ghost cells (a copy kernel whose
+// its boundary cells STRAIGHT INTO the neighbour's ghost cells (a put kernel whose
 // destination is the neighbour's field, mapped into this process with
 // hipIpcOpenMemHandle), then raises the neighbour's flag with a release store; the
 // neighbour's stream waits on its own flag with an acquire spin.  Every step of an
@@ -14,11 +14,35 @@
 // a peer mapping); with several ranks on ONE GPU (the test configuration of a 1-GPU box,
 // where RCCL refuses two ranks per device) the same code runs as same-device IPC.
 //
+// Memory ordering of one message (producer P -> consumer C), each link explicit:
+//  1. put (ipc_put_kernel, P's comm stream): every remote store is a SYSTEM-scope store
+//     (global_store ... sc0 sc1: written through P's L2 to C's memory, never parked as a
+//     dirty non-coherent line in the L2 of whichever XCD ran the wave), and each wave
+//     ends with s_waitcnt vmcnt(0), so the dispatch completes
+//     only after its stores are acknowledged.  Nothing depends on the scope of the
+//     dispatch's end-of-kernel cache action, nor on which XCD runs the signal.
+//  2. signal (ipc_signal_kernel, same stream => after the put dispatch completed): a
+//     system-scope RELEASE store of the message counter into C's flag block (uncached
+//     memory, coherent across devices while kernels run).
+//  3. wait (ipc_wait_kernel, C's comm stream): kIpcWaitWgs workgroups, dispatched
+//     round-robin over the 8 XCDs (>= 2 per XCD), each spin until the counter arrives with
+//     system-scope ACQUIRE loads and then issue a system-scope acquire fence
+//     (buffer_inv sc0 sc1) — so EVERY XCD's L2 drops lines of the ghost box it may hold
+//     from the previous step before any consumer reads them.  (A single-lane wait would
+//     invalidate only its own XCD's L2.)
+//  4. consume: C's compute stream waits for the comm stream's event; the consumer kernel
+//     starts after the wait dispatch completed, with fresh L1s.
+// Ranks that share one GPU share one L2/MALL, so tests on a 1-GPU box cannot expose a
+// missing link; the bench's ipc preflight (IpcPeers.preflight: stale-cache pattern round
+// trips between every pair of ranks) and its bitwise N-rank-vs-1-GPU check can.
+//
 // Flags block of a rank (device memory, exported): recv[world] (written by the peers: the
 // number of messages peer q has delivered), sent[world] (messages delivered to q, local),
-// expect[world] (messages consumed from q, local), err (wait timeouts).
+// expect[world][kIpcWaitWgs] (messages consumed from q, per wait workgroup), err (wait
+// timeouts).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -27,6 +51,7 @@
 #include <vector>
 
 #include "advdiff/kernels.h"
+#include "launch.hpp"
 
 struct advdiff_ipc {
   int world = 1, rank = 0;
@@ -35,15 +60,17 @@ struct advdiff_ipc {
   std::map<std::string, void*> opened;  // IPC handle bytes -> mapped base
   std::map<uintptr_t, hipIpcMemHandle_t> exported;  // allocation base -> handle
   std::mutex mu;
+  size_t block_bytes = 0;
   uint64_t* recv() const { return block; }
   uint64_t* sent() const { return block + world; }
-  uint64_t* expect() const { return block + 2 * world; }
-  unsigned long long* err() const { return (unsigned long long*)(block + 3 * world); }
+  uint64_t* expect() const { return block + 2 * world; }  // [world][kIpcWaitWgs]
+  unsigned long long* err() const;
 };
 
 namespace advdiff {
 
 constexpr int kIpcMaxPeers = 32;  // 3^3 - 1 = 26 neighbours of a direct exchange
+constexpr int kIpcWaitWgs = 16;   // wait workgroups: >= 2 per XCD (8 XCDs, round-robin)
 
 struct IpcSignalArgs {
   uint64_t* remote[kIpcMaxPeers];  // peer's recv[rank]
@@ -53,14 +80,33 @@ struct IpcSignalArgs {
 
 struct IpcWaitArgs {
   const uint64_t* flag[kIpcMaxPeers];  // own recv[peer]
-  uint64_t* expect[kIpcMaxPeers];      // own expect[peer]
+  uint64_t* expect[kIpcMaxPeers];      // own expect[peer][0..kIpcWaitWgs)
   int n;
   unsigned long long* err;
   uint64_t timeout_ticks;  // s_memrealtime runs at 100 MHz
 };
 
+// The put (link 1 above): dst box (peer memory) <- src box (own field), one row of ni
+// elements per (blockIdx.y, blockIdx.z), every store system-scope.  Elements move as
+// 32/64-bit words (bit-exact for any dtype).
+template <typename W>
+__global__ void ipc_put_kernel(W* __restrict__ dst, int64_t dsy, int64_t dsz,
+                               const W* __restrict__ src, int64_t ssy, int64_t ssz, int ni,
+                               int nj) {
+  const int j = blockIdx.y;
+  const int k = blockIdx.z;
+  if (j < nj) {
+    const W* s = src + (int64_t)k * ssz + (int64_t)j * ssy;
+    W* d = dst + (int64_t)k * dsz + (int64_t)j * dsy;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ni; i += gridDim.x * blockDim.x)
+      __hip_atomic_store(d + i, s[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // every store of this wave acknowledged before the wave (and so the dispatch) ends
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
 // lane q: sent[q] += 1, then publish it to the peer with a system-scope release store
-// (the puts before it on this stream are complete and written back by then)
+// (link 2: the put dispatch before it on this stream has completed)
 __global__ void ipc_signal_kernel(IpcSignalArgs a) {
   const int q = threadIdx.x;
   if (q >= a.n) return;
@@ -71,25 +117,34 @@ __global__ void ipc_signal_kernel(IpcSignalArgs a) {
   __hip_atomic_store(a.remote[q], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// lane q: expect[q] += 1, then spin (acquire loads, s_sleep) until recv[q] reaches it.
+// Link 3.  Workgroup w, lane q: expect[q][w] += 1 (each workgroup its own counter, so no
+// workgroup can see another's increment), spin (acquire loads, s_sleep) until recv[q]
+// reaches it, then a system-scope acquire fence invalidates this XCD's caches.
 // Bounded: after timeout_ticks the lane records a timeout and leaves, so the grid always
 // drains even if a peer died (the host checks advdiff_ipc_errors at its sync points).
 // Ranks SHARING one GPU (tests) need every queue of every rank mapped by the hardware
-// scheduler: a spinning wait on a mapped queue can starve a producer whose queue is not
-// (oversubscribed HWS) — run them with few hardware queues (GPU_MAX_HW_QUEUES=1).
+// scheduler: a spinning wait on a mapped queue can starve a producer whose queue is not.
+// The tests and scripts run them with GPU_MAX_HW_QUEUES=2: 1 serialises a rank's own
+// compute and comm streams onto one queue (the Python path then deadlocks: the comm
+// stream's spin blocks the compute kernels queued behind it), and the default 4 per
+// process oversubscribes the scheduler with 4+ ranks (a spinning queue starves a peer).
 __global__ void ipc_wait_kernel(IpcWaitArgs a) {
   const int q = threadIdx.x;
-  if (q >= a.n) return;
-  const uint64_t e = __hip_atomic_load(a.expect[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  __hip_atomic_store(a.expect[q], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(a.flag[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-    __builtin_amdgcn_s_sleep(4);
-    if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-      atomicAdd(a.err, 1ull);
-      break;
+  const int w = blockIdx.x;
+  if (q < a.n) {
+    uint64_t* ex = a.expect[q] + w;
+    const uint64_t e = __hip_atomic_load(ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    __hip_atomic_store(ex, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(a.flag[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      __builtin_amdgcn_s_sleep(4);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+        atomicAdd(a.err, 1ull);
+        break;
+      }
     }
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: buffer_inv sc0 sc1
 }
 
 static uint64_t wait_timeout_ticks() {
@@ -103,17 +158,22 @@ static uint64_t wait_timeout_ticks() {
 
 }  // namespace advdiff
 
+unsigned long long* advdiff_ipc::err() const {
+  return (unsigned long long*)(block + 2 * world + (size_t)world * advdiff::kIpcWaitWgs);
+}
+
 extern "C" int advdiff_ipc_create(int world, int rank, advdiff_ipc** out) {
   if (world < 1 || rank < 0 || rank >= world || out == nullptr) return hipErrorInvalidValue;
   auto* c = new advdiff_ipc;
   c->world = world;
   c->rank = rank;
   c->peer_cell.assign(world, nullptr);
-  const size_t bytes = (3 * (size_t)world + 1) * sizeof(uint64_t);
+  const size_t bytes = ((2 + (size_t)advdiff::kIpcWaitWgs) * world + 1) * sizeof(uint64_t);
+  c->block_bytes = bytes < 4096 ? 4096 : bytes;
   // Uncached device memory: a peer GPU's release store lands in this block WHILE the wait
   // kernel spins on it, and only fine-grained / uncached memory promises cross-device
   // coherence inside a dispatch (coarse-grained memory only at dispatch boundaries).
-  hipError_t e = hipExtMallocWithFlags((void**)&c->block, bytes < 4096 ? 4096 : bytes,
+  hipError_t e = hipExtMallocWithFlags((void**)&c->block, c->block_bytes,
                                        hipDeviceMallocUncached);
   if (e == hipSuccess) e = hipMemset(c->block, 0, bytes);
   if (e == hipSuccess) e = hipDeviceSynchronize();  // setup only: zeroed before any peer maps it
@@ -204,6 +264,31 @@ extern "C" int advdiff_ipc_set_peer(advdiff_ipc* c, int peer, const advdiff_ipc_
   return hipSuccess;
 }
 
+// the put of link 1: like advdiff_copy_box, but every store is system-scope (dst is a peer
+// mapping).  Elements are moved as 64-bit words when the element size, both bases and all
+// strides allow it, else as 32-bit words.
+extern "C" int advdiff_ipc_put(int dtype, void* dst, int64_t dsy, int64_t dsz, const void* src,
+                               int64_t ssy, int64_t ssz, int ni, int nj, int nk, void* stream) {
+  using namespace advdiff;
+  if (ni <= 0 || nj <= 0 || nk <= 0) return hipSuccess;
+  if (dtype != ADVDIFF_F64 && dtype != ADVDIFF_F32) return hipErrorInvalidValue;
+  if (nj > 65535 || nk > 65535) return hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const int esz = dtype == ADVDIFF_F64 ? 8 : 4;
+  const bool w64 = esz == 8 || (((uintptr_t)dst | (uintptr_t)src) % 8 == 0 && ni % 2 == 0 &&
+                                dsy % 2 == 0 && dsz % 2 == 0 && ssy % 2 == 0 && ssz % 2 == 0);
+  const int f = w64 ? 8 / esz : 1;  // elements per word
+  const int wi = ni / f;
+  dim3 block(256), grid(std::min(div_up(wi, 256), 8), nj, nk);
+  if (w64)
+    hipLaunchKernelGGL(ipc_put_kernel<uint64_t>, grid, block, 0, st, (uint64_t*)dst, dsy / f,
+                       dsz / f, (const uint64_t*)src, ssy / f, ssz / f, wi, nj);
+  else
+    hipLaunchKernelGGL(ipc_put_kernel<uint32_t>, grid, block, 0, st, (uint32_t*)dst, dsy, dsz,
+                       (const uint32_t*)src, ssy, ssz, wi, nj);
+  return hipGetLastError();
+}
+
 extern "C" int advdiff_ipc_signal(advdiff_ipc* c, const int* peers, int n, void* stream) {
   using namespace advdiff;
   if (n <= 0) return hipSuccess;
@@ -232,9 +317,9 @@ extern "C" int advdiff_ipc_wait(advdiff_ipc* c, const int* peers, int n, void* s
     const int p = peers[q];
     if (p < 0 || p >= c->world || p == c->rank) return hipErrorInvalidValue;
     a.flag[q] = c->recv() + p;
-    a.expect[q] = c->expect() + p;
+    a.expect[q] = c->expect() + (size_t)p * kIpcWaitWgs;
   }
-  hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(ipc_wait_kernel, dim3(kIpcWaitWgs), dim3(64), 0, (hipStream_t)stream, a);
   return hipGetLastError();
 }
 
@@ -247,8 +332,10 @@ extern "C" int advdiff_ipc_reset(advdiff_ipc* c) {
   std::lock_guard<std::mutex> g(c->mu);
   for (auto it = c->opened.begin(); it != c->opened.end();) {
     bool flags = false;  // a peer's flag block: keep it (the counters live there)
+    // (a peer's block is as large as ours: same world size)
     for (uint64_t* cell : c->peer_cell)
-      if (cell && (char*)cell >= (char*)it->second && (char*)cell < (char*)it->second + 4096)
+      if (cell && (char*)cell >= (char*)it->second &&
+          (char*)cell < (char*)it->second + c->block_bytes)
         flags = true;
     if (flags) {
       ++it;

@@ -462,8 +462,8 @@ class IpcTransport final : public Transport {
     if (dry_) return;  // handshake only
     for (size_t q = 0; q < msgs.size(); ++q) {  // the put: my box -> the peer's ghost box
       const BoxMsg& m = msgs[q];
-      KERNEL_CHECK(advdiff_copy_box(m.dtype, dst[q].ptr, dst[q].sy, dst[q].sz, m.send, m.ssy,
-                                    m.ssz, m.ni, m.nj, m.nk, s));
+      KERNEL_CHECK(advdiff_ipc_put(m.dtype, dst[q].ptr, dst[q].sy, dst[q].sz, m.send, m.ssy,
+                                   m.ssz, m.ni, m.nj, m.nk, s));
     }
     ipc_check(advdiff_ipc_signal(ctx_, peers.data(), (int)peers.size(), s), "advdiff_ipc_signal");
     ipc_check(advdiff_ipc_wait(ctx_, peers.data(), (int)peers.size(), s), "advdiff_ipc_wait");

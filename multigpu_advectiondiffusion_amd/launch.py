@@ -8,6 +8,13 @@ Two entry points:
   torchrun environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1,
   MASTER_PORT) — one process per GPU; ``--cpu`` runs P gloo ranks on the CPU (the
   oversubscription / no-cluster test mode of SURVEY.md §4, done properly).
+* ``--profile DIR``: every rank runs under its own profiler, ``rocprofv3 --kernel-trace
+  --output-format csv -d DIR/rank<r> -- <rank command>`` (the reference profiles each MPI
+  rank into its own file: ``nvprof -o X.%q{OMPI_COMM_WORLD_RANK}.nvprof``,
+  `MultiGPU/Diffusion3d_Baseline/run.sh:2`, `profile.sh:1-2`); bench/trace_overlap.py
+  reads the per-rank directories.
+* ``launch_cmd(P, cmd)``: the same fail-fast supervision for any command (bench.py
+  self-launches its ranks with it).
 * API: ``spawn_local(world, fn, *args)`` runs ``fn(comm, *args)`` in `world` fresh
   processes with an initialised process group and returns the per-rank results — used
   by the multi-rank tests.
@@ -65,26 +72,34 @@ def _child_env(rank: int, world: int, port: int, cpu: bool) -> dict:
     return env
 
 
-def launch(np_: int, argv: list[str], cpu: bool = False, timeout: float | None = None,
-           poll_s: float = 0.2, native: bool = False) -> int:
-    """Run P ranks; fail fast: the first rank that exits non-zero (or the wall-clock
+def profiled(cmd: list, profile_dir: str, rank: int) -> list:
+    """`cmd` under its own rocprofv3 kernel trace in profile_dir/rank<r> (the program
+    itself right after `--`: no env/shell hop the profiler's preload would exec through)."""
+    import shutil
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    return [prof, "--kernel-trace", "--output-format", "csv", "-d",
+            os.path.join(profile_dir, f"rank{rank}"), "--"] + list(cmd)
+
+
+def launch_cmd(np_: int, cmd, cpu: bool = False, timeout: float | None = None,
+               poll_s: float = 0.2, port: int | None = None,
+               profile_dir: str | None = None, extra_env: dict | None = None) -> int:
+    """Run `cmd` (a list, or a callable rank -> list) as P ranks with the torchrun
+    environment; fail fast: the first rank that exits non-zero (or the wall-clock
     `timeout`, rc 124) terminates the others, so a crashed rank never leaves its peers
-    blocked in a halo exchange until the collective timeout.  Returns the first
-    non-zero exit code (0 if all succeed)."""
+    blocked in a halo exchange until the collective timeout.  Returns the first non-zero
+    exit code (0 if all succeed).  The ranks are fresh subprocesses (never an exec)."""
     import time
-    # native ranks listen on MASTER_PORT+17 (rendezvous) and MASTER_PORT+18+i (socket mesh)
-    port = free_port_block(np_ + 18) if native else free_port()
-    if native:  # the C++ executables: bin/<app> <args...> (RCCL or --transport socket)
-        from pathlib import Path
-        exe = Path(__file__).resolve().parent.parent / "bin" / argv[0]
-        if not exe.exists():
-            raise FileNotFoundError(f"{exe} not built (make -C csrc apps)")
-        cmd = [str(exe)] + argv[1:]
-    else:
-        cmd = [sys.executable, "-m", "multigpu_advectiondiffusion_amd"] + argv
-    if cpu and not native and "--device" not in argv:
-        cmd += ["--device", "cpu"]
-    procs = [subprocess.Popen(cmd, env=_child_env(r, np_, port, cpu)) for r in range(np_)]
+    port = port or free_port()
+    procs = []
+    for r in range(np_):
+        c = cmd(r) if callable(cmd) else list(cmd)
+        if profile_dir:
+            c = profiled(c, profile_dir, r)
+        env = _child_env(r, np_, port, cpu)
+        if extra_env:
+            env.update(extra_env)
+        procs.append(subprocess.Popen(c, env=env))
     deadline = None if timeout is None else time.monotonic() + timeout
     rc = 0
     try:
@@ -113,6 +128,26 @@ def launch(np_: int, argv: list[str], cpu: bool = False, timeout: float | None =
             except subprocess.TimeoutExpired:
                 p.kill()
     return rc
+
+
+def launch(np_: int, argv: list[str], cpu: bool = False, timeout: float | None = None,
+           poll_s: float = 0.2, native: bool = False, profile_dir: str | None = None) -> int:
+    """Run P ranks of the Python front end (or, native=True, of bin/<app>); see
+    launch_cmd.  Returns the first non-zero exit code (0 if all succeed)."""
+    # native ranks listen on MASTER_PORT+17 (rendezvous) and MASTER_PORT+18+i (socket mesh)
+    port = free_port_block(np_ + 18) if native else free_port()
+    if native:  # the C++ executables: bin/<app> <args...> (RCCL or --transport socket)
+        from pathlib import Path
+        exe = Path(__file__).resolve().parent.parent / "bin" / argv[0]
+        if not exe.exists():
+            raise FileNotFoundError(f"{exe} not built (make -C csrc apps)")
+        cmd = [str(exe)] + argv[1:]
+    else:
+        cmd = [sys.executable, "-m", "multigpu_advectiondiffusion_amd"] + argv
+    if cpu and not native and "--device" not in argv:
+        cmd += ["--device", "cpu"]
+    return launch_cmd(np_, cmd, cpu=cpu, timeout=timeout, poll_s=poll_s, port=port,
+                      profile_dir=profile_dir)
 
 
 # ----------------------------------------------------------------------------------
@@ -175,9 +210,12 @@ def main(argv=None) -> int:
     ap.add_argument("--timeout", type=float, default=None)
     ap.add_argument("--native", action="store_true",
                     help="run the native executable bin/<app> instead of the Python front end")
+    ap.add_argument("--profile", default=None, metavar="DIR",
+                    help="run every rank under its own rocprofv3 kernel trace in DIR/rank<r>")
     ap.add_argument("rest", nargs=argparse.REMAINDER)
     ns = ap.parse_args(argv)
-    return launch(ns.nproc, ns.rest, cpu=ns.cpu, timeout=ns.timeout, native=ns.native)
+    return launch(ns.nproc, ns.rest, cpu=ns.cpu, timeout=ns.timeout, native=ns.native,
+                  profile_dir=ns.profile)
 
 
 if __name__ == "__main__":

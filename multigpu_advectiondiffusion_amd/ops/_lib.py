@@ -94,6 +94,8 @@ _IPC_SIGS = {
     "advdiff_ipc_flags_addr": [c_vp, ctypes.POINTER(IpcAddr)],
     "advdiff_ipc_map": [c_vp, ctypes.POINTER(IpcAddr), ctypes.POINTER(c_vp)],
     "advdiff_ipc_set_peer": [c_vp, c_int, ctypes.POINTER(IpcAddr)],
+    "advdiff_ipc_put": [c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int,
+                        c_vp],
     "advdiff_ipc_signal": [c_vp, ctypes.POINTER(c_int), c_int, c_vp],
     "advdiff_ipc_wait": [c_vp, ctypes.POINTER(c_int), c_int, c_vp],
     "advdiff_ipc_errors": [c_vp, ctypes.POINTER(ctypes.c_longlong)],

@@ -71,6 +71,18 @@ class Comm:
             raise ValueError("transport must be ipc, rccl or host")
         self._transport = v
 
+    @property
+    def rccl_world(self) -> int:
+        """Ranks of the RCCL communicator (0 when the process group is not nccl)."""
+        return self.size if (self.size > 1 and self.backend == "nccl") else 0
+
+    def transports(self) -> list:
+        """Halo transports of device fields available on this Comm, the default first."""
+        if self.size == 1 or self.device.type != "cuda":
+            return [self.transport]
+        alt = ["rccl", "ipc"] if self.backend == "nccl" else ["host", "ipc"]
+        return [self.transport] + [t for t in alt if t != self.transport]
+
     def ipc(self):
         """The process's IPC peer context (created on first use, collectively)."""
         if self._ipc is None:
@@ -103,7 +115,7 @@ class Comm:
             if ndev == 0:
                 raise RuntimeError("device=cuda requested but no GPU is visible")
             share = os.environ.get("ADVDIFF_SHARE_GPU", "0") == "1"
-            if share and transport == "ipc":
+            if share and size > 1:
                 backend = backend or "gloo"  # RCCL refuses two ranks per GPU
             if size > 1 and local_rank >= ndev and not (share and backend == "gloo"):
                 raise RuntimeError(f"local rank {local_rank} >= {ndev} visible GPUs "

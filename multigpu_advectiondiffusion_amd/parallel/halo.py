@@ -60,11 +60,18 @@ def _start_ipc(comm, comm_stream, phases, after_event=None) -> PendingExchange:
     return PendingExchange([], cs, lambda: torch.cuda.current_stream().wait_event(done))
 
 
+def _ipc_on(halo, field) -> bool:
+    return field.is_cuda and halo.comm.size > 1 and halo.transport == "ipc"
+
+
 class SlabHalo:
-    def __init__(self, comm, decomp: SlabDecomposition, comm_stream=None):
+    def __init__(self, comm, decomp: SlabDecomposition, comm_stream=None,
+                 transport: str | None = None):
+        """transport: "ipc", "rccl" or "host" (None: the Comm's default, Comm.transport)."""
         self.comm = comm
         self.d = decomp
         self.comm_stream = comm_stream
+        self.transport = transport or comm.transport
 
     def _ops(self, field: torch.Tensor):
         d = self.d
@@ -136,7 +143,7 @@ class SlabHalo:
     def prepare(self, field: torch.Tensor) -> None:
         """Collective, outside any graph capture: learn the peers' receive addresses of
         this field's exchange (ipc transport; a no-op otherwise)."""
-        if self.comm.size > 1 and field.is_cuda and self.comm.transport == "ipc":
+        if _ipc_on(self, field):
             self.comm.ipc()._resolve(self._ipc_msgs(field))
 
     def start(self, field: torch.Tensor, after_event=None) -> PendingExchange | None:
@@ -146,7 +153,7 @@ class SlabHalo:
         (or after all work currently queued on the current stream)."""
         if self.comm.size == 1:
             return None
-        if field.is_cuda and self.comm.transport == "ipc":
+        if _ipc_on(self, field):
             return _start_ipc(self.comm, self.comm_stream, [self._ipc_msgs(field)], after_event)
         ops = self._ops(field)
         if not ops:
@@ -197,9 +204,10 @@ class CartesianHalo:
     """
 
     def __init__(self, comm, decomp, comm_stream=None, corners: bool = False,
-                 direct: bool | None = None):
+                 direct: bool | None = None, transport: str | None = None):
         import os
         self.comm = comm
+        self.transport = transport or comm.transport
         self.cd = decomp
         self.comm_stream = comm_stream
         self.corners = corners
@@ -332,7 +340,7 @@ class CartesianHalo:
     def prepare(self, field: torch.Tensor) -> None:
         """Collective, outside any graph capture: learn the peers' receive addresses of
         this field's exchange (ipc transport; a no-op otherwise)."""
-        if self.comm.size > 1 and field.is_cuda and self.comm.transport == "ipc":
+        if _ipc_on(self, field):
             ipc = self.comm.ipc()
             for msgs in self._ipc_phases(field):
                 ipc._resolve(msgs)
@@ -340,7 +348,7 @@ class CartesianHalo:
     def start(self, field: torch.Tensor, after_event=None) -> PendingExchange | None:
         if self.comm.size == 1:
             return None
-        if field.is_cuda and self.comm.transport == "ipc":
+        if _ipc_on(self, field):
             return _start_ipc(self.comm, self.comm_stream, self._ipc_phases(field), after_event)
         phases = self._phases()
         if not field.is_cuda:  # gloo on the CPU: phases run to completion here

@@ -150,12 +150,73 @@ class IpcPeers:
         sp = stream.cuda_stream
         for (peer, send, _), (dptr, dsy, dsz) in zip(msgs, dests):
             ni, nj, nk, ssy, ssz = _box_geom(send)
-            _lib.check(self.lib.advdiff_copy_box(_dtype_code(send), dptr, dsy, dsz,
-                                                 send.data_ptr(), ssy, ssz, ni, nj, nk, sp),
+            _lib.check(self.lib.advdiff_ipc_put(_dtype_code(send), dptr, dsy, dsz,
+                                                send.data_ptr(), ssy, ssz, ni, nj, nk, sp),
                        "ipc put")
         arr = (ctypes.c_int * len(peers))(*peers)
         _lib.check(self.lib.advdiff_ipc_signal(self.ctx, arr, len(peers), sp), "advdiff_ipc_signal")
         _lib.check(self.lib.advdiff_ipc_wait(self.ctx, arr, len(peers), sp), "advdiff_ipc_wait")
+
+    def preflight(self, rounds: int = 3, box=(3, 24, 200)) -> dict:
+        """Collective validation of the transport between EVERY pair of ranks, before a
+        run relies on it (the first multi-GPU run must not trust an unexercised path):
+
+        * ranks on different GPUs: ``hipDeviceCanAccessPeer`` for each pair;
+        * `rounds` round trips of a distinct pattern per (sender, receiver, round) through
+          strided boxes (the shape of a halo face), each preceded by a read of the
+          receive boxes — so a receiver whose caches still hold the previous round's
+          lines after the wait (a broken link 3 of ipc.hip's ordering chain), or a put
+          whose stores are not visible when the flag is (link 1/2), shows up as a
+          mismatch; the receiver checks every box on the device.
+        Raises RuntimeError (on every rank) on any mismatch, wait timeout or missing peer
+        access; returns {"pairs", "rounds", "cross_device"}."""
+        comm, dev = self.comm, self.comm.device
+        peers = [q for q in range(comm.size) if q != comm.rank]
+        ids = comm.device_ids()
+        mine = dev.index
+        cross = sorted({ids[q] for q in peers} - {mine})
+        noacc = [d for d in cross if not torch.cuda.can_device_access_peer(mine, d)]
+        bad_access = comm.allreduce_max(float(len(noacc)))
+        if bad_access:
+            raise RuntimeError(f"ipc preflight: rank {comm.rank} (device {mine}) has no peer "
+                               f"access to devices {noacc}")
+        nk, nj, ni = box
+        pitch = ni + 56  # strided rows, like a face of a padded field
+        send = torch.zeros((len(peers), nk, nj, pitch), dtype=torch.float64, device=dev)
+        recv = torch.zeros_like(send)
+        msgs = [(p, send[i, :, :, :ni], recv[i, :, :, :ni]) for i, p in enumerate(peers)]
+        base = torch.arange(nk * nj * ni, dtype=torch.float64, device=dev).view(nk, nj, ni)
+
+        def pattern(src, dst, r):  # exact in fp64: distinct for every (src, dst, r, cell)
+            return base + (src * 64 + dst) * 1e6 + r * 1e9 + 0.5
+
+        stream = torch.cuda.Stream(device=dev)
+        cur = torch.cuda.current_stream(dev)
+        mism = []
+        for r in range(rounds):
+            for i, p in enumerate(peers):
+                send[i, :, :, :ni].copy_(pattern(comm.rank, p, r))
+            float(recv.sum())  # the stale boxes pass through this GPU's caches
+            comm.barrier()
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            stream.wait_event(ev)
+            self.exchange(msgs, stream)
+            cur.wait_stream(stream)
+            for i, p in enumerate(peers):
+                if not torch.equal(recv[i, :, :, :ni], pattern(p, comm.rank, r)):
+                    mism.append((p, r))
+            comm.barrier()  # nobody starts the next round's puts before all have compared
+        torch.cuda.synchronize(dev)
+        timeouts = self.errors()
+        del send, recv, msgs
+        self.reset()  # the peers' preflight boxes are freed: close their mappings
+        bad = comm.allreduce_max(float(len(mism) + timeouts))
+        if bad:
+            raise RuntimeError(f"ipc preflight failed: rank {comm.rank}: mismatching "
+                               f"(peer, round) {mism[:8]}, wait timeouts {timeouts}")
+        return {"pairs": comm.size * (comm.size - 1), "rounds": rounds,
+                "cross_device": comm.allreduce_max(float(len(cross))) > 0}
 
     def errors(self) -> int:
         n = ctypes.c_longlong(0)

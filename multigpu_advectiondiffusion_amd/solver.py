@@ -69,7 +69,8 @@ class Solver:
                  overlap: bool = True, pad_rows: bool = True, t0: float = 0.0,
                  check_every: int = 0, fused: bool | None = None, decomp=None,
                  integrator: str = "ssprk3", kernel: str = "native",
-                 device_dt: bool | None = None, exchange: str = "u"):
+                 device_dt: bool | None = None, exchange: str = "u",
+                 transport: str | None = None):
         """decomp: process grid — None/"slab" (split the slowest axis only, the
         reference's layout), "auto" (smallest halo surface) or "PZxPYxPX" / a tuple in
         array axis order ((pz, py, px) in 3-D, (py, px) in 2-D).
@@ -80,6 +81,9 @@ class Solver:
         device_dt: adaptive-CFL models compute dt on the device (no per-step host sync;
         graph-replayable); None = on for the native GPU path, False = the host-driven
         loop (bitwise the same step sequence, tests/test_adaptive_dt.py).
+        transport: halo transport of this solver ("ipc", "rccl", "host"; None = the
+        Comm's, Comm.transport) — solvers with different transports can coexist on one
+        Comm (bench.py tunes the transport this way).
         exchange: "u" (default: exchange the stage OUTPUT's ghost planes) or "lu" (the
         reference's MultiGPU scheme, `MultiGPU/Diffusion3d_Baseline/main.c:209-288,300`:
         exchange the boundary planes of the RHS L(u) and advance the ghost planes
@@ -100,6 +104,9 @@ class Solver:
             if comm.device.type == "cuda" and comm.device.index is None:
                 comm.device = torch.device("cuda", torch.cuda.current_device())
         self.comm = comm
+        if transport not in (None, "ipc", "rccl", "host"):
+            raise ValueError("transport must be ipc, rccl or host")
+        self.transport = transport or comm.transport
         self.device = comm.device
         if self.device.type == "cuda" and kernel != "torch":
             from .ops import _lib
@@ -165,11 +172,12 @@ class Solver:
             self.comm_stream = torch.cuda.Stream(device=self.device, priority=hi)
         if self.cart:
             # the fused step stacks three star stencils: it needs edge/corner ghosts too
-            self.halo = CartesianHalo(comm, self.cd, self.comm_stream, corners=self.fused)
+            self.halo = CartesianHalo(comm, self.cd, self.comm_stream, corners=self.fused,
+                                      transport=self.transport)
             self.full = self.cd.compute_box(model.border)
             self.interior, self.boundary = self.cd.split_boxes(model.border, G)
         else:
-            self.halo = SlabHalo(comm, self.d, self.comm_stream)
+            self.halo = SlabHalo(comm, self.d, self.comm_stream, transport=self.transport)
             self.full = self.d.compute_range(model.border)
             self.interior, blo, bhi = self.d.split_ranges(model.border, G)
             self.boundary = [blo, bhi]
@@ -186,7 +194,7 @@ class Solver:
 
     def _ipc_multi(self) -> bool:
         return (self.device.type == "cuda" and self.comm.size > 1
-                and self.comm.transport == "ipc")
+                and self.transport == "ipc")
 
     def _ipc_epoch(self) -> int:
         return self.comm.ipc().epoch if self._ipc_multi() else 0
@@ -486,7 +494,7 @@ class Solver:
         """Single process, or several ranks whose halos are device puts (ipc transport:
         every exchange step is a stream-ordered kernel, so a whole multi-rank step —
         interior, puts, flags, waits, boundary — replays as one graph)."""
-        multi_ok = self.comm.size == 1 or self.comm.transport == "ipc"
+        multi_ok = self.comm.size == 1 or self.transport == "ipc"
         return (self.device.type == "cuda" and multi_ok and self.exchange == "u"
                 and not trace.SYNC_DEBUG
                 and not trace.TRACE)
@@ -678,6 +686,42 @@ class Solver:
         if self.comm.allreduce_max(bad) > 0.0:
             raise FloatingPointError(f"non-finite solution at step {self.it}, t={self.t:g}")
         return self.comm.allreduce_max(mx)
+
+    def bit_hash(self, chunk_cells: int = 1 << 26) -> int:
+        """Order-independent 64-bit hash of the global solution's BIT PATTERNS: the sum
+        (mod 2^64) over the owned cells of mix(global linear index, raw bits).  Equal for
+        every decomposition, transport and rank count exactly when the solutions agree
+        bit for bit (up to a 2^-64 collision chance) — the N-rank-vs-1-GPU check of
+        bench.py compares it without gathering the field.  Collective (all ranks)."""
+        self.sync_halos()
+        own = self.owned
+        gb = self.cd.global_box()
+        gshape = self.cd.shape
+        dev = own.device
+        ibits = torch.int64 if own.element_size() == 8 else torch.int32
+        # strides of the global linear index, array order
+        gstr = [1] * len(gshape)
+        for a in range(len(gshape) - 2, -1, -1):
+            gstr[a] = gstr[a + 1] * gshape[a + 1]
+        rest = [torch.arange(s, s + c, dtype=torch.int64, device=dev) * st
+                for (s, c), st in zip(gb[1:], gstr[1:])]
+        inner = rest[0]
+        for r in rest[1:]:
+            inner = inner[..., None] + r
+        per = max(1, chunk_cells // max(inner.numel(), 1))
+        K1, K2 = -7046029254386353131, -4658895280553007687  # odd 64-bit mixers
+        h = torch.zeros((), dtype=torch.int64, device=dev)
+        n0 = own.shape[0]
+        for z0 in range(0, n0, per):
+            z1 = min(n0, z0 + per)
+            bits = own[z0:z1].contiguous().view(ibits).to(torch.int64)
+            zi = torch.arange(gb[0][0] + z0, gb[0][0] + z1, dtype=torch.int64, device=dev)
+            idx = zi.view((-1,) + (1,) * inner.dim()) * gstr[0] + inner
+            x = (bits ^ (idx * K1)) * K2
+            x = x ^ ((x >> 31) & 0x1FFFFFFFF)  # logical shift of the high half
+            h = h + (x * K1).sum()
+        tot = self.comm.allreduce_tensor(h.view(1), "sum") if self.comm.size > 1 else h.view(1)
+        return int(tot.item())
 
     def error_norms(self, exact: torch.Tensor | None = None, K: float | None = None,
                     t_exact: float | None = None):

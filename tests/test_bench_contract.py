@@ -1,0 +1,95 @@
+"""bench.py's driver contract on the CPU (gloo ranks): `--gpus N` without a launcher starts
+N ranks itself and reports n_gpus = N with the bitwise N-rank vs 1-rank checks; a rank
+count that does not match --gpus, or a failing rank, ends the run non-zero instead of
+reporting something else; Solver.bit_hash is decomposition-invariant and sensitive to a
+single bit."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from multigpu_advectiondiffusion_amd import Diffusion, Grid, Solver
+from multigpu_advectiondiffusion_amd.launch import spawn_local
+
+ROOT = Path(__file__).resolve().parent.parent
+SMALL = ["--device", "cpu", "--base", "20", "--burgers-base", "14", "--steps", "2",
+         "--warmup", "1", "--sustained-steps", "0", "--no-fd2", "--check-steps", "3"]
+
+
+def _bench(args, env_extra=None, timeout=300):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, str(ROOT / "bench.py")] + args, cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def _json_line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_self_launch_reports_n_ranks_and_bitwise_checks():
+    r = _bench(["--gpus", "3"] + SMALL)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = _json_line(r.stdout)
+    assert res["n_gpus"] == 3
+    assert res["config"]["cells_per_gpu"] * 3 == res["config"]["seq_len"]
+    assert res["bitwise_vs_1gpu"] == {"heat": True, "burgers3d": True}
+    assert res["rccl_world"] == 0 and res["comm_backend"] == "gloo"
+    assert res["halo_transport"] == "host"
+
+
+def test_world_mismatch_refused():
+    r = _bench(["--gpus", "2"] + SMALL, {"WORLD_SIZE": "1", "RANK": "0"})
+    assert r.returncode == 2
+    assert "refusing" in r.stderr
+
+
+def test_failing_rank_fails_the_run():
+    r = _bench(["--gpus", "2"] + SMALL, {"ADVDIFF_FAULT": "1:1"})
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def _hash(comm, decomp, poke):
+    grid = Grid((14, 12, 16), (1.0, 1.0, 1.0))
+    s = Solver(Diffusion(K=1.0, order=4), grid, comm, dtype=torch.float64, ic="sine",
+               decomp=decomp)
+    s.run(iters=3)
+    if poke and comm.rank == comm.size - 1:
+        o = s.owned
+        v = o[1, 2, 3].view(1).view(torch.int64)
+        o[1, 2, 3] = (v ^ 1).view(torch.float64)[0]  # flip the lowest mantissa bit
+    return s.bit_hash()
+
+
+@pytest.mark.parametrize("world,decomp", [(2, None), (4, "2x2x1"), (3, None)])
+def test_bit_hash_decomposition_invariant(world, decomp):
+    from multigpu_advectiondiffusion_amd.parallel import Comm
+    ref = _hash(Comm(device="cpu"), None, False)
+    out = spawn_local(world, _hash, decomp, False)
+    assert all(h == ref for h in out)
+    poked = spawn_local(world, _hash, decomp, True)
+    assert all(h == poked[0] for h in poked) and poked[0] != ref
+
+
+def test_bit_hash_sees_index_swaps():
+    """Two cells exchanging their values change the hash (the index is mixed in)."""
+    from multigpu_advectiondiffusion_amd.parallel import Comm
+    grid = Grid((10, 9, 8), (1.0, 1.0, 1.0))
+    s = Solver(Diffusion(K=1.0, order=4), grid, Comm(device="cpu"), dtype=torch.float64,
+               ic="sine")
+    s.run(iters=1)
+    h0 = s.bit_hash()
+    o = s.owned
+    a, b = o[2, 3, 4].clone(), o[5, 6, 7].clone()
+    assert not np.isclose(float(a), float(b))
+    o[2, 3, 4], o[5, 6, 7] = b, a
+    assert s.bit_hash() != h0

@@ -250,11 +250,14 @@ def _bench_tune(comm):
     model.bind(grid)
     dt = model.stable_dt()
 
-    def make(p):
-        return Solver(model, grid, comm, dtype=torch.float64, ic="sine", decomp=p)
+    def make(p, t):
+        return Solver(model, grid, comm, dtype=torch.float64, ic="sine", decomp=p, transport=t)
     cands = candidate_proc_grids(comm.size, (48, 96, 96), 6, 8, corners=True, keep=3)
-    best, trials = bench.tune_decomp(make, cands, dt, comm.device)
-    s = make(best)
+    best, trials = bench.tune(make, [(p, "host") for p in cands], dt, comm.device,
+                              trial_steps=3)
+    assert best[1] == "host"
+    best = best[0]
+    s = make(best, "host")
     s.run(iters=3, dt=dt)
     diag = bench.halo_diag(s)
     return best, trials, diag, cands

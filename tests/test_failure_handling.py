@@ -28,3 +28,29 @@ def test_launcher_success():
     assert launch(2, ARGS[:-1] + ["3"], cpu=True, timeout=240) == 0
 
 # NaN/Inf watchdog: tests/test_cli_and_io.py::test_nan_watchdog*
+
+
+def test_launcher_profile_wraps_each_rank(monkeypatch, tmp_path):
+    """--profile DIR: every rank's command is its own rocprofv3 kernel trace into
+    DIR/rank<r>, the program right after `--` (no shell / env hop)."""
+    from multigpu_advectiondiffusion_amd import launch as L
+    seen = []
+
+    class P:
+        def __init__(self, cmd, env):
+            seen.append((cmd, env["RANK"]))
+
+        def poll(self):
+            return 0
+
+        def wait(self, timeout=None):
+            return 0
+
+    monkeypatch.setattr(L.subprocess, "Popen", P)
+    assert L.launch(2, ["diffusion3d", "1", "1", "1", "1", "8", "8", "8", "2"], cpu=True,
+                    profile_dir=str(tmp_path)) == 0
+    for cmd, rank in seen:
+        i = cmd.index("--")
+        assert cmd[0].endswith("rocprofv3") and "--kernel-trace" in cmd[:i]
+        assert cmd[cmd.index("-d") + 1] == str(tmp_path / f"rank{rank}")
+        assert cmd[i + 1] == __import__("sys").executable

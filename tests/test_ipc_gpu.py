@@ -204,3 +204,29 @@ def test_native_poisoned_multirank_bitwise(tmp_path, app, args, shape, world, de
         bad = np.argwhere(a != b)
         pytest.fail(f"{len(bad)} cells differ, max {np.nanmax(np.abs(a - b))}, box "
                     f"{bad.min(axis=0)}..{bad.max(axis=0)} of {shape}\n{txt[-2000:]}")
+
+
+def _preflight_then_run(comm, kind, steps):
+    rec = comm.ipc().preflight(rounds=3)
+    model, grid, ic = _make(kind)
+    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, transport="ipc")
+    s.run(iters=steps, graph=True)
+    h = s.bit_hash()
+    assert comm.ipc().errors() == 0
+    return rec, h
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_preflight_all_pairs_then_solver(world):
+    """The preflight (every ordered pair of ranks, stale-cache pattern round trips) passes
+    and leaves the flag counters consistent: a graph-replayed solver afterwards matches the
+    1-rank run's bit hash."""
+    model, grid, ic = _make("diff3")
+    ref = Solver(model, grid, dtype=torch.float64, device="cuda", ic=ic)
+    ref.run(iters=16, graph=False)
+    h1 = ref.bit_hash()
+    out = spawn_local(world, _preflight_then_run, "diff3", 16, device="cuda", transport="ipc",
+                      timeout=240)
+    for rec, h in out:
+        assert rec["pairs"] == world * (world - 1) and not rec["cross_device"]
+        assert h == h1
