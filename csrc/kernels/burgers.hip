@@ -343,7 +343,7 @@ __global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(WPE))) 
     if constexpr (DB) __syncthreads();  // y faces of k and tile k+1 visible
 
     const T fyl = s_fy[cb][ty * TX + tx];
-    const T fxl = wave_shr1(fx);  // face i-½ from lane l-1 (lane 0: unused)
+    const T fxl = wave_shr1(fx);  // face i-½ from lane l-1 (column 0: unused)
     T L = -((fx - fxl) * rdx + (fy - fyl) * rdy + (fz_hi - fz_lo) * rdz);
     if constexpr (VISC) {
       L += vx * d2x + vy * d2y + vz * FD<4>::d2(U[R - 3], U[R - 2], ctr, U[R], U[R + 1]);
@@ -422,13 +422,24 @@ __device__ __forceinline__ T w5_combine6(T n1, T S1, T n2, T S2) {
 //     carried as 3 x the flux; z faces keep w5_side on the z rings (6 x the flux).
 // Requires a plane below 2^31 bytes (v9_fits); TY = 8 only (offsets < 64 KiB).
 // ------------------------------------------------------------------------------
-template <typename T, bool WZ, bool VISC, int MODE>
+//
+// TXL: cells per tile row.  64 (default shape): one row per wave, 63 outputs per row, 8
+// rows per tile.  32: each wave holds TWO 32-lane rows (lanes 0 and 32 supply a face
+// only), 31 outputs per row, 16 rows per tile — the launcher picks it where it wastes
+// fewer lanes on the last x tile: a 512 row has 506 active cells = 8.03 tiles of 63
+// (9 tiles, 88 % of the lanes busy) but 16.3 of 31 (17 tiles, 93 %); 1024: 94 % -> 96 %.
+// The 32 x 16 tile also stages fewer halo cells per output (38 x 22 / (31 x 16) = 1.69
+// vs 70 x 14 / (63 x 8) = 1.94).  wave_shr1 hands lane 32 the face of lane 31 — lane 32
+// is its row's face-only lane, so the DPP shift needs no change.
+template <typename T, bool WZ, bool VISC, int MODE, int TXL = 64>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void burgers3d_w5s_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
     int k1, int k0b, int k1b, int gza, int zchunk, int border, T rdx3, T rdy3, T rdz6, T vx,
     T vy, T vz, T dt, T a, T b, const double* __restrict__ dtp, int xcdmap) {
-  constexpr int TY = 8, R = 3, NR = 5, TX = 64, TXO = TX - 1;
-  constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NT = TX * TY, LT = LX * LY;
+  static_assert(TXL == 64 || TXL == 32, "tile row: 64 or 32 lanes");
+  constexpr int NW = 8, RW = 64 / TXL;  // waves per workgroup, tile rows per wave
+  constexpr int TY = NW * RW, R = 3, NR = 5, TX = TXL, TXO = TX - 1;
+  constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NT = 64 * NW, LT = LX * LY;
   constexpr int NPT = (LT + NT - 1) / NT;
   constexpr int E = (int)sizeof(T);
   constexpr int NARR = VISC ? 3 : 2;                 // staged arrays: f+, f- [, u]
@@ -442,20 +453,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
 
   const int tx = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
-  const int tid = w * TX + tx;
+  const int tid = w * 64 + tx;
+  const int col = tx % TX, row = w * RW + tx / TX;  // the lane's cell in the tile
   // xcdmap: XCD-contiguous tile order (common.hpp xcd_tile), so y-adjacent tiles — which
-  // share 6 of their 14 staged rows — run together on one XCD's L2
+  // share 6 of their staged rows — run together on one XCD's L2
   const Tile3 tl = xcdmap ? xcd_tile() : Tile3{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
-  const int ib = border - 1 + tl.x * TXO;  // x of lane 0 (supplies a face only)
-  const int jb = border + tl.y * TY;       // y of wave 0
-  const int i = ib + tx, j = jb + w;
+  const int ib = border - 1 + tl.x * TXO;  // x of column 0 (supplies a face only)
+  const int jb = border + tl.y * TY;       // y of row 0
+  const int i = ib + col, j = jb + row;
   // z chunks of the first plane range [k0, k1), then (tile z >= gza) of the second
   // [k0b, k1b): both boundary slabs of a rank in ONE launch
   const bool second = tl.z >= gza;
   const int kc0 = second ? k0b + (tl.z - gza) * zchunk : k0 + tl.z * zchunk;
   const int kc1 = min(kc0 + zchunk, second ? k1b : k1);
   const int klast = kc1 - 1;
-  const bool active = tx >= 1 && i < nx - border && j < ny - border;
+  const bool active = col >= 1 && i < nx - border && j < ny - border;
   const uint32_t goff = (uint32_t)(min(j, ny - 1) * (int)sy + min(i, nx - 1)) * (uint32_t)E;
   const int64_t szb = sz * E;
   auto plane = [&](const T* base, int k) {
@@ -476,9 +488,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
                          clampi(ib - R + lx, 0, nx - 1)) * (uint32_t)E;
   }
   // loop-invariant LDS lane bases (byte addresses); everything else is an immediate
-  const int lrb = ((w + R) * LX + tx + R) * E - XO;  // own-cell reads
-  const int brb = tx * E;                            // bottom y faces (row R-1) + its store
-  const int fyb = ((w + 1) * TX + tx) * E;           // y face above the own cell
+  const int lrb = ((row + R) * LX + col + R) * E - XO;  // own-cell reads
+  const int brb = col * E;                              // bottom y faces (row R-1) + its store
+  const int fyb = ((row + 1) * TX + col) * E;           // y face above the own cell
   const int stb = tid * E;                           // tile staging
   T pre[NPT];
   auto fetch_tile = [&](int k) {
@@ -564,7 +576,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
     if constexpr (reads_aux<MODE>()) ax = gld<T>(plane(aux, min(k + 1, klast)), goff);
 
     const T fy = lds_face3(lb + lrb, SB + XO, LX * E);  // y face j+½
-    if (w == (k - kc0) % TY)  // the tile's bottom y faces rotate over the waves
+    if (w == (k - kc0) % NW)  // the tile's bottom y faces rotate over the waves
+      // (TXL 32: both rows of the wave compute them; identical values, same slots)
       lds_st<T>(lb + brb, SB + OFY, lds_face3(lb + brb, SB + ((R - 1) * LX + R) * E, LX * E));
     lds_st<T>(lb + fyb, SB + OFY, fy);
     const T ctr = ru[sl(0)];
@@ -597,7 +610,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
     __syncthreads();  // y faces of k and tile k+1 visible
 
     const T fyl = lds_ld<T>(lb + fyb, SB + OFY - TX * E);
-    const T fxl = wave_shr1(fx);  // face i-½ from lane l-1 (lane 0: unused)
+    const T fxl = wave_shr1(fx);  // face i-½ from lane l-1 (column 0: unused)
     T L = -(((fx - fxl) * rdx3 + (fy - fyl) * rdy3) + (fz[sl(0)] - fz[sl(-1)]) * rdz6);
     if constexpr (VISC) L += vx * d2x + vy * d2y + vz * d2z;
     T dnew = T(0);
@@ -947,24 +960,56 @@ static hipError_t launch_b3_v3(const BArgs& p) {
   return hipGetLastError();
 }
 
-template <typename T, bool WZ, bool VISC, int MODE>
-static hipError_t launch_b3_v9(const BArgs& p) {
+// busy share of the lanes of a tiling: `act` active cells in tiles of `per` outputs of
+// `lanes` lanes each
+static double lane_share(int act, int per, int lanes) {
+  act = std::max(act, 1);
+  return (double)act / ((double)div_up(act, per) * lanes);
+}
+
+// v9 tile row width for an nx x ny plane (ADVDIFF_B3_TX / advdiff_set_b3_tx = 64 / 32
+// forces one, 0 = auto): the shape with the larger share of busy lanes over x and y, the
+// 64-wide one on a tie
+static int g_b3_tx = -1;
+static int b3_tx() {
+  if (g_b3_tx < 0) g_b3_tx = knob("B3_TX", 0);
+  return g_b3_tx;
+}
+static int b3_tile_row(int nx, int ny, int border) {
+  const int forced = b3_tx();
+  if (forced == 64 || forced == 32) return forced;
+  const int ax = nx - 2 * border, ay = ny - 2 * border;
+  const double s64 = lane_share(ax, 63, 64) * lane_share(ay, 8, 8);
+  const double s32 = lane_share(ax, 31, 32) * lane_share(ay, 16, 16);
+  return s32 > s64 * 1.01 ? 32 : 64;
+}
+
+template <typename T, bool WZ, bool VISC, int MODE, int TXL>
+static hipError_t launch_b3_v9_tx(const BArgs& p) {
   // XCD-contiguous tile order (default): 256^3 WENO5-Z + viscous step 0.584 -> 0.564 ms
   // (+3.7 %, 3 interleaved rounds, bitwise identical; profiles/burgers3d_xcd_r2.log)
   static const int xcdmap = knob("B3_XCD", 1);
-  const int gx = div_up(std::max(p.nx - 2 * p.border, 1), 63);
-  const int gy = div_up(std::max(p.ny - 2 * p.border, 1), 8);
+  constexpr int TY = 8 * (64 / TXL);
+  const int gx = div_up(std::max(p.nx - 2 * p.border, 1), TXL - 1);
+  const int gy = div_up(std::max(p.ny - 2 * p.border, 1), TY);
   const int na = std::max(p.hi - p.lo, 0), nb = std::max(p.hi2 - p.lo2, 0);
   const int zc = pick_chunk(na + nb, (long long)gx * gy, 8, 256);
   const int gza = div_up(na, zc);
   const int gz = gza + div_up(nb, zc);
   const double s = 1.0 / 12.0;
-  hipLaunchKernelGGL((burgers3d_w5s_kernel<T, WZ, VISC, MODE>), dim3(gx, gy, gz), dim3(64, 8, 1),
-                     0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx, p.ny, p.sy, p.sz,
-                     p.lo, p.hi, p.lo2, p.hi2, gza, zc, p.border, T(p.rdx / 3.0),
+  hipLaunchKernelGGL((burgers3d_w5s_kernel<T, WZ, VISC, MODE, TXL>), dim3(gx, gy, gz),
+                     dim3(64, 8, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx, p.ny,
+                     p.sy, p.sz, p.lo, p.hi, p.lo2, p.hi2, gza, zc, p.border, T(p.rdx / 3.0),
                      T(p.rdy / 3.0), T(p.rdz / 6.0), T(p.vx * s), T(p.vy * s), T(p.vz * s),
                      T(p.dt), T(p.a), T(p.b), p.dtp, xcdmap);
   return hipGetLastError();
+}
+
+template <typename T, bool WZ, bool VISC, int MODE>
+static hipError_t launch_b3_v9(const BArgs& p) {
+  if (b3_tile_row(p.nx, p.ny, p.border) == 32)
+    return launch_b3_v9_tx<T, WZ, VISC, MODE, 32>(p);
+  return launch_b3_v9_tx<T, WZ, VISC, MODE, 64>(p);
 }
 
 // (Round-3 A/B, rejected: the wave computing a plane's extra bottom faces raising its
@@ -1116,6 +1161,12 @@ static hipError_t run_b(int dtype, bool three_d, int scheme, bool ls, const BArg
 extern "C" int advdiff_set_b2_ver(int v) {
   const int old = advdiff::b2_ver();
   advdiff::g_b2_ver = v;
+  return old;
+}
+
+extern "C" int advdiff_set_b3_tx(int v) {
+  const int old = advdiff::b3_tx();
+  advdiff::g_b3_tx = v;
   return old;
 }
 

@@ -241,14 +241,21 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   double l1 = 0, l2 = 0, li = 0;
   const bool norms = opt.count("--error-norms") && (p.ic == 2 || p.ic == 3);
   if (norms) eng.error_norms(l1, l2, li);
-  // DtH: the barrier-fenced copy of the result to the host and its gather to rank 0
-  // (the reference's timed DtH + Merge_domains, MultiGPU/Diffusion3d_Baseline/main.c:313-335)
+  // DtH: the barrier-fenced copy of the result to the host and — when an output needs the
+  // global field (--write) — its gather to rank 0 (the reference's timed DtH +
+  // Merge_domains, MultiGPU/Diffusion3d_Baseline/main.c:313-335).  Without one, each rank
+  // times the copy of its own block only: no full-field copy on rank 0's host, no merge
+  // over the TCP star (at 2048^3 that would be ~70 GB per run for nothing)
   auto wall = [] {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
   };
   tr->barrier();
   const double tw = wall();
-  std::vector<float> g = eng.gather_float32();
+  std::vector<float> g;
+  if (opt.count("--write"))
+    g = eng.gather_float32();
+  else
+    eng.dtoh_local();
   tr->barrier();
   st.dtoh = tr->allreduce_max(wall() - tw);
   std::vector<float> gg;
@@ -317,10 +324,11 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
                                (dims == 3 ? ", " + std::to_string(p.nz) : std::string()) + "]";
       std::snprintf(line, sizeof line,
                     "{\"app\": \"%s\", \"grid\": %s, \"steps\": %d, \"seconds\": %.17g, "
-                    "\"mlups\": %.17g, \"n_procs\": %d, \"dtype\": \"%s\", \"t\": %.17g}",
+                    "\"mlups\": %.17g, \"n_procs\": %d, \"dtype\": \"%s\", \"t\": %.17g, "
+                    "\"device_field_bytes\": %zu}",
                     (std::string(diff ? "diffusion" : "burgers") + (dims == 3 ? "3d" : "2d")).c_str(),
                     grid.c_str(), st.steps, st.seconds, ml, env.size,
-                    p.dtype == ADVDIFF_F64 ? "fp64" : "fp32", st.t);
+                    p.dtype == ADVDIFF_F64 ? "fp64" : "fp32", st.t, eng.memory_bytes());
       std::cout << line << "\n";
     }
     std::cout.flush();

@@ -210,6 +210,18 @@ void Engine::save_checkpoint(const std::string& prefix, const std::string& ic_na
   }
   fs::rename(tmp, path);
   tr_->barrier();  // every shard is complete when any rank returns
+  if (env_.rank == 0) {
+    // shards of an earlier run on more ranks under this prefix would be read back with ours
+    const std::string head = fs::path(prefix).filename().string() + ".rank";
+    for (const std::string& q : list_shards(prefix)) {
+      const std::string n = fs::path(q).filename().string();
+      const std::string digits = n.substr(head.size(), n.size() - head.size() - 5);
+      if (!digits.empty() && digits.find_first_not_of("0123456789") == std::string::npos &&
+          std::stoi(digits) >= env_.size)
+        fs::remove(q);
+    }
+  }
+  tr_->barrier();
 }
 
 void Engine::load_checkpoint(const std::string& prefix) {
@@ -301,13 +313,17 @@ void Engine::load_checkpoint(const std::string& prefix) {
     }
     HIP_CHECK(hipMemcpy(dev, pl.data(), span, hipMemcpyHostToDevice));
   }
+  if (covered > (long long)bn[0] * bn[1] * bn[2])
+    throw std::runtime_error("checkpoint " + prefix +
+                             ": overlapping shards cover this rank's block more than once "
+                             "(shards of two runs?)");
   if (covered != (long long)bn[0] * bn[1] * bn[2])
     throw std::runtime_error("checkpoint " + prefix + " does not cover this rank's block");
   // the stage buffers start as copies of u, exactly as after the initial condition
   HIP_CHECK(hipMemcpyAsync(A_, u_, field_bytes_, hipMemcpyDeviceToDevice, compute_));
-  if (p_.integrator == 1)
+  if (B_ && p_.integrator == 1)
     HIP_CHECK(hipMemsetAsync(B_, 0, field_bytes_, compute_));
-  else
+  else if (B_)
     HIP_CHECK(hipMemcpyAsync(B_, u_, field_bytes_, hipMemcpyDeviceToDevice, compute_));
   HIP_CHECK(hipStreamSynchronize(compute_));
   t_ = t;

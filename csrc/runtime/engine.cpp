@@ -79,9 +79,12 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   HIP_CHECK(hipDeviceSynchronize());
   tr_->barrier();
   const double ts = now_s();
+  // fields: u and its ping-pong partner A; B only where a step uses a third buffer (the
+  // per-stage SSP-RK3 output, or the LSRK du) — the fused heat step ping-pongs u <-> A, so
+  // its largest grid per GPU is what utils/sizing.py promises (2 fields, like solver.py)
   HIP_CHECK(hipMalloc(&u_, field_bytes_));
   HIP_CHECK(hipMalloc(&A_, field_bytes_));
-  HIP_CHECK(hipMalloc(&B_, field_bytes_));
+  if (!fused_) HIP_CHECK(hipMalloc(&B_, field_bytes_));
   // Stream-ordered fill of the whole allocation (row padding included) BEFORE the IC.  A
   // synchronous hipMemset on the null stream is NOT ordered before work on the
   // non-blocking compute stream: it can land after the IC kernel and zero part of it
@@ -113,9 +116,9 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   // A (and B) start as copies of u, padding included: cells a step never writes (frozen
   // boundary cells, unwritten ghost edges) carry the IC in every buffer
   HIP_CHECK(hipMemcpyAsync(A_, u_, field_bytes_, hipMemcpyDeviceToDevice, compute_));
-  if (p.integrator == 1)
+  if (B_ && p.integrator == 1)
     HIP_CHECK(hipMemsetAsync(B_, 0, field_bytes_, compute_));  // du
-  else
+  else if (B_)
     HIP_CHECK(hipMemcpyAsync(B_, u_, field_bytes_, hipMemcpyDeviceToDevice, compute_));
   HIP_CHECK(hipStreamSynchronize(compute_));
   tr_->barrier();
@@ -139,9 +142,11 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
     graph_ = false;  // per-launch / per-step host checks
   if (graph_ && std::string(tr_->name()) == "socket")
     throw std::runtime_error("--graph: the socket transport synchronises the host inside a step");
+  if (env.size > 1) wd_ = std::make_unique<Watchdog>(tr_, env.rank, Watchdog::timeout_from_env());
 }
 
 Engine::~Engine() {
+  wd_.reset();
   (void)hipStreamSynchronize(compute_);
   (void)hipStreamSynchronize(comm_);
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
@@ -364,12 +369,15 @@ hipGraphExec_t Engine::graph_for(double dt) {
 
 void Engine::prepare_graphs(double dt) {
   if (!graph_) return;
-  if (tr_->needs_handshake() && warm_ < 2) {
-    // every buffer a step may exchange (fused / LSRK ping-pong u <-> A, SSP-RK3 stage
-    // outputs A, B, u): the same message patterns the steps will use, handshakes only
+  if (warm_ < 2) {
+    // Dry exchanges of every buffer a step may exchange (fused / LSRK ping-pong u <-> A,
+    // SSP-RK3 stage outputs A, B, u): the same message patterns the steps will use, with
+    // no device work — the transport's one-time handshakes (ipc) and its staging buffers
+    // (strided Cartesian boxes, any transport) are settled here, outside the capture.
     const bool pending = halo_pending_;
     tr_->set_dry(true);
     for (void* f : {u_, A_, B_}) {
+      if (f == nullptr) continue;
       if (cart_)
         start_halo_cart(f);
       else
@@ -390,25 +398,33 @@ void Engine::steps(int n, double dt) {
   if (!graph_) {
     for (int q = 0; q < n; ++q) {
       step(dt);
+      beat();
       watchdog();
     }
     return;
   }
   // eager steps first: the transport's one-time handshakes (host communication) must not
   // fall inside a capture, and the u/A ping-pong visits both parities in two steps
-  for (; warm_ < 2 && n > 0; ++warm_, --n) step(dt);
+  for (; warm_ < 2 && n > 0; ++warm_, --n) {
+    step(dt);
+    beat();
+  }
   if (n >= kGraphSteps && halo_pending_) {  // an event recorded outside a capture cannot
     HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));  // be waited on inside it
     halo_pending_ = false;
   }
   for (; n >= kGraphSteps; n -= kGraphSteps) {
     HIP_CHECK(hipGraphLaunch(graph_for(dt), compute_));
+    beat();
     for (int q = 0; q < kGraphSteps; ++q) {  // the same additions as kGraphSteps eager steps
       t_ += dt;
       ++it_;
     }
   }
-  for (; n > 0; --n) step(dt);
+  for (; n > 0; --n) {
+    step(dt);
+    beat();
+  }
 }
 
 Stats Engine::run_iters(int iters) {
@@ -416,6 +432,7 @@ Stats Engine::run_iters(int iters) {
   if (iters >= kGraphSteps) prepare_graphs(dt);
   HIP_CHECK(hipDeviceSynchronize());
   tr_->barrier();
+  Armed armed(wd_.get());
   const double t0 = now_s();
   steps(iters, dt);
   HIP_CHECK(hipStreamSynchronize(compute_));
@@ -437,6 +454,7 @@ void Engine::warmup(int n) {
   void* const roles[3] = {u_, A_, B_};
   void* saved[3] = {nullptr, nullptr, nullptr};
   for (int q = 0; q < 3; ++q) {
+    if (roles[q] == nullptr) continue;
     HIP_CHECK(hipMalloc(&saved[q], field_bytes_));
     HIP_CHECK(hipMemcpyAsync(saved[q], roles[q], field_bytes_, hipMemcpyDeviceToDevice, compute_));
   }
@@ -444,7 +462,11 @@ void Engine::warmup(int n) {
   const int it = it_;
   const double dt = stable_dt();
   if (n >= kGraphSteps) prepare_graphs(dt);
-  steps(n, dt);
+  {
+    Armed armed(wd_.get());
+    steps(n, dt);
+    HIP_CHECK(hipStreamSynchronize(compute_));
+  }
   if (halo_pending_) {
     HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
     halo_pending_ = false;
@@ -456,10 +478,12 @@ void Engine::warmup(int n) {
   A_ = roles[1];
   B_ = roles[2];
   for (int q = 0; q < 3; ++q) {
+    if (roles[q] == nullptr) continue;
     HIP_CHECK(hipMemcpyAsync(roles[q], saved[q], field_bytes_, hipMemcpyDeviceToDevice, compute_));
   }
   HIP_CHECK(hipStreamSynchronize(compute_));
-  for (void* b : saved) HIP_CHECK(hipFree(b));
+  for (void* b : saved)
+    if (b) HIP_CHECK(hipFree(b));
   t_ = t;
   it_ = it;
   tr_->barrier();
@@ -470,6 +494,7 @@ Stats Engine::run_until(double t_end) {
   prepare_graphs(dt0);
   HIP_CHECK(hipDeviceSynchronize());
   tr_->barrier();
+  Armed armed(wd_.get());
   const double t0 = now_s();
   // the steps of the full dt0 (graph-replayable), counted with the loop's own arithmetic
   int n = 0;
@@ -485,6 +510,7 @@ Stats Engine::run_until(double t_end) {
     double dt = dt0;
     if (t_ + dt > t_end) dt = t_end - t_;
     step(dt);
+    beat();
     watchdog();
     ++n;
   }
@@ -610,6 +636,31 @@ template std::vector<float> Engine::gather_as<float>();
 template std::vector<double> Engine::gather_as<double>();
 
 // every rank's planes with their ghost planes (slabs), concatenated in rank order
+void Engine::dtoh_local() {
+  HIP_CHECK(hipStreamSynchronize(comm_));
+  HIP_CHECK(hipStreamSynchronize(compute_));
+  int lo[3], g0[3], n[3];
+  own_box(lo, g0, n);
+  // 3-D: planes of n[1] rows of n[2] cells; 2-D (axis 0 a unit axis): one plane of rows
+  const size_t row = (size_t)n[2] * elem_;
+  const size_t plane = row * n[1];
+  const int per = (int)std::max<size_t>(1, ((size_t)64 << 20) / std::max<size_t>(plane, 1));
+  void* host = nullptr;
+  HIP_CHECK(hipHostMalloc(&host, plane * std::min(per, n[0])));
+  const int64_t pz = p_.dims == 3 ? sz_ : sz_ * alloc_[0];
+  for (int k0 = 0; k0 < n[0]; k0 += per) {
+    const int nk = std::min(per, n[0] - k0);
+    for (int k = 0; k < nk; ++k) {
+      const char* src = (const char*)u_ +
+                        ((int64_t)(lo[0] + k0 + k) * pz + (int64_t)lo[1] * sy_ + lo[2]) * elem_;
+      HIP_CHECK(hipMemcpy2DAsync((char*)host + (size_t)k * plane, row, src, (size_t)sy_ * elem_,
+                                 row, n[1], hipMemcpyDeviceToHost, compute_));
+    }
+    HIP_CHECK(hipStreamSynchronize(compute_));
+  }
+  HIP_CHECK(hipHostFree(host));
+}
+
 std::vector<float> Engine::gather_float32_ghosts() {
   HIP_CHECK(hipStreamSynchronize(comm_));
   HIP_CHECK(hipStreamSynchronize(compute_));

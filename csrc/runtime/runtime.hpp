@@ -9,13 +9,18 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "advdiff/kernels.h"
@@ -120,17 +125,59 @@ class Transport {
   // step can be captured into a hipGraph (local, ipc: yes; socket: host-staged, no; rccl:
   // capturable, but never run multi-rank on the 1-GPU test box -> opt-in with --graph)
   virtual bool graph_safe() const { return false; }
-  // one-time host handshakes per message pattern (ipc): dry mode runs them without any
-  // device work, so an engine can settle them before it captures a graph
+  // one-time host handshakes per message pattern (ipc)
   virtual bool needs_handshake() const { return false; }
-  virtual void set_dry(bool) {}
+  // Dry mode: an exchange runs only its host-side setup — the one-time handshakes (ipc)
+  // and the sizing of device staging buffers (strided boxes) — and enqueues no device
+  // work, so an engine settles both before it captures a graph (hipMalloc / hipFree /
+  // stream syncs are not allowed inside a stream capture).
+  virtual void set_dry(bool on) { dry_ = on; }
+  // Watchdog hooks (SURVEY §5 failure detection): a deferred asynchronous error of the
+  // transport (RCCL: ncclCommGetAsyncError), 0 if none; abort() tears the transport down
+  // so blocked device work of a dead peer's exchange cannot hold the process (RCCL:
+  // ncclCommAbort).  Both are called from the watchdog thread.
+  virtual int poll_error() { return 0; }
+  virtual void abort() {}
 
  protected:
   void* staging(size_t slot, size_t bytes, hipStream_t stream);  // device staging buffer
+  bool dry_ = false;
 
  private:
   std::vector<void*> stage_;
   std::vector<size_t> stage_cap_;
+};
+
+// Comm watchdog (watchdog.cpp): while armed, ends the process (exit 6, after
+// Transport::abort) when the transport reports an asynchronous error or the main thread
+// has not beaten for `timeout_s` seconds.  on_fail replaces that action (tests).
+class Watchdog {
+ public:
+  using FailFn = std::function<void(const std::string&)>;
+  Watchdog(Transport* tr, int rank, double timeout_s, FailFn on_fail = nullptr,
+           double poll_s = 0.1);
+  ~Watchdog();
+  Watchdog(const Watchdog&) = delete;
+  Watchdog& operator=(const Watchdog&) = delete;
+  void arm();
+  void disarm();
+  void beat();
+  bool fired() const { return fired_; }
+  static double timeout_from_env();  // ADVDIFF_COMM_TIMEOUT, default 600 s (<= 0: off)
+
+ private:
+  void loop();
+  Transport* tr_;
+  int rank_;
+  double timeout_, poll_;
+  FailFn on_fail_;
+  std::atomic<double> last_{0.0};
+  std::atomic<bool> armed_{false};
+  std::atomic<bool> fired_{false};
+  bool stop_ = false;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::thread th_;
 };
 
 // Debug: ADVDIFF_POISON=1 fills every device allocation of the runtime (fields incl. row
@@ -323,6 +370,11 @@ class Engine {
   // the reference's multi-GPU result.bin layout (each rank's Nx x Ny x (_Nz + 6) slab,
   // SaveBinary3D(h_u, Nx, Ny, NZ), MultiGPU/Diffusion3d_Baseline/main.c:341).  Slabs only.
   std::vector<float> gather_float32_ghosts();
+  // per-rank device-to-host copy of the owned block through one reused pinned buffer of a
+  // few planes (the reference's timed DtH without the rank-0 merge; host memory O(planes))
+  void dtoh_local();
+  // device bytes of the resident fields (u, A and, if a step uses it, B)
+  size_t memory_bytes() const { return field_bytes_ * ((u_ ? 1 : 0) + (A_ ? 1 : 0) + (B_ ? 1 : 0)); }
   // fp64 shard of the owned cells (utils/io.py format; collective: returns when every
   // rank's shard is written) / restart from the shards of ANY layout (owned + in-domain
   // ghost cells, then the stage buffers as after the IC; sets t and it)
@@ -382,6 +434,19 @@ class Engine {
   size_t elem_ = 8, plane_bytes_ = 0, field_bytes_ = 0;
   // SSP-RK3: u -> A -> B -> u.  Fused step / LSRK: u <-> A ping-pong (B = du for LSRK).
   void *u_ = nullptr, *A_ = nullptr, *B_ = nullptr;
+  std::unique_ptr<Watchdog> wd_;  // multi-rank runs: comm watchdog while stepping
+  void beat() {
+    if (wd_) wd_->beat();
+  }
+  struct Armed {  // the watchdog watches the stepping phase of a run
+    Watchdog* w;
+    explicit Armed(Watchdog* w_) : w(w_) {
+      if (w) w->arm();
+    }
+    ~Armed() {
+      if (w) w->disarm();
+    }
+  };
   bool fused_ = false;
   Range zact_;  // fused: local planes whose intermediate stages are updated
   bool cart_ = false;

@@ -84,8 +84,9 @@ void Transport::exchange_boxes(const std::vector<BoxMsg>& msgs, hipStream_t s) {
       f.send = m.send;
     } else {
       void* b = staging(slot++, f.bytes, s);
-      KERNEL_CHECK(advdiff_copy_box(m.dtype, b, m.ni, (int64_t)m.ni * m.nj, m.send, m.ssy, m.ssz,
-                                    m.ni, m.nj, m.nk, s));
+      if (!dry_)
+        KERNEL_CHECK(advdiff_copy_box(m.dtype, b, m.ni, (int64_t)m.ni * m.nj, m.send, m.ssy,
+                                      m.ssz, m.ni, m.nj, m.nk, s));
       f.send = b;
     }
     if (m.recv_contiguous()) {
@@ -96,6 +97,7 @@ void Transport::exchange_boxes(const std::vector<BoxMsg>& msgs, hipStream_t s) {
     }
     flat.push_back(f);
   }
+  if (dry_) return;  // staging sized (outside any capture); nothing enqueued
   exchange(flat, s);
   for (const Unpack& u : unpack) {
     const BoxMsg& m = *u.m;
@@ -292,8 +294,20 @@ class RcclTransport final : public Transport {
     if (comm_) ncclCommDestroy(comm_);
   }
   const char* name() const override { return "rccl"; }
+  int poll_error() override {
+    if (comm_ == nullptr) return 0;
+    ncclResult_t r = ncclSuccess;
+    if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return 1;
+    return r == ncclSuccess || r == ncclInProgress ? 0 : (int)r;
+  }
+  void abort() override {
+    if (comm_ == nullptr) return;
+    ncclComm_t c = comm_;
+    comm_ = nullptr;  // the destructor must not destroy an aborted communicator
+    (void)ncclCommAbort(c);
+  }
   void exchange(const std::vector<Msg>& msgs, hipStream_t s) override {
-    if (msgs.empty()) return;
+    if (msgs.empty() || dry_) return;
     NCCL_CHECK(ncclGroupStart());
     for (const Msg& m : msgs) {
       NCCL_CHECK(ncclSend(m.send, m.bytes, ncclChar, m.peer, comm_, s));
@@ -373,7 +387,7 @@ class SocketTransport final : public Transport {
   }
   const char* name() const override { return "socket"; }
   void exchange(const std::vector<Msg>& msgs, hipStream_t s) override {
-    if (msgs.empty()) return;
+    if (msgs.empty() || dry_) return;
     size_t total = 0;
     for (const Msg& m : msgs) total += m.bytes;
     if (total > cap_) {
@@ -451,7 +465,6 @@ class IpcTransport final : public Transport {
   const char* name() const override { return "ipc"; }
   bool graph_safe() const override { return true; }
   bool needs_handshake() const override { return true; }
-  void set_dry(bool on) override { dry_ = on; }
 
   void exchange_boxes(const std::vector<BoxMsg>& msgs, hipStream_t s) override {
     if (msgs.empty()) return;
@@ -581,7 +594,6 @@ class IpcTransport final : public Transport {
   advdiff_ipc* ctx_ = nullptr;
   std::map<Key, Dest> dest_;
   std::map<int, uint64_t> calls_;
-  bool dry_ = false;
 };
 
 // Single process: no communication at all.

@@ -12,6 +12,10 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <atomic>
+#include <chrono>
+#include <mutex>
+#include <thread>
 
 #include "runtime.hpp"
 
@@ -231,7 +235,71 @@ static void test_checkpoint_header() {
   EXPECT(shard_path("out/ck", 3) == "out/ck.rank00003.ckpt");
 }
 
+// the comm watchdog: fires on a transport's asynchronous error, and on a missing heartbeat
+// only while armed; beats keep it quiet (on_fail replaced: no abort, no exit)
+namespace {
+class FakeTransport final : public Transport {
+ public:
+  std::atomic<int> err{0};
+  std::atomic<int> aborted{0};
+  const char* name() const override { return "fake"; }
+  void exchange(const std::vector<Msg>&, hipStream_t) override {}
+  void halo(const void*, void*, const void*, void*, size_t, int, int, hipStream_t) override {}
+  double allreduce_max(double v) override { return v; }
+  double allreduce_sum(double v) override { return v; }
+  void barrier() override {}
+  std::vector<char> gather(const std::vector<char>& l) override { return l; }
+  int poll_error() override { return err.load(); }
+  void abort() override { ++aborted; }
+};
+}  // namespace
+
+static void test_watchdog() {
+  using namespace std::chrono_literals;
+  FakeTransport tr;
+  std::atomic<int> fired{0};
+  std::string why;
+  std::mutex m;
+  auto on_fail = [&](const std::string& w) {
+    std::lock_guard<std::mutex> g(m);
+    why = w;
+    ++fired;
+  };
+  {  // not armed: a silent main thread is fine (setup, output, gathers)
+    Watchdog wd(&tr, 0, 0.2, on_fail, 0.02);
+    std::this_thread::sleep_for(400ms);
+    EXPECT(fired.load() == 0);
+    wd.arm();  // armed and beating: quiet
+    for (int i = 0; i < 20; ++i) {
+      std::this_thread::sleep_for(20ms);
+      wd.beat();
+    }
+    EXPECT(fired.load() == 0);
+    std::this_thread::sleep_for(500ms);  // armed, no beat for > timeout: fires once
+    EXPECT(fired.load() == 1);
+    EXPECT(wd.fired());
+    EXPECT(why.find("no progress") != std::string::npos);
+  }
+  fired = 0;
+  {  // an asynchronous transport error fires at once, armed or not
+    Watchdog wd(&tr, 0, 100.0, on_fail, 0.02);
+    tr.err = 3;
+    std::this_thread::sleep_for(200ms);
+    EXPECT(fired.load() == 1);
+    EXPECT(why.find("asynchronous error 3") != std::string::npos);
+  }
+  tr.err = 0;
+  fired = 0;
+  {  // timeout <= 0: off
+    Watchdog wd(&tr, 0, 0.0, on_fail, 0.02);
+    wd.arm();
+    std::this_thread::sleep_for(100ms);
+    EXPECT(fired.load() == 0);
+  }
+}
+
 int main() {
+  test_watchdog();
   test_checkpoint_header();
   test_slab_partition();
   test_cart_partition();

@@ -228,9 +228,13 @@ def main(argv=None) -> int:
     if ns.error_norms and ic in ("sine", "heat"):
         l1, l2, li = solver.error_norms()
         extra = {"L1 norm": f"{l1:e}", "L2 norm": f"{l2:e}", "Linf norm": f"{li:e}"}
-    # DtH: the final field to the host and its gather on rank 0 (the reference's timed
-    # DtH + Merge_domains)
-    g, dtoh_s = fenced(solver.gather)
+    # DtH: the final field to the host and — when an output needs the global field — its
+    # gather on rank 0 (the reference's timed DtH + Merge_domains).  Without one, each rank
+    # times the copy of its own block only (no full-field copy on rank 0's host)
+    if ns.write or ns.ascii or ns.print_field:
+        g, dtoh_s = fenced(solver.gather)
+    else:
+        g, dtoh_s = fenced(solver.copy_to_host)
     stats.htod_s, stats.dtoh_s = htod_s, dtoh_s
     text = solver.summary(stats, style=ns.style, extra=extra)
     from .utils import io as aio
@@ -256,7 +260,8 @@ def main(argv=None) -> int:
                 "app": ns.app, "grid": list(grid.shape), "steps": stats.steps,
                 "seconds": stats.compute_s,
                 "mlups": metrics.mlups(stats.compute_s, stats.steps, grid.cells),
-                "n_procs": comm.size, "dtype": ns.dtype, "t": stats.t}))
+                "n_procs": comm.size, "dtype": ns.dtype, "t": stats.t,
+                "device_field_bytes": solver.memory_bytes()}))
     sys.stdout.flush()
     comm.finalize()
     return 0

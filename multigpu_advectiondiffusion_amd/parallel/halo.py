@@ -71,7 +71,7 @@ class SlabHalo:
         self.comm = comm
         self.d = decomp
         self.comm_stream = comm_stream
-        self.transport = transport or comm.transport
+        self.transport = transport or (comm.transport if comm is not None else None)
 
     def _ops(self, field: torch.Tensor):
         d = self.d
@@ -207,7 +207,7 @@ class CartesianHalo:
                  direct: bool | None = None, transport: str | None = None):
         import os
         self.comm = comm
-        self.transport = transport or comm.transport
+        self.transport = transport or (comm.transport if comm is not None else None)
         self.cd = decomp
         self.comm_stream = comm_stream
         self.corners = corners

@@ -761,6 +761,25 @@ class Solver:
             g = self.comm.gather_planes(self.owned.contiguous(), counts)
         return None if g is None else g.numpy()
 
+    def copy_to_host(self) -> None:
+        """Per-rank device-to-host copy of the owned block through one reused pinned
+        buffer of a few planes (the reference's timed DtH without the rank-0 merge; host
+        memory O(planes) at any grid size).  Returns None."""
+        self.sync_halos()
+        self._sync()
+        own = self.owned
+        if own.device.type != "cuda":
+            return None
+        n0 = own.shape[0]
+        per = max(1, (64 << 20) // max(own[0].numel() * own.element_size(), 1))
+        buf = torch.empty((min(per, n0),) + tuple(own.shape[1:]), dtype=own.dtype,
+                          pin_memory=True)
+        for z0 in range(0, n0, per):
+            z1 = min(n0, z0 + per)
+            buf[:z1 - z0].copy_(own[z0:z1], non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+        return None
+
     def gather_with_ghosts(self) -> np.ndarray | None:
         """Rank 0: every rank's slab INCLUDING its ghost planes, concatenated in rank
         order — the reference's multi-GPU result.bin layout (each rank's Nx*Ny*(_Nz+6)
@@ -792,8 +811,13 @@ class Solver:
         self._sync()
         local = self.owned.detach().to(torch.float64).cpu().numpy()
         box0 = [s for s, _ in self.cd.global_box()]
-        return aio.save_checkpoint(prefix, self.comm.rank, local, self.d.start, self.meta(),
+        path = aio.save_checkpoint(prefix, self.comm.rank, local, self.d.start, self.meta(),
                                    box0=box0)
+        self.comm.barrier()  # every shard written before stale ones are removed
+        if self.comm.rank == 0:
+            aio.remove_stale_shards(prefix, self.comm.size)
+        self.comm.barrier()
+        return path
 
     def load_checkpoint(self, prefix):
         """Restart from shards written by ANY decomposition of the same grid."""

@@ -84,6 +84,20 @@ def save_checkpoint(prefix, rank: int, local: np.ndarray, plane0: int, meta: dic
     return path
 
 
+def remove_stale_shards(prefix, world: int) -> list:
+    """Delete PREFIX.rankNNNNN.ckpt for every N >= world: shards of an earlier run on more
+    ranks under the same prefix would otherwise be read back with this run's (call on one
+    rank, after every rank's shard is written).  Returns the removed paths."""
+    prefix = Path(prefix)
+    gone = []
+    for p in prefix.parent.glob(f"{prefix.name}.rank*.ckpt"):
+        tail = p.name[len(prefix.name) + len(".rank"):-len(".ckpt")]
+        if tail.isdigit() and int(tail) >= world:
+            p.unlink()
+            gone.append(p)
+    return gone
+
+
 def read_header(path):
     with open(path, "rb") as f:
         if f.read(len(MAGIC)) != MAGIC:
@@ -117,6 +131,9 @@ def load_checkpoint_box(prefix, box0, extents):
             # e.g. stale shards of an earlier run on more ranks under the same prefix
             raise ValueError(f"{path}: shard of another checkpoint (it {h.get('it')} vs "
                              f"{meta.get('it')}) under the prefix {prefix}")
+        if "world" in h and int(h.get("rank", 0)) >= int(h["world"]):
+            raise ValueError(f"{path}: shard of rank {h.get('rank')} in a {h['world']}-rank "
+                             f"checkpoint")
         dt = np.dtype(h["dtype"]).newbyteorder("<")
         shape = tuple(h["shape"])
         sb = h.get("box0", [h["plane0"]] + [0] * (len(shape) - 1))
@@ -138,6 +155,9 @@ def load_checkpoint_box(prefix, box0, extents):
     total = 1
     for e in extents:
         total *= e
+    if covered > total:
+        raise ValueError(f"checkpoint {prefix}: overlapping shards cover box {box0} + "
+                         f"{extents} {covered / total:.2f} times (shards of two runs?)")
     if out is None or covered != total:
         raise ValueError(f"checkpoint {prefix} does not cover box {box0} + {extents}")
     return out, meta

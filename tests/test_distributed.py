@@ -276,3 +276,42 @@ def test_bench_decomposition_tuning_gloo():
     assert len(trials) == len(cands) and all(isinstance(v, float) for v in trials.values())
     assert diag["halo_exchange_ms"] > 0 and diag["halo_link_MB"] > 0
     assert diag["step_ms_without_exchange"] > 0
+
+
+def _ckpt_steps(comm, prefix, steps):
+    model, grid, ic = _make("diff3")
+    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic)
+    s.run(iters=steps)
+    s.save_checkpoint(prefix)
+    return s.it
+
+
+def test_checkpoint_fewer_ranks_removes_stale_shards(tmp_path):
+    """A checkpoint written by 2 ranks under a prefix that holds an earlier 3-rank
+    checkpoint: the writer removes the stale rank-2 shard, so a restart reads the new
+    checkpoint instead of failing on a mix of the two."""
+    from multigpu_advectiondiffusion_amd.utils import io as aio
+    prefix = str(tmp_path / "ck")
+    spawn_local(3, _ckpt_steps, prefix, 2)
+    spawn_local(2, _ckpt_steps, prefix, 3)
+    shards = aio.list_shards(prefix)
+    assert len(shards) == 2
+    model, grid, ic = _make("diff3")
+    s = Solver(model, grid, dtype=torch.float64, device="cpu", ic=ic)
+    meta = s.load_checkpoint(prefix)
+    assert meta["it"] == 3 and meta["world"] == 2
+
+
+def test_checkpoint_overlap_reported(tmp_path):
+    """Two shards covering the same cells (same it/t, e.g. copied in by hand) are reported
+    as overlapping, not as 'does not cover'."""
+    import shutil
+    from multigpu_advectiondiffusion_amd.utils import io as aio
+    prefix = tmp_path / "ck"
+    model, grid, ic = _make("diff3")
+    s = Solver(model, grid, dtype=torch.float64, device="cpu", ic=ic)
+    s.run(iters=1)
+    s.save_checkpoint(prefix)
+    shutil.copy(aio.list_shards(prefix)[0], tmp_path / "ck.rank00007.ckpt")
+    with pytest.raises(ValueError, match="rank 7|overlapping"):
+        s.load_checkpoint(prefix)

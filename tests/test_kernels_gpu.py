@@ -363,3 +363,37 @@ def test_watchdog_catches_an_isolated_nan_gpu():
     s.owned[7, 9, 11] = float("nan")
     with pytest.raises(FloatingPointError):
         s.check_finite()
+
+
+@pytest.mark.parametrize("tx", [32, 64])
+@pytest.mark.parametrize("shape", [(37, 45, 131), (40, 38, 70), (23, 70, 33)])
+def test_burgers3d_v9_tile_rows_vs_reference(tx, shape):
+    """Both v9 tile shapes (64-cell rows x 8, 32-cell rows x 16 — two rows per wave) against
+    the fp64 reference on odd sizes (partial x and y tiles), and bitwise equal to each
+    other."""
+    nz, ny, nx = shape
+    sx = (nx + 31) // 32 * 32
+    inp = _smooth3(nz, ny, sx, 21, torch.float64)
+    u0 = _smooth3(nz, ny, sx, 22, torch.float64)
+    rd = (1 / 0.02, 1 / 0.03, 1 / 0.025)
+    vv = tuple(0.01 * r * r for r in rd)
+    exp = u0.clone()
+    ref.burgers3d_stage(inp, u0, exp, nx, ny, 3, nz - 3, 3, True, *rd, *vv, 1e-3, 0.75, 0.25)
+    lib = _lib.require()
+    kw = dict(nx=nx, ny=ny, k0=3, k1=nz - 3, border=3, weno_z=True, rdx=rd[0], rdy=rd[1],
+              rdz=rd[2], vx=vv[0], vy=vv[1], vz=vv[2], dt=1e-3, a=0.75, b=0.25)
+    outs = {}
+    old_v, old_t = lib.advdiff_set_b3_ver(9), lib.advdiff_set_b3_tx(tx)
+    try:
+        for t in (tx, 96 - tx):
+            lib.advdiff_set_b3_tx(t)
+            g0 = u0.to(DEV)
+            gout = g0.clone()
+            stencil.burgers3d_stage(inp.to(DEV), g0, gout, **kw)
+            torch.cuda.synchronize()
+            outs[t] = gout.cpu()
+    finally:
+        lib.advdiff_set_b3_ver(old_v)
+        lib.advdiff_set_b3_tx(old_t)
+    assert (outs[tx] - exp).abs().max().item() < 1e-11
+    assert torch.equal(outs[32], outs[64])

@@ -463,3 +463,63 @@ def test_native_warmup_keeps_the_result(tmp_path, app, args, world, extra):
         os.environ.update(env)
     assert np.array_equal(np.fromfile(tmp_path / "a.bin", dtype=np.float32),
                           np.fromfile(tmp_path / "b.bin", dtype=np.float32)), txt[-400:]
+
+
+def test_native_watchdog_ends_survivor_without_launcher():
+    """Comm watchdog (SURVEY §5 failure detection): two native socket ranks started as
+    plain processes (NO fail-fast launcher); rank 1 is stopped (SIGSTOP: alive, sockets
+    open, silent) mid-run.  Rank 0, blocked in its next exchange, must end on its own with
+    the watchdog's exit code 6 within ADVDIFF_COMM_TIMEOUT (+ margin), not hang."""
+    import signal
+    import sys
+    import time
+    from multigpu_advectiondiffusion_amd.launch import _child_env
+    exe = ROOT / "bin" / "diffusion3d"
+    port = free_port_block(2 + 18)
+    cmd = [str(exe), "1", "1", "1", "1", "64", "60", "56", "200000", "--ic", "sine",
+           "--transport", "socket"]
+    procs = []
+    for r in range(2):
+        env = _child_env(r, 2, port, cpu=False)
+        env.update(ADVDIFF_SHARE_GPU="1", ADVDIFF_COMM_TIMEOUT="10")
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    try:
+        time.sleep(8.0)  # both ranks are stepping (200000 steps take minutes)
+        assert procs[0].poll() is None and procs[1].poll() is None, [p.poll() for p in procs]
+        os.kill(procs[1].pid, signal.SIGSTOP)
+        t0 = time.monotonic()
+        try:
+            _, err = procs[0].communicate(timeout=60)
+        except subprocess.TimeoutExpired:
+            pytest.fail("rank 0 still blocked 60 s after its peer stopped")
+        waited = time.monotonic() - t0
+        assert procs[0].returncode == 6, (procs[0].returncode, err[-1500:])
+        assert "[watchdog] rank 0" in err and "no progress" in err, err[-1500:]
+        assert waited < 40, waited
+        print(f"survivor exited {procs[0].returncode} after {waited:.1f} s", file=sys.stderr)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait(timeout=30)
+
+
+@pytest.mark.parametrize("app,args,model", [
+    ("diffusion3d", [1, 1, 1, 1, 60, 44, 36, 4], lambda: Diffusion(K=1.0, order=4)),
+    ("burgers3d", [0.01, 0.3, 2, 2, 2, 40, 36, 32], lambda: Burgers(viscosity=1e-5, weno="z", cfl=0.3)),
+])
+def test_native_field_memory_matches_python(tmp_path, app, args, model):
+    """--json reports the device bytes of the resident fields: the fused heat step keeps
+    u and its ping-pong partner only (2 fields, as solver.py and utils/sizing.py), the
+    per-stage Burgers step 3 — the same bytes as the Python solver's layout."""
+    import json
+    txt = _run(app, args, tmp_path / "r.bin", extra=["--json"])
+    rec = json.loads([ln for ln in txt.splitlines() if ln.startswith("{")][-1])
+    m = model()
+    shape = tuple(int(a) for a in args[4:7]) if app == "diffusion3d" else tuple(int(a) for a in args[5:8])
+    lengths = (1.0, 1.0, 1.0) if app == "diffusion3d" else (2.0, 2.0, 2.0)
+    s = Solver(m, Grid(shape, lengths), dtype=torch.float64, device="cuda",
+               ic="sine" if app == "diffusion3d" else "gaussian")
+    assert rec["device_field_bytes"] == s.memory_bytes(), (rec, s.memory_bytes())
+    assert rec["device_field_bytes"] == (2 if app == "diffusion3d" else 3) * s.u.numel() * 8
