@@ -13,15 +13,17 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from multigpu_advectiondiffusion_amd.ops import stencil  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("which", choices=["fused", "fused2", "stage", "burgers", "burgers_js"])
+ap.add_argument("which", choices=["fused", "fused2", "stage", "burgers", "burgers_js", "copy"])
 ap.add_argument("--n", type=int, default=512)
 ap.add_argument("--reps", type=int, default=5)
 a = ap.parse_args()
-n = a.n if a.which in ("fused", "fused2", "stage") else min(a.n, 256)
+n = a.n if a.which in ("fused", "fused2", "stage", "copy") else min(a.n, 256)
 u = torch.rand((n, n, n), dtype=torch.float64, device="cuda") * 0.5 + 0.1
 o = torch.rand_like(u)
 for _ in range(a.reps):
-    if a.which in ("fused", "fused2"):
+    if a.which == "copy":  # calibration: exactly n^3 x 8 B read and written
+        stencil.copy_box(o, u, n, n, n)
+    elif a.which in ("fused", "fused2"):
         R = 2 if a.which == "fused" else 1
         stencil.diffusion3d_step(u, o, nx=n, ny=n, k0=R, k1=n - R, zlo=R, zhi=n - R, border=R,
                                  order=2 * R, cx=1.0, cy=1.0, cz=1.0, dt=0.01)

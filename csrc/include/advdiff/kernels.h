@@ -201,6 +201,8 @@ int advdiff_set_step_edge(int on);
 // 3-D WENO5 stage kernel version (9 = default, 3 = the v3 fallback used for planes of
 // 2 GiB and more); returns the previous value.  Results agree to rounding (tests).
 int advdiff_set_b3_ver(int v);
+// fused heat step: forced z-chunk length (0 = automatic); returns the previous setting
+int advdiff_set_step_zchunk(int zc);
 // v9 tile row width: 64, 32 or 0 = chosen per plane shape (returns the previous setting)
 int advdiff_set_b3_tx(int v);
 // 2-D WENO5 stage kernel version (2 = the barrier-free wave-strip kernel, default; 1 = the

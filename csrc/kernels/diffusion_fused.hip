@@ -595,6 +595,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((
                                            q1, q2, q3);
 }
 
+// forced z-chunk length (ADVDIFF_STEP_ZCHUNK / advdiff_set_step_zchunk; 0 = the
+// pick_chunk_rounds model) — for chunk sweeps (bench/step_chunks.py)
+static int g_step_zchunk = -1;
+static int step_zchunk() {
+  if (g_step_zchunk < 0) g_step_zchunk = knob("STEP_ZCHUNK", 0);
+  return g_step_zchunk;
+}
+
 static int g_step_edge = -1;
 static int step_edge() {  // v3 edge tiles (axis_tile): ADVDIFF_STEP_EDGE / advdiff_set_step_edge
   if (g_step_edge < 0) g_step_edge = knob("STEP_EDGE", 1);
@@ -636,7 +644,9 @@ static hipError_t launch_step(const SArgs& a) {
   const int na = std::max(a.k1 - a.k0, 0), nb = std::max(a.k1b - a.k0b, 0);
   const long long slots = (long long)device_cus() * per_cu;
   StepSched sc{gx, gy, 0, 0, edge};
-  const int zc = pick_chunk_rounds(na + nb, (long long)gx * gy, slots, 4 * R, minc);
+  const int zforce = step_zchunk();
+  const int zc = zforce > 0 ? std::min(zforce, std::max(na, nb))
+                            : pick_chunk_rounds(na + nb, (long long)gx * gy, slots, 4 * R, minc);
   sc.gza = na > 0 ? div_up(na, zc) : 0;
   sc.zchunk = zc;
   const dim3 grid(gx, gy, sc.gza + (nb > 0 ? div_up(nb, zc) : 0));
@@ -708,6 +718,12 @@ static hipError_t dispatch_step(const SArgs& a) {
 extern "C" int advdiff_set_step_var(int v) {
   const int old = advdiff::step_var();
   advdiff::g_step_var = v;
+  return old;
+}
+
+extern "C" int advdiff_set_step_zchunk(int zc) {
+  const int old = advdiff::step_zchunk();
+  advdiff::g_step_zchunk = zc > 0 ? zc : 0;
   return old;
 }
 

@@ -159,6 +159,8 @@ def _load():
         lib.advdiff_set_step_edge.restype = c_int
         lib.advdiff_set_b3_ver.argtypes = [c_int]
         lib.advdiff_set_b3_ver.restype = c_int
+        lib.advdiff_set_step_zchunk.argtypes = [c_int]
+        lib.advdiff_set_step_zchunk.restype = c_int
         lib.advdiff_set_b3_tx.argtypes = [c_int]
         lib.advdiff_set_b3_tx.restype = c_int
         lib.advdiff_set_b2_ver.argtypes = [c_int]
