@@ -230,6 +230,9 @@ int advdiff_ipc_map(advdiff_ipc* c, const advdiff_ipc_addr* a, void** ptr);
 int advdiff_ipc_set_peer(advdiff_ipc* c, int peer, const advdiff_ipc_addr* peer_flags);
 int advdiff_ipc_put(int dtype, void* dst, int64_t dsy, int64_t dsz, const void* src,
                     int64_t ssy, int64_t ssz, int ni, int nj, int nk, void* stream);
+// channel ch (0..2) of the flag block: independent counters per (peer, channel)
+int advdiff_ipc_signal_ch(advdiff_ipc* c, int ch, const int* peers, int n, void* stream);
+int advdiff_ipc_wait_ch(advdiff_ipc* c, int ch, const int* peers, int n, void* stream);
 int advdiff_ipc_signal(advdiff_ipc* c, const int* peers, int n, void* stream);
 int advdiff_ipc_wait(advdiff_ipc* c, const int* peers, int n, void* stream);
 // close every peer mapping except the flag blocks (collective, no put in flight): after

@@ -36,10 +36,13 @@
 // missing link; the bench's ipc preflight (IpcPeers.preflight: stale-cache pattern round
 // trips between every pair of ranks) and its bitwise N-rank-vs-1-GPU check can.
 //
-// Flags block of a rank (device memory, exported): recv[world] (written by the peers: the
-// number of messages peer q has delivered), sent[world] (messages delivered to q, local),
-// expect[world][kIpcWaitWgs] (messages consumed from q, per wait workgroup), err (wait
-// timeouts).
+// Flags block of a rank (device memory, exported): kIpcChannels independent channels of
+// { recv[world] (written by the peers: the number of messages peer q has delivered on this
+// channel), sent[world] (messages delivered to q, local), expect[world][kIpcWaitWgs]
+// (messages consumed from q, per wait workgroup) }, then err (wait timeouts).  Channel 0
+// carries the symmetric neighbour exchanges; the striped (relayed) slab exchange uses 1
+// for source -> helper and 2 for helper -> destination, so a pair of ranks that meets in
+// several roles of one exchange never mixes its counts.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -53,24 +56,33 @@
 #include "advdiff/kernels.h"
 #include "launch.hpp"
 
+namespace advdiff {
+constexpr int kIpcWaitWgs = 16;   // wait workgroups: >= 2 per XCD (8 XCDs, round-robin)
+constexpr int kIpcChannels = 3;
+}  // namespace advdiff
+
 struct advdiff_ipc {
   int world = 1, rank = 0;
-  uint64_t* block = nullptr;          // recv | sent | expect | err
-  std::vector<uint64_t*> peer_cell;   // peer q's recv[rank] (mapped), or nullptr
+  uint64_t* block = nullptr;          // kIpcChannels x (recv | sent | expect), err
+  std::vector<uint64_t*> peer_block;  // peer q's flag block (mapped), or nullptr
   std::map<std::string, void*> opened;  // IPC handle bytes -> mapped base
   std::map<uintptr_t, hipIpcMemHandle_t> exported;  // allocation base -> handle
   std::mutex mu;
   size_t block_bytes = 0;
-  uint64_t* recv() const { return block; }
-  uint64_t* sent() const { return block + world; }
-  uint64_t* expect() const { return block + 2 * world; }  // [world][kIpcWaitWgs]
+  size_t chan_stride() const { return (2 + (size_t)advdiff::kIpcWaitWgs) * world; }
+  uint64_t* recv(int ch = 0) const { return block + ch * chan_stride(); }
+  uint64_t* sent(int ch = 0) const { return recv(ch) + world; }
+  uint64_t* expect(int ch = 0) const { return recv(ch) + 2 * world; }  // [world][kIpcWaitWgs]
+  // peer q's recv[rank] of channel ch (its block has our layout: same world)
+  uint64_t* peer_cell(int q, int ch) const {
+    return peer_block[q] ? peer_block[q] + ch * chan_stride() + rank : nullptr;
+  }
   unsigned long long* err() const;
 };
 
 namespace advdiff {
 
 constexpr int kIpcMaxPeers = 32;  // 3^3 - 1 = 26 neighbours of a direct exchange
-constexpr int kIpcWaitWgs = 16;   // wait workgroups: >= 2 per XCD (8 XCDs, round-robin)
 
 struct IpcSignalArgs {
   uint64_t* remote[kIpcMaxPeers];  // peer's recv[rank]
@@ -159,7 +171,7 @@ static uint64_t wait_timeout_ticks() {
 }  // namespace advdiff
 
 unsigned long long* advdiff_ipc::err() const {
-  return (unsigned long long*)(block + 2 * world + (size_t)world * advdiff::kIpcWaitWgs);
+  return (unsigned long long*)(block + advdiff::kIpcChannels * chan_stride());
 }
 
 extern "C" int advdiff_ipc_create(int world, int rank, advdiff_ipc** out) {
@@ -167,8 +179,9 @@ extern "C" int advdiff_ipc_create(int world, int rank, advdiff_ipc** out) {
   auto* c = new advdiff_ipc;
   c->world = world;
   c->rank = rank;
-  c->peer_cell.assign(world, nullptr);
-  const size_t bytes = ((2 + (size_t)advdiff::kIpcWaitWgs) * world + 1) * sizeof(uint64_t);
+  c->peer_block.assign(world, nullptr);
+  const size_t bytes =
+      (advdiff::kIpcChannels * (2 + (size_t)advdiff::kIpcWaitWgs) * world + 1) * sizeof(uint64_t);
   c->block_bytes = bytes < 4096 ? 4096 : bytes;
   // Uncached device memory: a peer GPU's release store lands in this block WHILE the wait
   // kernel spins on it, and only fine-grained / uncached memory promises cross-device
@@ -260,7 +273,7 @@ extern "C" int advdiff_ipc_set_peer(advdiff_ipc* c, int peer, const advdiff_ipc_
   void* base = nullptr;
   const int e = advdiff_ipc_map(c, flags, &base);
   if (e != hipSuccess) return e;
-  c->peer_cell[peer] = (uint64_t*)base + c->rank;  // the peer's recv[rank]
+  c->peer_block[peer] = (uint64_t*)base;
   return hipSuccess;
 }
 
@@ -289,26 +302,30 @@ extern "C" int advdiff_ipc_put(int dtype, void* dst, int64_t dsy, int64_t dsz, c
   return hipGetLastError();
 }
 
-extern "C" int advdiff_ipc_signal(advdiff_ipc* c, const int* peers, int n, void* stream) {
+extern "C" int advdiff_ipc_signal_ch(advdiff_ipc* c, int ch, const int* peers, int n,
+                                     void* stream) {
   using namespace advdiff;
   if (n <= 0) return hipSuccess;
-  if (c == nullptr || peers == nullptr || n > kIpcMaxPeers) return hipErrorInvalidValue;
+  if (c == nullptr || peers == nullptr || n > kIpcMaxPeers || ch < 0 || ch >= kIpcChannels)
+    return hipErrorInvalidValue;
   IpcSignalArgs a{};
   a.n = n;
   for (int q = 0; q < n; ++q) {
     const int p = peers[q];
-    if (p < 0 || p >= c->world || c->peer_cell[p] == nullptr) return hipErrorInvalidValue;
-    a.remote[q] = c->peer_cell[p];
-    a.sent[q] = c->sent() + p;
+    if (p < 0 || p >= c->world || c->peer_cell(p, ch) == nullptr) return hipErrorInvalidValue;
+    a.remote[q] = c->peer_cell(p, ch);
+    a.sent[q] = c->sent(ch) + p;
   }
   hipLaunchKernelGGL(ipc_signal_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
   return hipGetLastError();
 }
 
-extern "C" int advdiff_ipc_wait(advdiff_ipc* c, const int* peers, int n, void* stream) {
+extern "C" int advdiff_ipc_wait_ch(advdiff_ipc* c, int ch, const int* peers, int n,
+                                   void* stream) {
   using namespace advdiff;
   if (n <= 0) return hipSuccess;
-  if (c == nullptr || peers == nullptr || n > kIpcMaxPeers) return hipErrorInvalidValue;
+  if (c == nullptr || peers == nullptr || n > kIpcMaxPeers || ch < 0 || ch >= kIpcChannels)
+    return hipErrorInvalidValue;
   IpcWaitArgs a{};
   a.n = n;
   a.err = c->err();
@@ -316,11 +333,19 @@ extern "C" int advdiff_ipc_wait(advdiff_ipc* c, const int* peers, int n, void* s
   for (int q = 0; q < n; ++q) {
     const int p = peers[q];
     if (p < 0 || p >= c->world || p == c->rank) return hipErrorInvalidValue;
-    a.flag[q] = c->recv() + p;
-    a.expect[q] = c->expect() + (size_t)p * kIpcWaitWgs;
+    a.flag[q] = c->recv(ch) + p;
+    a.expect[q] = c->expect(ch) + (size_t)p * kIpcWaitWgs;
   }
   hipLaunchKernelGGL(ipc_wait_kernel, dim3(kIpcWaitWgs), dim3(64), 0, (hipStream_t)stream, a);
   return hipGetLastError();
+}
+
+extern "C" int advdiff_ipc_signal(advdiff_ipc* c, const int* peers, int n, void* stream) {
+  return advdiff_ipc_signal_ch(c, 0, peers, n, stream);
+}
+
+extern "C" int advdiff_ipc_wait(advdiff_ipc* c, const int* peers, int n, void* stream) {
+  return advdiff_ipc_wait_ch(c, 0, peers, n, stream);
 }
 
 // Close every peer mapping except the flag blocks (call with no put in flight,
@@ -333,9 +358,9 @@ extern "C" int advdiff_ipc_reset(advdiff_ipc* c) {
   for (auto it = c->opened.begin(); it != c->opened.end();) {
     bool flags = false;  // a peer's flag block: keep it (the counters live there)
     // (a peer's block is as large as ours: same world size)
-    for (uint64_t* cell : c->peer_cell)
-      if (cell && (char*)cell >= (char*)it->second &&
-          (char*)cell < (char*)it->second + c->block_bytes)
+    for (uint64_t* blk : c->peer_block)
+      if (blk && (char*)blk >= (char*)it->second &&
+          (char*)blk < (char*)it->second + c->block_bytes)
         flags = true;
     if (flags) {
       ++it;

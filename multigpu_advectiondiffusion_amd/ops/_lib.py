@@ -97,6 +97,8 @@ _IPC_SIGS = {
     "advdiff_ipc_put": [c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int,
                         c_vp],
     "advdiff_ipc_signal": [c_vp, ctypes.POINTER(c_int), c_int, c_vp],
+    "advdiff_ipc_signal_ch": [c_vp, c_int, ctypes.POINTER(c_int), c_int, c_vp],
+    "advdiff_ipc_wait_ch": [c_vp, c_int, ctypes.POINTER(c_int), c_int, c_vp],
     "advdiff_ipc_wait": [c_vp, ctypes.POINTER(c_int), c_int, c_vp],
     "advdiff_ipc_errors": [c_vp, ctypes.POINTER(ctypes.c_longlong)],
     "advdiff_ipc_reset": [c_vp],
