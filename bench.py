@@ -137,12 +137,24 @@ def tune(make, cands, dt, dev, trial_steps=8, rounds=3):
     return best[1], trials
 
 
+STRIPE = 2  # relay helpers per face message of the striped ipc slab exchange
+
+
+def solver_transport(t):
+    """(transport, stripe) of a candidate name: "ipc+stripe" = ipc with relayed parts."""
+    return ("ipc", STRIPE) if t == "ipc+stripe" else (t, 0)
+
+
 def transports_for(comm, want: str):
     """Halo transports to consider (N > 1 on GPUs) and the ipc preflight record.
     want: "tune" (every transport of this Comm whose preflight passes), or one name."""
     if comm.size == 1 or comm.device.type != "cuda":
         return [comm.transport], None
     names = comm.transports() if want == "tune" else [want]
+    if want == "tune" and "ipc" in names:
+        from multigpu_advectiondiffusion_amd.parallel.ipc import stripe_plan
+        if any(stripe_plan(comm.size, STRIPE).values()):  # 7-8 ranks: idle links exist
+            names.append("ipc+stripe")
     pre = None
     if "ipc" in names:
         try:
@@ -151,7 +163,7 @@ def transports_for(comm, want: str):
             pre = f"failed: {type(e).__name__}: {e}"
             if comm.rank == 0:
                 print(f"bench: ipc transport rejected ({pre})", file=sys.stderr, flush=True)
-            names = [t for t in names if t != "ipc"]
+            names = [t for t in names if not t.startswith("ipc")]
             if not names:
                 raise SystemExit(f"bench: the requested ipc transport failed its preflight: {pre}")
     return names, pre
@@ -203,9 +215,12 @@ def halo_diag(s, reps=5, dt=None):
     s._sync()
     s.comm.barrier()
     ms = s.comm.allreduce_max((_t.perf_counter() - t0) / reps * 1e3)
+    parts = 1
+    if getattr(s.halo, "striped", False):
+        parts = 1 + min(len(h) for h in s.halo._plan.values())
     link = halo_link_bytes(s.cd.shape, s.pgrid, s.ghost, s.u.element_size(),
                            corners=s.cart and s.fused,
-                           direct=getattr(s.halo, "direct", True))
+                           direct=getattr(s.halo, "direct", True), stripe_parts=parts)
     # the same steps with the exchange switched off (ghosts go stale — run LAST, after
     # the validation): the compute-only step time; the timed ms/step minus this is the
     # part of the exchange the overlap did not hide
@@ -298,8 +313,9 @@ def run(args):
     single = Comm(device=str(dev)) if dev.type == "cuda" else Comm(device="cpu")
     transports, preflight = transports_for(comm, args.transport)
 
-    def cands_of(grids):
-        return [(p, t) for p in grids for t in transports]
+    def cands_of(grids):  # striping applies to slabs only
+        return [(p, t) for p in grids for t in transports
+                if t != "ipc+stripe" or p in (None, "slab") or tuple(p)[1:] == (1, 1)]
 
     # ---- headline: 3-D heat, FD4, fp64, sine IC -------------------------------------
     grid_of = ((lambda b: weak_scaling_grid(b, n)) if args.scaling == "weak"
@@ -311,8 +327,9 @@ def run(args):
     dt = model.stable_dt()
 
     def make_heat(p, t, m=model, c=comm):
+        tr, st = solver_transport(t) if t else (None, 0)
         return Solver(m, grid, c, dtype=torch.float64, ic="sine",
-                      overlap=not args.no_overlap, decomp=p, transport=t)
+                      overlap=not args.no_overlap, decomp=p, transport=tr, stripe=st)
 
     ashape = tuple(reversed(shape))
     if args.decomp == "tune":
@@ -345,8 +362,8 @@ def run(args):
             raise SystemExit(f"bench validation failed: {n}-rank heat solution differs from "
                              f"the 1-GPU solution ({rec})")
 
-    link = {"ipc": "ipc device puts", "rccl": "RCCL", "host": "host-staged"}.get(transport,
-                                                                                 transport)
+    link = {"ipc": "ipc device puts", "rccl": "RCCL", "host": "host-staged",
+            "ipc+stripe": "ipc device puts striped over idle links"}.get(transport, transport)
     result = {
         "metric": METRIC,
         "value": round(mlups, 1),
@@ -410,8 +427,9 @@ def run(args):
         bdt = bmodel.stable_dt()
 
         def make_burgers(p, t, c=comm):
+            tr, st = solver_transport(t) if t else (None, 0)
             return Solver(bmodel, bgrid, c, dtype=torch.float64, ic="gaussian",
-                          overlap=not args.no_overlap, decomp=p, transport=t)
+                          overlap=not args.no_overlap, decomp=p, transport=tr, stripe=st)
         if args.decomp == "tune":
             bgrids = candidate_proc_grids(n, tuple(reversed(bshape)), bmodel.radius, 8)
         else:

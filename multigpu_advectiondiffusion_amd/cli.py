@@ -74,6 +74,9 @@ def build_parser():
     ap.add_argument("--exchange", choices=["u", "lu"], default="u",
                     help="halo payload: u (stage output) or lu (the reference's RHS exchange "
                          "with redundant ghost-plane updates; slab, PyTorch ops)")
+    ap.add_argument("--stripe", type=int, default=None,
+                    help="ipc slab halos: relay part of every face message through up to N "
+                         "helper ranks over idle xGMI links (default: ADVDIFF_STRIPE or 0)")
     ap.add_argument("--decomp", default=None,
                     help="process grid: slab (default), auto, or PZxPYxPX / PYxPX")
     ap.add_argument("--transport", choices=["rccl", "ipc", "host"], default=None,
@@ -189,7 +192,7 @@ def main(argv=None) -> int:
     solver, htod_s = fenced(lambda: Solver(
         model, grid, comm, dtype=dtype, ic=ic, overlap=not ns.no_overlap, t0=t0,
         check_every=ns.check_every, decomp=ns.decomp, integrator=ns.integrator,
-        kernel=ns.kernel, exchange=ns.exchange))
+        kernel=ns.kernel, exchange=ns.exchange, stripe=ns.stripe))
     if ns.geometry:  # decomposition only (no steps), one JSON line per rank in rank order
         geo = {"rank": comm.rank, "world": comm.size, "pgrid": list(solver.pgrid),
                "global_box": [list(b) for b in solver.cd.global_box()],

@@ -186,15 +186,21 @@ def parse_proc_grid(spec, world: int, shape_array: tuple, ghost: int) -> tuple:
 
 
 def halo_link_bytes(shape_array: tuple, pgrid: tuple, ghost: int, elem: int,
-                    corners: bool, direct: bool = True) -> float:
+                    corners: bool, direct: bool = True, stripe_parts: int = 1) -> float:
     """Bytes one rank moves over its busiest xGMI link per exchange (upper bound over
     ranks).  Every GPU pair of an 8-GPU node has its own point-to-point link, so messages
     to different neighbours overlap.  corners (the fused step) with direct = True: one
     phase, edges and corners straight from the diagonal neighbours, so the busiest link
     carries the largest face; direct = False (the phased exchange: axis by axis, fastest
     first, each phase carrying the ghosts of the axes before it): the phases run one after
-    another, so their per-phase maxima add up."""
+    another, so their per-phase maxima add up.
+    stripe_parts (slabs, parallel/ipc.py stripe_rows): each face in that many parts, the
+    direct one 2/(k+1) of the bytes and each relayed one 1/(k+1) crossing two links one
+    after the other — the critical path carries 2/(k+1) of the face (k = 2: 2/3)."""
     dims = len(shape_array)
+    if stripe_parts > 1 and all(p == 1 for p in pgrid[1:]):
+        return halo_link_bytes(shape_array, pgrid, ghost, elem, corners, direct) * \
+            2.0 / (stripe_parts + 1)
     local = [-(-n // p) for n, p in zip(shape_array, pgrid)]  # largest block
     split = [a for a in range(dims) if pgrid[a] > 1]
     if corners and direct:

@@ -43,6 +43,23 @@ class PendingExchange:
             self.finish = None
 
 
+def _start_ipc_routed(comm, comm_stream, phases, after_event=None) -> PendingExchange:
+    """Like _start_ipc for phases of one-way-capable routes: phases = [(channel, {peer:
+    (send_view | None, recv_view | None)})], run in order on the comm stream."""
+    cur = torch.cuda.current_stream()
+    cs = comm_stream or cur
+    if after_event is None:
+        after_event = torch.cuda.Event()
+        after_event.record(cur)
+    cs.wait_event(after_event)
+    ipc = comm.ipc()
+    for ch, pairs in phases:
+        ipc.route(pairs, cs, ch)
+    done = torch.cuda.Event()
+    done.record(cs)
+    return PendingExchange([], cs, lambda: torch.cuda.current_stream().wait_event(done))
+
+
 def _start_ipc(comm, comm_stream, phases, after_event=None) -> PendingExchange:
     """Device puts into the peers' ghost cells (parallel/ipc.py) on the comm stream after
     `after_event`, phases in order; the returned handle joins the current stream."""
@@ -66,12 +83,84 @@ def _ipc_on(halo, field) -> bool:
 
 class SlabHalo:
     def __init__(self, comm, decomp: SlabDecomposition, comm_stream=None,
-                 transport: str | None = None):
-        """transport: "ipc", "rccl" or "host" (None: the Comm's default, Comm.transport)."""
+                 transport: str | None = None, stripe: int = 0):
+        """transport: "ipc", "rccl" or "host" (None: the Comm's default, Comm.transport).
+        stripe (ipc, 3-D fields): up to this many relay helpers per face message — part
+        of every message goes source -> helper -> destination over the node's otherwise
+        idle xGMI links (parallel/ipc.py stripe_plan; 8 ranks: 1 helper each, the face
+        then crosses the busiest link as 2/3 of its bytes).  0: direct messages only."""
         self.comm = comm
         self.d = decomp
         self.comm_stream = comm_stream
         self.transport = transport or (comm.transport if comm is not None else None)
+        self.parity = 0  # striped: which of the two relay buffer sets the next exchange uses
+        self._plan = None
+        self._fwd = {}
+        if stripe and self.transport == "ipc" and comm is not None and comm.size > 1:
+            import os
+            from .ipc import stripe_plan
+            # ADVDIFF_STRIPE_SHARED=1 (tests): helpers may share links, so the relay
+            # mechanism runs on fewer ranks than the 7-8 that have idle links for it
+            plan = stripe_plan(comm.size, stripe,
+                               exclusive_links=os.environ.get("ADVDIFF_STRIPE_SHARED") != "1")
+            if any(plan.values()):
+                self._plan = plan
+
+    @property
+    def striped(self) -> bool:
+        return self._plan is not None
+
+    def _fwd_buf(self, key, like, shape):
+        b = self._fwd.get(key)
+        if b is None or tuple(b.shape) != tuple(shape) or b.dtype != like.dtype:
+            b = torch.zeros(shape, dtype=like.dtype, device=like.device)
+            self._fwd[key] = b
+        return b
+
+    def _stripe_phases(self, field, parity):
+        """The two phases of a striped exchange for this rank: channel 1 = the direct
+        parts to / from the neighbours and the relayed parts into the helpers' buffers,
+        channel 2 = the helpers' forwards into the destinations' ghost rows.  Parts are
+        row ranges of the G ghost planes (parallel/ipc.py stripe_rows).  The relay buffers
+        alternate between two sets by exchange parity: a source's next put into a set
+        comes only after the destination consumed that set's previous forward (it needed
+        it for the step whose output the source now sends), so no acknowledgement is
+        needed — the same argument as the direct puts'."""
+        from .ipc import stripe_rows
+        d, me = self.d, self.comm.rank
+        p1, p2 = {}, {}
+
+        def add(ph, peer, send=None, recv=None):
+            s0, r0 = ph.get(peer, (None, None))
+            ph[peer] = (send if send is not None else s0, recv if recv is not None else r0)
+        rows = field.shape[1]
+        for (src, dst), hs in self._plan.items():
+            if me != src and me != dst and me not in hs:
+                continue
+            parts = stripe_rows(rows, 1 + len(hs))
+            up = dst == src + 1  # the message goes to the upper neighbour
+            if me == src:
+                s0, s1 = d.send_upper() if up else d.send_lower()
+                (a, b) = parts[0]
+                add(p1, dst, send=field[s0:s1, a:b])
+                for h, (a, b) in zip(hs, parts[1:]):
+                    add(p1, h, send=field[s0:s1, a:b])
+            if me == dst:
+                r0, r1 = d.recv_lower() if up else d.recv_upper()
+                (a, b) = parts[0]
+                add(p1, src, recv=field[r0:r1, a:b])
+                for h, (a, b) in zip(hs, parts[1:]):
+                    add(p2, h, recv=field[r0:r1, a:b])
+            if me in hs:
+                (a, b) = parts[1 + hs.index(me)]
+                buf = self._fwd_buf((src, dst, parity), field,
+                                    (d.ghost, b - a, field.shape[2]))
+                add(p1, src, recv=buf)
+                add(p2, dst, send=buf)
+        return p1, p2
+
+    def _use_stripes(self, field) -> bool:
+        return self._plan is not None and field.is_cuda and field.dim() == 3
 
     def _ops(self, field: torch.Tensor):
         d = self.d
@@ -142,8 +231,15 @@ class SlabHalo:
 
     def prepare(self, field: torch.Tensor) -> None:
         """Collective, outside any graph capture: learn the peers' receive addresses of
-        this field's exchange (ipc transport; a no-op otherwise)."""
-        if _ipc_on(self, field):
+        this field's exchange (ipc transport; a no-op otherwise) — for both relay buffer
+        sets when striped (a graph replays exchanges of both parities)."""
+        if _ipc_on(self, field) and self._use_stripes(field):
+            ipc = self.comm.ipc()
+            for par in (0, 1):
+                p1, p2 = self._stripe_phases(field, par)
+                ipc._resolve_pairs(1, p1)
+                ipc._resolve_pairs(2, p2)
+        elif _ipc_on(self, field):
             self.comm.ipc()._resolve(self._ipc_msgs(field))
 
     def start(self, field: torch.Tensor, after_event=None) -> PendingExchange | None:
@@ -153,6 +249,11 @@ class SlabHalo:
         (or after all work currently queued on the current stream)."""
         if self.comm.size == 1:
             return None
+        if _ipc_on(self, field) and self._use_stripes(field):
+            p1, p2 = self._stripe_phases(field, self.parity)
+            self.parity ^= 1
+            return _start_ipc_routed(self.comm, self.comm_stream, [(1, p1), (2, p2)],
+                                     after_event)
         if _ipc_on(self, field):
             return _start_ipc(self.comm, self.comm_stream, [self._ipc_msgs(field)], after_event)
         ops = self._ops(field)

@@ -29,8 +29,8 @@ import torch.distributed as dist
 from ..ops import _lib
 from ..ops.stencil import _dtype_code
 
-# IpcAddr (80 B) | rsy, rsz (i64) | ni, nj, nk, dtype (i32) | call (u64)
-_ANN = struct.Struct("<80sqqiiiiQ")
+# IpcAddr (80 B) | rsy, rsz (i64) | ni, nj, nk, dtype (i32) | call (u64) | has_recv, has_send
+_ANN = struct.Struct("<80sqqiiiiQii")
 
 
 def _box_geom(t: torch.Tensor):
@@ -98,43 +98,68 @@ class IpcPeers:
         return [bytes(r.cpu().numpy().tobytes()) for r in recvs]
 
     def _resolve(self, msgs):
-        """Peer receive (pointer, sy, sz) of every message; handshake on first use."""
-        out, miss = [None] * len(msgs), []
-        for q, (peer, send, recv) in enumerate(msgs):
-            self._calls[peer] = self._calls.get(peer, 0) + 1
-            key = (peer, send.data_ptr(), recv.data_ptr(), tuple(send.shape))
-            d = self._dest.get(key)
-            if d is None:
-                miss.append(q)
+        """Peer receive (pointer, sy, sz) of every message of a symmetric exchange
+        (channel 0); handshake on first use."""
+        pairs = {peer: (send, recv) for peer, send, recv in msgs}
+        dests = self._resolve_pairs(0, pairs)
+        return [dests[peer] for peer, _, _ in msgs]
+
+    def _resolve_pairs(self, ch, pairs):
+        """pairs = {peer: (send_view | None, recv_view | None)} of one exchange phase on
+        flag channel `ch` (at most one message each way per peer; a phase may be one-way
+        for a pair, as the striped exchange's relay hops are).  Returns {peer: (pointer,
+        sy, sz) of the peer's receive box for my send, or None}.  First use of a pattern:
+        both ranks of the pair swap announcements of their receive boxes (every rank of
+        a pair runs the same phase sequence, so both miss or both hit)."""
+        out, miss = {}, []
+        for peer, (send, recv) in sorted(pairs.items()):
+            ck = (ch, peer)
+            self._calls[ck] = self._calls.get(ck, 0) + 1
+            key = (ch, peer, 0 if send is None else send.data_ptr(),
+                   () if send is None else tuple(send.shape),
+                   0 if recv is None else recv.data_ptr(),
+                   () if recv is None else tuple(recv.shape))
+            if key in self._dest:
+                out[peer] = self._dest[key]
             else:
-                out[q] = d
+                miss.append((peer, key))
         if not miss:
             return out
         anns, peers = [], []
-        for q in miss:
-            peer, send, recv = msgs[q]
+        for peer, _ in miss:
+            send, recv = pairs[peer]
             a = _lib.IpcAddr()
-            _lib.check(self.lib.advdiff_ipc_describe(self.ctx, recv.data_ptr(), ctypes.byref(a)),
-                       "advdiff_ipc_describe")
-            ni, nj, nk, sy, sz = _box_geom(recv)
-            anns.append(_ANN.pack(bytes(a), sy, sz, ni, nj, nk, _dtype_code(recv),
-                                  self._calls[peer]))
+            geo = (0, 0, 0, 0, 0, 0)
+            if recv is not None:
+                _lib.check(self.lib.advdiff_ipc_describe(self.ctx, recv.data_ptr(),
+                                                         ctypes.byref(a)), "advdiff_ipc_describe")
+                ni, nj, nk, sy, sz = _box_geom(recv)
+                geo = (sy, sz, ni, nj, nk, _dtype_code(recv))
+            anns.append(_ANN.pack(bytes(a), geo[0], geo[1], geo[2], geo[3], geo[4], geo[5],
+                                  self._calls[(ch, peer)], int(recv is not None),
+                                  int(send is not None)))
             peers.append(peer)
         theirs = self._swap(peers, anns)
-        for q, raw in zip(miss, theirs):
-            peer, send, recv = msgs[q]
-            addr, rsy, rsz, ni, nj, nk, dt, call = _ANN.unpack(raw)
-            gi, gj, gk, _, _ = _box_geom(send)
-            if (ni, nj, nk, dt) != (gi, gj, gk, _dtype_code(send)) or call != self._calls[peer]:
+        for (peer, key), raw in zip(miss, theirs):
+            send, recv = pairs[peer]
+            addr, rsy, rsz, ni, nj, nk, dt, call, has_recv, has_send = _ANN.unpack(raw)
+            bad = call != self._calls[(ch, peer)] or bool(has_recv) != (send is not None) \
+                or bool(has_send) != (recv is not None)
+            if send is not None and not bad:
+                gi, gj, gk, _, _ = _box_geom(send)
+                bad = (ni, nj, nk, dt) != (gi, gj, gk, _dtype_code(send))
+            if bad:
                 raise RuntimeError(f"ipc: rank {self.comm.rank} and peer {peer} disagree on a "
-                                   f"halo message ({(gi, gj, gk)} vs {(ni, nj, nk)})")
-            a = _lib.IpcAddr.from_buffer_copy(addr)
-            ptr = ctypes.c_void_p()
-            _lib.check(self.lib.advdiff_ipc_map(self.ctx, ctypes.byref(a), ctypes.byref(ptr)),
-                       "advdiff_ipc_map")
-            d = (ptr.value, rsy, rsz)
-            self._dest[(peer, send.data_ptr(), recv.data_ptr(), tuple(send.shape))] = d
-            out[q] = d
+                                   f"halo message (channel {ch})")
+            d = None
+            if send is not None:
+                a = _lib.IpcAddr.from_buffer_copy(addr)
+                ptr = ctypes.c_void_p()
+                _lib.check(self.lib.advdiff_ipc_map(self.ctx, ctypes.byref(a),
+                                                    ctypes.byref(ptr)), "advdiff_ipc_map")
+                d = (ptr.value, rsy, rsz)
+            self._dest[key] = d
+            out[peer] = d
         return out
 
     def exchange(self, msgs, stream) -> None:
@@ -146,16 +171,35 @@ class IpcPeers:
         peers = [m[0] for m in msgs]
         if len(set(peers)) != len(peers):
             raise ValueError("ipc: one message per peer and exchange")
-        dests = self._resolve(msgs)
+        self.route({peer: (send, recv) for peer, send, recv in msgs}, stream, 0)
+
+    def route(self, pairs, stream, ch: int) -> None:
+        """One exchange phase on flag channel `ch`: pairs = {peer: (send_view | None,
+        recv_view | None)}.  Enqueues the puts of every send box into the peer's receive
+        box, the signal of the peers I sent to, and the wait for the peers that send to
+        me (channel ch counts only this phase kind, so a pair that meets in several
+        phases of one exchange never mixes its counts)."""
+        if not pairs:
+            return
+        dests = self._resolve_pairs(ch, pairs)
         sp = stream.cuda_stream
-        for (peer, send, _), (dptr, dsy, dsz) in zip(msgs, dests):
+        to = sorted(p for p, (snd, _) in pairs.items() if snd is not None)
+        frm = sorted(p for p, (_, rcv) in pairs.items() if rcv is not None)
+        for peer in to:
+            send = pairs[peer][0]
+            dptr, dsy, dsz = dests[peer]
             ni, nj, nk, ssy, ssz = _box_geom(send)
             _lib.check(self.lib.advdiff_ipc_put(_dtype_code(send), dptr, dsy, dsz,
                                                 send.data_ptr(), ssy, ssz, ni, nj, nk, sp),
                        "ipc put")
-        arr = (ctypes.c_int * len(peers))(*peers)
-        _lib.check(self.lib.advdiff_ipc_signal(self.ctx, arr, len(peers), sp), "advdiff_ipc_signal")
-        _lib.check(self.lib.advdiff_ipc_wait(self.ctx, arr, len(peers), sp), "advdiff_ipc_wait")
+        if to:
+            arr = (ctypes.c_int * len(to))(*to)
+            _lib.check(self.lib.advdiff_ipc_signal_ch(self.ctx, ch, arr, len(to), sp),
+                       "advdiff_ipc_signal")
+        if frm:
+            arr = (ctypes.c_int * len(frm))(*frm)
+            _lib.check(self.lib.advdiff_ipc_wait_ch(self.ctx, ch, arr, len(frm), sp),
+                       "advdiff_ipc_wait")
 
     def preflight(self, rounds: int = 3, box=(3, 24, 200)) -> dict:
         """Collective validation of the transport between EVERY pair of ranks, before a
@@ -229,3 +273,87 @@ class IpcPeers:
             self.comm.barrier()  # nobody unmaps while a peer may still put into it
             self.lib.advdiff_ipc_destroy(self.ctx)
             self.ctx = None
+
+
+# ----------------------------------------------------------------------------------
+# Striped slab exchange: a face message also travels over the node's idle links
+# ----------------------------------------------------------------------------------
+def stripe_plan(world: int, max_helpers: int, exclusive_links: bool = True) -> dict:
+    """Relay helpers of every slab halo message {(src, dst): [helper, ...]}, the same on
+    every rank.  A slab rank uses 2 of the 7 xGMI links of a fully connected 8-GPU node
+    (its neighbours'); part of each face message instead goes src -> helper -> dst over
+    two links no other route uses: (src, h) and (h, dst) must be neither a neighbour link
+    (those carry the direct parts) nor a link of another route.  Every message gets the
+    same number of helpers t (the exchange waits for its slowest message, so an extra
+    helper for some messages only would buy nothing): the largest t <= max_helpers for
+    which a depth-first search finds such an assignment (8 ranks: t = 1; 42 spare
+    directed links, two per route).
+    exclusive_links=False (tests: the mechanism on fewer ranks): any helper other than
+    the pair itself, links shared."""
+    msgs = [(r, r + 1) for r in range(world - 1)] + [(r + 1, r) for r in range(world - 1)]
+    direct = {(a, b) for a, b in msgs}
+    if not exclusive_links:
+        # per phase, each directed link at most once (one message per peer, direction and
+        # phase — what SlabHalo's phases need); greedy, helper counts may differ
+        p1, p2 = set(direct), set()
+        plan = {m: [] for m in msgs}
+        for _ in range(max(0, max_helpers)):
+            for s, d in msgs:
+                for h in range(world):
+                    if h in (s, d) or h in plan[(s, d)] or (s, h) in p1 or (h, d) in p2:
+                        continue
+                    p1.add((s, h))
+                    p2.add((h, d))
+                    plan[(s, d)].append(h)
+                    break
+        return plan
+    def cands(s, d):  # farthest from the pair first: deterministic
+        return sorted((h for h in range(world) if h not in (s, d)),
+                      key=lambda h: (-min(abs(h - s), abs(h - d)), h))
+
+    def solve(t):
+        order = [m for _ in range(t) for m in msgs]  # round-robin slots
+        helpers = {m: [] for m in msgs}
+        used = set(direct)
+        budget = [20000]  # search steps: give up (a smaller t) rather than search long
+
+        def dfs(i):
+            if i == len(order):
+                return True
+            budget[0] -= 1
+            if budget[0] < 0:
+                return False
+            s, d = order[i]
+            for h in cands(s, d):
+                if h in helpers[(s, d)] or (s, h) in used or (h, d) in used:
+                    continue
+                used.update(((s, h), (h, d)))
+                helpers[(s, d)].append(h)
+                if dfs(i + 1):
+                    return True
+                helpers[(s, d)].pop()
+                used.difference_update(((s, h), (h, d)))
+            return False
+        return helpers if dfs(0) else None
+
+    for t in range(max(0, max_helpers), 0, -1):
+        plan = solve(t)
+        if plan is not None:
+            return plan
+    return {m: [] for m in msgs}
+
+
+def stripe_rows(rows: int, k: int) -> list:
+    """Row ranges of the k parts of a message: the direct part 2/(k+1) of the rows, the
+    k-1 relayed parts (two hops each) 1/(k+1) each — every part then spends the same time
+    on the links (a relayed part crosses two links one after the other)."""
+    if k <= 1:
+        return [(0, rows)]
+    w = [2.0] + [1.0] * (k - 1)
+    tot = sum(w)
+    cuts, acc = [0], 0.0
+    for x in w[:-1]:
+        acc += x
+        cuts.append(int(round(rows * acc / tot)))
+    cuts.append(rows)
+    return [(a, b) for a, b in zip(cuts[:-1], cuts[1:])]

@@ -70,7 +70,7 @@ class Solver:
                  check_every: int = 0, fused: bool | None = None, decomp=None,
                  integrator: str = "ssprk3", kernel: str = "native",
                  device_dt: bool | None = None, exchange: str = "u",
-                 transport: str | None = None):
+                 transport: str | None = None, stripe: int | None = None):
         """decomp: process grid — None/"slab" (split the slowest axis only, the
         reference's layout), "auto" (smallest halo surface) or "PZxPYxPX" / a tuple in
         array axis order ((pz, py, px) in 3-D, (py, px) in 2-D).
@@ -84,6 +84,9 @@ class Solver:
         transport: halo transport of this solver ("ipc", "rccl", "host"; None = the
         Comm's, Comm.transport) — solvers with different transports can coexist on one
         Comm (bench.py tunes the transport this way).
+        stripe: ipc slab exchanges of 3-D fields relay part of every face message through
+        up to this many helper ranks over otherwise idle xGMI links (parallel/halo.py
+        SlabHalo; None = ADVDIFF_STRIPE, default 0 = direct only).
         exchange: "u" (default: exchange the stage OUTPUT's ghost planes) or "lu" (the
         reference's MultiGPU scheme, `MultiGPU/Diffusion3d_Baseline/main.c:209-288,300`:
         exchange the boundary planes of the RHS L(u) and advance the ghost planes
@@ -177,7 +180,11 @@ class Solver:
             self.full = self.cd.compute_box(model.border)
             self.interior, self.boundary = self.cd.split_boxes(model.border, G)
         else:
-            self.halo = SlabHalo(comm, self.d, self.comm_stream, transport=self.transport)
+            if stripe is None:
+                import os
+                stripe = int(os.environ.get("ADVDIFF_STRIPE", "0") or 0)
+            self.halo = SlabHalo(comm, self.d, self.comm_stream, transport=self.transport,
+                                 stripe=stripe if grid.dims == 3 else 0)
             self.full = self.d.compute_range(model.border)
             self.interior, blo, bhi = self.d.split_ranges(model.border, G)
             self.boundary = [blo, bhi]
@@ -516,7 +523,9 @@ class Solver:
         # multi-rank ipc: the graph also bakes in the peers' receive addresses, valid for the
         # IpcPeers epoch it was captured in
         ep = self._ipc_epoch()
-        key = (None if dt is None else float(dt), t_end, self.GRAPH_STEPS, self.u.data_ptr(), ep)
+        # striped halos: the relay buffer set of the first exchange is baked in as well
+        key = (None if dt is None else float(dt), t_end, self.GRAPH_STEPS, self.u.data_ptr(),
+               getattr(self.halo, "parity", 0), ep)
         g = getattr(self, "_graphs", {}).get(key)
         if g is not None:
             return g

@@ -230,3 +230,29 @@ def test_ipc_preflight_all_pairs_then_solver(world):
     for rec, h in out:
         assert rec["pairs"] == world * (world - 1) and not rec["cross_device"]
         assert h == h1
+
+
+def _run_striped(comm, kind, steps, graph):
+    model, grid, ic = _make(kind)
+    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, transport="ipc", stripe=2)
+    assert s.halo.striped
+    s.run(iters=steps, graph=graph)
+    g = s.gather()
+    assert comm.ipc().errors() == 0
+    return None if g is None else g.copy()
+
+
+@pytest.mark.parametrize("kind", ["diff3", "burg3"])
+@pytest.mark.parametrize("world", [4, 5])
+def test_ipc_striped_slab_bitwise(kind, world, monkeypatch):
+    """Striped slab exchange (part of every face message relayed through helper ranks:
+    channel-1 puts into the helpers' parity buffers, channel-2 forwards into the ghost
+    rows) — fused heat (1 exchange per step) and Burgers (3 per step), eager and
+    graph-replayed (both relay buffer sets inside one graph), bitwise equal to 1 rank.
+    ADVDIFF_STRIPE_SHARED=1 lets routes share links so 4-5 ranks have helpers."""
+    monkeypatch.setenv("ADVDIFF_STRIPE_SHARED", "1")
+    ref = _reference(kind, 17)
+    for graph in (False, True):
+        out = spawn_local(world, _run_striped, kind, 17, graph, device="cuda",
+                          transport="ipc", timeout=240)[0]
+        assert np.array_equal(out, ref), (kind, world, graph, np.abs(out - ref).max())
