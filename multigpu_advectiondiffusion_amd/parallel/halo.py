@@ -43,9 +43,10 @@ class PendingExchange:
             self.finish = None
 
 
-def _start_ipc_routed(comm, comm_stream, phases, after_event=None) -> PendingExchange:
+def _start_ipc_routed(comm, comm_stream, phases, after_event=None, tag=0) -> PendingExchange:
     """Like _start_ipc for phases of one-way-capable routes: phases = [(channel, {peer:
-    (send_view | None, recv_view | None)})], run in order on the comm stream."""
+    (send_view | None, recv_view | None)})], run in order on the comm stream; `tag`
+    keys the handshake cache (IpcPeers._resolve_pairs)."""
     cur = torch.cuda.current_stream()
     cs = comm_stream or cur
     if after_event is None:
@@ -54,7 +55,7 @@ def _start_ipc_routed(comm, comm_stream, phases, after_event=None) -> PendingExc
     cs.wait_event(after_event)
     ipc = comm.ipc()
     for ch, pairs in phases:
-        ipc.route(pairs, cs, ch)
+        ipc.route(pairs, cs, ch, tag)
     done = torch.cuda.Event()
     done.record(cs)
     return PendingExchange([], cs, lambda: torch.cuda.current_stream().wait_event(done))
@@ -237,8 +238,8 @@ class SlabHalo:
             ipc = self.comm.ipc()
             for par in (0, 1):
                 p1, p2 = self._stripe_phases(field, par)
-                ipc._resolve_pairs(1, p1)
-                ipc._resolve_pairs(2, p2)
+                ipc._resolve_pairs(1, p1, par)
+                ipc._resolve_pairs(2, p2, par)
         elif _ipc_on(self, field):
             self.comm.ipc()._resolve(self._ipc_msgs(field))
 
@@ -250,10 +251,11 @@ class SlabHalo:
         if self.comm.size == 1:
             return None
         if _ipc_on(self, field) and self._use_stripes(field):
-            p1, p2 = self._stripe_phases(field, self.parity)
+            par = self.parity
+            p1, p2 = self._stripe_phases(field, par)
             self.parity ^= 1
             return _start_ipc_routed(self.comm, self.comm_stream, [(1, p1), (2, p2)],
-                                     after_event)
+                                     after_event, tag=par)
         if _ipc_on(self, field):
             return _start_ipc(self.comm, self.comm_stream, [self._ipc_msgs(field)], after_event)
         ops = self._ops(field)

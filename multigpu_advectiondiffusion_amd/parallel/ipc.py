@@ -104,18 +104,20 @@ class IpcPeers:
         dests = self._resolve_pairs(0, pairs)
         return [dests[peer] for peer, _, _ in msgs]
 
-    def _resolve_pairs(self, ch, pairs):
+    def _resolve_pairs(self, ch, pairs, tag=0):
         """pairs = {peer: (send_view | None, recv_view | None)} of one exchange phase on
         flag channel `ch` (at most one message each way per peer; a phase may be one-way
         for a pair, as the striped exchange's relay hops are).  Returns {peer: (pointer,
         sy, sz) of the peer's receive box for my send, or None}.  First use of a pattern:
         both ranks of the pair swap announcements of their receive boxes (every rank of
-        a pair runs the same phase sequence, so both miss or both hit)."""
+        a pair runs the same phase sequence, so both miss or both hit — which is why a
+        pattern whose boxes differ on one side only, like the striped exchange's relay
+        buffer sets, must carry a `tag` both sides agree on (its parity))."""
         out, miss = {}, []
         for peer, (send, recv) in sorted(pairs.items()):
             ck = (ch, peer)
             self._calls[ck] = self._calls.get(ck, 0) + 1
-            key = (ch, peer, 0 if send is None else send.data_ptr(),
+            key = (ch, tag, peer, 0 if send is None else send.data_ptr(),
                    () if send is None else tuple(send.shape),
                    0 if recv is None else recv.data_ptr(),
                    () if recv is None else tuple(recv.shape))
@@ -173,7 +175,7 @@ class IpcPeers:
             raise ValueError("ipc: one message per peer and exchange")
         self.route({peer: (send, recv) for peer, send, recv in msgs}, stream, 0)
 
-    def route(self, pairs, stream, ch: int) -> None:
+    def route(self, pairs, stream, ch: int, tag=0) -> None:
         """One exchange phase on flag channel `ch`: pairs = {peer: (send_view | None,
         recv_view | None)}.  Enqueues the puts of every send box into the peer's receive
         box, the signal of the peers I sent to, and the wait for the peers that send to
@@ -181,7 +183,7 @@ class IpcPeers:
         phases of one exchange never mixes its counts)."""
         if not pairs:
             return
-        dests = self._resolve_pairs(ch, pairs)
+        dests = self._resolve_pairs(ch, pairs, tag)
         sp = stream.cuda_stream
         to = sorted(p for p, (snd, _) in pairs.items() if snd is not None)
         frm = sorted(p for p, (_, rcv) in pairs.items() if rcv is not None)

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 4: striped ipc exchange (GPU bitwise tests with ranks sharing the GPU), then the
+# self-launched 8-rank bench rehearsal whose tuner sees the ipc+stripe candidate.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+step() { # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -4 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ]; then echo "$name FAILED rc=$rc"; exit $rc; fi
+}
+step ipc_tests2 500 python -u -m pytest tests/test_ipc_gpu.py -x -v --timeout 150 --timeout-method thread -k "striped or preflight"
+export ADVDIFF_SHARE_GPU=1 GPU_MAX_HW_QUEUES=2 ADVDIFF_IPC_TIMEOUT_S=60 ADVDIFF_TRANSPORT=ipc
+step rehearsal_self_n8 900 python bench.py --gpus 8 --steps 10 --warmup 3 --sustained-steps 0 --no-fd2
+grep '^{' gpurun_out/rehearsal_self_n8.log | python -c "import json,sys; r=json.loads(sys.stdin.read()); print({k: r.get(k) for k in ('n_gpus','value','halo_transport','transport_trials_ms_per_step','bitwise_vs_1gpu','ipc_preflight','halo_link_MB','config')}); print('burgers', {k: r['burgers3d'].get(k) for k in ('halo_transport','transport_trials_ms_per_step','pgrid')})"
