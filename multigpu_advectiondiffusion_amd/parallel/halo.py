@@ -43,7 +43,7 @@ class PendingExchange:
             self.finish = None
 
 
-def _start_ipc_routed(comm, comm_stream, phases, after_event=None, tag=0) -> PendingExchange:
+def _start_ipc_routed(comm, comm_stream, phases, after_event=None, tag=None) -> PendingExchange:
     """Like _start_ipc for phases of one-way-capable routes: phases = [(channel, {peer:
     (send_view | None, recv_view | None)})], run in order on the comm stream; `tag`
     keys the handshake cache (IpcPeers._resolve_pairs)."""
@@ -97,6 +97,7 @@ class SlabHalo:
         self.parity = 0  # striped: which of the two relay buffer sets the next exchange uses
         self._plan = None
         self._fwd = {}
+        self._fid = {}  # field address -> ordinal (the same on every rank: same call order)
         if stripe and self.transport == "ipc" and comm is not None and comm.size > 1:
             import os
             from .ipc import stripe_plan
@@ -114,7 +115,8 @@ class SlabHalo:
     def _fwd_buf(self, key, like, shape):
         b = self._fwd.get(key)
         if b is None or tuple(b.shape) != tuple(shape) or b.dtype != like.dtype:
-            b = torch.zeros(shape, dtype=like.dtype, device=like.device)
+            # no fill: an (asynchronous) fill kernel could land after a peer's first put
+            b = torch.empty(shape, dtype=like.dtype, device=like.device)
             self._fwd[key] = b
         return b
 
@@ -162,6 +164,11 @@ class SlabHalo:
 
     def _use_stripes(self, field) -> bool:
         return self._plan is not None and field.is_cuda and field.dim() == 3
+
+    def _tag(self, field, parity):
+        """Handshake key of a striped exchange that every rank derives alike: the field's
+        ordinal (fields reach the halo in the same order on every rank) and the parity."""
+        return (self._fid.setdefault(field.data_ptr(), len(self._fid)), parity)
 
     def _ops(self, field: torch.Tensor):
         d = self.d
@@ -238,8 +245,8 @@ class SlabHalo:
             ipc = self.comm.ipc()
             for par in (0, 1):
                 p1, p2 = self._stripe_phases(field, par)
-                ipc._resolve_pairs(1, p1, par)
-                ipc._resolve_pairs(2, p2, par)
+                ipc._resolve_pairs(1, p1, self._tag(field, par))
+                ipc._resolve_pairs(2, p2, self._tag(field, par))
         elif _ipc_on(self, field):
             self.comm.ipc()._resolve(self._ipc_msgs(field))
 
@@ -255,7 +262,7 @@ class SlabHalo:
             p1, p2 = self._stripe_phases(field, par)
             self.parity ^= 1
             return _start_ipc_routed(self.comm, self.comm_stream, [(1, p1), (2, p2)],
-                                     after_event, tag=par)
+                                     after_event, tag=self._tag(field, par))
         if _ipc_on(self, field):
             return _start_ipc(self.comm, self.comm_stream, [self._ipc_msgs(field)], after_event)
         ops = self._ops(field)

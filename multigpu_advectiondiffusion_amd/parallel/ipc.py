@@ -104,25 +104,33 @@ class IpcPeers:
         dests = self._resolve_pairs(0, pairs)
         return [dests[peer] for peer, _, _ in msgs]
 
-    def _resolve_pairs(self, ch, pairs, tag=0):
+    def _resolve_pairs(self, ch, pairs, tag=None):
         """pairs = {peer: (send_view | None, recv_view | None)} of one exchange phase on
         flag channel `ch` (at most one message each way per peer; a phase may be one-way
         for a pair, as the striped exchange's relay hops are).  Returns {peer: (pointer,
         sy, sz) of the peer's receive box for my send, or None}.  First use of a pattern:
-        both ranks of the pair swap announcements of their receive boxes (every rank of
-        a pair runs the same phase sequence, so both miss or both hit — which is why a
-        pattern whose boxes differ on one side only, like the striped exchange's relay
-        buffer sets, must carry a `tag` both sides agree on (its parity))."""
+        both ranks of the pair swap announcements of their receive boxes.  Both must agree
+        on "first use", so the cache key may only hold what both sides know: tag=None (a
+        symmetric exchange, both boxes of a pair cut from the same field on each side):
+        the own boxes' addresses; otherwise the caller's `tag` (the striped exchange: the
+        field's ordinal and the relay-set parity), the own boxes being checked against the
+        cached pattern instead (a changed box under a known tag is an error, not a silent
+        hang)."""
         out, miss = {}, []
-        for peer, (send, recv) in sorted(pairs.items()):
+        for peer, (send, recv) in sorted(pairs.items(), key=lambda kv: kv[0]):
             ck = (ch, peer)
             self._calls[ck] = self._calls.get(ck, 0) + 1
-            key = (ch, tag, peer, 0 if send is None else send.data_ptr(),
-                   () if send is None else tuple(send.shape),
-                   0 if recv is None else recv.data_ptr(),
-                   () if recv is None else tuple(recv.shape))
+            mine = (0 if send is None else send.data_ptr(),
+                    () if send is None else tuple(send.shape),
+                    0 if recv is None else recv.data_ptr(),
+                    () if recv is None else tuple(recv.shape))
+            key = (ch, None, peer) + mine if tag is None else (ch, tag, peer)
             if key in self._dest:
-                out[peer] = self._dest[key]
+                d, was = self._dest[key]
+                if was != mine:
+                    raise RuntimeError(f"ipc: rank {self.comm.rank}: halo pattern {tag} with "
+                                       f"peer {peer} changed its boxes (reset() missing?)")
+                out[peer] = d
             else:
                 miss.append((peer, key))
         if not miss:
@@ -151,8 +159,11 @@ class IpcPeers:
                 gi, gj, gk, _, _ = _box_geom(send)
                 bad = (ni, nj, nk, dt) != (gi, gj, gk, _dtype_code(send))
             if bad:
-                raise RuntimeError(f"ipc: rank {self.comm.rank} and peer {peer} disagree on a "
-                                   f"halo message (channel {ch})")
+                raise RuntimeError(
+                    f"ipc: rank {self.comm.rank} and peer {peer} disagree on a halo message "
+                    f"(channel {ch}: calls {self._calls[(ch, peer)]} vs {call}, mine send/recv "
+                    f"{send is not None}/{recv is not None}, theirs {bool(has_send)}/"
+                    f"{bool(has_recv)}, box {(ni, nj, nk, dt)})")
             d = None
             if send is not None:
                 a = _lib.IpcAddr.from_buffer_copy(addr)
@@ -160,7 +171,11 @@ class IpcPeers:
                 _lib.check(self.lib.advdiff_ipc_map(self.ctx, ctypes.byref(a),
                                                     ctypes.byref(ptr)), "advdiff_ipc_map")
                 d = (ptr.value, rsy, rsz)
-            self._dest[key] = d
+            send, recv = pairs[peer]
+            self._dest[key] = (d, (0 if send is None else send.data_ptr(),
+                                   () if send is None else tuple(send.shape),
+                                   0 if recv is None else recv.data_ptr(),
+                                   () if recv is None else tuple(recv.shape)))
             out[peer] = d
         return out
 
@@ -175,7 +190,7 @@ class IpcPeers:
             raise ValueError("ipc: one message per peer and exchange")
         self.route({peer: (send, recv) for peer, send, recv in msgs}, stream, 0)
 
-    def route(self, pairs, stream, ch: int, tag=0) -> None:
+    def route(self, pairs, stream, ch: int, tag=None) -> None:
         """One exchange phase on flag channel `ch`: pairs = {peer: (send_view | None,
         recv_view | None)}.  Enqueues the puts of every send box into the peer's receive
         box, the signal of the peers I sent to, and the wait for the peers that send to

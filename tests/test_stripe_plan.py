@@ -95,3 +95,74 @@ def test_link_model_striped():
     base = halo_link_bytes((1024, 1024, 1024), (8, 1, 1), 6, 8, True)
     assert halo_link_bytes((1024, 1024, 1024), (8, 1, 1), 6, 8, True, stripe_parts=2) == \
         pytest.approx(base * 2 / 3)
+
+
+def _mock_striped(comm, world, exchanges):
+    """Every rank runs the striped phases through IpcPeers.route with the native calls
+    replaced by recorders: returns the (signal / wait, channel, peer) counts."""
+    import collections
+    import os
+    os.environ["ADVDIFF_STRIPE_SHARED"] = "1"
+    from multigpu_advectiondiffusion_amd.parallel import ipc as ipcmod
+    log = collections.Counter()
+
+    class FakeLib:
+        def advdiff_ipc_describe(self, ctx, ptr, out):
+            return 0
+
+        def advdiff_ipc_map(self, ctx, a, p):
+            return 0
+
+        def advdiff_ipc_put(self, *a):
+            return 0
+
+        def advdiff_ipc_signal_ch(self, ctx, ch, arr, n, sp):
+            for i in range(n):
+                log[("sig", ch, arr[i])] += 1
+            return 0
+
+        def advdiff_ipc_wait_ch(self, ctx, ch, arr, n, sp):
+            for i in range(n):
+                log[("wait", ch, arr[i])] += 1
+            return 0
+    ip = object.__new__(ipcmod.IpcPeers)
+    ip.comm, ip.lib, ip.ctx, ip._dest, ip._calls, ip.epoch = comm, FakeLib(), None, {}, {}, 0
+    ipcmod._lib.check = lambda code, what: None
+    ipcmod._dtype_code = lambda t: 1
+    comm._ipc = ip
+
+    class S:
+        cuda_stream = None
+    d = SlabDecomposition(6 * world, world, comm.rank, 3)
+    h = SlabHalo(comm, d, transport="ipc", stripe=2)
+    f = torch.zeros((d.alloc, 9, 8), dtype=torch.float64)
+    g = torch.zeros_like(f)
+    for e in range(exchanges):  # two fields in an irregular order, both parities
+        fld = f if e % 3 else g
+        par = h.parity
+        p1, p2 = h._stripe_phases(fld, par)
+        h.parity ^= 1
+        ip.route(p1, S, 1, h._tag(fld, par))
+        ip.route(p2, S, 2, h._tag(fld, par))
+    comm._ipc = None
+    return dict(log)
+
+
+@pytest.mark.parametrize("world", [3, 5, 8])
+def test_striped_handshakes_and_counts_match(world):
+    """All ranks' striped exchanges: every pair agrees on each handshake (no rank waits in
+    a swap its peer skips — the one-way relay hops key their cache by a tag both sides
+    derive alike) and every signal on a channel meets exactly one wait."""
+    from multigpu_advectiondiffusion_amd.launch import spawn_local
+    logs = spawn_local(world, _mock_striped, world, 12, device="cpu", backend="gloo",
+                       timeout=120)
+    n = 0
+    for r in range(world):
+        for (kind, ch, p), k in logs[r].items():
+            if kind == "sig":
+                assert logs[p].get(("wait", ch, r), 0) == k, (r, p, ch)
+                n += k
+        for (kind, ch, p), k in logs[r].items():
+            if kind == "wait":
+                assert logs[p].get(("sig", ch, r), 0) == k, (r, p, ch)
+    assert n > 0
