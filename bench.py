@@ -24,7 +24,7 @@ Laplacian named by BASELINE.json is measured on the same grid and reported as `f
 number): --sustained-steps more steps of the same solver, timed the same way.  The fp64
 stencil load runs the chip at its power limit and the clock controller dips for a few ms
 after a load starts, so a 20-step window (15 ms) mostly sees that dip; 200 steps show the
-settled rate (profiles/launch_times_r2s5.txt has the per-launch times).
+settled rate (profiles/archive/launch_times_r2s5.txt has the per-launch times).
 """
 from __future__ import annotations
 

@@ -357,7 +357,7 @@ extern "C" const char* advdiff_build_info(void) {
 // Load every kernel translation unit's code object now (outside any timed region).  With
 // deferred loading (the HIP default) a code object is loaded at the first launch of one
 // of its kernels — for the WENO5 file (many template instances) ~20-25 ms, which landed
-// inside the first timed step of a run (profiles/native_apps_r2.log).
+// inside the first timed step of a run (profiles/archive/native_apps_r2.log).
 extern "C" int advdiff_preload_burgers(void);
 extern "C" int advdiff_preload_diffusion(void);
 extern "C" int advdiff_preload_diffusion_fused(void);

@@ -36,7 +36,7 @@ namespace advdiff {
 // NP = 2R-1 values per side of a face.  MODE: stage epilogue (common.hpp).
 template <typename T, int W, bool WZ, bool VISC, int MODE, int TX, int TY>
 // WENO7 (136 VGPRs unconstrained): capped at 128 for 4 waves/SIMD = two 8-wave groups
-// per CU; a 20-byte spill, -12 % stage time (profiles/kbench_latest.log)
+// per CU; a 20-byte spill, -12 % stage time (profiles/archive/kbench_latest.log)
 __global__ __launch_bounds__(TX* TY)
 __attribute__((amdgpu_waves_per_eu(W == 7 ? 4 : 1))) void burgers3d_stage_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
@@ -987,7 +987,7 @@ static int b3_tile_row(int nx, int ny, int border) {
 template <typename T, bool WZ, bool VISC, int MODE, int TXL>
 static hipError_t launch_b3_v9_tx(const BArgs& p) {
   // XCD-contiguous tile order (default): 256^3 WENO5-Z + viscous step 0.584 -> 0.564 ms
-  // (+3.7 %, 3 interleaved rounds, bitwise identical; profiles/burgers3d_xcd_r2.log)
+  // (+3.7 %, 3 interleaved rounds, bitwise identical; profiles/archive/burgers3d_xcd_r2.log)
   static const int xcdmap = knob("B3_XCD", 1);
   constexpr int TY = 8 * (64 / TXL);
   const int gx = div_up(std::max(p.nx - 2 * p.border, 1), TXL - 1);
@@ -1024,10 +1024,10 @@ static bool v9_fits(const BArgs& p) {
 // 3-D WENO5 kernel version (ADVDIFF_B3_VER / advdiff_set_b3_ver): 9 (default) = the v9
 // kernel (ring renaming, compile-time LDS sets, unconditional prefetches, SGPR constants,
 // w5_side_h x/y faces: 256^3 WENO5-Z + viscous stage 195 us, 290 lane-ops per cell,
-// profiles/burgers_v9_r2.md); 3 = v3 (double-buffered tile, one barrier per plane, 242
+// profiles/archive/burgers_v9_r2.md); 3 = v3 (double-buffered tile, one barrier per plane, 242
 // us), also the fallback for planes of 2 GiB and more.  The round-1/2 variants v1, v2,
-// v4-v8 and the 16-row tiles were removed after their A/Bs (profiles/burgers_variants_r2.log,
-// profiles/burgers_v6_r2.md, docs/DESIGN.md); WENO7 runs the generic scheme kernel.
+// v4-v8 and the 16-row tiles were removed after their A/Bs (profiles/archive/burgers_variants_r2.log,
+// profiles/archive/burgers_v6_r2.md, docs/DESIGN.md); WENO7 runs the generic scheme kernel.
 static int g_b3_ver = -1;
 static int b3_ver() {
   if (g_b3_ver < 0) g_b3_ver = knob("B3_VER", 9);
@@ -1078,7 +1078,7 @@ static hipError_t launch_b2(const BArgs& p) {
   const int gx = div_up(p.nx, kBTX2);
   // fewest rows per y chunk: 1 — small grids (the reference's 400x406 rows) are latency-
   // bound, and a wave walking fewer rows in sequence wins there (400x406 WENO5-JS step
-  // 23.4 -> 20.4 us with 4 -> 1, profiles/small2d_r2.log); from ~1000^2 up the chunk
+  // 23.4 -> 20.4 us with 4 -> 1, profiles/archive/small2d_r2.log); from ~1000^2 up the chunk
   // comes from the block target and this floor is inactive
   static const int minc = std::max(knob("B2_MINC", 1), 1);
   const int yc = pick_chunk(p.hi - p.lo, gx, minc, 256);

@@ -42,7 +42,7 @@ struct Box2 {
 // z >= gza belong to the second plane range), as many rounds of resident groups as the
 // grid needs — the dispatcher balances the load dynamically.  (A persistent schedule —
 // one round of groups each marching an equal share of the linearised (tile, plane) space
-// — measured 9-11 % slower at 512^3 and was removed: profiles/step_variants_r2.log.  Uneven
+// — measured 9-11 % slower at 512^3 and was removed: profiles/archive/step_variants_r2.log.  Uneven
 // XCD-balanced chunk lengths gained 1.4 % at 512^3 but lost 6-13 % at other sizes and for
 // FD2: profiles/split_ab_r3.log, split_sizes_r3.log.)
 struct StepSched {
@@ -577,7 +577,7 @@ constexpr int step_min_waves() {
 
 // The march variant: DPP x neighbours in stages 2/3 (XS = 1), prefetch distance 2,
 // unmerged LDS reads (SEP).  The other (XS, PF, SEP) combinations measured 1-9 % slower
-// at 512^3 (profiles/step_variants_r2.log, step_cfgs_edge_r2.log) and were removed.
+// at 512^3 (profiles/archive/step_variants_r2.log, step_cfgs_edge_r2.log) and were removed.
 template <typename T, int ORDER, int NW, int RPW, int VAR>
 __global__ __launch_bounds__(64 * NW) __attribute__((
     amdgpu_waves_per_eu(step_min_waves<T, ORDER, NW, RPW>()))) void diffusion3d_step_kernel(
@@ -639,7 +639,7 @@ static hipError_t launch_step(const SArgs& a) {
   }();
   // chunk floor 16 (was 32): lets small grids fill one round of CUs (201x199x200 FD4:
   // 6 -> 7 chunks, 216 -> 252 groups, 51.6 -> 45.1 us per step); 512^3 and 400x200x206
-  // pick the same chunking either way (profiles/heat3d_min_chunk_r2.log)
+  // pick the same chunking either way (profiles/archive/heat3d_min_chunk_r2.log)
   static const int minc = knob("STEP_MIN_CHUNK", 16);
   const int na = std::max(a.k1 - a.k0, 0), nb = std::max(a.k1b - a.k0b, 0);
   const long long slots = (long long)device_cus() * per_cu;
@@ -662,7 +662,7 @@ static hipError_t launch_step(const SArgs& a) {
 
 // Tile shape per order.  With the edge tiles (axis_tile), interleaved medians at 512^3:
 // FD4 16 waves x 2 rows (32 stage-1 rows) 662 us vs 715 us for 12 x 3; FD2 12 x 3 rows
-// 535 us vs 549 us for 16 x 2 (profiles/step_cfgs_edge_r2.log).  48 rows overflow the
+// 535 us vs 549 us for 16 x 2 (profiles/archive/step_cfgs_edge_r2.log).  48 rows overflow the
 // 16-bit DS offsets, 10 x 4 spills at 168 VGPRs.
 // Phase-overlap variant (v3_march VAR) per order, from the round-3 interleaved A/B at
 // 512^3 fp64 (bench/step_ab.py, profiles/step_ab_r3.log; medians of 7 rounds x 10):
@@ -703,7 +703,7 @@ static hipError_t launch_step_var(const SArgs& a) {
 
 // Tile shape per order.  With the edge tiles (axis_tile), interleaved medians at 512^3:
 // FD4 16 waves x 2 rows (32 stage-1 rows) 662 us vs 715 us for 12 x 3; FD2 12 x 3 rows
-// 535 us vs 549 us for 16 x 2 (profiles/step_cfgs_edge_r2.log).  48 rows overflow the
+// 535 us vs 549 us for 16 x 2 (profiles/archive/step_cfgs_edge_r2.log).  48 rows overflow the
 // 16-bit DS offsets, 10 x 4 spills at 168 VGPRs.
 template <typename T, int ORDER>
 static hipError_t dispatch_step(const SArgs& a) {
