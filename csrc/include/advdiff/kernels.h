@@ -203,6 +203,8 @@ int advdiff_set_step_edge(int on);
 int advdiff_set_b3_ver(int v);
 // fused heat step: forced z-chunk length (0 = automatic); returns the previous setting
 int advdiff_set_step_zchunk(int zc);
+// fp32 fused heat step tile: 0 = the fp64 shapes, 3 / 4 = 16 waves x 3 / 4 rows
+int advdiff_set_step_f32_tile(int t);
 // v9 tile row width: 64, 32 or 0 = chosen per plane shape (returns the previous setting)
 int advdiff_set_b3_tx(int v);
 // 2-D WENO5 stage kernel version (2 = the barrier-free wave-strip kernel, default; 1 = the

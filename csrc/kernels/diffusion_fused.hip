@@ -705,8 +705,23 @@ static hipError_t launch_step_var(const SArgs& a) {
 // FD4 16 waves x 2 rows (32 stage-1 rows) 662 us vs 715 us for 12 x 3; FD2 12 x 3 rows
 // 535 us vs 549 us for 16 x 2 (profiles/archive/step_cfgs_edge_r2.log).  48 rows overflow the
 // 16-bit DS offsets, 10 x 4 spills at 168 VGPRs.
+// fp32 tile (ADVDIFF_STEP_F32_TILE / advdiff_set_step_f32_tile): 4-B elements halve the
+// LDS planes and the register rings, so taller tiles fit: 0 = the fp64 shapes, 3 / 4 =
+// 16 waves x 3 / 4 rows (48 / 64 stage-1 rows: fewer redundant rim rows and halo re-reads
+// per output).
+static int g_step_f32_tile = -1;
+static int step_f32_tile() {
+  if (g_step_f32_tile < 0) g_step_f32_tile = knob("STEP_F32_TILE", 0);
+  return g_step_f32_tile;
+}
+
 template <typename T, int ORDER>
 static hipError_t dispatch_step(const SArgs& a) {
+  if constexpr (sizeof(T) == 4) {
+    const int t = step_f32_tile();
+    if (t == 3) return launch_step<T, ORDER, 16, 3, ORDER == 4 ? 3 : 23>(a);
+    if (t == 4) return launch_step<T, ORDER, 16, 4, ORDER == 4 ? 3 : 23>(a);
+  }
   if constexpr (ORDER == 4)
     return launch_step_var<T, ORDER, 16, 2>(a);
   else
@@ -718,6 +733,12 @@ static hipError_t dispatch_step(const SArgs& a) {
 extern "C" int advdiff_set_step_var(int v) {
   const int old = advdiff::step_var();
   advdiff::g_step_var = v;
+  return old;
+}
+
+extern "C" int advdiff_set_step_f32_tile(int t) {
+  const int old = advdiff::step_f32_tile();
+  advdiff::g_step_f32_tile = t;
   return old;
 }
 
