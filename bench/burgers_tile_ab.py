@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
-"""A/B of the WENO5 v9 tile row width (ADVDIFF_B3_TX = 64 / 32 / auto) on the 3-D viscous
-Burgers stage, fp64, in the solver (hipGraph-replayed steps): cubes and the per-rank
-blocks of the multi-GPU Burgers configs.  The knob is read once per process, so every
-variant runs in its own child process; rounds alternate the variants (clock drift).
+"""A/B of WENO5 v9 launch variants on the 3-D viscous Burgers stage, fp64, in the solver
+(hipGraph-replayed steps): cubes and the per-rank blocks of the multi-GPU Burgers configs.
+Variants are environment knobs (read once per process), so every variant runs in its own
+child process; rounds alternate the variants (clock drift).  Bitwise: the solution after
+a fixed 8 steps must be the same for every variant.
 
-    python bench/burgers_tile_ab.py [--rounds 3]
+    python bench/burgers_tile_ab.py [--rounds 3] [--variants "B3_TX=64 B3_TX=32 B3_TX=0"]
 """
 import argparse
 import json
@@ -26,6 +27,7 @@ for shape in %r:
     s = Solver(m, Grid(shape, (2.0, 2.0, 2.0)), dtype=torch.float64, ic="gaussian")
     dt = m.stable_dt()
     s.run(iters=8, dt=dt)
+    h = s.bit_hash()
     t0 = time.perf_counter(); s.run(iters=8, dt=dt); per = (time.perf_counter() - t0) / 8
     steps = max(16, int(0.06 / per) // 8 * 8)
     s.run(iters=steps, dt=dt)
@@ -33,7 +35,7 @@ for shape in %r:
     ms = st.compute_s / steps * 1e3
     cells = shape[0] * shape[1] * shape[2]
     out.append({"shape": list(shape), "ms": round(ms, 4), "mlups": round(cells / ms / 1e3, 1),
-                "hash": s.bit_hash()})
+                "hash": h})
     del s; torch.cuda.empty_cache()
 print(json.dumps(out))
 '''
@@ -42,12 +44,17 @@ print(json.dumps(out))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="B3_TX=64 B3_TX=32 B3_TX=0")
     a = ap.parse_args()
+    variants = a.variants.split()
     best = {}
     hashes = {}
     for r in range(a.rounds):
-        for var in ("64", "32", "0"):
-            env = dict(os.environ, ADVDIFF_B3_TX=var)
+        for var in variants:
+            env = dict(os.environ)
+            for kv in var.split(","):
+                k, v = kv.split("=")
+                env["ADVDIFF_" + k] = v
             res = subprocess.run([sys.executable, "-c", CHILD % (ROOT, SHAPES)], env=env,
                                  capture_output=True, text=True, check=True, timeout=600)
             for rec in json.loads(res.stdout.strip().splitlines()[-1]):
@@ -56,10 +63,9 @@ def main():
                 hashes.setdefault(tuple(rec["shape"]), set()).add(rec["hash"])
             print(f"round {r} variant {var} done", flush=True)
     for shape in SHAPES:
-        row = {v: best[(shape, v)] for v in ("64", "32", "0")}
-        print(json.dumps({"shape": shape, "mlups_tx64": row["64"], "mlups_tx32": row["32"],
-                          "mlups_auto": row["0"], "bitwise_equal": len(hashes[shape]) == 1}),
-              flush=True)
+        print(json.dumps({"shape": shape, **{f"mlups[{v}]": best[(tuple(shape), v)]
+                                             for v in variants},
+                          "bitwise_equal": len(hashes[tuple(shape)]) == 1}), flush=True)
 
 
 if __name__ == "__main__":

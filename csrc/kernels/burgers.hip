@@ -993,7 +993,22 @@ static hipError_t launch_b3_v9_tx(const BArgs& p) {
   const int gx = div_up(std::max(p.nx - 2 * p.border, 1), TXL - 1);
   const int gy = div_up(std::max(p.ny - 2 * p.border, 1), TY);
   const int na = std::max(p.hi - p.lo, 0), nb = std::max(p.hi2 - p.lo2, 0);
-  const int zc = pick_chunk(na + nb, (long long)gx * gy, 8, 256);
+  // z chunks by the rounds model of the fused heat step (launch.hpp pick_chunk_rounds:
+  // resident workgroups = CUs x occupancy, cost = rounds x (chunk + warm-up)).  The old
+  // target-count rule (ADVDIFF_B3_CHUNKS=0) gave 512^3 two chunks of 253 planes = 1088
+  // workgroups for 512 resident slots: a third round with 64 workgroups alone on the chip.
+  static const int rounds_model = knob("B3_CHUNKS", 1);
+  static const int per_cu = [] {
+    int nbk = 0;
+    const void* fn = (const void*)burgers3d_w5s_kernel<T, WZ, VISC, MODE, TXL>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nbk, fn, 512, 0) != hipSuccess || nbk < 1)
+      nbk = 1;
+    return nbk;
+  }();
+  const int zc = rounds_model
+                     ? pick_chunk_rounds(na + nb, (long long)gx * gy,
+                                         (long long)device_cus() * per_cu, 4, 8)
+                     : pick_chunk(na + nb, (long long)gx * gy, 8, 256);
   const int gza = div_up(na, zc);
   const int gz = gza + div_up(nb, zc);
   const double s = 1.0 / 12.0;
