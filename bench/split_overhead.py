@@ -62,16 +62,39 @@ def main():
     def interior():
         stencil.diffusion3d_step(u, v, k0=o0 + G, k1=o1 - G, **kw)
 
+    lo_pri, hi_pri = torch.cuda.Stream.priority_range()
+    side = torch.cuda.Stream(priority=hi_pri)
+
+    def split_conc():  # (d) the boundary launch on a high-priority stream BESIDE the interior
+        cur = torch.cuda.current_stream()
+        side.wait_stream(cur)
+        stencil.diffusion3d_step(u, v, k0=o0 + G, k1=o1 - G, **kw)
+        with torch.cuda.stream(side):
+            stencil.diffusion3d_step(u, v, k0=o0, k1=o0 + G, k0b=o1 - G, k1b=o1, **kw)
+        cur.wait_stream(side)
+
+    def split_conc_first():  # (e) boundary first (on the side stream), interior behind it
+        cur = torch.cuda.current_stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            stencil.diffusion3d_step(u, v, k0=o0, k1=o0 + G, k0b=o1 - G, k1b=o1, **kw)
+        stencil.diffusion3d_step(u, v, k0=o0 + G, k1=o1 - G, **kw)
+        cur.wait_stream(side)
+
     def boundary1():
         stencil.diffusion3d_step(u, v, k0=o0, k1=o0 + G, k0b=o1 - G, k1b=o1, **kw)
 
     res = {"slab": [a.n, a.n, a.planes], "ghost": G}
     for name, fn in (("full_us", full), ("interior_us", interior),
                      ("boundary_merged_us", boundary1), ("split_3_launches_us", split2),
-                     ("split_2_launches_us", split1)):
+                     ("split_2_launches_us", split1), ("split_concurrent_us", split_conc),
+                     ("split_concurrent_bfirst_us", split_conc_first)):
         res[name] = round(timeit(fn, a.reps), 1)
     res["overhead_3_launches_pct"] = round(100 * (res["split_3_launches_us"] / res["full_us"] - 1), 1)
     res["overhead_2_launches_pct"] = round(100 * (res["split_2_launches_us"] / res["full_us"] - 1), 1)
+    res["overhead_concurrent_pct"] = round(100 * (res["split_concurrent_us"] / res["full_us"] - 1), 1)
+    res["overhead_concurrent_bfirst_pct"] = round(
+        100 * (res["split_concurrent_bfirst_us"] / res["full_us"] - 1), 1)
     print(json.dumps(res))
 
 
