@@ -70,7 +70,8 @@ class Solver:
                  check_every: int = 0, fused: bool | None = None, decomp=None,
                  integrator: str = "ssprk3", kernel: str = "native",
                  device_dt: bool | None = None, exchange: str = "u",
-                 transport: str | None = None, stripe: int | None = None):
+                 transport: str | None = None, stripe: int | None = None,
+                 boundary_stream: bool | None = None):
         """decomp: process grid — None/"slab" (split the slowest axis only, the
         reference's layout), "auto" (smallest halo surface) or "PZxPYxPX" / a tuple in
         array axis order ((pz, py, px) in 3-D, (py, px) in 2-D).
@@ -84,6 +85,9 @@ class Solver:
         transport: halo transport of this solver ("ipc", "rccl", "host"; None = the
         Comm's, Comm.transport) — solvers with different transports can coexist on one
         Comm (bench.py tunes the transport this way).
+        boundary_stream (fused heat step, N > 1, overlap): the boundary launch on its own
+        high-priority stream beside the interior launch, its exchange started right after
+        it (None = ADVDIFF_BSTREAM, default off).
         stripe: ipc slab exchanges of 3-D fields relay part of every face message through
         up to this many helper ranks over otherwise idle xGMI links (parallel/halo.py
         SlabHalo; None = ADVDIFF_STRIPE, default 0 = direct only).
@@ -170,9 +174,18 @@ class Solver:
         self.t = float(t0)
         self.it = 0
         self.comm_stream = None
+        self.bstream = None
         if self.device.type == "cuda" and comm.size > 1:
             lo, hi = torch.cuda.Stream.priority_range()
             self.comm_stream = torch.cuda.Stream(device=self.device, priority=hi)
+            if boundary_stream is None:
+                import os
+                boundary_stream = os.environ.get("ADVDIFF_BSTREAM", "0") == "1"
+            if boundary_stream and self.fused and overlap:
+                # the fused step's boundary launch runs on its own high-priority stream
+                # BESIDE the interior launch, and the exchange of its planes starts as soon
+                # as it ends (not after the interior): _step_fused
+                self.bstream = torch.cuda.Stream(device=self.device, priority=hi)
         if self.cart:
             # the fused step stacks three star stencils: it needs edge/corner ghosts too
             self.halo = CartesianHalo(comm, self.cd, self.comm_stream, corners=self.fused,
@@ -413,6 +426,9 @@ class Solver:
 
     def _step_fused(self, dt: float) -> None:
         pend = self._pending.pop(id(self.u), None)
+        if self.bstream is not None and self.comm.size > 1:
+            self._step_fused_bstream(dt, pend)
+            return
         if self.comm.size == 1:
             self._launch_fused(self.full, dt, exclusive=True)
         elif self.overlap:
@@ -435,6 +451,37 @@ class Solver:
         if self.comm.size > 1:
             with trace.range_("halo_start"):
                 self._pending[id(self.u)] = self.halo.start(self.u)
+        self.t += dt
+        self.it += 1
+
+    def _step_fused_bstream(self, dt: float, pend) -> None:
+        """Overlapped fused step with the boundary launch on its own stream: the interior
+        launch (compute stream) and — once the halo of u has arrived — the boundary
+        launch (high-priority side stream) run side by side, and the exchange of the new
+        boundary planes starts right after the boundary launch, overlapping the rest of
+        the interior.  The compute stream joins the side stream before the next step (its
+        launches read the new boundary planes and overwrite u)."""
+        cur = torch.cuda.current_stream(self.device)
+        bs = self.bstream
+        bs.wait_stream(cur)  # everything before this step precedes both launches
+        with trace.range_("interior"):
+            self._launch_fused(self.interior, dt)
+        with torch.cuda.stream(bs):
+            with trace.range_("halo_wait"):
+                if pend is not None:
+                    pend.wait()  # the side stream waits for the halo of u
+            with trace.range_("boundary"):
+                if self.cart:
+                    for box in self.boundary:
+                        self._launch_fused_box(box, dt)
+                else:
+                    self._launch_fused(self.boundary[0], dt, self.boundary[1])
+            bdone = torch.cuda.Event()
+            bdone.record(bs)
+        self.u, self.un = self.un, self.u
+        with trace.range_("halo_start"):
+            self._pending[id(self.u)] = self.halo.start(self.u, after_event=bdone)
+        cur.wait_stream(bs)
         self.t += dt
         self.it += 1
 

@@ -256,3 +256,26 @@ def test_ipc_striped_slab_bitwise(kind, world, monkeypatch):
         out = spawn_local(world, _run_striped, kind, 17, graph, device="cuda",
                           transport="ipc", timeout=240)[0]
         assert np.array_equal(out, ref), (kind, world, graph, np.abs(out - ref).max())
+
+
+def _run_bstream(comm, kind, steps, decomp, graph):
+    model, grid, ic = _make(kind)
+    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, transport="ipc", decomp=decomp,
+               boundary_stream=True)
+    assert s.bstream is not None
+    s.run(iters=steps, graph=graph)
+    g = s.gather()
+    assert comm.ipc().errors() == 0
+    return None if g is None else g.copy()
+
+
+@pytest.mark.parametrize("world,decomp", [(2, None), (3, None), (4, (2, 2, 1))])
+def test_ipc_boundary_stream_bitwise(world, decomp):
+    """Fused heat step with the boundary launch on its own stream beside the interior and
+    the exchange started right after it: eager and graph-replayed, slab and Cartesian,
+    bitwise equal to one rank."""
+    ref = _reference("diff3", 17)
+    for graph in (False, True):
+        out = spawn_local(world, _run_bstream, "diff3", 17, decomp, graph, device="cuda",
+                          transport="ipc", timeout=240)[0]
+        assert np.array_equal(out, ref), (world, decomp, graph, np.abs(out - ref).max())
