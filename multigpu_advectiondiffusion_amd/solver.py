@@ -181,10 +181,10 @@ class Solver:
             if boundary_stream is None:
                 import os
                 boundary_stream = os.environ.get("ADVDIFF_BSTREAM", "0") == "1"
-            if boundary_stream and self.fused and overlap:
-                # the fused step's boundary launch runs on its own high-priority stream
-                # BESIDE the interior launch, and the exchange of its planes starts as soon
-                # as it ends (not after the interior): _step_fused
+            if boundary_stream and overlap and exchange == "u":
+                # the boundary launch runs on its own high-priority stream BESIDE the
+                # interior launch, and the exchange of its planes starts as soon as it
+                # ends (not after the interior): _step_fused_bstream / _stage_bstream
                 self.bstream = torch.cuda.Stream(device=self.device, priority=hi)
         if self.cart:
             # the fused step stacks three star stencils: it needs edge/corner ghosts too
@@ -327,8 +327,37 @@ class Solver:
         self.model.stage(v(inp), v(u0), v(out), z0, z1, dt, a, b, ls=ls, **kw)
         trace.sync_check(f"{self.model.name} stage box {box}", self.device)
 
+    def _stage_bstream(self, inp, u0, out, a, b, dt, ls, pend):
+        """Per-stage counterpart of _step_fused_bstream: interior on the compute stream,
+        boundary (after the halo of `inp`) on the side stream beside it, the exchange of
+        `out` right after the boundary launch; the compute stream joins the side stream
+        before the next stage."""
+        cur = torch.cuda.current_stream(self.device)
+        bs = self.bstream
+        bs.wait_stream(cur)
+        with trace.range_("interior"):
+            self._launch(inp, u0, out, self.interior, dt, a, b, ls)
+        with torch.cuda.stream(bs):
+            with trace.range_("halo_wait"):
+                if pend is not None:
+                    pend.wait()
+            with trace.range_("boundary"):
+                if not self.cart and getattr(self.model, "two_range_stage", False):
+                    self._launch(inp, u0, out, self.boundary[0], dt, a, b, ls, self.boundary[1])
+                else:
+                    for rng in self.boundary:
+                        self._launch(inp, u0, out, rng, dt, a, b, ls)
+            bdone = torch.cuda.Event()
+            bdone.record(bs)
+        with trace.range_("halo_start"):
+            self._pending[id(out)] = self.halo.start(out, after_event=bdone)
+        cur.wait_stream(bs)
+
     def _stage(self, inp, u0, out, a, b, dt, ls=False):
         pend = self._pending.pop(id(inp), None)
+        if self.bstream is not None and self.comm.size > 1:
+            self._stage_bstream(inp, u0, out, a, b, dt, ls, pend)
+            return
         if self.comm.size == 1:
             self._launch(inp, u0, out, self.full, dt, a, b, ls)
             return

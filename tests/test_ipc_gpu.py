@@ -258,7 +258,7 @@ def test_ipc_striped_slab_bitwise(kind, world, monkeypatch):
         assert np.array_equal(out, ref), (kind, world, graph, np.abs(out - ref).max())
 
 
-def _run_bstream(comm, kind, steps, decomp, graph):
+def _run_bstream(comm, kind, steps, decomp, graph):  # noqa: D103
     model, grid, ic = _make(kind)
     s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, transport="ipc", decomp=decomp,
                boundary_stream=True)
@@ -269,13 +269,15 @@ def _run_bstream(comm, kind, steps, decomp, graph):
     return None if g is None else g.copy()
 
 
-@pytest.mark.parametrize("world,decomp", [(2, None), (3, None), (4, (2, 2, 1))])
-def test_ipc_boundary_stream_bitwise(world, decomp):
-    """Fused heat step with the boundary launch on its own stream beside the interior and
-    the exchange started right after it: eager and graph-replayed, slab and Cartesian,
-    bitwise equal to one rank."""
-    ref = _reference("diff3", 17)
+@pytest.mark.parametrize("kind,world,decomp", [("diff3", 2, None), ("diff3", 3, None),
+                                               ("diff3", 4, (2, 2, 1)), ("burg3", 3, None),
+                                               ("burg3", 4, (2, 2, 1))])
+def test_ipc_boundary_stream_bitwise(kind, world, decomp):
+    """Boundary launch on its own stream beside the interior, the exchange started right
+    after it — fused heat step and per-stage Burgers, eager and graph-replayed, slab and
+    Cartesian: bitwise equal to one rank."""
+    ref = _reference(kind, 17)
     for graph in (False, True):
-        out = spawn_local(world, _run_bstream, "diff3", 17, decomp, graph, device="cuda",
+        out = spawn_local(world, _run_bstream, kind, 17, decomp, graph, device="cuda",
                           transport="ipc", timeout=240)[0]
-        assert np.array_equal(out, ref), (world, decomp, graph, np.abs(out - ref).max())
+        assert np.array_equal(out, ref), (kind, world, decomp, graph, np.abs(out - ref).max())
