@@ -456,6 +456,93 @@ class IpcTransport final : public Transport {
     for (size_t q = 0; q < peers.size(); ++q)
       ipc_check(advdiff_ipc_set_peer(ctx_, peers[q], &theirs[q]), "advdiff_ipc_set_peer");
     star_.reduce(0.0, false);  // all mapped before anyone signals
+    if (env_int("ADVDIFF_IPC_PREFLIGHT", 1)) preflight(peers);
+  }
+  // Validated round trips between every pair of ranks before a run relies on the
+  // transport (the Python counterpart: parallel/ipc.py IpcPeers.preflight): peer access
+  // between the devices, then rounds of a distinct 32-bit pattern per (sender, receiver,
+  // round), each receiver first reading its buffers through its caches (a reduction
+  // kernel) so a put that the flag overtakes or a stale cache line shows up as a mismatch.
+  void preflight(const std::vector<int>& peers) {
+    if (peers.empty()) return;
+    int mydev = 0;
+    HIP_CHECK(hipGetDevice(&mydev));
+    std::vector<int> devs(peers.size(), -1);
+    {
+      std::vector<const void*> o(peers.size(), &mydev);
+      std::vector<void*> in;
+      for (int& d : devs) in.push_back(&d);
+      mesh_.swap(peers, o, in, std::vector<size_t>(peers.size(), sizeof(int)));
+    }
+    double bad = 0;
+    for (size_t q = 0; q < peers.size(); ++q) {
+      if (devs[q] == mydev) continue;
+      int ok = 0;
+      HIP_CHECK(hipDeviceCanAccessPeer(&ok, mydev, devs[q]));
+      if (!ok) {
+        std::fprintf(stderr, "ipc preflight: rank %d (device %d) has no peer access to rank %d "
+                     "(device %d)\n", env_.rank, mydev, peers[q], devs[q]);
+        bad = 1;
+      }
+    }
+    if (star_.reduce(bad, true) > 0) std::exit(2);
+    const size_t words = 3 * 24 * 200, bytes = words * 4;
+    hipStream_t st;
+    HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    std::vector<void*> snd(peers.size()), rcv(peers.size());
+    for (size_t q = 0; q < peers.size(); ++q) {
+      HIP_CHECK(hipMalloc(&snd[q], bytes));
+      HIP_CHECK(hipMalloc(&rcv[q], bytes));
+      // stream-ordered fill (a null-stream hipMemset is not ordered before `st`)
+      HIP_CHECK(hipMemsetAsync(rcv[q], 0, bytes, st));
+    }
+    HIP_CHECK(hipStreamSynchronize(st));
+    void* ws = nullptr;
+    double* red = nullptr;
+    HIP_CHECK(hipMalloc(&ws, advdiff_reduce_workspace_bytes()));
+    HIP_CHECK(hipMalloc((void**)&red, 3 * sizeof(double)));
+    std::vector<uint32_t> host(words);
+    long long mism = 0;
+    for (uint32_t round = 1; round <= 3; ++round) {
+      std::vector<Msg> msgs;
+      for (size_t q = 0; q < peers.size(); ++q) {
+        const uint32_t v = 0x10000u * (uint32_t)env_.rank + 0x100u * (uint32_t)peers[q] + round;
+        HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)snd[q], v, words, st));
+        // the (stale) receive buffer passes through this GPU's caches first
+        KERNEL_CHECK(advdiff_reduce_norms(ADVDIFF_F32, rcv[q], nullptr, 200, 200 * 24, 0, 200, 0,
+                                          24, 0, 3, ws, red, st));
+        msgs.push_back(Msg{peers[q], snd[q], rcv[q], bytes});
+      }
+      HIP_CHECK(hipStreamSynchronize(st));
+      star_.reduce(0.0, false);
+      exchange(msgs, st);
+      HIP_CHECK(hipStreamSynchronize(st));
+      for (size_t q = 0; q < peers.size(); ++q) {
+        const uint32_t want = 0x10000u * (uint32_t)peers[q] + 0x100u * (uint32_t)env_.rank + round;
+        HIP_CHECK(hipMemcpy(host.data(), rcv[q], bytes, hipMemcpyDeviceToHost));
+        for (uint32_t w : host) mism += w != want;
+      }
+      star_.reduce(0.0, false);  // nobody starts the next round's puts before all compared
+    }
+    const long long to = errors();
+    const double worst = star_.reduce((double)(mism + to), true);
+    HIP_CHECK(hipDeviceSynchronize());
+    ipc_check(advdiff_ipc_reset(ctx_), "advdiff_ipc_reset");  // unmap the preflight buffers
+    dest_.clear();
+    calls_.clear();
+    star_.reduce(0.0, false);
+    for (size_t q = 0; q < peers.size(); ++q) {
+      (void)hipFree(snd[q]);
+      (void)hipFree(rcv[q]);
+    }
+    (void)hipFree(ws);
+    (void)hipFree(red);
+    (void)hipStreamDestroy(st);
+    if (worst > 0) {
+      std::fprintf(stderr, "ipc preflight failed on rank %d: %lld mismatching words, %lld wait "
+                   "timeouts (worst rank: %.0f)\n", env_.rank, mism, to, worst);
+      std::exit(2);
+    }
   }
   ~IpcTransport() override {
     (void)hipDeviceSynchronize();
