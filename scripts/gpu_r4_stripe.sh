@@ -13,6 +13,7 @@ step() { # name seconds cmd...
   if [ $rc -ne 0 ]; then echo "$name FAILED rc=$rc"; exit $rc; fi
 }
 step ipc_tests2 500 python -u -m pytest tests/test_ipc_gpu.py -x -v --timeout 150 --timeout-method thread -k "striped or preflight or boundary_stream"
+step native_ipc 400 python -u -m pytest tests/test_native_apps_gpu.py tests/test_ipc_gpu.py -x -v --timeout 150 --timeout-method thread -k "native and ipc"
 export ADVDIFF_SHARE_GPU=1 GPU_MAX_HW_QUEUES=2 ADVDIFF_IPC_TIMEOUT_S=60 ADVDIFF_TRANSPORT=ipc
 step rehearsal_self_n8 900 python bench.py --gpus 8 --steps 10 --warmup 3 --sustained-steps 0 --no-fd2
 grep '^{' gpurun_out/rehearsal_self_n8.log | python -c "import json,sys; r=json.loads(sys.stdin.read()); print({k: r.get(k) for k in ('n_gpus','value','halo_transport','transport_trials_ms_per_step','bitwise_vs_1gpu','ipc_preflight','halo_link_MB','config')}); print('burgers', {k: r['burgers3d'].get(k) for k in ('halo_transport','transport_trials_ms_per_step','pgrid')})"
