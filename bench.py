@@ -95,6 +95,15 @@ def _fingerprint(s):
     return (s.comm.allreduce_sum(a), s.comm.allreduce_sum(b), s.comm.allreduce_max(c))
 
 
+_T0 = time.perf_counter()
+
+
+def progress(comm, msg):
+    """One stderr line per bench phase (rank 0): long multi-rank runs show they are alive."""
+    if comm.rank == 0:
+        print(f"bench [{time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def tune(make, cands, dt, dev, trial_steps=8, rounds=3):
     """Autotuning of the (process grid, halo transport) pair, N > 1, outside the timed
     region.  cands = [(pgrid, transport)]: the slab + grids of
@@ -311,6 +320,7 @@ def run(args):
         raise SystemExit(f"bench: world {n} != --gpus {args.gpus}")
     dev = comm.device
     single = Comm(device=str(dev)) if dev.type == "cuda" else Comm(device="cpu")
+    progress(comm, f"{n} rank(s) on {comm.device_ids()}, backend {comm.backend}")
     transports, preflight = transports_for(comm, args.transport)
 
     def cands_of(grids):  # striping applies to slabs only
@@ -336,7 +346,9 @@ def run(args):
         grids = candidate_proc_grids(n, ashape, 3 * model.radius, 8, corners=True)
     else:
         grids = [None if args.decomp == "slab" else args.decomp]
+    progress(comm, f"heat: tuning {len(cands_of(grids))} (grid, transport) candidates")
     (decomp, transport), trials = tune(make_heat, cands_of(grids), dt, dev)
+    progress(comm, f"heat: timed run ({decomp}, {transport})")
     solver = make_heat(decomp, transport)
     secs = timed(solver, args.steps, args.warmup, dt)
     mlups = grid.cells * args.steps / secs / 1e6
@@ -354,6 +366,7 @@ def run(args):
         raise SystemExit(f"bench validation failed: L_inf vs exact = {linf:.3e} > {bound:.3e}")
     checks = {}
     if n > 1 and args.check_steps > 0:
+        progress(comm, "heat: bitwise check against one GPU")
         ok, rec = bitwise_vs_1gpu(lambda: make_heat(decomp, transport),
                                   lambda: make_heat(None, None, c=single),
                                   args.check_steps, dt, comm, dev)
@@ -401,6 +414,7 @@ def run(args):
 
     # ---- the 7-point (FD2) Laplacian named by BASELINE.json, same grid ----------------
     if not args.no_fd2:
+        progress(comm, "FD2 7-point run")
         m2 = Diffusion(K=1.0, order=2)
         s2 = make_heat(decomp, transport, m=m2)
         secs2 = timed(s2, args.steps, args.warmup, m2.stable_dt())
@@ -434,7 +448,9 @@ def run(args):
             bgrids = candidate_proc_grids(n, tuple(reversed(bshape)), bmodel.radius, 8)
         else:
             bgrids = [None if args.decomp == "slab" else args.decomp]
+        progress(comm, f"burgers: tuning {len(cands_of(bgrids))} candidates")
         (bdecomp, btransport), btrials = tune(make_burgers, cands_of(bgrids), bdt, dev)
+        progress(comm, f"burgers: timed run ({bdecomp}, {btransport})")
         bsolver = make_burgers(bdecomp, btransport)
         bsteps = args.burgers_steps or args.steps
         bsecs = timed(bsolver, bsteps, args.warmup, bdt)
@@ -453,6 +469,7 @@ def run(args):
                                "transport_trials_ms_per_step": btrials,
                                **({"sustained": bsust} if bsust else {})}
         if n > 1 and args.check_steps > 0:
+            progress(comm, "burgers: bitwise check against one GPU")
             ok, rec = bitwise_vs_1gpu(lambda: make_burgers(bdecomp, btransport),
                                       lambda: make_burgers(None, None, c=single),
                                       args.check_steps, bdt, comm, dev)
