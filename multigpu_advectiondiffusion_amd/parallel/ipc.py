@@ -267,7 +267,11 @@ class IpcPeers:
             for i, p in enumerate(peers):
                 if not torch.equal(recv[i, :, :, :ni], pattern(p, comm.rank, r)):
                     mism.append((p, r))
-            comm.barrier()  # nobody starts the next round's puts before all have compared
+            # every rank knows after each round (a broken path costs one wait timeout,
+            # not one per round); also: nobody starts the next round's puts before all
+            # have compared
+            if comm.allreduce_max(float(len(mism) + self.errors())) > 0:
+                break
         torch.cuda.synchronize(dev)
         timeouts = self.errors()
         del send, recv, msgs
