@@ -201,6 +201,12 @@ int advdiff_set_step_edge(int on);
 // 3-D WENO5 stage kernel version (9 = default, 3 = the v3 fallback used for planes of
 // 2 GiB and more); returns the previous value.  Results agree to rounding (tests).
 int advdiff_set_b3_ver(int v);
+// TWO fused SSP-RK3 steps of the 7-point heat equation in one launch (8 B of HBM traffic
+// per cell and step): uout[k0:k1] = RK3(RK3(uin)), bit-identical to two one-step launches
+int advdiff_diffusion3d_step2x(int dtype, const void* uin, void* uout, int nx, int ny,
+                               int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int zlo,
+                               int zhi, const int* box, double cx, double cy, double cz,
+                               double dt, void* stream);
 // fused heat step: forced z-chunk length (0 = automatic); returns the previous setting
 int advdiff_set_step_zchunk(int zc);
 // fp32 fused heat step tile: 0 = the fp64 shapes, 3 / 4 = 16 waves x 3 / 4 rows

@@ -70,35 +70,41 @@ struct AxisTile {
 struct AxisSpan {
   int p0, p1, lol, hir;
 };
+// SH: the output shrink of an interior tile side (2R for the 3-stage step, 5R for the
+// two-step 6-stage kernel); an edge tile anchored on frozen Dirichlet cells shrinks by R.
 __host__ __device__ inline AxisSpan axis_span(int W, int R, int a0, int a1, int o0, int o1,
-                                              int nmax, int edge) {
+                                              int nmax, int edge, int SH) {
   AxisSpan s;
   s.p0 = o0 > a0 ? o0 : a0;
   s.p1 = o1 < a1 ? o1 : a1;
   const bool el = edge && s.p0 == a0 && a0 - R >= 0;
   const bool er = edge && s.p1 == a1 && a1 + R <= nmax;
-  s.lol = el ? R : 2 * R;
-  s.hir = er ? W - R : W - 2 * R;
+  s.lol = el ? R : SH;
+  s.hir = er ? W - R : W - SH;
   return s;
 }
 
 __host__ __device__ inline int axis_tile_count(int W, int R, int a0, int a1, int o0, int o1,
-                                               int nmax, int edge) {
-  const AxisSpan s = axis_span(W, R, a0, a1, o0, o1, nmax, edge);
-  const int L = s.p1 - s.p0, TO = W - 4 * R;
+                                               int nmax, int edge, int SH) {
+  const AxisSpan s = axis_span(W, R, a0, a1, o0, o1, nmax, edge, SH);
+  const int L = s.p1 - s.p0, TO = W - 2 * SH;
   if (L <= s.hir - s.lol) return 1;
-  const int rest = L - (W - 2 * R - s.lol) - (s.hir - 2 * R);
+  const int rest = L - (W - SH - s.lol) - (s.hir - SH);
   return 2 + (rest > 0 ? (rest + TO - 1) / TO : 0);
+}
+__host__ __device__ inline int axis_tile_count(int W, int R, int a0, int a1, int o0, int o1,
+                                               int nmax, int edge) {
+  return axis_tile_count(W, R, a0, a1, o0, o1, nmax, edge, 2 * R);
 }
 
 __device__ __forceinline__ AxisTile axis_tile(int t, int n, int W, int R, int a0, int a1,
-                                              int o0, int o1, int nmax, int edge) {
-  const AxisSpan s = axis_span(W, R, a0, a1, o0, o1, nmax, edge);
-  const int TO = W - 4 * R;
-  const int e0 = s.p0 + (W - 2 * R - s.lol);  // end of tile 0's outputs
+                                              int o0, int o1, int nmax, int edge, int SH) {
+  const AxisSpan s = axis_span(W, R, a0, a1, o0, o1, nmax, edge, SH);
+  const int TO = W - 2 * SH;
+  const int e0 = s.p0 + (W - SH - s.lol);  // end of tile 0's outputs
   AxisTile a;
-  a.lo = t == 0 ? s.lol : 2 * R;
-  a.hi = t == n - 1 ? s.hir : W - 2 * R;
+  a.lo = t == 0 ? s.lol : SH;
+  a.hi = t == n - 1 ? s.hir : W - SH;
   if (t == 0) {
     a.org = s.p0 - s.lol;
     a.wlo = s.p0;
@@ -107,9 +113,13 @@ __device__ __forceinline__ AxisTile axis_tile(int t, int n, int W, int R, int a0
     a.wlo = e0 + (t - 1) * TO;
   } else {
     a.wlo = e0 + (t - 1) * TO;
-    a.org = a.wlo - 2 * R;
+    a.org = a.wlo - SH;
   }
   return a;
+}
+__device__ __forceinline__ AxisTile axis_tile(int t, int n, int W, int R, int a0, int a1,
+                                              int o0, int o1, int nmax, int edge) {
+  return axis_tile(t, n, W, R, a0, a1, o0, o1, nmax, edge, 2 * R);
 }
 
 // ---------------------------------------------------------------------------------
@@ -564,6 +574,308 @@ __device__ __forceinline__ void v3_march(
   }
 }
 
+// ---------------------------------------------------------------------------------
+// TWO SSP-RK3 steps in one launch, 7-point (FD2) Laplacian: six stages on chip
+// (A, B, U1 = u^{n+1}, C, D, U2 = u^{n+2}), u^n read once and u^{n+2} written once —
+// 8 B of HBM traffic per cell and step instead of 16.  The FD2 step is the lighter one
+// (about a third of the FD4 step's VALU work per cell, 79 % of the copy rate at one step
+// per launch: profiles/roofline.md), so it has the VALU headroom to trade: the trapezoid
+// rims grow from 2R to 5R per side (the x/y tile outputs 54 x (S1R - 10) of 64 x S1R), and
+// the z warm-up from 4R to 10R planes.
+// Iteration k of the z march: A(k+5), B(k+4), U1(k+3), C(k+2), D(k+1), U2(k) (R = 1).
+// Register rings of 4 slots per plane kind (u k+3..k+6, A k+2..k+5, B k+1..k+4, U1 k..k+3,
+// C k-1..k+2, D k-2..k+1), the march unrolled by 4 so every slot and the LDS buffer set
+// (k & 1) are static; six double-buffered LDS planes (u with its rim for stage 1's x/y
+// neighbours; A, B, U1, C, D for the y neighbours of the stages they feed — x comes from
+// the wave's own lanes by DPP) written at the top of the iteration: one barrier per plane.
+// The arithmetic is the per-stage kernels' (fd_ctr, fd2_axis / fd_apply in the order
+// centre, z, x, y; stage bases a u^n with u^n = U1 for the second step), so two steps
+// of this kernel equal two launches of the one-step kernel — and six stage launches —
+// bit for bit (tests/test_fused_step_gpu.py).
+// ---------------------------------------------------------------------------------
+template <typename T, int NW, int RPW>
+struct V6Geom {
+  static constexpr int R = 1, W = 64, S1R = NW * RPW;
+  static constexpr int UW = W + 2 * R, UH = S1R + 2 * R;
+  static constexpr int USET = UH * UW;
+  static constexpr int ASET = S1R * W + 2 * W;    // + one pad row above and below
+  static constexpr int OFF_P = 2 * USET;            // first of the 5 x 2 A-type planes
+  static constexpr int TOTAL = OFF_P + 10 * ASET;
+};
+
+template <typename T, int NW, int RPW>
+__device__ __forceinline__ void v6_march(
+    T* lds, int tx, int ty, int gx, int gy, int edge, int kc0, int kc1,
+    const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
+    int nz_alloc, int zlo, int zhi, const Box2& bx, const FdCoef<T>& q1, const FdCoef<T>& q2,
+    const FdCoef<T>& q3) {
+  using G = V6Geom<T, NW, RPW>;
+  constexpr int R = 1, W = G::W, S1R = G::S1R, UW = G::UW, UH = G::UH, NR = 4, PF = 2;
+  constexpr int SH = 5 * R;  // interior output shrink per side
+  constexpr int NT = 64 * NW;
+  constexpr int NHALO = UW * UH - W * S1R;
+  constexpr int NH = (NHALO + NT - 1) / NT;
+  constexpr int E = (int)sizeof(T);
+  constexpr int USETB = G::USET * E, ASETB = G::ASET * E;
+  static_assert(S1R - 2 * SH > 0, "tile too small");
+  static_assert(USETB + (2 * UW + 2) * E < 65536 && ASETB + 2 * W * E < 65536,
+                "LDS immediates must fit the 16-bit DS offset");
+
+  const int lane = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
+  const int tid = w * 64 + lane;
+  const AxisTile atx = axis_tile(tx, gx, W, R, bx.xa0, bx.xa1, bx.xo0, bx.xo1, nx, edge, SH);
+  const AxisTile aty = axis_tile(ty, gy, S1R, R, bx.ya0, bx.ya1, bx.yo0, bx.yo1, ny, edge, SH);
+  const int x = atx.org + lane;
+  const bool xin = x >= bx.xa0 && x < bx.xa1;
+  const bool xout = x >= max(bx.xo0, atx.wlo) && x < bx.xo1 && lane >= atx.lo && lane < atx.hi;
+  const int ywlo = max(bx.yo0, aty.wlo);
+  const int xc = clampi(x, 0, nx - 1);
+  char* lb = (char*)lds;
+  auto ld = [&](int off) {
+    asm volatile("" ::: "memory");  // keep every LDS read a separate ds_read_b64
+    return lds_ld<T>(lb, off);
+  };
+
+  uint32_t goff[RPW];
+  int ub[RPW], pb[RPW];
+  bool m1[RPW], m6[RPW];
+  int rowq[RPW];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const int row = w + q * NW;  // rows interleaved over the waves
+    rowq[q] = row;
+    const int y = aty.org + row;
+    const bool inxy = xin && y >= bx.ya0 && y < bx.ya1;
+    m1[q] = inxy;
+    m6[q] = inxy && xout && y >= ywlo && y < bx.yo1 && row >= aty.lo && row < aty.hi;
+    goff[q] = (uint32_t)(clampi(y, 0, ny - 1) * (int)sy + xc) * (uint32_t)E;
+    ub[q] = (row * UW + lane) * E;                      // u: top-left of the 3x3 window
+    pb[q] = (G::OFF_P + W + row * W + lane) * E;        // A-type plane 0, set 0: own cell
+  }
+  // rows of stage s (1..6) of this tile: [min((s-1)R, lo), max(S1R-(s-1)R, hi)) — an
+  // anchored edge tile computes every stage from its first output row
+  auto srow = [&](int s, int row) {
+    const int lo = min((s - 1) * R, aty.lo), hi = max(S1R - (s - 1) * R, aty.hi);
+    return row >= lo && row < hi;
+  };
+  uint32_t hoff[NH];
+  int hl[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    int idx = tid + h * NT;
+    hl[h] = -1;
+    hoff[h] = 0;
+    if (idx < NHALO) {
+      int ur, uc;
+      if (idx < R * UW) {
+        ur = idx / UW;
+        uc = idx - ur * UW;
+      } else if ((idx -= R * UW) < R * UW) {
+        ur = S1R + R + idx / UW;
+        uc = idx % UW;
+      } else {
+        idx -= R * UW;
+        ur = R + idx / (2 * R);
+        const int cc = idx % (2 * R);
+        uc = cc < R ? cc : W + cc;
+      }
+      hl[h] = (ur * UW + uc) * E;
+      hoff[h] = (uint32_t)(clampi(aty.org - R + ur, 0, ny - 1) * (int)sy +
+                           clampi(atx.org - R + uc, 0, nx - 1)) * (uint32_t)E;
+    }
+  }
+  const int64_t szb = sz * E;
+  auto plane = [&](int k) {
+    return plane_rsrc((const char*)uin + (int64_t)clampi(k, 0, nz_alloc - 1) * szb);
+  };
+
+  // rings, slot of plane p = (p - kst) % NR
+  T ru[RPW][NR], ra[RPW][NR], rb[RPW][NR], r1[RPW][NR], rc[RPW][NR], rd[RPW][NR];
+  const int kst = kc0 - 10 * R;
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+#pragma unroll
+    for (int s = 0; s < NR; ++s) ra[q][s] = rb[q][s] = r1[q][s] = rc[q][s] = rd[q][s] = T(0);
+    // u(kst+3..kst+5) into slots 3, 0, 1 (u(kst+6) arrives at the top of iteration kst)
+    ru[q][3] = gld<T>(plane(kst + 3), goff[q]);
+    ru[q][0] = gld<T>(plane(kst + 4), goff[q]);
+    ru[q][1] = gld<T>(plane(kst + 5), goff[q]);
+    ru[q][2] = T(0);
+  }
+  T hv[PF][NH], un[PF][RPW];
+#pragma unroll
+  for (int f = 0; f < PF; ++f) {
+    const auto p5 = plane(kst + f + 5);
+    const auto p6 = plane(kst + f + 6);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) hv[f][h] = gld<T>(p5, hoff[h]);
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) un[f][q] = gld<T>(p6, goff[q]);
+  }
+  const T third = T(1.0 / 3.0), tq = T(0.75);
+
+  auto body = [&]<int PH>(int k) {
+    auto sl = [](int d) { return (PH + d + 4 * NR) % NR; };  // slot of plane k + d
+    constexpr int SET = PH & 1;
+    constexpr int UO = SET * USETB, AO = SET * ASETB;
+    constexpr int PF0 = PH % PF;
+    constexpr int PA = 0, PB_ = 2 * ASETB, PU = 4 * ASETB, PC = 6 * ASETB, PD = 8 * ASETB;
+    // ---- top: u(k+6) enters the ring; LDS planes u(k+5) (+ rim), A(k+4), B(k+3),
+    //      U1(k+2), C(k+1), D(k) ----
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      ru[q][sl(6)] = un[PF0][q];
+      lds_st<T>(lb, ub[q] + UO + (R * UW + R) * E, ru[q][sl(5)]);
+      lds_st<T>(lb + PA, pb[q] + AO, ra[q][sl(4)]);
+      lds_st<T>(lb + PB_, pb[q] + AO, rb[q][sl(3)]);
+      lds_st<T>(lb + PU, pb[q] + AO, r1[q][sl(2)]);
+      lds_st<T>(lb + PC, pb[q] + AO, rc[q][sl(1)]);
+      lds_st<T>(lb + PD, pb[q] + AO, rd[q][sl(0)]);
+    }
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+      if (hl[h] >= 0) lds_st<T>(lb, hl[h] + UO, hv[PF0][h]);
+    {
+      const auto p5 = plane(k + PF + 5);
+      const auto p6 = plane(k + PF + 6);
+#pragma unroll
+      for (int h = 0; h < NH; ++h) hv[PF0][h] = gld<T>(p5, hoff[h]);
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) un[PF0][q] = gld<T>(p6, goff[q]);
+    }
+    __syncthreads();
+
+    auto zin = [&](int p) { return p >= zlo && p < zhi; };
+    // y neighbours of an A-type plane (base offset PL) at row q
+    auto ysum = [&](const char* base, int q) {
+      return fd2_sum(lds_ld<T>(base, pb[q] + AO - W * E), lds_ld<T>(base, pb[q] + AO + W * E));
+    };
+    // ---- stage 1: A(k+5) from u(k+5) (x, y from the LDS u plane with its rim) ----
+    {
+      const bool zv = zin(k + 5);
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const int b = ub[q] + UO;
+        const T c = ru[q][sl(5)];
+        T acc = fd_ctr(q1.kc, c);
+        acc = fd2_axis(acc, q1.k[2], ru[q][sl(4)], ru[q][sl(6)]);
+        acc = fd2_axis(acc, q1.k[0], ld(b + (UW + 0) * E), ld(b + (UW + 2) * E));
+        acc = fd2_axis(acc, q1.k[1], ld(b + 1 * E), ld(b + (2 * UW + 1) * E));
+        acc = pin(acc);
+        ra[q][sl(5)] = (zv && m1[q]) ? acc : c;
+      }
+    }
+    // ---- stage 2: B(k+4) from A(k+4) ----
+    if (k >= kc0 - 8 * R) {
+      const bool zv = zin(k + 4);
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const T uo = ru[q][sl(4)];
+        if (!srow(2, rowq[q])) {  // scalar branch
+          rb[q][sl(4)] = uo;
+          continue;
+        }
+        const T c = ra[q][sl(4)];
+        T acc = fd_ctr(q2.kc, c, tq * uo);
+        acc = fd2_axis(acc, q2.k[2], ra[q][sl(3)], ra[q][sl(5)]);
+        acc = fd2_axis(acc, q2.k[0], wave_shr1(c), wave_shl1(c));
+        acc = fd_apply(acc, q2.k[1], ysum(lb + PA, q));
+        acc = pin(acc);
+        rb[q][sl(4)] = (zv && m1[q]) ? acc : uo;
+      }
+    }
+    // ---- stage 3: U1(k+3) = u^{n+1} from B(k+3) ----
+    if (k >= kc0 - 6 * R) {
+      const bool zv = zin(k + 3);
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const T uo = ru[q][sl(3)];
+        if (!srow(3, rowq[q])) {
+          r1[q][sl(3)] = uo;
+          continue;
+        }
+        const T c = rb[q][sl(3)];
+        T acc = fd_ctr(q3.kc, c, third * uo);
+        acc = fd2_axis(acc, q3.k[2], rb[q][sl(2)], rb[q][sl(4)]);
+        acc = fd2_axis(acc, q3.k[0], wave_shr1(c), wave_shl1(c));
+        acc = fd_apply(acc, q3.k[1], ysum(lb + PB_, q));
+        acc = pin(acc);
+        r1[q][sl(3)] = (zv && m1[q]) ? acc : uo;
+      }
+    }
+    // ---- stage 4: C(k+2) from U1(k+2) (second step, stage 1) ----
+    if (k >= kc0 - 4 * R) {
+      const bool zv = zin(k + 2);
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const T c = r1[q][sl(2)];
+        if (!srow(4, rowq[q])) {
+          rc[q][sl(2)] = c;
+          continue;
+        }
+        T acc = fd_ctr(q1.kc, c);
+        acc = fd2_axis(acc, q1.k[2], r1[q][sl(1)], r1[q][sl(3)]);
+        acc = fd2_axis(acc, q1.k[0], wave_shr1(c), wave_shl1(c));
+        acc = fd_apply(acc, q1.k[1], ysum(lb + PU, q));
+        acc = pin(acc);
+        rc[q][sl(2)] = (zv && m1[q]) ? acc : c;
+      }
+    }
+    // ---- stage 5: D(k+1) from C(k+1), base 3/4 U1(k+1) ----
+    if (k >= kc0 - 2 * R) {
+      const bool zv = zin(k + 1);
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const T uo = r1[q][sl(1)];
+        if (!srow(5, rowq[q])) {
+          rd[q][sl(1)] = uo;
+          continue;
+        }
+        const T c = rc[q][sl(1)];
+        T acc = fd_ctr(q2.kc, c, tq * uo);
+        acc = fd2_axis(acc, q2.k[2], rc[q][sl(0)], rc[q][sl(2)]);
+        acc = fd2_axis(acc, q2.k[0], wave_shr1(c), wave_shl1(c));
+        acc = fd_apply(acc, q2.k[1], ysum(lb + PC, q));
+        acc = pin(acc);
+        rd[q][sl(1)] = (zv && m1[q]) ? acc : uo;
+      }
+    }
+    // ---- stage 6: U2(k) = u^{n+2} from D(k), base 1/3 U1(k) -> global ----
+    if (k >= kc0) {
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        if (rowq[q] < aty.lo || rowq[q] >= aty.hi) continue;  // scalar branch
+        const T c = rd[q][sl(0)];
+        T acc = fd_ctr(q3.kc, c, third * r1[q][sl(0)]);
+        acc = fd2_axis(acc, q3.k[2], rd[q][sl(-1)], rd[q][sl(1)]);
+        acc = fd2_axis(acc, q3.k[0], wave_shr1(c), wave_shl1(c));
+        acc = fd_apply(acc, q3.k[1], ysum(lb + PD, q));
+        acc = pin(acc);
+        if (m6[q]) gst<T>(plane_rsrc((char*)uout + (int64_t)k * szb), goff[q], acc);
+      }
+    }
+  };
+  for (int kb = kst; kb < kc1; kb += NR) {
+    [&]<int... P>(std::integer_sequence<int, P...>) {
+      (void)((kb + P < kc1 ? (body.template operator()<P>(kb + P), true) : false) && ...);
+    }(std::make_integer_sequence<int, NR>{});
+  }
+}
+
+template <typename T, int NW, int RPW>
+__global__ __launch_bounds__(64 * NW) void diffusion3d_step2x_kernel(
+    const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
+    int nz_alloc, int k0, int k1, StepSched sc, int zlo, int zhi, Box2 bx, FdCoef<T> q1,
+    FdCoef<T> q2, FdCoef<T> q3) {
+  __shared__ T lds[V6Geom<T, NW, RPW>::TOTAL];
+  const Tile3 tile = xcd_tile();
+  const int kc0 = k0 + tile.z * sc.zchunk;
+  const int kc1 = min(kc0 + sc.zchunk, k1);
+  v6_march<T, NW, RPW>(lds, tile.x, tile.y, sc.gx, sc.gy, sc.edge, kc0, kc1, uin, uout, nx, ny,
+                       sy, sz, nz_alloc, zlo, zhi, bx, q1, q2, q3);
+}
+
 // Waves per SIMD to budget registers for (fp64): as many workgroups as the LDS admits
 // (FD4 16 waves: 1/CU -> 4; FD2 12 waves: 2/CU -> 6).  Without it the compiler spent 86
 // VGPRs on the FD2 step and lost the second workgroup per CU (-25 %).
@@ -660,10 +972,6 @@ static hipError_t launch_step(const SArgs& a) {
   return hipGetLastError();
 }
 
-// Tile shape per order.  With the edge tiles (axis_tile), interleaved medians at 512^3:
-// FD4 16 waves x 2 rows (32 stage-1 rows) 662 us vs 715 us for 12 x 3; FD2 12 x 3 rows
-// 535 us vs 549 us for 16 x 2 (profiles/archive/step_cfgs_edge_r2.log).  48 rows overflow the
-// 16-bit DS offsets, 10 x 4 spills at 168 VGPRs.
 // Phase-overlap variant (v3_march VAR) per order, from the round-3 interleaved A/B at
 // 512^3 fp64 (bench/step_ab.py, profiles/step_ab_r3.log; medians of 7 rounds x 10):
 //   FD4 (16 x 2): graded priority (VAR 3) 655.5 us vs 691.9 plain (-5.3 %); deferring
@@ -726,6 +1034,40 @@ static hipError_t dispatch_step(const SArgs& a) {
     return launch_step_var<T, ORDER, 16, 2>(a);
   else
     return launch_step_var<T, ORDER, 12, 3>(a);
+}
+
+// two-step FD2 launch (v6_march): 12 waves x 2 rows (24 stage-1 rows, 14 output rows;
+// six double-buffered LDS planes = 160.6 KB of the CU's 160 KiB)
+template <typename T, int NW, int RPW>
+static hipError_t launch_step2x(const SArgs& a) {
+  constexpr int R = 1, SH = 5 * R;
+  const int edge = step_edge();
+  const int gx = axis_tile_count(64, R, a.bx.xa0, a.bx.xa1, a.bx.xo0, a.bx.xo1, a.nx, edge, SH);
+  const int gy = axis_tile_count(NW * RPW, R, a.bx.ya0, a.bx.ya1, a.bx.yo0, a.bx.yo1, a.ny, edge,
+                                 SH);
+  static const int per_cu = [] {
+    int nb = 0;
+    const void* fn = (const void*)diffusion3d_step2x_kernel<T, NW, RPW>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * NW, 0) != hipSuccess || nb < 1)
+      nb = 1;
+    return nb;
+  }();
+  static const int minc = knob("STEP_MIN_CHUNK", 16);
+  const int na = std::max(a.k1 - a.k0, 0);
+  const long long slots = (long long)device_cus() * per_cu;
+  StepSched sc{gx, gy, 0, 0, edge};
+  const int zforce = step_zchunk();
+  const int zc = zforce > 0 ? std::min(zforce, na)
+                            : pick_chunk_rounds(na, (long long)gx * gy, slots, 10 * R, minc);
+  sc.gza = div_up(na, zc);
+  sc.zchunk = zc;
+  const FdCoef<T> q1 = fd_coef<T>(2, a.cx, a.cy, a.cz, a.dt, 1.0, true);
+  const FdCoef<T> q2 = fd_coef<T>(2, a.cx, a.cy, a.cz, a.dt, 0.25, true);
+  const FdCoef<T> q3 = fd_coef<T>(2, a.cx, a.cy, a.cz, a.dt, 2.0 / 3.0, true);
+  hipLaunchKernelGGL((diffusion3d_step2x_kernel<T, NW, RPW>), dim3(gx, gy, sc.gza),
+                     dim3(64, NW, 1), 0, a.st, (const T*)a.uin, (T*)a.uout, a.nx, a.ny, a.sy,
+                     a.sz, a.nz_alloc, a.k0, a.k1, sc, a.zlo, a.zhi, a.bx, q1, q2, q3);
+  return hipGetLastError();
 }
 
 }  // namespace advdiff
@@ -791,6 +1133,27 @@ extern "C" int advdiff_diffusion3d_step_box_ex(int dtype, const void* uin, void*
     if (order == 4) return dispatch_step<float, 4>(a);
     if (order == 2) return dispatch_step<float, 2>(a);
   }
+  return hipErrorInvalidValue;
+}
+
+// TWO fused SSP-RK3 steps of the 7-point heat equation in one launch (order 2 only, one
+// plane range): uout[k0:k1] = RK3(RK3(uin)), bit-identical to two advdiff_diffusion3d_step
+// launches.  The planes within 5 of [k0, k1) must hold u^n (ghosts included); the frozen
+// cells (outside [zlo, zhi) and the box's active x/y range) keep their values.
+extern "C" int advdiff_diffusion3d_step2x(int dtype, const void* uin, void* uout, int nx, int ny,
+                                          int64_t sy, int64_t sz, int nz_alloc, int k0, int k1,
+                                          int zlo, int zhi, const int* box, double cx, double cy,
+                                          double cz, double dt, void* stream) {
+  using namespace advdiff;
+  if (k1 <= k0) return hipSuccess;
+  if (nx <= 0 || ny <= 0 || uin == uout || k0 < 0 || k1 > nz_alloc || box == nullptr)
+    return hipErrorInvalidValue;
+  if (sy * (int64_t)ny >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+  const Box2 bx{box[0], box[1], box[2], box[3], box[4], box[5], box[6], box[7]};
+  const SArgs a{uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, 0, 0, zlo, zhi, bx,
+                cx, cy, cz, dt, (hipStream_t)stream};
+  if (dtype == ADVDIFF_F64) return launch_step2x<double, 12, 2>(a);
+  if (dtype == ADVDIFF_F32) return launch_step2x<float, 12, 2>(a);
   return hipErrorInvalidValue;
 }
 

@@ -66,6 +66,7 @@ class Model:
     bytes_per_cell_step = 64.0  # HBM traffic estimate of the fused path (metric only)
     needs_umax = False
     supports_fused = False   # one launch per full RK3 step (ghost width 3R)
+    supports_step2 = False   # one launch per TWO RK3 steps (single rank)
 
     def bind(self, grid: Grid) -> None:
         self.grid = grid

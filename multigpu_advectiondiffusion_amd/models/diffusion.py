@@ -15,6 +15,8 @@ Deliberate deltas from the reference:
 """
 from __future__ import annotations
 
+import os
+
 from ..ops import stencil
 from .base import Model
 
@@ -52,6 +54,20 @@ class Diffusion(Model):
     def bytes_per_cell_step(self):
         # fused step: read u^n + write u^{n+1}; per-stage: 16 + 24 + 24 B
         return 16.0 if self.supports_fused else 64.0
+
+    @property
+    def supports_step2(self) -> bool:
+        """Two RK3 steps per launch (3-D FD2, one rank: diffusion_fused.hip v6_march, half
+        the HBM traffic per step).  ADVDIFF_STEP2=0 keeps one step per launch."""
+        return (self.fused and self.dims == 3 and self.order == 2
+                and os.environ.get("ADVDIFF_STEP2", "1") != "0")
+
+    def step2(self, uin, uout, lo, hi, zlo, zhi, dt, stream=None):
+        """Two fused RK3 steps on planes [lo, hi) of a whole (one-rank) field."""
+        g = self.grid
+        stencil.diffusion3d_step2x(uin, uout, nx=g.nx, ny=g.ny, k0=lo, k1=hi, zlo=zlo, zhi=zhi,
+                                   border=self.border, cx=self.coef[0], cy=self.coef[1],
+                                   cz=self.coef[2], dt=dt, stream=stream)
 
     def step(self, uin, uout, lo, hi, zlo, zhi, dt, stream=None, lo2=0, hi2=0, nx=None,
              ny=None, box=None, exclusive=False):

@@ -134,6 +134,35 @@ def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, 
                                          cz, dt)
 
 
+def diffusion3d_step2x(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, cx, cy, cz, dt,
+                       stream=None, box=None):
+    """TWO FD2 SSP-RK3 steps in one launch (diffusion_fused.hip v6_march): uout[k0:k1] =
+    RK3(RK3(uin)), bit-identical to two diffusion3d_step calls through a scratch field.
+    u^n is read once and u^{n+2} written once: half the HBM traffic per step.  The planes
+    within 5 of [k0, k1) must hold u^n (one rank: the whole field)."""
+    _check_layout(uin, uout)
+    if uin.data_ptr() == uout.data_ptr():
+        raise ValueError("the fused step needs distinct input/output buffers")
+    if box is None:
+        box = (border, nx - border, border, ny - border, 0, nx, 0, ny)
+    if _native(uin):
+        lib = _lib.require()
+        nz = uin.shape[0]
+        assert 0 <= k0 and k1 <= nz and 0 <= zlo and zhi <= nz
+        assert nx <= uin.shape[2] and ny <= uin.shape[1]
+        code = lib.advdiff_diffusion3d_step2x(
+            _dtype_code(uin), _ptr(uin), _ptr(uout), nx, ny, uin.stride(1), uin.stride(0), nz,
+            k0, k1, zlo, zhi, _int_array(box), cx, cy, cz, dt, _stream_ptr(stream))
+        _lib.check(code, "diffusion3d_step2x")
+    elif k1 > k0:
+        # the kernel's dependency cone: U1 on [k0-5, k1+5) from u^n, then u^{n+2}
+        nz = uin.shape[0]
+        mid = uin.clone()
+        ref.diffusion3d_step_box(uin, mid, nx, ny, max(k0 - 5, zlo, 1), min(k1 + 5, zhi, nz - 1),
+                                 zlo, zhi, box, 2, cx, cy, cz, dt)
+        ref.diffusion3d_step_box(mid, uout, nx, ny, k0, k1, zlo, zhi, box, 2, cx, cy, cz, dt)
+
+
 def diffusion2d_step(uin, uout, *, nx, j0, j1, ylo, yhi, border, order, cx, cy, dt,
                      stream=None, box=None):
     """A FULL 2-D SSP-RK3 step in one launch: uout[j0:j1] = RK3(uin) (rows).

@@ -22,6 +22,7 @@ replay the step loop as hipGraphs.
 """
 from __future__ import annotations
 
+import contextlib
 import time
 
 import numpy as np
@@ -514,6 +515,38 @@ class Solver:
         self.t += dt
         self.it += 1
 
+    def step2_capable(self) -> bool:
+        """Two fixed-dt steps in one launch (single-rank 3-D FD2 heat: the model's step2,
+        bit-identical to two steps)."""
+        return (self.fused and self.comm.size == 1 and not self.cart and self.du is None
+                and self.model.supports_step2 and self._dt_dev is None)
+
+    def step2(self, dt: float) -> None:
+        """Two steps at the same dt (one launch when step2_capable)."""
+        if not self.step2_capable():
+            self.step(dt)
+            self.step(dt)
+            return
+        ctx = stencil.use_torch_reference() if self.kernel == "torch" else contextlib.nullcontext()
+        with ctx:
+            self._pending.pop(id(self.u), None)
+            lo, hi = self.full
+            self.model.step2(self.u, self.un, lo, hi, self.zact[0], self.zact[1], dt)
+            trace.sync_check(f"{self.model.name} fused 2-step [{lo},{hi})", self.device)
+        self.u, self.un = self.un, self.u
+        for _ in range(2):  # same rounding as two steps
+            self.t += dt
+        self.it += 2
+
+    def _steps(self, n: int, dt: float) -> None:
+        """n steps at a fixed dt: pairs in one launch where possible."""
+        if self.step2_capable():
+            for _ in range(n // 2):
+                self.step2(dt)
+            n %= 2
+        for _ in range(n):
+            self.step(dt)
+
     def step(self, dt: float) -> None:
         if self.kernel == "torch":
             with stencil.use_torch_reference():
@@ -616,11 +649,11 @@ class Solver:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.stream(side):
             with torch.cuda.graph(graph, stream=side):
-                for _ in range(self.GRAPH_STEPS):
-                    if dt is None:
+                if dt is None:
+                    for _ in range(self.GRAPH_STEPS):
                         self._step_device_dt(t_end)
-                    else:
-                        self.step(dt)
+                else:
+                    self._steps(self.GRAPH_STEPS, dt)
                 if self.comm.size > 1:
                     self.sync_halos()  # every comm-stream fork joins back into the capture
         torch.cuda.current_stream().wait_stream(side)
@@ -639,8 +672,7 @@ class Solver:
                     self.t += dt
                 self.it += self.GRAPH_STEPS
             n %= self.GRAPH_STEPS
-        for _ in range(n):
-            self.step(dt)
+        self._steps(n, dt)
 
     # ------------------------------------------------------------------------------
     # adaptive CFL on the device: max|u| (norm reducer) -> RCCL MAX allreduce on the
@@ -734,6 +766,9 @@ class Solver:
                 while n > 0 and self.t + n * fixed_dt > t_end:
                     n -= 1
             self._advance(n, fixed_dt, True)
+        # two steps per launch where the model has it and nothing runs between steps
+        pair_ok = (fixed_dt is not None and callback is None and not self.check_every
+                   and _FAULT is None and self.step2_capable())
         while not dev_dt:
             if iters is not None and self.it - steps0 >= iters:
                 break
@@ -742,6 +777,16 @@ class Solver:
             h = fixed_dt if fixed_dt is not None else self.dt()
             if t_end is not None and self.t + h > t_end:
                 h = t_end - self.t
+            if pair_ok and h == fixed_dt:
+                if iters is not None:
+                    pair = iters - (self.it - steps0) >= 2
+                else:  # the second step is a full one as well (same test as the loop's)
+                    t1 = self.t + h
+                    pair = t1 < t_end * (1 - 1e-14) and t1 + h <= t_end
+                if pair:
+                    with trace.range_(f"steps {self.it}-{self.it + 1}"):
+                        self.step2(h)
+                    continue
             with trace.range_(f"step {self.it}"):
                 self.step(h)
             if _FAULT is not None and _FAULT == (self.comm.rank, self.it):

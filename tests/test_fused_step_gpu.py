@@ -229,3 +229,81 @@ def test_fused_step_edge_tiles_bitwise(order, boxkind, shape):
         written = ~outs[0].isnan().cpu()
         assert torch.equal(written, ~ref_out.isnan())
         assert (outs[0].cpu()[written] - ref_out[written]).abs().max().item() < 1e-12
+
+
+# ---- two steps per launch (v6_march, FD2): == two one-step launches, bit for bit ----
+STEP2_CASES = CASES + [
+    (24, 33, 50, 64, 1, 23, 1, 23, 1),        # border 1 (the solver's FD2 default), thin
+    (150, 90, 300, 320, 1, 149, 1, 149, 1),   # several tiles and z chunks per axis
+]
+
+
+def _two_steps(u, nx, ny, k0, k1, zlo, zhi, border, c, dt, box=None):
+    kw = dict(nx=nx, ny=ny, zlo=zlo, zhi=zhi, border=border, order=2, cx=c[0], cy=c[1],
+              cz=c[2], dt=dt, box=box)
+    nz = u.shape[0]
+    mid, out = u.clone(), u.clone()
+    stencil.diffusion3d_step(u, mid, k0=max(k0 - 5, 0), k1=min(k1 + 5, nz), **kw)
+    stencil.diffusion3d_step(mid, out, k0=k0, k1=k1, **kw)
+    return out
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("case", STEP2_CASES)
+def test_two_step_kernel_bitwise_equals_two_steps(dtype, case):
+    nz, ny, nx, sx, k0, k1, zlo, zhi, border = case
+    g = torch.Generator().manual_seed(5)
+    u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).to(dtype).cuda()
+    c = (0.21, 0.17, 0.13)
+    dt = 0.9 / (2 * sum(c))
+    exp = _two_steps(u, nx, ny, k0, k1, zlo, zhi, border, c, dt)
+    got = u.clone()
+    stencil.diffusion3d_step2x(u, got, nx=nx, ny=ny, k0=k0, k1=k1, zlo=zlo, zhi=zhi,
+                               border=border, cx=c[0], cy=c[1], cz=c[2], dt=dt)
+    torch.cuda.synchronize()
+    assert torch.equal(got, exp), (got - exp).abs().max().item()
+
+
+@pytest.mark.parametrize("edge", [1, 0])
+def test_two_step_kernel_box_and_tiles(edge):
+    """An explicit active / output box (a Cartesian block's view) and both tile partitions
+    (boundary-anchored edge tiles and the plain one)."""
+    from multigpu_advectiondiffusion_amd.ops import _lib
+    lib = _lib.require()
+    old = lib.advdiff_set_step_edge(edge)
+    try:
+        nz, ny, nx, sx = 60, 70, 150, 160
+        g = torch.Generator().manual_seed(9)
+        u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).cuda()
+        c = (0.21, 0.17, 0.13)
+        dt = 0.9 / (2 * sum(c))
+        box = (3, 140, 2, 66, 10, 120, 7, 60)
+        exp = _two_steps(u, nx, ny, 6, 54, 1, 59, 1, c, dt, box=box)
+        got = u.clone()
+        stencil.diffusion3d_step2x(u, got, nx=nx, ny=ny, k0=6, k1=54, zlo=1, zhi=59, border=1,
+                                   cx=c[0], cy=c[1], cz=c[2], dt=dt, box=box)
+        torch.cuda.synchronize()
+        assert torch.equal(got, exp), (got - exp).abs().max().item()
+    finally:
+        lib.advdiff_set_step_edge(old)
+
+
+def test_solver_two_step_path_bitwise(monkeypatch):
+    """A single-rank FD2 heat run pairs its steps into two-step launches (eager and graph
+    replay, odd step counts too) with results identical to one step per launch."""
+    from multigpu_advectiondiffusion_amd.models.base import Grid
+    from multigpu_advectiondiffusion_amd.models.diffusion import Diffusion
+    from multigpu_advectiondiffusion_amd.solver import Solver
+
+    def run(flag, iters, graph):
+        monkeypatch.setenv("ADVDIFF_STEP2", flag)
+        s = Solver(Diffusion(order=2), Grid((67, 45, 38), (1.0, 1.0, 1.0)), device="cuda")
+        assert s.step2_capable() == (flag == "1")
+        s.run(iters=iters, graph=graph)
+        return s.owned.clone(), s.it, s.t
+
+    for iters, graph in ((5, False), (19, True)):
+        a, ita, ta = run("1", iters, graph)
+        b, itb, tb = run("0", iters, graph)
+        assert (ita, ta) == (itb, tb)
+        assert torch.equal(a, b), (a - b).abs().max().item()

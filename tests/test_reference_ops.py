@@ -133,3 +133,37 @@ def test_burgers3d_reference_axis_symmetry(z):
     Lz = ref.burgers_rhs_3d(uz, **kw)
     assert torch.allclose(Lx[5, 5, :], Ly[5, :, 5], atol=1e-14)
     assert torch.allclose(Lx[5, 5, :], Lz[:, 5, 5], atol=1e-14)
+
+
+def test_two_step_fallback_and_solver_pairing(monkeypatch):
+    """CPU semantics of the two-step FD2 launch (ops/stencil.py::diffusion3d_step2x: two
+    reference steps through a scratch field) and the solver's step pairing (eager, odd
+    counts, t_end runs): identical to one step per launch."""
+    from multigpu_advectiondiffusion_amd.models.base import Grid
+    from multigpu_advectiondiffusion_amd.models.diffusion import Diffusion
+    from multigpu_advectiondiffusion_amd.ops import stencil
+    from multigpu_advectiondiffusion_amd.solver import Solver
+
+    g = torch.Generator().manual_seed(3)
+    u = torch.rand((20, 17, 19), generator=g, dtype=torch.float64)
+    c, dt = (0.2, 0.15, 0.1), 0.9 / (2 * 0.45)
+    kw = dict(nx=19, ny=17, zlo=1, zhi=19, border=1, cx=c[0], cy=c[1], cz=c[2], dt=dt)
+    got = u.clone()
+    stencil.diffusion3d_step2x(u, got, k0=1, k1=19, **kw)
+    mid, exp = u.clone(), u.clone()
+    for a, b in ((u, mid), (mid, exp)):
+        stencil.diffusion3d_step(a, b, k0=1, k1=19, order=2, **kw)
+    assert torch.equal(got, exp)
+
+    def run(flag, **rk):
+        monkeypatch.setenv("ADVDIFF_STEP2", flag)
+        s = Solver(Diffusion(order=2), Grid((19, 17, 20), (1.0, 1.0, 1.0)), device="cpu")
+        assert s.step2_capable() == (flag == "1")
+        s.run(**rk)
+        return s.owned.clone(), s.it, s.t
+
+    for rk in (dict(iters=5), dict(t_end=0.05)):
+        a, ita, ta = run("1", **rk)
+        b, itb, tb = run("0", **rk)
+        assert (ita, ta) == (itb, tb)
+        assert torch.equal(a, b)
