@@ -211,6 +211,9 @@ int advdiff_diffusion3d_step2x(int dtype, const void* uin, void* uout, int nx, i
 int advdiff_set_step_zchunk(int zc);
 // fp32 fused heat step tile: 0 = the fp64 shapes, 3 / 4 = 16 waves x 3 / 4 rows
 int advdiff_set_step_f32_tile(int t);
+// fp32 3-D WENO5 stage: packed pairs (1, default) or one cell per lane (0); returns the
+// previous setting.  Bit-identical either way.
+int advdiff_set_b3_pack(int on);
 // v9 tile row width: 64, 32 or 0 = chosen per plane shape (returns the previous setting)
 int advdiff_set_b3_tx(int v);
 // 2-D WENO5 stage kernel version (2 = the barrier-free wave-strip kernel, default; 1 = the

@@ -377,7 +377,7 @@ __global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(WPE))) 
 template <typename T>
 __device__ __forceinline__ T fast_div1(T n, T d) {
 #pragma clang fp contract(off)
-  if constexpr (sizeof(T) == 8) {
+  if constexpr (std::is_same_v<T, double>) {
     T r = __builtin_amdgcn_rcp(d);
     r = fma(fma(-d, r, T(1)), r, r);
     const T q = n * r;
@@ -391,16 +391,31 @@ __device__ __forceinline__ T fast_div1(T n, T d) {
 // numerator times a reciprocal refined by one Newton step (relative error ~2^-46, i.e.
 // ~1e-14 of the flux; fast_div1's residual correction to a correctly rounded quotient
 // costs 2 more fp64 ops per face and buys nothing the scheme can see)
+__device__ __forceinline__ float rcp_hw(float d) { return __builtin_amdgcn_rcpf(d); }
+__device__ __forceinline__ f32x2 rcp_hw(f32x2 d) {
+  return f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+// fp32 reciprocal: hardware estimate + one Newton step (~1 ulp; packed for pairs)
+template <typename T>
+__device__ __forceinline__ T rcp_nr(T d) {
+#pragma clang fp contract(off)
+  const T r = rcp_hw(d);
+  return fma(fma(-d, r, T(1)), r, r);
+}
+
+// fp32 (one cell or a packed pair) keeps one reciprocal per side: S1 S2 of the JS weights
+// can fall below the fp32 normal range.  The IEEE quotients of rounds 1-3 cost ~10
+// unpacked ops each; the refined reciprocals are 1 + 2 (packed) ops per element and side.
 template <typename T>
 __device__ __forceinline__ T w5_combine6(T n1, T S1, T n2, T S2) {
 #pragma clang fp contract(off)
-  if constexpr (sizeof(T) == 8) {
+  if constexpr (std::is_same_v<T, double>) {
     const T d = S1 * S2;
     T r = __builtin_amdgcn_rcp(d);
     r = fma(fma(-d, r, T(1)), r, r);
     return fma(n1, S2, n2 * S1) * r;
   } else {
-    return fast_div1(n1, S1) + fast_div1(n2, S2);
+    return fma(n1, rcp_nr(S1), n2 * rcp_nr(S2));
   }
 }
 
@@ -431,25 +446,27 @@ __device__ __forceinline__ T w5_combine6(T n1, T S1, T n2, T S2) {
 // The 32 x 16 tile also stages fewer halo cells per output (38 x 22 / (31 x 16) = 1.69
 // vs 70 x 14 / (63 x 8) = 1.94).  wave_shr1 hands lane 32 the face of lane 31 — lane 32
 // is its row's face-only lane, so the DPP shift needs no change.
-template <typename T, bool WZ, bool VISC, int MODE, int TXL = 64>
+template <typename T, bool WZ, bool VISC, int MODE, int TXL = 64, bool PK = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void burgers3d_w5s_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
     int k1, int k0b, int k1b, int gza, int zchunk, int border, T rdx3, T rdy3, T rdz6, T vx,
     T vy, T vz, T dt, T a, T b, const double* __restrict__ dtp, int xcdmap) {
   static_assert(TXL == 64 || TXL == 32, "tile row: 64 or 32 lanes");
+  static_assert(!PK || std::is_same_v<T, float>, "packed pairs: fp32");
+  using V = std::conditional_t<PK, f32x2, T>;  // a lane's value: one cell or a z pair
   constexpr int NW = 8, RW = 64 / TXL;  // waves per workgroup, tile rows per wave
   constexpr int TY = NW * RW, R = 3, NR = 5, TX = TXL, TXO = TX - 1;
   constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NT = 64 * NW, LT = LX * LY;
   constexpr int NPT = (LT + NT - 1) / NT;
-  constexpr int E = (int)sizeof(T);
+  constexpr int E = (int)sizeof(V), EG = (int)sizeof(T);  // LDS / global element bytes
   constexpr int NARR = VISC ? 3 : 2;                 // staged arrays: f+, f- [, u]
   constexpr int SET = NARR * LT + (TY + 1) * TX;     // elements per buffer set (+ y faces)
   constexpr int OM = LT * E, OU = 2 * LT * E, OFY = NARR * LT * E, SETB = SET * E;
   constexpr int XO = 2 * LX * E + 2 * E;             // own cell - lane read base
   static_assert(SETB + XO + NARR * LT * E + 3 * LX * E < 65536, "DS immediate offsets");
-  __shared__ T lds[2 * SET];
+  __shared__ V lds[2 * SET];
   char* lb = (char*)lds;
-  const W5Sgpr<T> kk;  // fp64 constants in SGPRs (VOP3 operands, no v_fmac copies)
+  const W5Sgpr<V> kk;  // fp64 constants in SGPRs (VOP3 operands, no v_fmac copies)
 
   const int tx = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.y);
@@ -466,10 +483,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
   const bool second = tl.z >= gza;
   const int kc0 = second ? k0b + (tl.z - gza) * zchunk : k0 + tl.z * zchunk;
   const int kc1 = min(kc0 + zchunk, second ? k1b : k1);
-  const int klast = kc1 - 1;
+  // PK: the chunk's halves [kc0, kc0 + H) and [kc0 + H, kc1) march side by side, plane
+  // k of the first with plane k + H of the second (the second may be one plane shorter:
+  // its last iteration is then a dummy — plane indices clamped, stores dropped)
+  const int H = PK ? (kc1 - kc0 + 1) / 2 : kc1 - kc0;
+  const int kce = kc0 + H;  // end of the march
+  const int klast = kce - 1;
   const bool active = col >= 1 && i < nx - border && j < ny - border;
-  const uint32_t goff = (uint32_t)(min(j, ny - 1) * (int)sy + min(i, nx - 1)) * (uint32_t)E;
-  const int64_t szb = sz * E;
+  const uint32_t goff = (uint32_t)(min(j, ny - 1) * (int)sy + min(i, nx - 1)) * (uint32_t)EG;
+  const int64_t szb = sz * EG;
   auto plane = [&](const T* base, int k) {
     return plane_rsrc((const char*)base + (int64_t)k * szb);
   };
@@ -478,6 +500,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
       for (int k = kc0; k < kc1; ++k) gst<T>(plane(out, k), goff, gld<T>(plane(in, k), goff));
     return;
   }
+  // global load of plane k (PK: and of plane k + H, clamped to the last plane the
+  // unpacked march reads) / store of plane k (PK: and k + H if it is in the chunk)
+  auto gl = [&](const T* base, int k, uint32_t off) -> V {
+    if constexpr (PK)
+      return V{gld<T>(plane(base, k), off), gld<T>(plane(base, min(k + H, kc1 + R - 1)), off)};
+    else
+      return gld<T>(plane(base, k), off);
+  };
+  auto gs = [&](T* base, int k, V v) {
+    if constexpr (PK) {
+      gst<T>(plane(base, k), goff, v.x);
+      if (k + H < kc1) gst<T>(plane(base, k + H), goff, v.y);
+    } else {
+      gst<T>(plane(base, k), goff, v);
+    }
+  };
 
   uint32_t toff[NPT];
 #pragma unroll
@@ -485,61 +523,60 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
     const int idx = min(tid + r * NT, LT - 1);
     const int ly = idx / LX, lx = idx - ly * LX;
     toff[r] = (uint32_t)(clampi(jb - R + ly, 0, ny - 1) * (int)sy +
-                         clampi(ib - R + lx, 0, nx - 1)) * (uint32_t)E;
+                         clampi(ib - R + lx, 0, nx - 1)) * (uint32_t)EG;
   }
   // loop-invariant LDS lane bases (byte addresses); everything else is an immediate
   const int lrb = ((row + R) * LX + col + R) * E - XO;  // own-cell reads
   const int brb = col * E;                              // bottom y faces (row R-1) + its store
   const int fyb = ((row + 1) * TX + col) * E;           // y face above the own cell
   const int stb = tid * E;                           // tile staging
-  T pre[NPT];
+  V pre[NPT];
   auto fetch_tile = [&](int k) {
-    const auto rs = plane(in, k);
 #pragma unroll
-    for (int r = 0; r < NPT; ++r) pre[r] = gld<T>(rs, toff[r]);
+    for (int r = 0; r < NPT; ++r) pre[r] = gl(in, k, toff[r]);
   };
   auto stage_tile = [&]<int SB>() {  // SB: byte offset of the buffer set
 #pragma unroll
     for (int r = 0; r < NPT; ++r) {
       const int idx = tid + r * NT;
       if (NPT * NT == LT || idx < LT) {
-        T p, m;
+        V p, m;
         lf_split(pre[r], p, m);
-        lds_st<T>(lb + stb, SB + r * NT * E, p);
-        lds_st<T>(lb + stb, SB + OM + r * NT * E, m);
-        if constexpr (VISC) lds_st<T>(lb + stb, SB + OU + r * NT * E, pre[r]);
+        lds_st<V>(lb + stb, SB + r * NT * E, p);
+        lds_st<V>(lb + stb, SB + OM + r * NT * E, m);
+        if constexpr (VISC) lds_st<V>(lb + stb, SB + OU + r * NT * E, pre[r]);
       }
     }
   };
   // 3 x flux at the face to the right of the cell at immediate offset c (relative to the
   // base pointer bp) along stride st
   auto lds_face3 = [&](const char* bp, int c, int st) {
-    T pv[5], mv[5];
+    V pv[5], mv[5];
 #pragma unroll
     for (int d = 0; d < 5; ++d) {
-      pv[d] = lds_ld<T>(bp, c + (d - 2) * st);
-      mv[d] = lds_ld<T>(bp, c + OM + (d - 1) * st);
+      pv[d] = lds_ld<V>(bp, c + (d - 2) * st);
+      mv[d] = lds_ld<V>(bp, c + OM + (d - 1) * st);
     }
-    T n1, S1, n2, S2;
-    w5_face3_sides<T, WZ>(pv, mv, n1, S1, n2, S2, kk);
+    V n1, S1, n2, S2;
+    w5_face3_sides<V, WZ>(pv, mv, n1, S1, n2, S2, kk);
     return w5_combine6(n1, S1, n2, S2);
   };
 
   // ---- rings: plane p lives in slot (p - kc0 + 2 NR) % NR ----
-  T rp[NR], rm[NR], ru[NR], cp[NR], cm[NR], fz[NR];  // f+, f-, u, C(f+), C(f-), 6 x z face
+  V rp[NR], rm[NR], ru[NR], cp[NR], cm[NR], fz[NR];  // f+, f-, u, C(f+), C(f-), 6 x z face
   {
-    T uz[2 * R], fp[2 * R], fm[2 * R];  // planes kc0-3 .. kc0+2
+    V uz[2 * R], fp[2 * R], fm[2 * R];  // planes kc0-3 .. kc0+2
 #pragma unroll
     for (int q = 0; q < 2 * R; ++q) {
-      uz[q] = gld<T>(plane(in, kc0 - R + q), goff);
+      uz[q] = gl(in, kc0 - R + q, goff);
       lf_split(uz[q], fp[q], fm[q]);
     }
     auto sl = [](int p) { return (p + 2 * NR) % NR; };  // slot of plane kc0 + p
     {  // face kc0-½: the march's z-face arithmetic (bit-identical to it)
-      T n1, S1, n2, S2;
-      w5_side<T, WZ>(fp[0], fp[1], fp[2], fp[3], fp[4], w5_curv(fp[0], fp[1], fp[2], kk),
+      V n1, S1, n2, S2;
+      w5_side<V, WZ>(fp[0], fp[1], fp[2], fp[3], fp[4], w5_curv(fp[0], fp[1], fp[2], kk),
                      w5_curv(fp[1], fp[2], fp[3], kk), w5_curv(fp[2], fp[3], fp[4], kk), n1, S1, kk);
-      w5_side<T, WZ>(fm[5], fm[4], fm[3], fm[2], fm[1], w5_curv(fm[5], fm[4], fm[3], kk),
+      w5_side<V, WZ>(fm[5], fm[4], fm[3], fm[2], fm[1], w5_curv(fm[5], fm[4], fm[3], kk),
                      w5_curv(fm[4], fm[3], fm[2], kk), w5_curv(fm[3], fm[2], fm[1], kk), n2, S2, kk);
       fz[sl(-1)] = w5_combine6(n1, S1, n2, S2);
     }
@@ -558,47 +595,47 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
   fetch_tile(kc0);
   stage_tile.template operator()<0>();
   fetch_tile(min(kc0 + 1, klast));
-  T un = gld<T>(plane(in, kc0 + R), goff);  // u(k+3) of the current iteration
-  T ax = T(0);
-  if constexpr (reads_aux<MODE>()) ax = gld<T>(plane(aux, kc0), goff);
+  V un = gl(in, kc0 + R, goff);  // u(k+3) of the current iteration
+  V ax = V(0);
+  if constexpr (reads_aux<MODE>()) ax = gl(aux, kc0, goff);
   __syncthreads();
 
   auto body = [&]<int PH>(int k) {
     auto sl = [](int d) { return (PH + d + 2 * NR) % NR; };  // slot of plane k + d
     constexpr int SB = (PH & 1) * SETB, SBN = SETB - SB;    // this / the other set
     // new plane k+3 of the own column: f-(k+3) now; f+(k+3) and u(k+3) after their use
-    T pn, mn;
+    V pn, mn;
     lf_split(un, pn, mn);
     rm[sl(3)] = mn;
-    const T unew = un;
-    un = gld<T>(plane(in, min(k + 1, klast) + R), goff);
-    T axk = ax;
-    if constexpr (reads_aux<MODE>()) ax = gld<T>(plane(aux, min(k + 1, klast)), goff);
+    const V unew = un;
+    un = gl(in, min(k + 1, klast) + R, goff);
+    V axk = ax;
+    if constexpr (reads_aux<MODE>()) ax = gl(aux, min(k + 1, klast), goff);
 
-    const T fy = lds_face3(lb + lrb, SB + XO, LX * E);  // y face j+½
+    const V fy = lds_face3(lb + lrb, SB + XO, LX * E);  // y face j+½
     if (w == (k - kc0) % NW)  // the tile's bottom y faces rotate over the waves
       // (TXL 32: both rows of the wave compute them; identical values, same slots)
-      lds_st<T>(lb + brb, SB + OFY, lds_face3(lb + brb, SB + ((R - 1) * LX + R) * E, LX * E));
-    lds_st<T>(lb + fyb, SB + OFY, fy);
-    const T ctr = ru[sl(0)];
-    T d2x = T(0), d2y = T(0), d2z = T(0);
-    const T fx = lds_face3(lb + lrb, SB + XO, E);  // x face i+½
+      lds_st<V>(lb + brb, SB + OFY, lds_face3(lb + brb, SB + ((R - 1) * LX + R) * E, LX * E));
+    lds_st<V>(lb + fyb, SB + OFY, fy);
+    const V ctr = ru[sl(0)];
+    V d2x = V(0), d2y = V(0), d2z = V(0);
+    const V fx = lds_face3(lb + lrb, SB + XO, E);  // x face i+½
     if constexpr (VISC) {
       const int c = SB + OU + XO;
       const char* bp = lb + lrb;
-      d2x = fd4_d2k(lds_ld<T>(bp, c - 2 * E), lds_ld<T>(bp, c - E), ctr,
-                    lds_ld<T>(bp, c + E), lds_ld<T>(bp, c + 2 * E), kk);
-      d2y = fd4_d2k(lds_ld<T>(bp, c - 2 * LX * E), lds_ld<T>(bp, c - LX * E), ctr,
-                    lds_ld<T>(bp, c + LX * E), lds_ld<T>(bp, c + 2 * LX * E), kk);
+      d2x = fd4_d2k(lds_ld<V>(bp, c - 2 * E), lds_ld<V>(bp, c - E), ctr,
+                    lds_ld<V>(bp, c + E), lds_ld<V>(bp, c + 2 * E), kk);
+      d2y = fd4_d2k(lds_ld<V>(bp, c - 2 * LX * E), lds_ld<V>(bp, c - LX * E), ctr,
+                    lds_ld<V>(bp, c + LX * E), lds_ld<V>(bp, c + 2 * LX * E), kk);
       d2z = fd4_d2k(ru[sl(-2)], ru[sl(-1)], ctr, ru[sl(1)], ru[sl(2)], kk);
     }
     cp[sl(1)] = w5_curv(rp[sl(0)], rp[sl(1)], rp[sl(2)], kk);
     cm[sl(2)] = w5_curv(rm[sl(1)], rm[sl(2)], rm[sl(3)], kk);
     {
-      T n1, S1, n2, S2;
-      w5_side<T, WZ>(rp[sl(-2)], rp[sl(-1)], rp[sl(0)], rp[sl(1)], rp[sl(2)], cp[sl(-1)],
+      V n1, S1, n2, S2;
+      w5_side<V, WZ>(rp[sl(-2)], rp[sl(-1)], rp[sl(0)], rp[sl(1)], rp[sl(2)], cp[sl(-1)],
                      cp[sl(0)], cp[sl(1)], n1, S1, kk);
-      w5_side<T, WZ>(rm[sl(3)], rm[sl(2)], rm[sl(1)], rm[sl(0)], rm[sl(-1)], cm[sl(2)],
+      w5_side<V, WZ>(rm[sl(3)], rm[sl(2)], rm[sl(1)], rm[sl(0)], rm[sl(-1)], cm[sl(2)],
                      cm[sl(1)], cm[sl(0)], n2, S2, kk);
       fz[sl(0)] = w5_combine6(n1, S1, n2, S2);  // face k+½
     }
@@ -609,22 +646,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
     fetch_tile(min(k + 2, klast));
     __syncthreads();  // y faces of k and tile k+1 visible
 
-    const T fyl = lds_ld<T>(lb + fyb, SB + OFY - TX * E);
-    const T fxl = wave_shr1(fx);  // face i-½ from lane l-1 (column 0: unused)
-    T L = -(((fx - fxl) * rdx3 + (fy - fyl) * rdy3) + (fz[sl(0)] - fz[sl(-1)]) * rdz6);
+    const V fyl = lds_ld<V>(lb + fyb, SB + OFY - TX * E);
+    const V fxl = wave_shr1(fx);  // face i-½ from lane l-1 (column 0: unused)
+    V L = -(((fx - fxl) * rdx3 + (fy - fyl) * rdy3) + (fz[sl(0)] - fz[sl(-1)]) * rdz6);
     if constexpr (VISC) L += vx * d2x + vy * d2y + vz * d2z;
-    T dnew = T(0);
-    const T v = stage_value<T, MODE>(axk, ctr, L, dt, a, b, dnew);
+    V dnew = V(0);
+    const V v = stage_value<V, MODE>(axk, ctr, L, V(dt), V(a), V(b), dnew);
     if (active) {
-      gst<T>(plane(out, k), goff, v);
-      if constexpr (MODE == kLs1 || MODE == kLs) gst<T>(plane(aux, k), goff, dnew);
+      gs(out, k, v);
+      if constexpr (MODE == kLs1 || MODE == kLs) gs(aux, k, dnew);
     }
     rp[sl(3)] = pn;  // f+(k+3), u(k+3) replace f+(k-2), u(k-2)
     ru[sl(3)] = unew;
   };
-  for (int kb = kc0; kb < kc1; kb += 2 * NR) {
+  for (int kb = kc0; kb < kce; kb += 2 * NR) {
     [&]<int... P>(std::integer_sequence<int, P...>) {
-      (void)((kb + P < kc1 ? (body.template operator()<P>(kb + P), true) : false) && ...);
+      (void)((kb + P < kce ? (body.template operator()<P>(kb + P), true) : false) && ...);
     }(std::make_integer_sequence<int, 2 * NR>{});
   }
 }
@@ -984,7 +1021,7 @@ static int b3_tile_row(int nx, int ny, int border) {
   return s32 > s64 * 1.01 ? 32 : 64;
 }
 
-template <typename T, bool WZ, bool VISC, int MODE, int TXL>
+template <typename T, bool WZ, bool VISC, int MODE, int TXL, bool PK = false>
 static hipError_t launch_b3_v9_tx(const BArgs& p) {
   // XCD-contiguous tile order (default): 256^3 WENO5-Z + viscous step 0.584 -> 0.564 ms
   // (+3.7 %, 3 interleaved rounds, bitwise identical; profiles/archive/burgers3d_xcd_r2.log)
@@ -1000,19 +1037,22 @@ static hipError_t launch_b3_v9_tx(const BArgs& p) {
   static const int rounds_model = knob("B3_CHUNKS", 1);
   static const int per_cu = [] {
     int nbk = 0;
-    const void* fn = (const void*)burgers3d_w5s_kernel<T, WZ, VISC, MODE, TXL>;
+    const void* fn = (const void*)burgers3d_w5s_kernel<T, WZ, VISC, MODE, TXL, PK>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nbk, fn, 512, 0) != hipSuccess || nbk < 1)
       nbk = 1;
     return nbk;
   }();
-  const int zc = rounds_model
-                     ? pick_chunk_rounds(na + nb, (long long)gx * gy,
+  // PK: a workgroup marches two half chunks side by side — choose the half length
+  const int nm = PK ? div_up(na + nb, 2) : na + nb;
+  const int zm = rounds_model
+                     ? pick_chunk_rounds(nm, (long long)gx * gy,
                                          (long long)device_cus() * per_cu, 4, 8)
-                     : pick_chunk(na + nb, (long long)gx * gy, 8, 256);
+                     : pick_chunk(nm, (long long)gx * gy, 8, 256);
+  const int zc = PK ? 2 * zm : zm;
   const int gza = div_up(na, zc);
   const int gz = gza + div_up(nb, zc);
   const double s = 1.0 / 12.0;
-  hipLaunchKernelGGL((burgers3d_w5s_kernel<T, WZ, VISC, MODE, TXL>), dim3(gx, gy, gz),
+  hipLaunchKernelGGL((burgers3d_w5s_kernel<T, WZ, VISC, MODE, TXL, PK>), dim3(gx, gy, gz),
                      dim3(64, 8, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx, p.ny,
                      p.sy, p.sz, p.lo, p.hi, p.lo2, p.hi2, gza, zc, p.border, T(p.rdx / 3.0),
                      T(p.rdy / 3.0), T(p.rdz / 6.0), T(p.vx * s), T(p.vy * s), T(p.vz * s),
@@ -1020,10 +1060,25 @@ static hipError_t launch_b3_v9_tx(const BArgs& p) {
   return hipGetLastError();
 }
 
+// fp32: packed pairs (two z half chunks per lane, v_pk_* arithmetic) by default;
+// ADVDIFF_B3_PACK=0 / advdiff_set_b3_pack(0) runs one cell per lane.  Both give the same
+// bits (the pair elements take the scalar operation sequence; tests/test_kernels_gpu.py).
+static int g_b3_pack = -1;
+static int b3_pack() {
+  if (g_b3_pack < 0) g_b3_pack = knob("B3_PACK", 1);
+  return g_b3_pack;
+}
+
 template <typename T, bool WZ, bool VISC, int MODE>
 static hipError_t launch_b3_v9(const BArgs& p) {
-  if (b3_tile_row(p.nx, p.ny, p.border) == 32)
-    return launch_b3_v9_tx<T, WZ, VISC, MODE, 32>(p);
+  const bool tx32 = b3_tile_row(p.nx, p.ny, p.border) == 32;
+  if constexpr (std::is_same_v<T, float>) {
+    if (b3_pack()) {
+      if (tx32) return launch_b3_v9_tx<T, WZ, VISC, MODE, 32, true>(p);
+      return launch_b3_v9_tx<T, WZ, VISC, MODE, 64, true>(p);
+    }
+  }
+  if (tx32) return launch_b3_v9_tx<T, WZ, VISC, MODE, 32>(p);
   return launch_b3_v9_tx<T, WZ, VISC, MODE, 64>(p);
 }
 
@@ -1176,6 +1231,12 @@ static hipError_t run_b(int dtype, bool three_d, int scheme, bool ls, const BArg
 extern "C" int advdiff_set_b2_ver(int v) {
   const int old = advdiff::b2_ver();
   advdiff::g_b2_ver = v;
+  return old;
+}
+
+extern "C" int advdiff_set_b3_pack(int on) {
+  const int old = advdiff::b3_pack();
+  advdiff::g_b3_pack = on ? 1 : 0;
   return old;
 }
 

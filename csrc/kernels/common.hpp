@@ -26,6 +26,24 @@ namespace advdiff {
 
 constexpr int kWave = 64;  // CDNA wavefront width (never 32)
 
+// Packed fp32 pair: two cells per lane in one 64-bit register pair, so the templated
+// helpers below (explicit fma, contraction off) compile to v_pk_fma_f32 / v_pk_mul_f32 /
+// v_pk_add_f32 — CDNA4's 2x fp32 VALU rate (the fp64 and scalar-fp32 rates are equal).
+// Each element goes through exactly the scalar operation sequence, so a packed kernel's
+// results are the scalar-fp32 kernel's, cell by cell.  The using-declarations keep the
+// float / double overloads visible next to the pair ones.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+using ::fabs;
+using ::fma;
+__device__ __forceinline__ f32x2 fma(f32x2 a, f32x2 b, f32x2 c) {
+  return __builtin_elementwise_fma(a, b, c);
+}
+__device__ __forceinline__ f32x2 fabs(f32x2 a) { return __builtin_elementwise_abs(a); }
+template <typename T>
+inline constexpr bool is_pair_v = false;
+template <>
+inline constexpr bool is_pair_v<f32x2> = true;
+
 template <typename T>
 __device__ __forceinline__ T clampi(T v, T lo, T hi) {
   return v < lo ? lo : (v > hi ? hi : v);
@@ -568,6 +586,10 @@ __device__ __forceinline__ double dpp_move(double v) {
 template <int CTRL>
 __device__ __forceinline__ float dpp_move(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, true));
+}
+template <int CTRL>
+__device__ __forceinline__ f32x2 dpp_move(f32x2 v) {
+  return f32x2{dpp_move<CTRL>(v.x), dpp_move<CTRL>(v.y)};
 }
 template <typename T>
 __device__ __forceinline__ T wave_shr1(T v) { return dpp_move<0x138>(v); }  // from lane i-1

@@ -168,6 +168,8 @@ def _load():
         lib.advdiff_set_step_f32_tile.restype = c_int
         lib.advdiff_set_step_zchunk.argtypes = [c_int]
         lib.advdiff_set_step_zchunk.restype = c_int
+        lib.advdiff_set_b3_pack.argtypes = [c_int]
+        lib.advdiff_set_b3_pack.restype = c_int
         lib.advdiff_set_b3_tx.argtypes = [c_int]
         lib.advdiff_set_b3_tx.restype = c_int
         lib.advdiff_set_b2_ver.argtypes = [c_int]

@@ -14,6 +14,8 @@ step() { # name seconds cmd...
 }
 step step2_tests 300 python -u -m pytest tests/test_fused_step_gpu.py -x -v --timeout 120 --timeout-method thread -k "two_step"
 step step2_ab 300 python bench/step2_ab.py --rounds 4
+step packed_tests 400 python -u -m pytest tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread -k "packed or burgers3d_stage or tile_rows"
+step fp32_pack_ab 300 python bench/burgers_fp32_ab.py --rounds 4
 step ipc_tests2 500 python -u -m pytest tests/test_ipc_gpu.py -x -v --timeout 150 --timeout-method thread -k "striped or preflight or boundary_stream"
 step native_ipc 400 python -u -m pytest tests/test_native_apps_gpu.py tests/test_ipc_gpu.py -x -v --timeout 150 --timeout-method thread -k "native and ipc"
 step fp32_tiles 300 python bench/step_fp32_ab.py --rounds 4

@@ -397,3 +397,57 @@ def test_burgers3d_v9_tile_rows_vs_reference(tx, shape):
         lib.advdiff_set_b3_tx(old_t)
     assert (outs[tx] - exp).abs().max().item() < 1e-11
     assert torch.equal(outs[32], outs[64])
+
+
+@pytest.mark.parametrize("tx", [64, 32])
+@pytest.mark.parametrize("weno_z,visc", [(True, 0.01), (False, 0.0)])
+@pytest.mark.parametrize("mode", ["ssp1", "ssp", "ls"])
+@pytest.mark.parametrize("ranges", [((3, 58), (0, 0)), ((3, 4), (0, 0)), ((3, 6), (7, 18)),
+                                    ((5, 30), (31, 58))])
+def test_burgers3d_fp32_packed_pairs(tx, weno_z, visc, mode, ranges):
+    """fp32 3-D WENO5 (v9): packed z pairs (two half chunks per lane, v_pk_* arithmetic —
+    the default) bitwise equal to one cell per lane, on odd / one-plane / two-range
+    launches (a dummy last pair iteration) in every stage epilogue, both tile shapes; and
+    against the fp64 reference to fp32 rounding."""
+    lib = _lib.require()
+    (k0, k1), (k0b, k1b) = ranges
+    nz, ny, nx, sx = 61, 37, 131, 136
+    inp = _smooth3(nz, ny, sx, 31, torch.float32)
+    u0 = _smooth3(nz, ny, sx, 32, torch.float32)
+    aux = _smooth3(nz, ny, sx, 33, torch.float32)
+    rd = (1 / 0.02, 1 / 0.03, 1 / 0.025)
+    vv = tuple(visc * r * r for r in rd)
+    a, b = {"ssp1": (0.0, 1.0), "ssp": (0.75, 0.25), "ls": (-0.4, 0.3)}[mode]
+    ls = mode == "ls"
+    kw = dict(nx=nx, ny=ny, k0=k0, k1=k1, k0b=k0b, k1b=k1b, border=3, weno_z=weno_z,
+              rdx=rd[0], rdy=rd[1], rdz=rd[2], vx=vv[0], vy=vv[1], vz=vv[2], dt=1e-3, a=a, b=b)
+    outs = {}
+    old_v, old_t, old_p = (lib.advdiff_set_b3_ver(9), lib.advdiff_set_b3_tx(tx),
+                           lib.advdiff_set_b3_pack(1))
+    try:
+        for pk in (1, 0):
+            lib.advdiff_set_b3_pack(pk)
+            gout, gaux = u0.to(DEV), aux.to(DEV)
+            if ls:
+                stencil.burgers3d_stage(inp.to(DEV), gaux, gout, ls=True, **kw)
+            else:
+                stencil.burgers3d_stage(inp.to(DEV), gout.clone(), gout, **kw)
+            torch.cuda.synchronize()
+            outs[pk] = (gout.cpu(), gaux.cpu())
+    finally:
+        lib.advdiff_set_b3_ver(old_v)
+        lib.advdiff_set_b3_tx(old_t)
+        lib.advdiff_set_b3_pack(old_p)
+    assert torch.equal(outs[1][0], outs[0][0]), (outs[1][0] - outs[0][0]).abs().max().item()
+    assert torch.equal(outs[1][1], outs[0][1])
+    exp_out, exp_aux = u0.double(), aux.double()
+    for lo, hi in ((k0, k1), (k0b, k1b)):
+        if hi <= lo:
+            continue
+        if ls:
+            ref.burgers3d_stage(inp.double(), exp_aux, exp_out, nx, ny, lo, hi, 3, weno_z, *rd,
+                                *vv, 1e-3, a, b, ls=True)
+        else:
+            ref.burgers3d_stage(inp.double(), u0.double(), exp_out, nx, ny, lo, hi, 3, weno_z,
+                                *rd, *vv, 1e-3, a, b)
+    assert (outs[1][0].double() - exp_out).abs().max().item() < 5e-4
