@@ -20,11 +20,16 @@ compared with the exact decaying sine mode exp(-3 pi^2 K t) sin sin sin (L_inf, 
 the initial amplitude) and the run fails if it exceeds linf_bound().  The 7-point (FD2)
 Laplacian named by BASELINE.json is measured on the same grid and reported as `fd2_7pt`.
 
-`sustained` (informational, AFTER the K timed steps; the headline `value` is the K-step
-number): --sustained-steps more steps of the same solver, timed the same way.  The fp64
-stencil load runs the chip at its power limit and the clock controller dips for a few ms
-after a load starts, so a 20-step window (15 ms) mostly sees that dip; 200 steps show the
-settled rate (profiles/archive/launch_times_r2s5.txt has the per-launch times).
+Clock settling: the fp64 stencil load runs the chip at its power limit, and the clock
+controller dips for tens of ms after a load starts (per-launch times rise from 676 to 862
+us and decay over ~20 launches: profiles/archive/launch_times_r2s5.txt), so a 20-step
+window right behind a few warm-up steps times the dip.  After the W warm-up steps the
+bench therefore runs --settle-ms (default 300 ms) more untimed steps of the same solver,
+then times exactly K steps; the count is reported as `settle`.  `sustained`
+(informational, AFTER the K timed steps): --sustained-steps more steps timed the same way.
+
+FD2 on one GPU runs two RK3 steps per launch (diffusion_fused.hip v6_march; bit-identical
+to one step per launch): `fd2_7pt.steps_per_launch`.
 """
 from __future__ import annotations
 
@@ -64,9 +69,30 @@ def linf_bound(grid, K: float, t: float, order: int) -> float:
     return 2.0 * frozen + trunc
 
 
-def timed(solver, steps: int, warmup: int, dt: float) -> float:
+SETTLE = {}  # model -> settle record of its last timed() call (reported in the JSON)
+
+
+def timed(solver, steps: int, warmup: int, dt: float, settle_ms: float = 0.0,
+          key: str = "heat") -> float:
+    """W warm-up steps, then settle_ms of further untimed steps of the same solver (the
+    power controller's clock dip after a load starts lasts tens of ms: a short window
+    right behind a few warm-up steps times the dip, not the solver), then exactly K timed
+    steps between a barrier + device sync on both sides (max over ranks)."""
+    per = None
     if warmup:
-        solver.run(iters=warmup, dt=dt)
+        per = solver.run(iters=warmup, dt=dt).compute_s / warmup
+    n_settle = 0
+    if settle_ms > 0:
+        if per is None:
+            per = solver.run(iters=2, dt=dt).compute_s / 2
+            n_settle += 2
+        # compute_s is the max over ranks, so every rank takes the same count; even keeps
+        # the u/un parity of the timed run
+        n = int(settle_ms * 1e-3 / max(per, 1e-6)) + 1
+        n += n % 2
+        solver.run(iters=n, dt=dt)
+        n_settle += n
+    SETTLE[key] = {"steps": n_settle, "target_ms": settle_ms}
     st = solver.run(iters=steps, dt=dt)  # barrier + sync on both sides, max over ranks
     return st.compute_s
 
@@ -270,6 +296,10 @@ def parse_args(argv=None):
                     help="weak: base^3 cells per GPU (default); strong: the 8-GPU grid "
                          "(2*base)^3 on any N")
     ap.add_argument("--device", default=None)
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="untimed steps after the W warm-up steps, in ms of stepping, so the "
+                         "timed window sees the settled clock, not the power controller's "
+                         "dip after the load starts (reported as 'settle'; 0 = off)")
     ap.add_argument("--sustained-steps", type=int, default=200,
                     help="extra steps timed after the headline window (informational "
                          "'sustained' fields; 0 = off)")
@@ -350,7 +380,7 @@ def run(args):
     (decomp, transport), trials = tune(make_heat, cands_of(grids), dt, dev)
     progress(comm, f"heat: timed run ({decomp}, {transport})")
     solver = make_heat(decomp, transport)
-    secs = timed(solver, args.steps, args.warmup, dt)
+    secs = timed(solver, args.steps, args.warmup, dt, args.settle_ms, "heat")
     mlups = grid.cells * args.steps / secs / 1e6
     sust = sustained(solver, args.sustained_steps, dt, grid.cells)
     # self-validation against the exact solution (outside the timed region)
@@ -384,6 +414,7 @@ def run(args):
         "n_gpus": n,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle": SETTLE.get("heat"),
         "ms_per_step": round(secs / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": args.scaling,
@@ -417,7 +448,7 @@ def run(args):
         progress(comm, "FD2 7-point run")
         m2 = Diffusion(K=1.0, order=2)
         s2 = make_heat(decomp, transport, m=m2)
-        secs2 = timed(s2, args.steps, args.warmup, m2.stable_dt())
+        secs2 = timed(s2, args.steps, args.warmup, m2.stable_dt(), args.settle_ms, "fd2")
         _, _, linf2 = s2.error_norms()
         bound2 = linf_bound(grid, m2.K, s2.t, 2)
         del s2
@@ -430,6 +461,8 @@ def run(args):
                              "ms_per_step": round(secs2 / args.steps * 1e3, 4),
                              "vs_baseline": round(ml2 / BASE_DIFFUSION, 2),
                              "linf_vs_exact": float(f"{linf2:.3e}"),
+                             "settle": SETTLE.get("fd2"),
+                             "steps_per_launch": 2 if n == 1 else 1,
                              "model": "diffusion3d FD2 7-point + SSP-RK3"}
 
     # ---- secondary: 3-D Burgers WENO5-Z + C∇²u, fp64 ----------------------------------
@@ -453,7 +486,7 @@ def run(args):
         progress(comm, f"burgers: timed run ({bdecomp}, {btransport})")
         bsolver = make_burgers(bdecomp, btransport)
         bsteps = args.burgers_steps or args.steps
-        bsecs = timed(bsolver, bsteps, args.warmup, bdt)
+        bsecs = timed(bsolver, bsteps, args.warmup, bdt, args.settle_ms, "burgers")
         bml = bgrid.cells * bsteps / bsecs / 1e6
         bsust = sustained(bsolver, args.sustained_steps, bdt, bgrid.cells)
         bsolver.check_finite()
@@ -462,6 +495,7 @@ def run(args):
         _free(dev)
         result["burgers3d"] = {"value": round(bml, 1), "unit": "MLUPS", "grid": list(bshape),
                                "steps": bsteps, "ms_per_step": round(bsecs / bsteps * 1e3, 4),
+                               "settle": SETTLE.get("burgers"),
                                "vs_baseline": round(bml / BASE_BURGERS, 2),
                                "model": "burgers3d WENO5-Z + FD4 viscous (C=1e-5) + SSP-RK3",
                                "pgrid": bpg,

@@ -977,6 +977,8 @@ class Solver:
         # the per-stage 64 B, not the fused step's 16 B)
         bpc = (5 * 32.0 - 8.0 if self.du is not None
                else self.model.bytes_per_cell_step if self.fused else 64.0)
+        if self.step2_capable():  # two steps per launch: u^n read and u^{n+2} written once
+            bpc /= 2.0
         bw = bpc * cells * stats.steps / max(stats.compute_s, 1e-30)
         ex = {("MLUPS (cells x RK steps / s)" if self.du is not None
                else "MLUPS (cells x RK3 steps / s)"): f"{ml:.1f}",
