@@ -138,6 +138,7 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   if (const char* f = std::getenv("ADVDIFF_FAULT")) {  // "RANK:STEP"
     if (std::sscanf(f, "%d:%d", &fault_rank_, &fault_step_) != 2) fault_rank_ = fault_step_ = -1;
   }
+  if (const char* s2 = std::getenv("ADVDIFF_STEP2")) step2_env_ = std::atoi(s2) != 0;
   if (sync_debug_enabled() || p.check_every > 0 || fault_rank_ >= 0)
     graph_ = false;  // per-launch / per-step host checks
   if (graph_ && std::string(tr_->name()) == "socket")
@@ -269,6 +270,31 @@ void Engine::step_fused(double dt) {
   start_halo(u_);
 }
 
+bool Engine::step2_ok() const {
+  return step2_env_ && fused_ && env_.size == 1 && !cart_ && p_.dims == 3 && p_.order == 2 &&
+         p_.physics == Physics::Diffusion;
+}
+
+void Engine::step2(double dt) {
+  if (!step2_ok()) {
+    step(dt);
+    step(dt);
+    return;
+  }
+  const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
+  const int B = p_.border();
+  const int box[8] = {B, p_.nx - B, B, p_.ny - B, 0, p_.nx, 0, p_.ny};
+  KERNEL_CHECK(advdiff_diffusion3d_step2x(p_.dtype, u_, A_, p_.nx, p_.ny, sy_, sz_,
+                                          slab_.alloc(), full_.lo, full_.hi, zact_.lo,
+                                          zact_.hi, box, p_.K / (dx * dx), p_.K / (dy * dy),
+                                          p_.K / (dz * dz), dt, compute_));
+  std::swap(u_, A_);
+  for (int q = 0; q < 2; ++q) {  // the same additions as two steps
+    t_ += dt;
+    ++it_;
+  }
+}
+
 void Engine::start_halo(void* field) {
   if (env_.size == 1) return;
   const int G = slab_.ghost, c = slab_.count();
@@ -351,7 +377,15 @@ hipGraphExec_t Engine::graph_for(double dt) {
   const int itn = it_;
   void *u = u_, *a = A_, *b = B_;
   HIP_CHECK(hipStreamBeginCapture(compute_, hipStreamCaptureModeThreadLocal));
-  for (int q = 0; q < kGraphSteps; ++q) step(dt);
+  for (int q = 0; q < kGraphSteps;) {
+    if (step2_ok()) {
+      step2(dt);
+      q += 2;
+    } else {
+      step(dt);
+      ++q;
+    }
+  }
   if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
   halo_pending_ = false;
   hipGraph_t g = nullptr;
@@ -395,7 +429,14 @@ void Engine::prepare_graphs(double dt) {
 }
 
 void Engine::steps(int n, double dt) {
+  // pairs of steps in one launch where nothing runs between steps (per-step host checks
+  // and fault injection keep single steps)
+  const bool pairs = step2_ok() && fault_rank_ < 0 && p_.check_every <= 0;
   if (!graph_) {
+    for (; pairs && n >= 2; n -= 2) {
+      step2(dt);
+      beat();
+    }
     for (int q = 0; q < n; ++q) {
       step(dt);
       beat();
@@ -420,6 +461,10 @@ void Engine::steps(int n, double dt) {
       t_ += dt;
       ++it_;
     }
+  }
+  for (; pairs && n >= 2; n -= 2) {
+    step2(dt);
+    beat();
   }
   for (; n > 0; --n) {
     step(dt);

@@ -345,6 +345,10 @@ class Engine {
   ~Engine();
   double stable_dt() const;
   void step(double dt);
+  // two steps of dt in ONE launch where the step has it (single-rank 3-D FD2 heat:
+  // advdiff_diffusion3d_step2x, bit-identical to two steps), else two steps
+  void step2(double dt);
+  bool step2_ok() const;
   // n steps of constant dt: through hipGraphs of kGraphSteps steps when enabled (after two
   // eager steps that run the transport's one-time handshakes for both buffer parities)
   void steps(int n, double dt);
@@ -473,6 +477,7 @@ class Engine {
   }
   // hipGraph stepping: one executable graph per (dt, u_ parity) of kGraphSteps steps
   bool graph_ = false;
+  bool step2_env_ = true;  // ADVDIFF_STEP2=0: one step per launch
   int warm_ = 0;  // eager steps run so far (handshakes)
   struct GraphKey {
     double dt;

@@ -523,3 +523,21 @@ def test_native_field_memory_matches_python(tmp_path, app, args, model):
                ic="sine" if app == "diffusion3d" else "gaussian")
     assert rec["device_field_bytes"] == s.memory_bytes(), (rec, s.memory_bytes())
     assert rec["device_field_bytes"] == (2 if app == "diffusion3d" else 3) * s.u.numel() * 8
+
+
+@pytest.mark.parametrize("graph", ["--graph", "--no-graph"])
+def test_native_fd2_two_step_launch_bitwise(tmp_path, monkeypatch, graph):
+    """Single-rank FD2 heat: the engine pairs its steps into two-step launches
+    (Engine::step2, advdiff_diffusion3d_step2x) — bitwise equal to one step per launch
+    (ADVDIFF_STEP2=0) and to the Python solver (which pairs the same way); odd step count."""
+    args = [1.0, 1.0, 1.0, 1.0, 70, 60, 56, 21]
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("ADVDIFF_STEP2", flag)
+        out = tmp_path / f"s{flag}.bin"
+        _run("diffusion3d", args, out, extra=["--ic", "sine", "--order", "2", graph])
+        outs[flag] = np.fromfile(out, dtype=np.float32).reshape(56, 60, 70)
+    assert np.array_equal(outs["1"], outs["0"]), np.abs(outs["1"] - outs["0"]).max()
+    monkeypatch.setenv("ADVDIFF_STEP2", "1")
+    exp = _py(Diffusion(K=1.0, order=2), Grid((70, 60, 56), (1.0, 1.0, 1.0)), "sine", iters=21)
+    assert np.array_equal(outs["1"], exp), np.abs(outs["1"] - exp).max()
