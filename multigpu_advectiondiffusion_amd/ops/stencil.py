@@ -137,7 +137,8 @@ def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, 
 def diffusion3d_step2x(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, cx, cy, cz, dt,
                        stream=None, box=None):
     """TWO FD2 SSP-RK3 steps in one launch (diffusion_fused.hip v6_march): uout[k0:k1] =
-    RK3(RK3(uin)), bit-identical to two diffusion3d_step calls through a scratch field.
+    RK3(RK3(uin)), bit-identical to two diffusion3d_step calls through a scratch field
+    (the first on the whole active box, the second on the output box).
     u^n is read once and u^{n+2} written once: half the HBM traffic per step.  The planes
     within 5 of [k0, k1) must hold u^n (one rank: the whole field)."""
     _check_layout(uin, uout)
@@ -156,10 +157,12 @@ def diffusion3d_step2x(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, cx, cy, c
         _lib.check(code, "diffusion3d_step2x")
     elif k1 > k0:
         # the kernel's dependency cone: U1 on [k0-5, k1+5) from u^n, then u^{n+2}
+        # (u^{n+1} on the whole active box: the output box applies to u^{n+2})
         nz = uin.shape[0]
         mid = uin.clone()
+        box1 = tuple(box[:4]) + (0, nx, 0, ny)
         ref.diffusion3d_step_box(uin, mid, nx, ny, max(k0 - 5, zlo, 1), min(k1 + 5, zhi, nz - 1),
-                                 zlo, zhi, box, 2, cx, cy, cz, dt)
+                                 zlo, zhi, box1, 2, cx, cy, cz, dt)
         ref.diffusion3d_step_box(mid, uout, nx, ny, k0, k1, zlo, zhi, box, 2, cx, cy, cz, dt)
 
 

@@ -14,6 +14,7 @@ step() { # name seconds cmd...
 }
 step step2_tests 300 python -u -m pytest tests/test_fused_step_gpu.py -x -v --timeout 120 --timeout-method thread -k "two_step"
 step native_step2 300 python -u -m pytest tests/test_native_apps_gpu.py -x -v --timeout 120 --timeout-method thread -k "two_step"
+step burgers_det 300 python bench/burgers_determinism.py --reps 3
 step step2_ab 300 python bench/step2_ab.py --rounds 4
 step packed_tests 400 python -u -m pytest tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread -k "packed or burgers3d_stage or tile_rows"
 step fp32_pack_ab 300 python bench/burgers_fp32_ab.py --rounds 4

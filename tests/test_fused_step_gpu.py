@@ -240,12 +240,15 @@ STEP2_CASES = CASES + [
 
 def _two_steps(u, nx, ny, k0, k1, zlo, zhi, border, c, dt, box=None):
     kw = dict(nx=nx, ny=ny, zlo=zlo, zhi=zhi, border=border, order=2, cx=c[0], cy=c[1],
-              cz=c[2], dt=dt, box=box)
+              cz=c[2], dt=dt)
+    # u^{n+1} on the whole active box (the two-step launch's intermediate), u^{n+2} on
+    # the output box
+    box1 = None if box is None else tuple(box[:4]) + (0, nx, 0, ny)
     # the first step on the active planes the outputs depend on (a one-step launch asked
     # for a frozen plane would overwrite it: the solver never does)
     mid, out = u.clone(), u.clone()
-    stencil.diffusion3d_step(u, mid, k0=max(k0 - 5, zlo), k1=min(k1 + 5, zhi), **kw)
-    stencil.diffusion3d_step(mid, out, k0=k0, k1=k1, **kw)
+    stencil.diffusion3d_step(u, mid, k0=max(k0 - 5, zlo), k1=min(k1 + 5, zhi), box=box1, **kw)
+    stencil.diffusion3d_step(mid, out, k0=k0, k1=k1, box=box, **kw)
     return out
 
 
