@@ -202,7 +202,8 @@ int advdiff_set_step_edge(int on);
 // 2 GiB and more); returns the previous value.  Results agree to rounding (tests).
 int advdiff_set_b3_ver(int v);
 // TWO fused SSP-RK3 steps of the 7-point heat equation in one launch (8 B of HBM traffic
-// per cell and step): uout[k0:k1] = RK3(RK3(uin)), bit-identical to two one-step launches
+// per cell and step): uout[k0:k1] = RK3(RK3(uin)) on the output box (the intermediate over
+// the active box), bit-identical to two one-step launches
 int advdiff_diffusion3d_step2x(int dtype, const void* uin, void* uout, int nx, int ny,
                                int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int zlo,
                                int zhi, const int* box, double cx, double cy, double cz,

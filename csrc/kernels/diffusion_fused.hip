@@ -1137,9 +1137,11 @@ extern "C" int advdiff_diffusion3d_step_box_ex(int dtype, const void* uin, void*
 }
 
 // TWO fused SSP-RK3 steps of the 7-point heat equation in one launch (order 2 only, one
-// plane range): uout[k0:k1] = RK3(RK3(uin)), bit-identical to two advdiff_diffusion3d_step
-// launches.  The planes within 5 of [k0, k1) must hold u^n (ghosts included); the frozen
-// cells (outside [zlo, zhi) and the box's active x/y range) keep their values.
+// plane range): uout[k0:k1] = RK3(RK3(uin)) on the box's output x/y range, with the
+// intermediate u^{n+1} taken over the whole active box — bit-identical to a one-step
+// launch on the active box followed by one on the output box.  The planes within 5 of
+// [k0, k1) must hold u^n (ghosts included); the frozen cells (outside [zlo, zhi) and the
+// box's active x/y range) keep their values.
 extern "C" int advdiff_diffusion3d_step2x(int dtype, const void* uin, void* uout, int nx, int ny,
                                           int64_t sy, int64_t sz, int nz_alloc, int k0, int k1,
                                           int zlo, int zhi, const int* box, double cx, double cy,
