@@ -93,3 +93,23 @@ def test_bit_hash_sees_index_swaps():
     assert not np.isclose(float(a), float(b))
     o[2, 3, 4], o[5, 6, 7] = b, a
     assert s.bit_hash() != h0
+
+
+def test_single_rank_contract_fields_and_settle():
+    """One rank (the driver's N = 1 run): the JSON line carries the contract fields, the
+    timed window is exactly --steps after --warmup plus the reported settle steps, and the
+    FD2 run pairs its steps (two steps per launch on one GPU)."""
+    args = ["--device", "cpu", "--base", "18", "--burgers-base", "12", "--steps", "3",
+            "--warmup", "2", "--sustained-steps", "0", "--settle-ms", "30"]
+    r = _bench(args)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = _json_line(r.stdout)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in res, k
+    assert res["n_gpus"] == 1 and res["steps"] == 3 and res["warmup"] == 2
+    for rec in (res["settle"], res["fd2_7pt"]["settle"], res["burgers3d"]["settle"]):
+        assert rec["target_ms"] == 30.0 and rec["steps"] >= 2 and rec["steps"] % 2 == 0
+    assert res["fd2_7pt"]["steps_per_launch"] == 2
+    assert abs(res["value"] - res["config"]["seq_len"] * 3 / (res["ms_per_step"] * 3e-3) / 1e6) \
+        < 0.01 * res["value"]
