@@ -217,6 +217,8 @@ int advdiff_set_step_f32_tile(int t);
 int advdiff_set_b3_pack(int on);
 // v9 tile row width: 64, 32 or 0 = chosen per plane shape (returns the previous setting)
 int advdiff_set_b3_tx(int v);
+// v9 stage: forced z-chunk length (0 = the rounds model); returns the previous setting
+int advdiff_set_b3_zchunk(int zc);
 // 2-D WENO5 stage kernel version (2 = the barrier-free wave-strip kernel, default; 1 = the
 // generic row-tile kernel); returns the previous value.
 int advdiff_set_b2_ver(int v);

@@ -1021,6 +1021,10 @@ static int b3_tile_row(int nx, int ny, int border) {
   return s32 > s64 * 1.01 ? 32 : 64;
 }
 
+// forced z-chunk length of the v9 stage (advdiff_set_b3_zchunk; 0 = the rounds model):
+// the bit-reproducibility tests move the chunk boundaries with it
+static int g_b3_zchunk = 0;
+
 template <typename T, bool WZ, bool VISC, int MODE, int TXL, bool PK = false>
 static hipError_t launch_b3_v9_tx(const BArgs& p) {
   // XCD-contiguous tile order (default): 256^3 WENO5-Z + viscous step 0.584 -> 0.564 ms
@@ -1044,10 +1048,10 @@ static hipError_t launch_b3_v9_tx(const BArgs& p) {
   }();
   // PK: a workgroup marches two half chunks side by side — choose the half length
   const int nm = PK ? div_up(na + nb, 2) : na + nb;
-  const int zm = rounds_model
-                     ? pick_chunk_rounds(nm, (long long)gx * gy,
-                                         (long long)device_cus() * per_cu, 4, 8)
-                     : pick_chunk(nm, (long long)gx * gy, 8, 256);
+  const int zm = g_b3_zchunk > 0 ? std::max(1, PK ? div_up(g_b3_zchunk, 2) : g_b3_zchunk)
+                 : rounds_model ? pick_chunk_rounds(nm, (long long)gx * gy,
+                                                    (long long)device_cus() * per_cu, 4, 8)
+                                : pick_chunk(nm, (long long)gx * gy, 8, 256);
   const int zc = PK ? 2 * zm : zm;
   const int gza = div_up(na, zc);
   const int gz = gza + div_up(nb, zc);
@@ -1243,6 +1247,12 @@ extern "C" int advdiff_set_b3_pack(int on) {
 extern "C" int advdiff_set_b3_tx(int v) {
   const int old = advdiff::b3_tx();
   advdiff::g_b3_tx = v;
+  return old;
+}
+
+extern "C" int advdiff_set_b3_zchunk(int zc) {
+  const int old = advdiff::g_b3_zchunk;
+  advdiff::g_b3_zchunk = zc > 0 ? zc : 0;
   return old;
 }
 

@@ -153,9 +153,16 @@ def launch(np_: int, argv: list[str], cpu: bool = False, timeout: float | None =
 # ----------------------------------------------------------------------------------
 # in-process API for tests
 # ----------------------------------------------------------------------------------
-def _spawn_entry(rank, world, port, device, backend, fn, args, queue, transport=None):
+def _spawn_entry(rank, world, port, device, backend, fn, args, queue, transport=None,
+                 dump_after=None):
     os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    import faulthandler
+    faulthandler.enable()  # a crashing rank (SIGSEGV / SIGABRT) prints its Python stack
+    if dump_after:
+        # a rank still running shortly before the parent gives up prints every thread's
+        # stack (captured with the test's stderr): a deadlock names its call site
+        faulthandler.dump_traceback_later(dump_after, exit=False)
     try:
         import torch
         torch.set_num_threads(1)
@@ -179,16 +186,30 @@ def spawn_local(world: int, fn, *args, device: str = "cpu", backend: str | None 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
+    import queue as _queue
+    import time
+    dump_after = max(timeout - 20.0, timeout * 0.75)
     procs = [ctx.Process(target=_spawn_entry,
-                         args=(r, world, port, device, backend, fn, args, q, transport))
+                         args=(r, world, port, device, backend, fn, args, q, transport,
+                               dump_after))
              for r in range(world)]
     for p in procs:
         p.start()
     results = [None] * world
     errors = []
+    done = set()
+    deadline = time.monotonic() + timeout
     try:
         for _ in range(world):
-            rank, status, payload = q.get(timeout=timeout)
+            try:
+                rank, status, payload = q.get(timeout=max(deadline - time.monotonic(), 0.1))
+            except _queue.Empty:
+                late = [r for r in range(world) if r not in done]
+                dead = [(r, procs[r].exitcode) for r in late if not procs[r].is_alive()]
+                raise TimeoutError(f"spawn_local: ranks {late} did not finish within "
+                                   f"{timeout:g} s (exited without reporting: {dead}); "
+                                   "their stacks were dumped to stderr") from None
+            done.add(rank)
             if status == "ok":
                 results[rank] = payload
             else:

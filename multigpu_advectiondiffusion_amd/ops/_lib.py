@@ -172,6 +172,8 @@ def _load():
         lib.advdiff_set_b3_pack.restype = c_int
         lib.advdiff_set_b3_tx.argtypes = [c_int]
         lib.advdiff_set_b3_tx.restype = c_int
+        lib.advdiff_set_b3_zchunk.argtypes = [c_int]
+        lib.advdiff_set_b3_zchunk.restype = c_int
         lib.advdiff_set_b2_ver.argtypes = [c_int]
         lib.advdiff_set_b2_ver.restype = c_int
         for name, args in _IPC_SIGS.items():

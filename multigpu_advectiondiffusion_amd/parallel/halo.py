@@ -43,22 +43,44 @@ class PendingExchange:
             self.finish = None
 
 
+def _joinable(cs) -> PendingExchange:
+    """Handle whose wait() joins the comm stream `cs` (at this point) into the current
+    stream — nothing to do when the current stream IS `cs` (stream order)."""
+    done = torch.cuda.Event()
+    done.record(cs)
+
+    def join():
+        s = torch.cuda.current_stream()
+        if s != cs:
+            s.wait_event(done)
+    return PendingExchange([], cs, join)
+
+
+def _order_after(cs, cur, after_event) -> None:
+    """Order the comm stream `cs` after the producer of the field: after `after_event`,
+    or (None) after everything queued on the current stream `cur` so far.  False: the
+    producer ran on `cs` itself (the boundary launch on the comm stream), so stream order
+    already holds — no event, and no same-stream event wait inside a graph capture
+    (hipStreamEndCapture crashed on those, profiles/r5/diag_bstream.md)."""
+    if after_event is False or (after_event is None and cs == cur):
+        return
+    if after_event is None:
+        after_event = torch.cuda.Event()
+        after_event.record(cur)
+    cs.wait_event(after_event)
+
+
 def _start_ipc_routed(comm, comm_stream, phases, after_event=None, tag=None) -> PendingExchange:
     """Like _start_ipc for phases of one-way-capable routes: phases = [(channel, {peer:
     (send_view | None, recv_view | None)})], run in order on the comm stream; `tag`
     keys the handshake cache (IpcPeers._resolve_pairs)."""
     cur = torch.cuda.current_stream()
     cs = comm_stream or cur
-    if after_event is None:
-        after_event = torch.cuda.Event()
-        after_event.record(cur)
-    cs.wait_event(after_event)
+    _order_after(cs, cur, after_event)
     ipc = comm.ipc()
     for ch, pairs in phases:
         ipc.route(pairs, cs, ch, tag)
-    done = torch.cuda.Event()
-    done.record(cs)
-    return PendingExchange([], cs, lambda: torch.cuda.current_stream().wait_event(done))
+    return _joinable(cs)
 
 
 def _start_ipc(comm, comm_stream, phases, after_event=None) -> PendingExchange:
@@ -66,16 +88,11 @@ def _start_ipc(comm, comm_stream, phases, after_event=None) -> PendingExchange:
     `after_event`, phases in order; the returned handle joins the current stream."""
     cur = torch.cuda.current_stream()
     cs = comm_stream or cur
-    if after_event is None:
-        after_event = torch.cuda.Event()
-        after_event.record(cur)
-    cs.wait_event(after_event)
+    _order_after(cs, cur, after_event)
     ipc = comm.ipc()
     for msgs in phases:
         ipc.exchange(msgs, cs)
-    done = torch.cuda.Event()
-    done.record(cs)
-    return PendingExchange([], cs, lambda: torch.cuda.current_stream().wait_event(done))
+    return _joinable(cs)
 
 
 def _ipc_on(halo, field) -> bool:
@@ -194,10 +211,7 @@ class SlabHalo:
         d = self.d
         cur = torch.cuda.current_stream()
         cs = self.comm_stream or cur
-        if after_event is None:
-            after_event = torch.cuda.Event()
-            after_event.record(cur)
-        cs.wait_event(after_event)
+        _order_after(cs, cur, after_event)
         sends, recvs, ops = [], [], []
         with torch.cuda.stream(cs):
             for peer, (s0, s1), (r0, r1) in ((d.lower, d.send_lower(), d.recv_lower()),
@@ -254,7 +268,8 @@ class SlabHalo:
         """Begin exchanging the ghost planes of `field` (axis 0).
 
         On device: the transfers are issued on the comm stream after `after_event`
-        (or after all work currently queued on the current stream)."""
+        (None: after all work currently queued on the current stream; False: the field's
+        producer ran on the comm stream itself)."""
         if self.comm.size == 1:
             return None
         if _ipc_on(self, field) and self._use_stripes(field):
@@ -271,11 +286,7 @@ class SlabHalo:
         if field.is_cuda and self.comm.backend != "nccl":
             return self._start_host_staged(field, after_event)
         if field.is_cuda and self.comm_stream is not None:
-            cur = torch.cuda.current_stream()
-            if after_event is None:
-                after_event = torch.cuda.Event()
-                after_event.record(cur)
-            self.comm_stream.wait_event(after_event)
+            _order_after(self.comm_stream, torch.cuda.current_stream(), after_event)
             with torch.cuda.stream(self.comm_stream):
                 works = dist.batch_isend_irecv(ops)
             return PendingExchange(works, self.comm_stream)
@@ -472,10 +483,7 @@ class CartesianHalo:
             return None
         cur = torch.cuda.current_stream()
         cs = self.comm_stream or cur
-        if after_event is None:
-            after_event = torch.cuda.Event()
-            after_event.record(cur)
-        cs.wait_event(after_event)
+        _order_after(cs, cur, after_event)
         if self.comm.backend != "nccl":
             # device tensors over gloo (one-GPU multi-process tests): host-staged, blocking
             for axes in phases:
@@ -492,9 +500,7 @@ class CartesianHalo:
                     for dst, src in unpack:
                         self._copy(dst, src)
                 cs.synchronize()
-            done = torch.cuda.Event()
-            done.record(cs)
-            return PendingExchange([], cs, lambda: torch.cuda.current_stream().wait_event(done))
+            return _joinable(cs)
         with torch.cuda.stream(cs):
             for axes in phases:  # stream-ordered phases: pack -> RCCL -> unpack
                 sends, recvs, unpack = self._plan(field, axes)
@@ -503,9 +509,7 @@ class CartesianHalo:
                     w.wait()  # comm stream waits for RCCL (no host block)
                 for dst, src in unpack:
                     self._copy(dst, src)
-            done = torch.cuda.Event()
-            done.record(cs)
-        return PendingExchange([], cs, lambda: torch.cuda.current_stream().wait_event(done))
+        return _joinable(cs)
 
     def exchange(self, field: torch.Tensor) -> None:
         p = self.start(field)

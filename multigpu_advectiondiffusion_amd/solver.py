@@ -72,7 +72,7 @@ class Solver:
                  integrator: str = "ssprk3", kernel: str = "native",
                  device_dt: bool | None = None, exchange: str = "u",
                  transport: str | None = None, stripe: int | None = None,
-                 boundary_stream: bool | None = None):
+                 boundary_stream: bool | None = None, boundary_on_comm: bool | None = None):
         """decomp: process grid — None/"slab" (split the slowest axis only, the
         reference's layout), "auto" (smallest halo surface) or "PZxPYxPX" / a tuple in
         array axis order ((pz, py, px) in 3-D, (py, px) in 2-D).
@@ -86,9 +86,11 @@ class Solver:
         transport: halo transport of this solver ("ipc", "rccl", "host"; None = the
         Comm's, Comm.transport) — solvers with different transports can coexist on one
         Comm (bench.py tunes the transport this way).
-        boundary_stream (fused heat step, N > 1, overlap): the boundary launch on its own
-        high-priority stream beside the interior launch, its exchange started right after
-        it (None = ADVDIFF_BSTREAM, default off).
+        boundary_on_comm (N > 1 device ranks, overlap, ipc / rccl transport): the boundary
+        launch on the COMM stream, right after the wait for the halo of its input and
+        right before the puts of its output — two streams per rank, the interior launch
+        beside the whole exchange (None = ADVDIFF_BCOMM, default off).  boundary_stream is
+        its round-4 name (that version used a third stream; see _step_fused_bcomm).
         stripe: ipc slab exchanges of 3-D fields relay part of every face message through
         up to this many helper ranks over otherwise idle xGMI links (parallel/halo.py
         SlabHalo; None = ADVDIFF_STRIPE, default 0 = direct only).
@@ -175,18 +177,20 @@ class Solver:
         self.t = float(t0)
         self.it = 0
         self.comm_stream = None
-        self.bstream = None
+        self.bcomm = False
         if self.device.type == "cuda" and comm.size > 1:
             lo, hi = torch.cuda.Stream.priority_range()
             self.comm_stream = torch.cuda.Stream(device=self.device, priority=hi)
-            if boundary_stream is None:
+            if boundary_on_comm is None:
+                boundary_on_comm = boundary_stream
+            if boundary_on_comm is None:
                 import os
-                boundary_stream = os.environ.get("ADVDIFF_BSTREAM", "0") == "1"
-            if boundary_stream and overlap and exchange == "u":
-                # the boundary launch runs on its own high-priority stream BESIDE the
-                # interior launch, and the exchange of its planes starts as soon as it
-                # ends (not after the interior): _step_fused_bstream / _stage_bstream
-                self.bstream = torch.cuda.Stream(device=self.device, priority=hi)
+                boundary_on_comm = (os.environ.get("ADVDIFF_BCOMM")
+                                    or os.environ.get("ADVDIFF_BSTREAM", "0")) == "1"
+            # the boundary launch on the (high-priority) comm stream, between the wait for
+            # the halo of its input and the puts of its output: _step_fused_bcomm
+            self.bcomm = bool(boundary_on_comm and overlap and exchange == "u"
+                              and self.transport in ("ipc", "rccl"))
         if self.cart:
             # the fused step stacks three star stencils: it needs edge/corner ghosts too
             self.halo = CartesianHalo(comm, self.cd, self.comm_stream, corners=self.fused,
@@ -328,36 +332,35 @@ class Solver:
         self.model.stage(v(inp), v(u0), v(out), z0, z1, dt, a, b, ls=ls, **kw)
         trace.sync_check(f"{self.model.name} stage box {box}", self.device)
 
-    def _stage_bstream(self, inp, u0, out, a, b, dt, ls, pend):
-        """Per-stage counterpart of _step_fused_bstream: interior on the compute stream,
-        boundary (after the halo of `inp`) on the side stream beside it, the exchange of
-        `out` right after the boundary launch; the compute stream joins the side stream
-        before the next stage."""
+    def _launch_boundary(self, inp, u0, out, a, b, dt, ls):
+        if not self.cart and getattr(self.model, "two_range_stage", False):
+            self._launch(inp, u0, out, self.boundary[0], dt, a, b, ls, self.boundary[1])
+        else:
+            for rng in self.boundary:
+                self._launch(inp, u0, out, rng, dt, a, b, ls)
+
+    def _stage_bcomm(self, inp, u0, out, a, b, dt, ls, pend):
+        """Per-stage counterpart of _step_fused_bcomm."""
         cur = torch.cuda.current_stream(self.device)
-        bs = self.bstream
-        bs.wait_stream(cur)
+        cs = self.comm_stream
+        cs.wait_stream(cur)  # the previous stage's interior launch has read / written
         with trace.range_("interior"):
             self._launch(inp, u0, out, self.interior, dt, a, b, ls)
-        with torch.cuda.stream(bs):
-            with trace.range_("halo_wait"):
-                if pend is not None:
-                    pend.wait()
+        with torch.cuda.stream(cs):
+            if pend is not None:
+                pend.wait()  # ipc: stream order on cs already (no event); rccl: joins RCCL
             with trace.range_("boundary"):
-                if not self.cart and getattr(self.model, "two_range_stage", False):
-                    self._launch(inp, u0, out, self.boundary[0], dt, a, b, ls, self.boundary[1])
-                else:
-                    for rng in self.boundary:
-                        self._launch(inp, u0, out, rng, dt, a, b, ls)
+                self._launch_boundary(inp, u0, out, a, b, dt, ls)
             bdone = torch.cuda.Event()
-            bdone.record(bs)
-        with trace.range_("halo_start"):
-            self._pending[id(out)] = self.halo.start(out, after_event=bdone)
-        cur.wait_stream(bs)
+            bdone.record(cs)
+            with trace.range_("halo_start"):
+                self._pending[id(out)] = self.halo.start(out, after_event=False)
+        cur.wait_event(bdone)
 
     def _stage(self, inp, u0, out, a, b, dt, ls=False):
         pend = self._pending.pop(id(inp), None)
-        if self.bstream is not None and self.comm.size > 1:
-            self._stage_bstream(inp, u0, out, a, b, dt, ls, pend)
+        if self.bcomm and self.comm.size > 1:
+            self._stage_bcomm(inp, u0, out, a, b, dt, ls, pend)
             return
         if self.comm.size == 1:
             self._launch(inp, u0, out, self.full, dt, a, b, ls)
@@ -456,8 +459,8 @@ class Solver:
 
     def _step_fused(self, dt: float) -> None:
         pend = self._pending.pop(id(self.u), None)
-        if self.bstream is not None and self.comm.size > 1:
-            self._step_fused_bstream(dt, pend)
+        if self.bcomm and self.comm.size > 1:
+            self._step_fused_bcomm(dt, pend)
             return
         if self.comm.size == 1:
             self._launch_fused(self.full, dt, exclusive=True)
@@ -484,22 +487,28 @@ class Solver:
         self.t += dt
         self.it += 1
 
-    def _step_fused_bstream(self, dt: float, pend) -> None:
-        """Overlapped fused step with the boundary launch on its own stream: the interior
-        launch (compute stream) and — once the halo of u has arrived — the boundary
-        launch (high-priority side stream) run side by side, and the exchange of the new
-        boundary planes starts right after the boundary launch, overlapping the rest of
-        the interior.  The compute stream joins the side stream before the next step (its
-        launches read the new boundary planes and overwrite u)."""
+    def _step_fused_bcomm(self, dt: float, pend) -> None:
+        """Overlapped fused step, boundary launch on the comm stream: per rank two streams,
+
+            compute : [interior n] ---------------------wait(bdone n)--> [interior n+1] ...
+            comm    : [wait halo n-1][boundary n] bdone [puts n, signal, wait halo n] ...
+
+        so the boundary launch starts as soon as the halo of u has arrived (not after the
+        interior launch, as on the default path), the puts of its planes start right after
+        it, and the interior launch runs beside the whole exchange.  The compute stream
+        joins the comm stream at bdone only (the next interior launch reads the new
+        boundary planes and overwrites the buffer the boundary launch read), never at the
+        wait for the peers, so a spinning device wait never blocks a compute launch; the
+        comm stream joins the compute stream before each boundary launch (the interior
+        launch of the previous step read the buffer it overwrites).  No third stream."""
         cur = torch.cuda.current_stream(self.device)
-        bs = self.bstream
-        bs.wait_stream(cur)  # everything before this step precedes both launches
+        cs = self.comm_stream
+        cs.wait_stream(cur)
         with trace.range_("interior"):
             self._launch_fused(self.interior, dt)
-        with torch.cuda.stream(bs):
-            with trace.range_("halo_wait"):
-                if pend is not None:
-                    pend.wait()  # the side stream waits for the halo of u
+        with torch.cuda.stream(cs):
+            if pend is not None:
+                pend.wait()  # ipc: stream order on cs already (no event); rccl: joins RCCL
             with trace.range_("boundary"):
                 if self.cart:
                     for box in self.boundary:
@@ -507,11 +516,11 @@ class Solver:
                 else:
                     self._launch_fused(self.boundary[0], dt, self.boundary[1])
             bdone = torch.cuda.Event()
-            bdone.record(bs)
-        self.u, self.un = self.un, self.u
-        with trace.range_("halo_start"):
-            self._pending[id(self.u)] = self.halo.start(self.u, after_event=bdone)
-        cur.wait_stream(bs)
+            bdone.record(cs)
+            self.u, self.un = self.un, self.u
+            with trace.range_("halo_start"):
+                self._pending[id(self.u)] = self.halo.start(self.u, after_event=False)
+        cur.wait_event(bdone)
         self.t += dt
         self.it += 1
 
