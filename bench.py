@@ -48,6 +48,11 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 METRIC = "MLUPS (whole node), 3D diffusion 512^3 + Burgers3D WENO5, 1/2/4/8 MI355X"
 BASE_DIFFUSION = 927.2   # best published 3-D heat MLUPS (SingleGPU/Diffusion3d_Blocking/Run.m:3-12)
 BASE_BURGERS = 344.4     # best published 3-D Burgers MLUPS (SingleGPU/Burgers3d_WENO5_PitchedMem/Run.m:15-25)
+# L_inf bound of the timed Burgers solution vs the same steps through the PyTorch fp64
+# reference ops (ops/reference.py): both are fp64 WENO5-Z with different operation orders,
+# so they agree to accumulated rounding (measured: profiles/r5/bench_burgers_ref.log); a
+# wrong face, halo or stage gives O(dt |u|) ~ 1e-3 and fails it
+BURGERS_REF_BOUND = 1e-9
 
 
 def linf_bound(grid, K: float, t: float, order: int) -> float:
@@ -283,6 +288,9 @@ def parse_args(argv=None):
     ap.add_argument("--burgers-steps", type=int, default=None)
     ap.add_argument("--no-burgers", action="store_true")
     ap.add_argument("--no-fd2", action="store_true")
+    ap.add_argument("--burgers-ref-bound", type=float, default=BURGERS_REF_BOUND,
+                    help="fail if the timed Burgers solution differs from the fp64 torch "
+                         "reference ops by more than this (L_inf); <= 0 skips the check")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--decomp", default="tune",
                     help="process grid: 'tune' (default: the fastest of the candidate grids "
@@ -491,14 +499,36 @@ def run(args):
         bsust = sustained(bsolver, args.sustained_steps, bdt, bgrid.cells)
         bsolver.check_finite()
         bpg = list(bsolver.pgrid)
+        bref = None
+        if args.burgers_ref_bound > 0:
+            # self-check (outside the timed region): every step the timed solver took,
+            # again through the fp64 PyTorch reference ops on the same decomposition
+            progress(comm, f"burgers: {bsolver.it} reference steps (torch ops)")
+            tr, st = solver_transport(btransport) if btransport else (None, 0)
+            ref = Solver(bmodel, bgrid, comm, dtype=torch.float64, ic="gaussian",
+                         overlap=not args.no_overlap, decomp=bdecomp, transport=tr,
+                         stripe=st, kernel="torch")
+            t_ref = time.perf_counter()
+            ref.run(iters=bsolver.it, dt=bdt, graph=False)
+            ref.sync_halos()
+            _, _, blinf = bsolver.error_norms(exact=ref.u)
+            bref = {"linf_vs_torch": float(f"{blinf:.3e}"), "bound": args.burgers_ref_bound,
+                    "steps": bsolver.it, "t": bsolver.t,
+                    "torch_s": round(time.perf_counter() - t_ref, 1)}
+            del ref
         del bsolver
         _free(dev)
+        if bref is not None and not bref["linf_vs_torch"] <= args.burgers_ref_bound:
+            raise SystemExit(f"bench validation failed: Burgers L_inf vs the torch reference "
+                             f"= {bref['linf_vs_torch']:.3e} > {args.burgers_ref_bound:.1e}")
         result["burgers3d"] = {"value": round(bml, 1), "unit": "MLUPS", "grid": list(bshape),
                                "steps": bsteps, "ms_per_step": round(bsecs / bsteps * 1e3, 4),
                                "settle": SETTLE.get("burgers"),
                                "vs_baseline": round(bml / BASE_BURGERS, 2),
                                "model": "burgers3d WENO5-Z + FD4 viscous (C=1e-5) + SSP-RK3",
                                "pgrid": bpg,
+                               **({"linf_vs_torch": bref["linf_vs_torch"],
+                                   "reference_check": bref} if bref else {}),
                                "halo_transport": btransport if n > 1 else None,
                                "transport_trials_ms_per_step": btrials,
                                **({"sustained": bsust} if bsust else {})}

@@ -60,12 +60,15 @@ def main():
             for rec in json.loads(res.stdout.strip().splitlines()[-1]):
                 key = (tuple(rec["shape"]), var)
                 best[key] = max(best.get(key, 0.0), rec["mlups"])
-                hashes.setdefault(tuple(rec["shape"]), set()).add(rec["hash"])
+                hashes.setdefault(tuple(rec["shape"]), {}).setdefault(var, []).append(rec["hash"])
             print(f"round {r} variant {var} done", flush=True)
     for shape in SHAPES:
+        per = hashes[tuple(shape)]  # variant -> hash of every round (one process each)
+        allh = {h for hs in per.values() for h in hs}
         print(json.dumps({"shape": shape, **{f"mlups[{v}]": best[(tuple(shape), v)]
                                              for v in variants},
-                          "bitwise_equal": len(hashes[tuple(shape)]) == 1}), flush=True)
+                          "bitwise_equal": len(allh) == 1,
+                          "hashes_per_variant": {v: hs for v, hs in per.items()}}), flush=True)
 
 
 if __name__ == "__main__":

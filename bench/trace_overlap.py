@@ -33,6 +33,31 @@ def _is_step(name):
     return ("step_kernel" in name or "stage" in name or "_step" in name) and not _is_put(name)
 
 
+def _union(iv):
+    """Sorted, merged intervals (a put beside two concurrent step launches counts once)."""
+    out = []
+    for s, e in sorted(iv):
+        if out and s <= out[-1][1]:
+            out[-1][1] = max(out[-1][1], e)
+        else:
+            out.append([s, e])
+    return out
+
+
+def _overlap(a, b):
+    """Total length of (union a) ∩ (union b)."""
+    a, b = _union(a), _union(b)
+    i = j = tot = 0
+    while i < len(a) and j < len(b):
+        lo, hi = max(a[i][0], b[j][0]), min(a[i][1], b[j][1])
+        tot += max(0, hi - lo)
+        if a[i][1] < b[j][1]:
+            i += 1
+        else:
+            j += 1
+    return tot
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
@@ -50,8 +75,8 @@ def main():
         puts = [(s, e) for s, e, n in ks if _is_put(n)]
         if not steps or not puts:
             continue
-        tot = sum(e - s for s, e in puts)
-        hid = sum(max(0, min(ce, se) - max(cs, ss)) for cs, ce in puts for ss, se in steps)
+        tot = sum(e - s for s, e in _union(puts))
+        hid = _overlap(puts, steps)
         mean_step = sum(e - s for s, e in steps) / len(steps) / 1e3
         out.append(f"| {tid} | {len(steps)} | {mean_step:.1f} | {len(puts)} | {tot / 1e3:.1f} | "
                    f"{hid / 1e3:.1f} ({hid / max(tot, 1):.0%}) |")

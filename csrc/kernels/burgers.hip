@@ -648,8 +648,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
 
     const V fyl = lds_ld<V>(lb + fyb, SB + OFY - TX * E);
     const V fxl = wave_shr1(fx);  // face i-½ from lane l-1 (column 0: unused)
-    V L = -(((fx - fxl) * rdx3 + (fy - fyl) * rdy3) + (fz[sl(0)] - fz[sl(-1)]) * rdz6);
-    if constexpr (VISC) L += vx * d2x + vy * d2y + vz * d2z;
+    // explicit fma, no contraction left to the compiler: the packed (f32x2) and the
+    // scalar instances must round alike (fast contraction fused this sum differently in
+    // the two, 1 ulp apart: round-5 test_burgers3d_fp32_packed_pairs)
+    V L;
+    {
+#pragma clang fp contract(off)
+      L = -fma(fz[sl(0)] - fz[sl(-1)], rdz6, fma(fx - fxl, rdx3, (fy - fyl) * rdy3));
+      if constexpr (VISC) L = fma(vx, d2x, fma(vy, d2y, fma(vz, d2z, L)));
+    }
     V dnew = V(0);
     const V v = stage_value<V, MODE>(axk, ctr, L, V(dt), V(a), V(b), dnew);
     if (active) {
@@ -1039,13 +1046,8 @@ static hipError_t launch_b3_v9_tx(const BArgs& p) {
   // target-count rule (ADVDIFF_B3_CHUNKS=0) gave 512^3 two chunks of 253 planes = 1088
   // workgroups for 512 resident slots: a third round with 64 workgroups alone on the chip.
   static const int rounds_model = knob("B3_CHUNKS", 1);
-  static const int per_cu = [] {
-    int nbk = 0;
-    const void* fn = (const void*)burgers3d_w5s_kernel<T, WZ, VISC, MODE, TXL, PK>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nbk, fn, 512, 0) != hipSuccess || nbk < 1)
-      nbk = 1;
-    return nbk;
-  }();
+  const int per_cu =
+      occupancy_per_cu((const void*)burgers3d_w5s_kernel<T, WZ, VISC, MODE, TXL, PK>, 512);
   // PK: a workgroup marches two half chunks side by side — choose the half length
   const int nm = PK ? div_up(na + nb, 2) : na + nb;
   const int zm = g_b3_zchunk > 0 ? std::max(1, PK ? div_up(g_b3_zchunk, 2) : g_b3_zchunk)
@@ -1346,6 +1348,17 @@ extern "C" int advdiff_burgers2d_stage_ls(int dtype, const void* in, void* du, v
 // Code-object preload (see advdiff_preload in aux.hip): the attributes query makes the
 // runtime load this translation unit's code object now instead of at the first launch.
 extern "C" int advdiff_preload_burgers(void) {
+  using namespace advdiff;
   hipFuncAttributes a;
-  return hipFuncGetAttributes(&a, (const void*)advdiff::burgers3d_w5s_kernel<double, true, true, 1>);
+  const hipError_t e =
+      hipFuncGetAttributes(&a, (const void*)burgers3d_w5s_kernel<double, true, true, 1>);
+  // occupancies of the default 3-D stage instances (launch.hpp occupancy_per_cu): WENO5-Z
+  // viscous, RK3 modes 0-2, both tile rows
+  (void)occupancy_per_cu((const void*)burgers3d_w5s_kernel<double, true, true, 0, 64>, 512);
+  (void)occupancy_per_cu((const void*)burgers3d_w5s_kernel<double, true, true, 1, 64>, 512);
+  (void)occupancy_per_cu((const void*)burgers3d_w5s_kernel<double, true, true, 2, 64>, 512);
+  (void)occupancy_per_cu((const void*)burgers3d_w5s_kernel<double, true, true, 0, 32>, 512);
+  (void)occupancy_per_cu((const void*)burgers3d_w5s_kernel<double, true, true, 1, 32>, 512);
+  (void)occupancy_per_cu((const void*)burgers3d_w5s_kernel<double, true, true, 2, 32>, 512);
+  return e;
 }

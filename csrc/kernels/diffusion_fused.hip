@@ -942,13 +942,8 @@ static hipError_t launch_step(const SArgs& a) {
   const int gy = axis_tile_count(NW * RPW, R, a.bx.ya0, a.bx.ya1, a.bx.yo0, a.bx.yo1, a.ny, edge);
   // z chunks: minimise (rounds of resident workgroups) x (chunk + 4R warm-up planes);
   // resident workgroups = CUs x occupancy of this instance (LDS / VGPR bound: 1-2 per CU)
-  static const int per_cu = [] {
-    int nb = 0;
-    const void* fn = (const void*)diffusion3d_step_kernel<T, ORDER, NW, RPW, VAR>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * NW, 0) != hipSuccess || nb < 1)
-      nb = 1;
-    return nb;
-  }();
+  const int per_cu =
+      occupancy_per_cu((const void*)diffusion3d_step_kernel<T, ORDER, NW, RPW, VAR>, 64 * NW);
   // chunk floor 16 (was 32): lets small grids fill one round of CUs (201x199x200 FD4:
   // 6 -> 7 chunks, 216 -> 252 groups, 51.6 -> 45.1 us per step); 512^3 and 400x200x206
   // pick the same chunking either way (profiles/archive/heat3d_min_chunk_r2.log)
@@ -1045,13 +1040,8 @@ static hipError_t launch_step2x(const SArgs& a) {
   const int gx = axis_tile_count(64, R, a.bx.xa0, a.bx.xa1, a.bx.xo0, a.bx.xo1, a.nx, edge, SH);
   const int gy = axis_tile_count(NW * RPW, R, a.bx.ya0, a.bx.ya1, a.bx.yo0, a.bx.yo1, a.ny, edge,
                                  SH);
-  static const int per_cu = [] {
-    int nb = 0;
-    const void* fn = (const void*)diffusion3d_step2x_kernel<T, NW, RPW>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 64 * NW, 0) != hipSuccess || nb < 1)
-      nb = 1;
-    return nb;
-  }();
+  const int per_cu =
+      occupancy_per_cu((const void*)diffusion3d_step2x_kernel<T, NW, RPW>, 64 * NW);
   static const int minc = knob("STEP_MIN_CHUNK", 16);
   const int na = std::max(a.k1 - a.k0, 0);
   const long long slots = (long long)device_cus() * per_cu;
@@ -1178,8 +1168,18 @@ extern "C" int advdiff_diffusion3d_step(int dtype, const void* uin, void* uout, 
 }
 
 // Code-object preload (see advdiff_preload in aux.hip).
+// The default kernels' occupancies are cached here too (launch.hpp occupancy_per_cu), so
+// no launch inside a hipGraph capture is the first to query one.
 extern "C" int advdiff_preload_diffusion_fused(void) {
+  using namespace advdiff;
   hipFuncAttributes a;
-  return hipFuncGetAttributes(
-      &a, (const void*)advdiff::diffusion3d_step_kernel<double, 4, 16, 2, 3>);
+  const hipError_t e =
+      hipFuncGetAttributes(&a, (const void*)diffusion3d_step_kernel<double, 4, 16, 2, 3>);
+  (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 4, 16, 2, 3>, 64 * 16);
+  (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 2, 12, 3, 23>, 64 * 12);
+  (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<float, 4, 16, 2, 3>, 64 * 16);
+  (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<float, 2, 12, 3, 23>, 64 * 12);
+  (void)occupancy_per_cu((const void*)diffusion3d_step2x_kernel<double, 12, 2>, 64 * 12);
+  (void)occupancy_per_cu((const void*)diffusion3d_step2x_kernel<float, 12, 2>, 64 * 12);
+  return e;
 }

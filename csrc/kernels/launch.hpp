@@ -4,6 +4,9 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <utility>
 #include <stdint.h>
 
 namespace advdiff {
@@ -43,6 +46,28 @@ inline int device_cus() {
     cache[dev] = n;
   }
   return cache[dev];
+}
+
+// Resident workgroups per CU of kernel `fn` at `threads` threads per group, cached per
+// (device, kernel).  The preload entry points (advdiff_preload_*) fill the cache for the
+// default kernels, so no launch inside a hipGraph capture is the first to ask; a failed
+// query is not cached (1 is returned for that launch and the error cleared).
+inline int occupancy_per_cu(const void* fn, int threads) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, int> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(mu);
+  const auto key = std::make_pair(dev, fn);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, threads, 0) != hipSuccess || nb < 1) {
+    (void)hipGetLastError();
+    return 1;
+  }
+  cache.emplace(key, nb);
+  return nb;
 }
 
 // Chunking of the marched axis for a kernel whose workgroups each pay `warm` planes of

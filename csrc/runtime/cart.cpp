@@ -328,7 +328,7 @@ void Engine::launch_fused_box(const Box& bx, double dt, bool exclusive) {
         p_.dtype, at(u_, 0, vy.lo, vx.lo), at(A_, 0, vy.lo, vx.lo), vx.hi - vx.lo, vy.hi - vy.lo,
         sy_, sz_, alloc_[0], bx.r[0].lo, bx.r[0].hi, 0, 0, zact_.lo, zact_.hi, box, p_.order,
         p_.K / (dx * dx), p_.K / (dy * dy), p_.K / (dz * dz), dt,
-        exclusive ? ADVDIFF_EXCLUSIVE : 0, compute_));
+        exclusive ? ADVDIFF_EXCLUSIVE : 0, ls_));
   } else {
     Range vx, xa, xo;
     fused_view(1, bx.r[1].lo, bx.r[1].hi, vx, xa, xo);
@@ -336,11 +336,21 @@ void Engine::launch_fused_box(const Box& bx, double dt, bool exclusive) {
     KERNEL_CHECK(advdiff_diffusion2d_step_box(
         p_.dtype, at(u_, 0, 0, vx.lo), at(A_, 0, 0, vx.lo), vx.hi - vx.lo, sy_, alloc_[0],
         bx.r[0].lo, bx.r[0].hi, zact_.lo, zact_.hi, box, p_.order, p_.K / (dx * dx),
-        p_.K / (dy * dy), dt, compute_));
+        p_.K / (dy * dy), dt, ls_));
   }
 }
 
 void Engine::stage_cart(void* in, void* aux, void* out, double a, double b, double dt, bool ls) {
+  if (p_.overlap && bcomm_) {  // boundary boxes on the comm stream (engine.cpp bcomm_begin)
+    bcomm_begin();
+    launch_box(in, aux, out, interior_box_, dt, a, b, ls);
+    ls_ = comm_;
+    for (const Box& bx : boundary_boxes_) launch_box(in, aux, out, bx, dt, a, b, ls);
+    bcomm_end();
+    halo_pending_ = false;
+    start_halo_cart(out, true);
+    return;
+  }
   if (p_.overlap) {
     launch_box(in, aux, out, interior_box_, dt, a, b, ls);
     if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
@@ -354,6 +364,17 @@ void Engine::stage_cart(void* in, void* aux, void* out, double a, double b, doub
 }
 
 void Engine::step_fused_cart(double dt) {
+  if (p_.overlap && bcomm_) {
+    bcomm_begin();
+    launch_fused_box(interior_box_, dt, false);
+    ls_ = comm_;
+    for (const Box& bx : boundary_boxes_) launch_fused_box(bx, dt, false);
+    bcomm_end();
+    halo_pending_ = false;
+    std::swap(u_, A_);
+    start_halo_cart(u_, true);
+    return;
+  }
   if (p_.overlap) {
     launch_fused_box(interior_box_, dt, false);
     if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
@@ -367,9 +388,11 @@ void Engine::step_fused_cart(double dt) {
   start_halo_cart(u_);
 }
 
-void Engine::start_halo_cart(void* field) {
-  HIP_CHECK(hipEventRecord(ready_, compute_));
-  HIP_CHECK(hipStreamWaitEvent(comm_, ready_, 0));
+void Engine::start_halo_cart(void* field, bool on_comm) {
+  if (!on_comm) {  // on_comm: the producer ran on comm_ (stream order)
+    HIP_CHECK(hipEventRecord(ready_, compute_));
+    HIP_CHECK(hipStreamWaitEvent(comm_, ready_, 0));
+  }
   const int dims = p_.dims;
   auto origin = [&](const Box& b) {
     return dims == 3 ? at(field, b.r[0].lo, b.r[1].lo, b.r[2].lo)

@@ -73,6 +73,9 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   HIP_CHECK(hipStreamCreateWithPriority(&comm_, hipStreamNonBlocking, hi_pri));
   HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&halo_done_, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&cready_, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&bdone_, hipEventDisableTiming));
+  ls_ = compute_;
   // Field setup, timed like the reference's barrier-fenced HtD copy of the initial
   // subdomain (MultiGPU/Diffusion3d_Baseline/main.c:137-148): here the IC is generated
   // on the device, so this is the allocation + IC kernel + stage-buffer copies.
@@ -139,6 +142,16 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
     if (std::sscanf(f, "%d:%d", &fault_rank_, &fault_step_) != 2) fault_rank_ = fault_step_ = -1;
   }
   if (const char* s2 = std::getenv("ADVDIFF_STEP2")) step2_env_ = std::atoi(s2) != 0;
+  {
+    int bc = p.bcomm;
+    if (bc < 0) {
+      const char* v = std::getenv("ADVDIFF_BCOMM");
+      bc = v ? std::atoi(v) : 0;
+    }
+    // the exchange must be stream-ordered device work on comm_ (a host-staged transport
+    // blocks the host on comm_ inside start_halo: keep its boundary on compute_)
+    bcomm_ = bc != 0 && env.size > 1 && p.overlap && std::string(tr_->name()) != "socket";
+  }
   if (sync_debug_enabled() || p.check_every > 0 || fault_rank_ >= 0)
     graph_ = false;  // per-launch / per-step host checks
   if (graph_ && std::string(tr_->name()) == "socket")
@@ -153,6 +166,8 @@ Engine::~Engine() {
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   (void)hipEventDestroy(ready_);
   (void)hipEventDestroy(halo_done_);
+  (void)hipEventDestroy(cready_);
+  (void)hipEventDestroy(bdone_);
   (void)hipStreamDestroy(compute_);
   (void)hipStreamDestroy(comm_);
   (void)hipFree(u_);
@@ -193,18 +208,18 @@ void Engine::launch_view(const void* in, void* aux, void* out, int nx, int ny, R
       if (ls)
         KERNEL_CHECK(advdiff_diffusion3d_stage_ls(p_.dtype, in, aux, out, nx, ny, sy_, sz_,
                                                   r.lo, r.hi, B, p_.order, cx, cy, cz, dt, a, b,
-                                                  compute_));
+                                                  ls_));
       else
         KERNEL_CHECK(advdiff_diffusion3d_stage(p_.dtype, in, aux, out, nx, ny, sy_, sz_,
                                                r.lo, r.hi, B, p_.order, cx, cy, cz, dt, a, b,
-                                               compute_));
+                                               ls_));
     } else {
       if (ls)
         KERNEL_CHECK(advdiff_diffusion2d_stage_ls(p_.dtype, in, aux, out, nx, sy_, r.lo, r.hi,
-                                                  B, p_.order, cx, cy, dt, a, b, compute_));
+                                                  B, p_.order, cx, cy, dt, a, b, ls_));
       else
         KERNEL_CHECK(advdiff_diffusion2d_stage(p_.dtype, in, aux, out, nx, sy_, r.lo, r.hi, B,
-                                               p_.order, cx, cy, dt, a, b, compute_));
+                                               p_.order, cx, cy, dt, a, b, ls_));
     }
   } else {
     const double vx = p_.C / (dx * dx), vy = p_.C / (dy * dy), vz = p_.C / (dz * dz);
@@ -212,20 +227,20 @@ void Engine::launch_view(const void* in, void* aux, void* out, int nx, int ny, R
       if (ls)
         KERNEL_CHECK(advdiff_burgers3d_stage_ls(p_.dtype, in, aux, out, nx, ny, sy_, sz_,
                                                 r.lo, r.hi, B, p_.weno, 1.0 / dx, 1.0 / dy,
-                                                1.0 / dz, vx, vy, vz, dt, a, b, compute_));
+                                                1.0 / dz, vx, vy, vz, dt, a, b, ls_));
       else
         KERNEL_CHECK(advdiff_burgers3d_stage(p_.dtype, in, aux, out, nx, ny, sy_, sz_, r.lo,
                                              r.hi, B, p_.weno, 1.0 / dx, 1.0 / dy, 1.0 / dz, vx,
-                                             vy, vz, dt, a, b, compute_));
+                                             vy, vz, dt, a, b, ls_));
     } else {
       if (ls)
         KERNEL_CHECK(advdiff_burgers2d_stage_ls(p_.dtype, in, aux, out, nx, sy_, r.lo, r.hi, B,
                                                 p_.weno, 1.0 / dx, 1.0 / dy, vx, vy, dt, a, b,
-                                                compute_));
+                                                ls_));
       else
         KERNEL_CHECK(advdiff_burgers2d_stage(p_.dtype, in, aux, out, nx, sy_, r.lo, r.hi, B,
                                              p_.weno, 1.0 / dx, 1.0 / dy, vx, vy, dt, a, b,
-                                             compute_));
+                                             ls_));
     }
   }
 }
@@ -239,7 +254,7 @@ void Engine::launch_fused(Range r, double dt, Range r2, bool exclusive) {
         KERNEL_CHECK(advdiff_diffusion2d_step(p_.dtype, u_, A_, p_.nx, sy_, slab_.alloc(), q.lo,
                                               q.hi, zact_.lo, zact_.hi, p_.border(), p_.order,
                                               p_.K / (dx * dx), p_.K / (dy * dy), dt,
-                                              compute_));
+                                              ls_));
     return;
   }
   const int B = p_.border();
@@ -247,7 +262,7 @@ void Engine::launch_fused(Range r, double dt, Range r2, bool exclusive) {
   KERNEL_CHECK(advdiff_diffusion3d_step_box_ex(
       p_.dtype, u_, A_, p_.nx, p_.ny, sy_, sz_, slab_.alloc(), r.lo, r.hi, r2.lo, r2.hi,
       zact_.lo, zact_.hi, box, p_.order, p_.K / (dx * dx), p_.K / (dy * dy), p_.K / (dz * dz),
-      dt, exclusive ? ADVDIFF_EXCLUSIVE : 0, compute_));
+      dt, exclusive ? ADVDIFF_EXCLUSIVE : 0, ls_));
 }
 
 void Engine::step_fused(double dt) {
@@ -257,6 +272,16 @@ void Engine::step_fused(double dt) {
   }
   if (env_.size == 1) {
     launch_fused(full_, dt, Range{}, true);
+  } else if (p_.overlap && bcomm_) {
+    bcomm_begin();
+    launch_fused(interior_, dt);  // compute_, beside the whole exchange
+    ls_ = comm_;                  // after the halo of u in stream order
+    launch_fused(blo_, dt, bhi_);
+    bcomm_end();
+    halo_pending_ = false;
+    std::swap(u_, A_);
+    start_halo(u_, true);
+    return;
   } else if (p_.overlap) {
     launch_fused(interior_, dt);  // overlaps the RCCL exchange: grid schedule
     if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
@@ -295,11 +320,30 @@ void Engine::step2(double dt) {
   }
 }
 
-void Engine::start_halo(void* field) {
+// Boundary launch on the comm stream (bcomm_): before it, comm_ joins compute_ (the
+// previous interior launch read / wrote what the boundary launch overwrites); after it,
+// compute_ joins comm_ at bdone_ — recorded BEFORE the puts and the wait for the peers, so
+// a spinning device wait never holds a compute launch.  Every cross-stream wait forks from
+// or joins into compute_ (a hipGraph capture's origin): no event is waited on by the
+// stream that recorded it (profiles/r5/diag_bstream.md).
+void Engine::bcomm_begin() {
+  HIP_CHECK(hipEventRecord(cready_, compute_));
+  HIP_CHECK(hipStreamWaitEvent(comm_, cready_, 0));
+}
+
+void Engine::bcomm_end() {
+  ls_ = compute_;
+  HIP_CHECK(hipEventRecord(bdone_, comm_));
+  HIP_CHECK(hipStreamWaitEvent(compute_, bdone_, 0));
+}
+
+void Engine::start_halo(void* field, bool on_comm) {
   if (env_.size == 1) return;
   const int G = slab_.ghost, c = slab_.count();
-  HIP_CHECK(hipEventRecord(ready_, compute_));
-  HIP_CHECK(hipStreamWaitEvent(comm_, ready_, 0));
+  if (!on_comm) {  // on_comm: the producer ran on comm_ (stream order)
+    HIP_CHECK(hipEventRecord(ready_, compute_));
+    HIP_CHECK(hipStreamWaitEvent(comm_, ready_, 0));
+  }
   tr_->halo(plane(field, G), plane(field, 0), plane(field, G + c - G), plane(field, G + c),
             (size_t)G * plane_bytes_, slab_.lower(), slab_.upper(), comm_);
   HIP_CHECK(hipEventRecord(halo_done_, comm_));
@@ -316,17 +360,27 @@ void Engine::stage(void* in, void* aux, void* out, double a, double b, double dt
     return;
   }
   if (p_.overlap) {
+    if (bcomm_) bcomm_begin();
     launch(in, aux, out, interior_, dt, a, b, ls);
-    if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
+    if (bcomm_)
+      ls_ = comm_;  // after the halo of `in` in stream order
+    else if (halo_pending_)
+      HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
     if (p_.physics == Physics::Burgers && p_.dims == 3) {  // both boundary slabs, one launch
       const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
       KERNEL_CHECK(advdiff_burgers3d_stage2_dt(
           p_.dtype, in, aux, out, p_.nx, p_.ny, sy_, sz_, blo_.lo, blo_.hi, bhi_.lo, bhi_.hi,
           p_.border(), p_.weno, 1.0 / dx, 1.0 / dy, 1.0 / dz, p_.C / (dx * dx),
-          p_.C / (dy * dy), p_.C / (dz * dz), dt, a, b, ls ? 1 : 0, nullptr, compute_));
+          p_.C / (dy * dy), p_.C / (dz * dz), dt, a, b, ls ? 1 : 0, nullptr, ls_));
     } else {
       launch(in, aux, out, blo_, dt, a, b, ls);
       launch(in, aux, out, bhi_, dt, a, b, ls);
+    }
+    if (bcomm_) {
+      bcomm_end();
+      halo_pending_ = false;
+      start_halo(out, true);
+      return;
     }
   } else {
     if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));

@@ -306,6 +306,9 @@ struct Problem {
   double ic_p0 = 1.0, ic_p1 = 0.1;
   double t0 = 0.0;
   bool overlap = true;
+  // overlap: the boundary launch on the comm stream, between the wait for its input's
+  // halo and the puts of its output (-1 = ADVDIFF_BCOMM, default off; --boundary-on-comm)
+  int bcomm = -1;
   int integrator = 0;              // 0 SSP-RK3, 1 low-storage RK4(5)
   bool fused = true;               // 3-D heat + SSP-RK3: one launch per step (3R ghosts)
   int graph = -1;                  // hipGraph stepping: -1 auto (graph-safe transports), 0, 1
@@ -406,7 +409,7 @@ class Engine {
   // wait) -> persistent schedule of the 3-D step kernel (ADVDIFF_EXCLUSIVE)
   void launch_fused(Range r, double dt, Range r2 = Range{}, bool exclusive = false);
   void step_fused(double dt);
-  void start_halo(void* field);
+  void start_halo(void* field, bool on_comm = false);
   void* plane(void* base, int l) const { return (char*)base + (size_t)l * plane_bytes_; }
   // checkpoint views: array order padded to three axes (2-D: axis 0 is a unit axis whose
   // one "plane" is the whole field)
@@ -423,7 +426,7 @@ class Engine {
   void fused_view(int a, int lo, int hi, Range& view, Range& act, Range& outr) const;
   void stage_cart(void* in, void* aux, void* out, double a, double b, double dt, bool ls);
   void step_fused_cart(double dt);
-  void start_halo_cart(void* field);
+  void start_halo_cart(void* field, bool on_comm = false);
   void error_norms_cart(double& l1, double& l2, double& linf);
   template <typename V>
   std::vector<V> gather_cart();
@@ -461,7 +464,13 @@ class Engine {
   std::vector<std::vector<HaloPlanMsg>> plan_;  // Cartesian halo phases
   double init_s_ = 0;                          // barrier-fenced field setup time
   hipStream_t compute_ = nullptr, comm_ = nullptr;
+  hipStream_t ls_ = nullptr;  // stream of the stencil launches (compute_, or comm_ for the
+                              // boundary launch of the bcomm_ schedule)
   hipEvent_t ready_ = nullptr, halo_done_ = nullptr;
+  hipEvent_t cready_ = nullptr, bdone_ = nullptr;  // bcomm_: compute_ -> comm_, comm_ -> compute_
+  bool bcomm_ = false;
+  void bcomm_begin();
+  void bcomm_end();
   bool halo_pending_ = false;
   Range full_, interior_, blo_, bhi_;
   double t_ = 0;

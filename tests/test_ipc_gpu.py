@@ -206,6 +206,27 @@ def test_native_poisoned_multirank_bitwise(tmp_path, app, args, shape, world, de
                     f"{bad.min(axis=0)}..{bad.max(axis=0)} of {shape}\n{txt[-2000:]}")
 
 
+@pytest.mark.parametrize("app,args,shape,world,decomp,extra", [
+    NATIVE_CASES[1], NATIVE_CASES[3], NATIVE_CASES[4], NATIVE_CASES[5], NATIVE_CASES[6],
+    NATIVE_CASES[7]])
+def test_native_boundary_on_comm_bitwise(tmp_path, app, args, shape, world, decomp, extra):
+    """Native engine, --boundary-on-comm: the boundary launch on the comm stream between
+    the wait for its input's halo and the puts of its output (fused heat slab and 2x2x2,
+    per-stage heat and Burgers, slab and Cartesian, 2-D), ipc transport, graph-replayed
+    (the default), poisoned allocations: bitwise equal to one rank."""
+    one, many = tmp_path / "one.bin", tmp_path / "many.bin"
+    env = {"ADVDIFF_POISON": "1"}
+    env.update(e.split("=", 1) for e in extra if e.startswith("ADVDIFF_"))
+    extra = [e for e in extra if not e.startswith("ADVDIFF_")]
+    _native(app, args, one, extra=extra, env_extra=env)
+    dec = [] if decomp == "slab" else ["--decomp", decomp]
+    txt = _native(app, args, many, world=world,
+                  extra=extra + ["--transport", "ipc", "--boundary-on-comm"] + dec, env_extra=env)
+    a = np.fromfile(one, dtype=np.float32).reshape(shape)
+    b = np.fromfile(many, dtype=np.float32).reshape(shape)
+    assert np.isfinite(a).all() and np.array_equal(a, b), txt[-2000:]
+
+
 def _preflight_then_run(comm, kind, steps):
     rec = comm.ipc().preflight(rounds=3)
     model, grid, ic = _make(kind)

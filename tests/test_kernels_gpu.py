@@ -450,4 +450,7 @@ def test_burgers3d_fp32_packed_pairs(tx, weno_z, visc, mode, ranges):
         else:
             ref.burgers3d_stage(inp.double(), u0.double(), exp_out, nx, ny, lo, hi, 3, weno_z,
                                 *rd, *vv, 1e-3, a, b)
-    assert (outs[1][0].double() - exp_out).abs().max().item() < 5e-4
+    # fp32 arithmetic on inputs that are exact in fp64: error-scaled bound (round 4 had an
+    # absolute 5e-4, ~1e4 ulps)
+    err = (outs[1][0].double() - exp_out).abs().max().item()
+    assert err <= 1e-5 * exp_out.abs().max().item(), err
