@@ -30,7 +30,10 @@ def _is_put(name):
 
 
 def _is_step(name):
-    return ("step_kernel" in name or "stage" in name or "_step" in name) and not _is_put(name)
+    """A stencil launch: the fused heat step, a per-stage kernel or a WENO stage
+    (burgers*_w5*_kernel / burgers*_stage_kernel)."""
+    return (("step_kernel" in name or "stage" in name or "_step" in name or "burgers" in name)
+            and not _is_put(name))
 
 
 def _union(iv):

@@ -8,7 +8,8 @@
 //
 // plus named options (runtime replacements of the reference's #defines, §2.7):
 //   --ic NAME  --order 2|4  --safety S  --weno js|z|js7  --visc C  --fp32  --no-overlap
-//   --boundary-on-comm (overlap: the boundary launch on the comm stream; ADVDIFF_BCOMM=1)
+//   --[no-]boundary-on-comm (overlap: the boundary launch on the comm stream; default on
+//   for --transport ipc; ADVDIFF_BCOMM=0/1)
 //   --integrator ssprk3|lsrk45  --no-fused  --transport rccl|ipc|socket  --write FILE
 //   --write-ghosts FILE (the reference's multi-GPU result.bin: every rank's slab WITH its
 //   ghost planes, MultiGPU/Diffusion3d_Baseline/main.c:341)  --error-norms
@@ -127,6 +128,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
     std::string a = argv[q];
     if (a.rfind("--", 0) == 0) {
       const bool flag = a == "--fp32" || a == "--no-overlap" || a == "--boundary-on-comm" ||
+                        a == "--no-boundary-on-comm" ||
                         a == "--error-norms" || a == "--no-fused" || a == "--geometry" || a == "--graph" ||
                         a == "--no-graph" || a == "--print" || a == "--json";
       if (flag || q + 1 >= argc) {
@@ -145,7 +147,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
     std::cerr << "usage: " << argv[0]
               << (diff ? (dims == 3 ? " K L W H Nx Ny Nz iters [bx by bz]" : " K L W Nx Ny iters [bx by]")
                        : (dims == 3 ? " tEnd CFL L W H Nx Ny Nz [bx by bz]" : " tEnd CFL L W Nx Ny [bx by]"))
-              << " [--ic NAME] [--order 2|4] [--weno js|z|js7] [--integrator ssprk3|lsrk45] [--no-fused] [--visc C] [--fp32] [--no-overlap] [--boundary-on-comm]"
+              << " [--ic NAME] [--order 2|4] [--weno js|z|js7] [--integrator ssprk3|lsrk45] [--no-fused] [--visc C] [--fp32] [--no-overlap] [--[no-]boundary-on-comm]"
                  " [--transport rccl|ipc|socket] [--decomp slab|PZxPYxPX|PYxPX] [--write FILE]"
                  " [--write-ghosts FILE] [--error-norms] [--geometry] [--graph|--no-graph]"
                  " [--restart PREFIX] [--checkpoint PREFIX] [--check-every N] [--ascii FILE]"
@@ -189,6 +191,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   if (opt.count("--fp32")) p.dtype = ADVDIFF_F32;
   if (opt.count("--no-overlap")) p.overlap = false;
   if (opt.count("--boundary-on-comm")) p.bcomm = 1;
+  if (opt.count("--no-boundary-on-comm")) p.bcomm = 0;
   if (opt.count("--graph")) p.graph = 1;
   if (opt.count("--no-graph")) p.graph = 0;
   if (opt.count("--check-every")) p.check_every = std::stoi(opt["--check-every"]);

@@ -307,7 +307,8 @@ struct Problem {
   double t0 = 0.0;
   bool overlap = true;
   // overlap: the boundary launch on the comm stream, between the wait for its input's
-  // halo and the puts of its output (-1 = ADVDIFF_BCOMM, default off; --boundary-on-comm)
+  // halo and the puts of its output (-1 = ADVDIFF_BCOMM, default on for the ipc transport;
+  // --boundary-on-comm / --no-boundary-on-comm)
   int bcomm = -1;
   int integrator = 0;              // 0 SSP-RK3, 1 low-storage RK4(5)
   bool fused = true;               // 3-D heat + SSP-RK3: one launch per step (3R ghosts)

@@ -74,6 +74,10 @@ def build_parser():
     ap.add_argument("--exchange", choices=["u", "lu"], default="u",
                     help="halo payload: u (stage output) or lu (the reference's RHS exchange "
                          "with redundant ghost-plane updates; slab, PyTorch ops)")
+    ap.add_argument("--boundary-on-comm", dest="bcomm", action="store_true", default=None,
+                    help="overlap: boundary launch on the comm stream between the halo wait "
+                         "and the puts (default on for --transport ipc; ADVDIFF_BCOMM)")
+    ap.add_argument("--no-boundary-on-comm", dest="bcomm", action="store_false")
     ap.add_argument("--stripe", type=int, default=None,
                     help="ipc slab halos: relay part of every face message through up to N "
                          "helper ranks over idle xGMI links (default: ADVDIFF_STRIPE or 0)")
@@ -192,7 +196,7 @@ def main(argv=None) -> int:
     solver, htod_s = fenced(lambda: Solver(
         model, grid, comm, dtype=dtype, ic=ic, overlap=not ns.no_overlap, t0=t0,
         check_every=ns.check_every, decomp=ns.decomp, integrator=ns.integrator,
-        kernel=ns.kernel, exchange=ns.exchange, stripe=ns.stripe))
+        kernel=ns.kernel, exchange=ns.exchange, stripe=ns.stripe, boundary_on_comm=ns.bcomm))
     if ns.geometry:  # decomposition only (no steps), one JSON line per rank in rank order
         geo = {"rank": comm.rank, "world": comm.size, "pgrid": list(solver.pgrid),
                "global_box": [list(b) for b in solver.cd.global_box()],

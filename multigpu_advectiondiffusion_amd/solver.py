@@ -185,8 +185,12 @@ class Solver:
                 boundary_on_comm = boundary_stream
             if boundary_on_comm is None:
                 import os
-                boundary_on_comm = (os.environ.get("ADVDIFF_BCOMM")
-                                    or os.environ.get("ADVDIFF_BSTREAM", "0")) == "1"
+                # default: on for the ipc transport (every exchange step is a kernel on
+                # the comm stream; 2 ranks on one GPU: 90-100 % of the put time beside the
+                # interior launch instead of 8-33 %, profiles/r5/overlap.md), off for rccl
+                # until it has run on distinct GPUs
+                env = os.environ.get("ADVDIFF_BCOMM") or os.environ.get("ADVDIFF_BSTREAM")
+                boundary_on_comm = (env == "1") if env else self.transport == "ipc"
             # the boundary launch on the (high-priority) comm stream, between the wait for
             # the halo of its input and the puts of its output: _step_fused_bcomm
             self.bcomm = bool(boundary_on_comm and overlap and exchange == "u"

@@ -43,9 +43,16 @@ def _reference(kind, steps):
 
 
 def _run(comm, kind, steps, overlap, decomp, graph):
+    """overlap: True (the default schedule: boundary launch on the comm stream), "plain"
+    (boundary launch on the compute stream after the halo wait) or False."""
     assert comm.transport == "ipc"
     model, grid, ic = _make(kind)
-    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, overlap=overlap, decomp=decomp)
+    bc = None
+    if overlap == "plain":
+        overlap, bc = True, False
+    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, overlap=overlap, decomp=decomp,
+               boundary_on_comm=bc)
+    assert s.bcomm == (overlap and bc is None)
     assert s.graph_capable()
     s.run(iters=steps, graph=graph)
     g = s.gather()
@@ -72,11 +79,13 @@ def _shared_gpu_env(monkeypatch):
 @pytest.mark.parametrize("kind", ["diff3", "burg3", "diff2", "burg2", "diff3o2"])
 def test_ipc_slab_bitwise(kind, monkeypatch):
     """z/y slabs, per-stage (Burgers) and fused-step (heat) exchanges, 2 and 3 ranks,
-    overlap on/off, eager and hipGraph replay (16 steps = 2 graphs of 8) — all bitwise
-    equal to the 1-rank run."""
+    overlap on (boundary on the comm stream, the default; and the plain schedule) / off,
+    eager and hipGraph replay (16 steps = 2 graphs of 8) — all bitwise equal to the 1-rank
+    run."""
     monkeypatch.setenv("ADVDIFF_SHARE_GPU", "1")
     ref = _reference(kind, 16)
-    for world, overlap, graph in ((2, True, False), (3, True, True), (2, False, True)):
+    for world, overlap, graph in ((2, True, False), (3, True, True), (2, False, True),
+                                  (3, "plain", True)):
         out = _spawn(world, kind, 16, overlap, None, graph)
         assert np.array_equal(out, ref), (kind, world, overlap, graph, np.abs(out - ref).max())
 
@@ -209,11 +218,12 @@ def test_native_poisoned_multirank_bitwise(tmp_path, app, args, shape, world, de
 @pytest.mark.parametrize("app,args,shape,world,decomp,extra", [
     NATIVE_CASES[1], NATIVE_CASES[3], NATIVE_CASES[4], NATIVE_CASES[5], NATIVE_CASES[6],
     NATIVE_CASES[7]])
-def test_native_boundary_on_comm_bitwise(tmp_path, app, args, shape, world, decomp, extra):
-    """Native engine, --boundary-on-comm: the boundary launch on the comm stream between
-    the wait for its input's halo and the puts of its output (fused heat slab and 2x2x2,
-    per-stage heat and Burgers, slab and Cartesian, 2-D), ipc transport, graph-replayed
-    (the default), poisoned allocations: bitwise equal to one rank."""
+def test_native_plain_overlap_bitwise(tmp_path, app, args, shape, world, decomp, extra):
+    """Native engine, ipc transport, --no-boundary-on-comm: the plain overlap schedule
+    (boundary launch on the compute stream after the halo wait; the ipc default since
+    round 5 is the boundary launch on the comm stream, which the poisoned test above
+    runs) — fused heat slab and 2x2x2, per-stage heat and Burgers, slab and Cartesian,
+    2-D, graph-replayed, poisoned allocations: bitwise equal to one rank."""
     one, many = tmp_path / "one.bin", tmp_path / "many.bin"
     env = {"ADVDIFF_POISON": "1"}
     env.update(e.split("=", 1) for e in extra if e.startswith("ADVDIFF_"))
@@ -221,7 +231,8 @@ def test_native_boundary_on_comm_bitwise(tmp_path, app, args, shape, world, deco
     _native(app, args, one, extra=extra, env_extra=env)
     dec = [] if decomp == "slab" else ["--decomp", decomp]
     txt = _native(app, args, many, world=world,
-                  extra=extra + ["--transport", "ipc", "--boundary-on-comm"] + dec, env_extra=env)
+                  extra=extra + ["--transport", "ipc", "--no-boundary-on-comm"] + dec,
+                  env_extra=env)
     a = np.fromfile(one, dtype=np.float32).reshape(shape)
     b = np.fromfile(many, dtype=np.float32).reshape(shape)
     assert np.isfinite(a).all() and np.array_equal(a, b), txt[-2000:]
