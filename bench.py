@@ -28,8 +28,10 @@ bench therefore runs --settle-ms (default 300 ms) more untimed steps of the same
 then times exactly K steps; the count is reported as `settle`.  `sustained`
 (informational, AFTER the K timed steps): --sustained-steps more steps timed the same way.
 
-FD2 on one GPU runs two RK3 steps per launch (diffusion_fused.hip v6_march; bit-identical
-to one step per launch): `fd2_7pt.steps_per_launch`.
+FD2 on one GPU runs one RK3 step per launch or two (diffusion_fused.hip v6_march;
+bit-identical), whichever the solver measured faster for the shape at construction
+(advdiff_diffusion3d_step2_pick; at 512^3 fp64 one step per launch wins by 3 %):
+`fd2_7pt.steps_per_launch`.
 """
 from __future__ import annotations
 
@@ -457,6 +459,7 @@ def run(args):
         m2 = Diffusion(K=1.0, order=2)
         s2 = make_heat(decomp, transport, m=m2)
         secs2 = timed(s2, args.steps, args.warmup, m2.stable_dt(), args.settle_ms, "fd2")
+        per_launch = 2 if s2.step2_capable() else 1
         _, _, linf2 = s2.error_norms()
         bound2 = linf_bound(grid, m2.K, s2.t, 2)
         del s2
@@ -470,7 +473,7 @@ def run(args):
                              "vs_baseline": round(ml2 / BASE_DIFFUSION, 2),
                              "linf_vs_exact": float(f"{linf2:.3e}"),
                              "settle": SETTLE.get("fd2"),
-                             "steps_per_launch": 2 if n == 1 else 1,
+                             "steps_per_launch": per_launch,
                              "model": "diffusion3d FD2 7-point + SSP-RK3"}
 
     # ---- secondary: 3-D Burgers WENO5-Z + C∇²u, fp64 ----------------------------------

@@ -208,6 +208,12 @@ int advdiff_diffusion3d_step2x(int dtype, const void* uin, void* uout, int nx, i
                                int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int zlo,
                                int zhi, const int* box, double cx, double cy, double cz,
                                double dt, void* stream);
+// one FD2 step or two per launch for this shape (measured once per shape and process,
+// uin untouched, uout used as scratch; ADVDIFF_STEP2=0/1 forces): *use2 = 1 for two
+int advdiff_diffusion3d_step2_pick(int dtype, const void* uin, void* uout, int nx, int ny,
+                                   int64_t sy, int64_t sz, int nz_alloc, int k0, int k1,
+                                   int zlo, int zhi, const int* box, double cx, double cy,
+                                   double cz, double dt, void* stream, int* use2);
 // fused heat step: forced z-chunk length (0 = automatic); returns the previous setting
 int advdiff_set_step_zchunk(int zc);
 // fp32 fused heat step tile: 0 = the fp64 shapes, 3 / 4 = 16 waves x 3 / 4 rows

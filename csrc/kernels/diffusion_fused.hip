@@ -25,7 +25,11 @@
 #include "launch.hpp"
 #include "advdiff/kernels.h"
 
+#include <cstdio>
+#include <map>
+#include <mutex>
 #include <utility>
+#include <vector>
 
 namespace advdiff {
 
@@ -1147,6 +1151,85 @@ extern "C" int advdiff_diffusion3d_step2x(int dtype, const void* uin, void* uout
   if (dtype == ADVDIFF_F64) return launch_step2x<double, 12, 2>(a);
   if (dtype == ADVDIFF_F32) return launch_step2x<float, 12, 2>(a);
   return hipErrorInvalidValue;
+}
+
+// One step or two per launch for this FD2 shape: measured, once per (dtype, shape) and
+// process.  The two-step launch halves the HBM traffic but grows the trapezoid rims from
+// 2R to 5R; which wins depends on how the two tilings quantise on the 256 CUs: two per
+// launch is 9-25 % faster at 384^3, 640^3-1024^3 fp64 and 16-22 % in fp32, but 3 % slower
+// at 512^3 fp64, where the one-step tiling fits unusually well (profiles/r5/ab/
+// step2_ab.log, step2_sizes.log, step2_chunks.log).  Protocol: 3 warm-up one-step
+// launches, then 3 interleaved rounds of two one-step launches and one two-step launch
+// (uin -> uout only: uin is untouched, uout's output box is scratch), min per step; two
+// per launch only if it is >= 3 % faster.  ADVDIFF_STEP2=0 / 1 forces the choice.
+// Synchronous (host waits on events): call it outside any graph capture.
+extern "C" int advdiff_diffusion3d_step2_pick(int dtype, const void* uin, void* uout, int nx,
+                                              int ny, int64_t sy, int64_t sz, int nz_alloc,
+                                              int k0, int k1, int zlo, int zhi, const int* box,
+                                              double cx, double cy, double cz, double dt,
+                                              void* stream, int* use2) {
+  using namespace advdiff;
+  if (use2 == nullptr || box == nullptr) return hipErrorInvalidValue;
+  if (const char* v = std::getenv("ADVDIFF_STEP2"); v && (v[0] == '0' || v[0] == '1')) {
+    *use2 = v[0] == '1';
+    return hipSuccess;
+  }
+  static std::mutex mu;
+  static std::map<std::vector<int64_t>, int> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::vector<int64_t> key{dtype, dev, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi};
+  for (int q = 0; q < 8; ++q) key.push_back(box[q]);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) {
+      *use2 = it->second;
+      return hipSuccess;
+    }
+  }
+  hipStream_t st = (hipStream_t)stream;
+  auto one = [&]() {
+    return advdiff_diffusion3d_step_box_ex(dtype, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1,
+                                           0, 0, zlo, zhi, box, 2, cx, cy, cz, dt,
+                                           ADVDIFF_EXCLUSIVE, stream);
+  };
+  auto two = [&]() {
+    return advdiff_diffusion3d_step2x(dtype, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo,
+                                      zhi, box, cx, cy, cz, dt, stream);
+  };
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipError_t e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  float t1 = 1e30f, t2 = 1e30f;
+  for (int w = 0; w < 3 && e == hipSuccess; ++w) e = (hipError_t)one();
+  for (int r = 0; r < 3 && e == hipSuccess; ++r) {
+    float ms = 0.f;
+    e = hipEventRecord(e0, st);
+    if (e == hipSuccess) e = (hipError_t)one();
+    if (e == hipSuccess) e = (hipError_t)one();
+    if (e == hipSuccess) e = hipEventRecord(e1, st);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e == hipSuccess) t1 = std::min(t1, ms / 2.f);
+    if (e == hipSuccess) e = hipEventRecord(e0, st);
+    if (e == hipSuccess) e = (hipError_t)two();
+    if (e == hipSuccess) e = hipEventRecord(e1, st);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e == hipSuccess) t2 = std::min(t2, ms / 2.f);
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (e != hipSuccess) return e;
+  *use2 = t2 < 0.97f * t1;
+  if (std::getenv("ADVDIFF_STEP2_LOG"))
+    std::fprintf(stderr, "advdiff: FD2 %dx%dx%d %s: one step %.1f us, two per launch %.1f us/step"
+                 " -> %s\n", nx, ny, k1 - k0, dtype == ADVDIFF_F64 ? "fp64" : "fp32",
+                 t1 * 1e3f, t2 * 1e3f, *use2 ? "two" : "one");
+  std::lock_guard<std::mutex> g(mu);
+  cache[key] = *use2;
+  return hipSuccess;
 }
 
 extern "C" int advdiff_diffusion3d_step2(int dtype, const void* uin, void* uout, int nx, int ny,

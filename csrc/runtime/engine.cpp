@@ -157,6 +157,21 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   if (graph_ && std::string(tr_->name()) == "socket")
     throw std::runtime_error("--graph: the socket transport synchronises the host inside a step");
   if (env.size > 1) wd_ = std::make_unique<Watchdog>(tr_, env.rank, Watchdog::timeout_from_env());
+  // one FD2 step or two per launch: measured for this shape (kernels.h
+  // advdiff_diffusion3d_step2_pick; ADVDIFF_STEP2=0/1 forces), before any capture
+  if (step2_env_ && fused_ && env_.size == 1 && !cart_ && p_.dims == 3 && p_.order == 2 &&
+      p_.physics == Physics::Diffusion) {
+    const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
+    const int B = p_.border();
+    const int box[8] = {B, p_.nx - B, B, p_.ny - B, 0, p_.nx, 0, p_.ny};
+    int use2 = 1;
+    HIP_CHECK((hipError_t)advdiff_diffusion3d_step2_pick(
+        p_.dtype, u_, A_, p_.nx, p_.ny, sy_, sz_, slab_.alloc(), full_.lo, full_.hi, zact_.lo,
+        zact_.hi, box, p_.K / (dx * dx), p_.K / (dy * dy), p_.K / (dz * dz), stable_dt(),
+        compute_, &use2));
+    HIP_CHECK(hipStreamSynchronize(compute_));
+    step2_env_ = use2 != 0;
+  }
 }
 
 Engine::~Engine() {

@@ -40,6 +40,9 @@ _SIGS = {
     "advdiff_diffusion3d_step2x": [c_int, c_vp, c_vp, c_int, c_int, c_i64, c_i64, c_int, c_int,
                                    c_int, c_int, c_int, ctypes.POINTER(c_int), c_dbl, c_dbl,
                                    c_dbl, c_dbl, c_vp],
+    "advdiff_diffusion3d_step2_pick": [c_int, c_vp, c_vp, c_int, c_int, c_i64, c_i64, c_int,
+                                       c_int, c_int, c_int, c_int, ctypes.POINTER(c_int), c_dbl,
+                                       c_dbl, c_dbl, c_dbl, c_vp, ctypes.POINTER(c_int)],
     "advdiff_diffusion3d_step_box": [c_int, c_vp, c_vp, c_int, c_int, c_i64, c_i64, c_int,
                                      c_int, c_int, c_int, c_int, c_int, c_int,
                                      ctypes.POINTER(c_int), c_int, c_dbl, c_dbl, c_dbl, c_dbl,

@@ -9,6 +9,8 @@ All ops enqueue on the current HIP stream (``torch.cuda.current_stream()``) unle
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -132,6 +134,28 @@ def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, 
             if b > a:
                 ref.diffusion3d_step_box(uin, uout, nx, ny, a, b, zlo, zhi, box, order, cx, cy,
                                          cz, dt)
+
+
+def diffusion3d_step2_pick(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, cx, cy, cz, dt,
+                           stream=None, box=None) -> bool:
+    """True if two FD2 steps per launch beat one step per launch for this shape on this
+    GPU (advdiff_diffusion3d_step2_pick: measured once per shape and process; uin is not
+    modified, uout is used as scratch; ADVDIFF_STEP2=0/1 forces).  Synchronous: call it
+    outside a graph capture.  Not a native device field: True (the CPU path pairs)."""
+    import os
+    if not _native(uin):
+        return os.environ.get("ADVDIFF_STEP2", "1") != "0"
+    _check_layout(uin, uout)
+    if box is None:
+        box = (border, nx - border, border, ny - border, 0, nx, 0, ny)
+    lib = _lib.require()
+    use2 = ctypes.c_int(0)
+    code = lib.advdiff_diffusion3d_step2_pick(
+        _dtype_code(uin), _ptr(uin), _ptr(uout), nx, ny, uin.stride(1), uin.stride(0),
+        uin.shape[0], k0, k1, zlo, zhi, _int_array(box), cx, cy, cz, dt, _stream_ptr(stream),
+        ctypes.byref(use2))
+    _lib.check(code, "diffusion3d_step2_pick")
+    return bool(use2.value)
 
 
 def diffusion3d_step2x(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, cx, cy, cz, dt,

@@ -220,6 +220,8 @@ class Solver:
         if device_dt is None:
             device_dt = self.device.type == "cuda" and kernel == "native"
         self.device_dt = bool(device_dt) and model.needs_umax and exchange == "u"
+        self._step2_on = False
+        self._step2_on = self._pick_step2()
 
     def _ipc_multi(self) -> bool:
         return (self.device.type == "cuda" and self.comm.size > 1
@@ -530,9 +532,25 @@ class Solver:
 
     def step2_capable(self) -> bool:
         """Two fixed-dt steps in one launch (single-rank 3-D FD2 heat: the model's step2,
-        bit-identical to two steps)."""
+        bit-identical to two steps) — where that is the faster launch for this shape
+        (measured once per shape on the GPU at construction: _pick_step2)."""
         return (self.fused and self.comm.size == 1 and not self.cart and self.du is None
-                and self.model.supports_step2 and self._dt_dev is None)
+                and self.model.supports_step2 and self._dt_dev is None and self._step2_on)
+
+    def _pick_step2(self) -> bool:
+        """One FD2 step or two per launch, decided before any graph capture: two per
+        launch halves the HBM traffic but wins or loses by shape (+9-25 % at 384^3 and
+        640^3-1024^3 fp64, -3 % at 512^3: profiles/r5/ab/step2_*.log).  The pick times
+        both launches u -> un (u untouched; un is the step's scratch partner)."""
+        if not (self.fused and self.comm.size == 1 and not self.cart and self.du is None
+                and self.model.supports_step2):
+            return False
+        if self.kernel == "torch" or self.device.type != "cuda":
+            return True
+        lo, hi = self.full
+        dt = self.model.stable_dt() if not self.model.needs_umax else 0.0
+        return self.model.step2_preferred(self.u, self.un, lo, hi, self.zact[0], self.zact[1],
+                                          dt)
 
     def step2(self, dt: float) -> None:
         """Two steps at the same dt (one launch when step2_capable)."""

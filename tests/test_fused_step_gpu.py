@@ -311,3 +311,35 @@ def test_solver_two_step_path_bitwise(monkeypatch):
         b, itb, tb = run("0", iters, graph)
         assert (ita, ta) == (itb, tb)
         assert torch.equal(a, b), (a - b).abs().max().item()
+
+
+def test_step2_pick_measured_leaves_u_and_results(monkeypatch):
+    """ADVDIFF_STEP2 unset: the solver measures one step vs two per launch for its shape
+    at construction (advdiff_diffusion3d_step2_pick, u -> un only).  u must come out of
+    the measurement untouched, the pick must be cached per shape, and the run must equal
+    the one-step-per-launch run bitwise whichever launch the pick chose."""
+    from multigpu_advectiondiffusion_amd.models.base import Grid
+    from multigpu_advectiondiffusion_amd.models.diffusion import Diffusion
+    from multigpu_advectiondiffusion_amd.ops import stencil
+    from multigpu_advectiondiffusion_amd.solver import Solver
+
+    g = Grid((67, 45, 38), (1.0, 1.0, 1.0))
+    monkeypatch.delenv("ADVDIFF_STEP2", raising=False)
+    s = Solver(Diffusion(order=2), g, device="cuda")
+    picked = s.step2_capable()
+    assert isinstance(picked, bool)
+    u_after_pick = s.u.clone()
+    m = s.model
+    again = stencil.diffusion3d_step2_pick(s.u, s.un, nx=g.nx, ny=g.ny, k0=s.full[0],
+                                           k1=s.full[1], zlo=s.zact[0], zhi=s.zact[1],
+                                           border=m.border, cx=m.coef[0], cy=m.coef[1],
+                                           cz=m.coef[2], dt=m.stable_dt())
+    assert again == picked  # cached
+    s.run(iters=9, graph=True)
+    monkeypatch.setenv("ADVDIFF_STEP2", "0")
+    s0 = Solver(Diffusion(order=2), g, device="cuda")
+    assert not s0.step2_capable()
+    assert torch.equal(u_after_pick, s0.u)
+    s0.run(iters=9, graph=True)
+    assert (s.it, s.t) == (s0.it, s0.t)
+    assert torch.equal(s.owned, s0.owned), (s.owned - s0.owned).abs().max().item()
