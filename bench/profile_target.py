@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run ONE stencil kernel repeatedly (for rocprofv3 --pmc / --kernel-trace).
 
-    python bench/profile_target.py {fused,stage,burgers} [--n 512] [--reps 5]
+    python bench/profile_target.py {fused,fused2,step2x,stage,burgers,copy} [--n 512] [--reps 5]
 """
 import argparse
 import os
@@ -13,11 +13,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from multigpu_advectiondiffusion_amd.ops import stencil  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("which", choices=["fused", "fused2", "stage", "burgers", "burgers_js", "copy"])
+ap.add_argument("which", choices=["fused", "fused2", "step2x", "stage", "burgers", "burgers_js",
+                                  "copy"])
 ap.add_argument("--n", type=int, default=512)
 ap.add_argument("--reps", type=int, default=5)
 a = ap.parse_args()
-n = a.n if a.which in ("fused", "fused2", "stage", "copy") else min(a.n, 256)
+n = a.n if a.which in ("fused", "fused2", "step2x", "stage", "copy") else min(a.n, 256)
 u = torch.rand((n, n, n), dtype=torch.float64, device="cuda") * 0.5 + 0.1
 o = torch.rand_like(u)
 for _ in range(a.reps):
@@ -27,6 +28,9 @@ for _ in range(a.reps):
         R = 2 if a.which == "fused" else 1
         stencil.diffusion3d_step(u, o, nx=n, ny=n, k0=R, k1=n - R, zlo=R, zhi=n - R, border=R,
                                  order=2 * R, cx=1.0, cy=1.0, cz=1.0, dt=0.01)
+    elif a.which == "step2x":  # two FD2 steps per launch (the bench's 512^3 shape)
+        stencil.diffusion3d_step2x(u, o, nx=n, ny=n, k0=1, k1=n - 1, zlo=1, zhi=n - 1, border=1,
+                                   cx=1.0, cy=1.0, cz=1.0, dt=0.01)
     elif a.which == "stage":
         stencil.diffusion3d_stage(u, u, o, nx=n, ny=n, k0=2, k1=n - 2, border=2, order=4, cx=1.0,
                                   cy=1.0, cz=1.0, dt=0.01, a=0.75, b=0.25)
