@@ -199,16 +199,29 @@ def spawn_local(world: int, fn, *args, device: str = "cpu", backend: str | None 
     errors = []
     done = set()
     deadline = time.monotonic() + timeout
+    dead_since = None
     try:
-        for _ in range(world):
+        while len(done) < world:
             try:
-                rank, status, payload = q.get(timeout=max(deadline - time.monotonic(), 0.1))
+                rank, status, payload = q.get(timeout=1.0)
             except _queue.Empty:
                 late = [r for r in range(world) if r not in done]
-                dead = [(r, procs[r].exitcode) for r in late if not procs[r].is_alive()]
-                raise TimeoutError(f"spawn_local: ranks {late} did not finish within "
-                                   f"{timeout:g} s (exited without reporting: {dead}); "
-                                   "their stacks were dumped to stderr") from None
+                # a rank that died (signal / non-zero exit) without reporting: give the
+                # queue a short grace, then fail now instead of at the deadline (its
+                # faulthandler stack is in the captured stderr)
+                dead = [(r, procs[r].exitcode) for r in late
+                        if procs[r].exitcode not in (None, 0)]
+                if dead:
+                    dead_since = dead_since or time.monotonic()
+                    if time.monotonic() - dead_since > 3.0:
+                        raise RuntimeError(f"spawn_local: ranks {dead} (rank, exit code) died "
+                                           "without reporting; their stacks are in stderr")
+                if time.monotonic() > deadline:
+                    gone = [(r, procs[r].exitcode) for r in late if not procs[r].is_alive()]
+                    raise TimeoutError(f"spawn_local: ranks {late} did not finish within "
+                                       f"{timeout:g} s (exited without reporting: {gone}); "
+                                       "their stacks were dumped to stderr") from None
+                continue
             done.add(rank)
             if status == "ok":
                 results[rank] = payload

@@ -2,6 +2,8 @@
 errors): fail-fast launcher, fault injection, launcher timeout, NaN/Inf watchdog."""
 import time
 
+import pytest
+
 from multigpu_advectiondiffusion_amd.launch import launch
 
 ARGS = ["diffusion3d", "1", "1", "1", "1", "20", "20", "24", "400"]
@@ -54,3 +56,23 @@ def test_launcher_profile_wraps_each_rank(monkeypatch, tmp_path):
         assert cmd[0].endswith("rocprofv3") and "--kernel-trace" in cmd[:i]
         assert cmd[cmd.index("-d") + 1] == str(tmp_path / f"rank{rank}")
         assert cmd[i + 1] == __import__("sys").executable
+
+
+def _die_on_rank1(comm):
+    import os
+    if comm.rank == 1:
+        os._exit(7)  # no report, no traceback: like a segfault inside a HIP call
+    comm.barrier()  # rank 0 blocks in a collective its peer never joins
+    return comm.rank
+
+
+def test_spawn_local_reports_a_dead_rank_fast():
+    """A rank that dies without reporting (the round-4 graph-capture crash looked like a
+    240 s hang) fails spawn_local within seconds, naming the rank and its exit code."""
+    import time
+
+    from multigpu_advectiondiffusion_amd.launch import spawn_local
+    t0 = time.monotonic()
+    with pytest.raises(RuntimeError, match=r"\(1, 7\)"):
+        spawn_local(2, _die_on_rank1, timeout=120)
+    assert time.monotonic() - t0 < 60
