@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Fused FD2 heat step: tile A/B (advdiff_set_step_fd2_tile 0 = 12 waves x 3 rows, one
+workgroup per CU; 1 = 8 waves x 3 rows, two workgroups per CU), fp64, per size;
+interleaved rounds of back-to-back launches after a settling burst, min over rounds;
+bitwise comparison of one step across the tiles.
+
+    python bench/step_fd2_tile_ab.py [--sizes 384,512,640,768,1024] [--rounds 4]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from multigpu_advectiondiffusion_amd.ops import _lib, stencil  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", default="384,512,640,768,1024")
+    ap.add_argument("--dtype", default="float64")
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=8)
+    a = ap.parse_args()
+    lib = _lib.require()
+    dtype = getattr(torch, a.dtype)
+    for n in (int(v) for v in a.sizes.split(",")):
+        u = torch.rand((n, n, n), dtype=dtype, device="cuda")
+        pair = [u, u.clone()]
+        kw = dict(nx=n, ny=n, k0=1, k1=n - 1, zlo=1, zhi=n - 1, border=1, cx=1.0, cy=1.0,
+                  cz=1.0, dt=0.1, order=2, exclusive=True)
+        outs = {}
+        for t in (0, 1):
+            old = lib.advdiff_set_step_fd2_tile(t)
+            o = u.clone()
+            stencil.diffusion3d_step(u, o, **kw)
+            torch.cuda.synchronize()
+            lib.advdiff_set_step_fd2_tile(old)
+            outs[t] = o
+        same = torch.equal(outs[0], outs[1])
+        del outs
+
+        def step():
+            stencil.diffusion3d_step(pair[0], pair[1], **kw)
+            pair.reverse()
+        best = {0: float("inf"), 1: float("inf")}
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(30):
+            step()
+        for _ in range(a.rounds):
+            for t in (0, 1):
+                old = lib.advdiff_set_step_fd2_tile(t)
+                try:
+                    for _ in range(2):
+                        step()
+                    s.record()
+                    for _ in range(a.reps):
+                        step()
+                    e.record()
+                    torch.cuda.synchronize()
+                finally:
+                    lib.advdiff_set_step_fd2_tile(old)
+                best[t] = min(best[t], s.elapsed_time(e) * 1e3 / a.reps)
+        cells = (n - 2) ** 3
+        print(json.dumps({"n": n, "dtype": a.dtype, "bitwise_equal": same,
+                          "tile12x3_us": round(best[0], 1), "tile8x3_us": round(best[1], 1),
+                          "tile12x3_mlups": round(cells / best[0], 1),
+                          "tile8x3_mlups": round(cells / best[1], 1),
+                          "speedup_8x3": round(best[0] / best[1], 3)}), flush=True)
+        del u, pair
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

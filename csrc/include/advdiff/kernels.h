@@ -216,6 +216,9 @@ int advdiff_diffusion3d_step2_pick(int dtype, const void* uin, void* uout, int n
                                    double cz, double dt, void* stream, int* use2);
 // fused heat step: forced z-chunk length (0 = automatic); returns the previous setting
 int advdiff_set_step_zchunk(int zc);
+// fused FD2 step tile: 0 = 12 waves x 3 rows (default), 1 = 8 x 3 (two workgroups per CU);
+// returns the previous setting
+int advdiff_set_step_fd2_tile(int t);
 // fp32 fused heat step tile: 0 = the fp64 shapes, 3 / 4 = 16 waves x 3 / 4 rows
 int advdiff_set_step_f32_tile(int t);
 // fp32 3-D WENO5 stage: packed pairs (1, default) or one cell per lane (0); returns the

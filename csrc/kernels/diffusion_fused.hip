@@ -1022,6 +1022,17 @@ static int step_f32_tile() {
   return g_step_f32_tile;
 }
 
+// FD2 tile (ADVDIFF_STEP_FD2_TILE / advdiff_set_step_fd2_tile, round-5 A/B): 0 = 12 waves
+// x 3 rows (36 stage-1 rows, 114 KB of LDS: one workgroup per CU, 3 waves per SIMD); 1 =
+// 8 waves x 3 rows (24 rows, 77 KB: TWO workgroups per CU, 4 waves per SIMD — one
+// workgroup's barrier and LDS waits overlap the other's arithmetic, for 3.5 % more
+// stage work and shorter tiles' halo re-reads).
+static int g_step_fd2_tile = -1;
+static int step_fd2_tile() {
+  if (g_step_fd2_tile < 0) g_step_fd2_tile = knob("STEP_FD2_TILE", 0);
+  return g_step_fd2_tile;
+}
+
 template <typename T, int ORDER>
 static hipError_t dispatch_step(const SArgs& a) {
   if constexpr (sizeof(T) == 4) {
@@ -1029,10 +1040,12 @@ static hipError_t dispatch_step(const SArgs& a) {
     if (t == 3) return launch_step<T, ORDER, 16, 3, ORDER == 4 ? 3 : 23>(a);
     if (t == 4) return launch_step<T, ORDER, 16, 4, ORDER == 4 ? 3 : 23>(a);
   }
-  if constexpr (ORDER == 4)
+  if constexpr (ORDER == 4) {
     return launch_step_var<T, ORDER, 16, 2>(a);
-  else
+  } else {
+    if (step_fd2_tile() == 1) return launch_step<T, ORDER, 8, 3, 23>(a);
     return launch_step_var<T, ORDER, 12, 3>(a);
+  }
 }
 
 // two-step FD2 launch (v6_march): 12 waves x 2 rows (24 stage-1 rows, 14 output rows;
@@ -1075,6 +1088,12 @@ extern "C" int advdiff_set_step_var(int v) {
 extern "C" int advdiff_set_step_f32_tile(int t) {
   const int old = advdiff::step_f32_tile();
   advdiff::g_step_f32_tile = t;
+  return old;
+}
+
+extern "C" int advdiff_set_step_fd2_tile(int t) {
+  const int old = advdiff::step_fd2_tile();
+  advdiff::g_step_fd2_tile = t;
   return old;
 }
 
@@ -1260,6 +1279,7 @@ extern "C" int advdiff_preload_diffusion_fused(void) {
       hipFuncGetAttributes(&a, (const void*)diffusion3d_step_kernel<double, 4, 16, 2, 3>);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 4, 16, 2, 3>, 64 * 16);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 2, 12, 3, 23>, 64 * 12);
+  (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 2, 8, 3, 23>, 64 * 8);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<float, 4, 16, 2, 3>, 64 * 16);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<float, 2, 12, 3, 23>, 64 * 12);
   (void)occupancy_per_cu((const void*)diffusion3d_step2x_kernel<double, 12, 2>, 64 * 12);

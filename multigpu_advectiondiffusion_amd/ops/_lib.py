@@ -169,6 +169,8 @@ def _load():
         lib.advdiff_set_b3_ver.restype = c_int
         lib.advdiff_set_step_f32_tile.argtypes = [c_int]
         lib.advdiff_set_step_f32_tile.restype = c_int
+        lib.advdiff_set_step_fd2_tile.argtypes = [c_int]
+        lib.advdiff_set_step_fd2_tile.restype = c_int
         lib.advdiff_set_step_zchunk.argtypes = [c_int]
         lib.advdiff_set_step_zchunk.restype = c_int
         lib.advdiff_set_b3_pack.argtypes = [c_int]
