@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
-"""Fused FD2 heat step: tile A/B (advdiff_set_step_fd2_tile 0 = 12 waves x 3 rows, one
-workgroup per CU; 1 = 8 waves x 3 rows, two workgroups per CU), fp64, per size;
-interleaved rounds of back-to-back launches after a settling burst, min over rounds;
-bitwise comparison of one step across the tiles.
+"""Fused FD2 heat step: tile A/B (advdiff_set_step_fd2_tile: 0 = 12 waves x 3 rows, one
+workgroup per CU; 1 = 8 waves x 3 rows, two per CU), fp64, per size; interleaved rounds
+of back-to-back launches after a settling burst, min over rounds; bitwise comparison of
+one step across the tiles.  (An FD4 8 x 2 / 8 x 3 / 12 x 2 counterpart was not built:
+8 x 3 and 12 x 2 spill 86 / 102 VGPRs at two workgroups per CU, and 8 x 2 carries 29 %
+more stage work than 16 x 2 — after FD2 8 x 3 lost 5-13 %, profiles/r5/ab/step_tile_ab.log.)
 
-    python bench/step_fd2_tile_ab.py [--sizes 384,512,640,768,1024] [--rounds 4]
+    python bench/step_tile_ab.py [--sizes 384,512,640,768,1024] [--rounds 4]
 """
 import argparse
 import json
@@ -26,18 +28,21 @@ def main():
     a = ap.parse_args()
     lib = _lib.require()
     dtype = getattr(torch, a.dtype)
+    setter = lib.advdiff_set_step_fd2_tile
+    R = 1
+    names = ("tile12x3", "tile8x3")
     for n in (int(v) for v in a.sizes.split(",")):
         u = torch.rand((n, n, n), dtype=dtype, device="cuda")
         pair = [u, u.clone()]
-        kw = dict(nx=n, ny=n, k0=1, k1=n - 1, zlo=1, zhi=n - 1, border=1, cx=1.0, cy=1.0,
-                  cz=1.0, dt=0.1, order=2, exclusive=True)
+        kw = dict(nx=n, ny=n, k0=R, k1=n - R, zlo=R, zhi=n - R, border=R, cx=1.0, cy=1.0,
+                  cz=1.0, dt=0.05, order=2, exclusive=True)
         outs = {}
         for t in (0, 1):
-            old = lib.advdiff_set_step_fd2_tile(t)
+            old = setter(t)
             o = u.clone()
             stencil.diffusion3d_step(u, o, **kw)
             torch.cuda.synchronize()
-            lib.advdiff_set_step_fd2_tile(old)
+            setter(old)
             outs[t] = o
         same = torch.equal(outs[0], outs[1])
         del outs
@@ -51,7 +56,7 @@ def main():
             step()
         for _ in range(a.rounds):
             for t in (0, 1):
-                old = lib.advdiff_set_step_fd2_tile(t)
+                old = setter(t)
                 try:
                     for _ in range(2):
                         step()
@@ -61,14 +66,14 @@ def main():
                     e.record()
                     torch.cuda.synchronize()
                 finally:
-                    lib.advdiff_set_step_fd2_tile(old)
+                    setter(old)
                 best[t] = min(best[t], s.elapsed_time(e) * 1e3 / a.reps)
-        cells = (n - 2) ** 3
+        cells = (n - 2 * R) ** 3
         print(json.dumps({"n": n, "dtype": a.dtype, "bitwise_equal": same,
-                          "tile12x3_us": round(best[0], 1), "tile8x3_us": round(best[1], 1),
-                          "tile12x3_mlups": round(cells / best[0], 1),
-                          "tile8x3_mlups": round(cells / best[1], 1),
-                          "speedup_8x3": round(best[0] / best[1], 3)}), flush=True)
+                          f"{names[0]}_us": round(best[0], 1), f"{names[1]}_us": round(best[1], 1),
+                          f"{names[0]}_mlups": round(cells / best[0], 1),
+                          f"{names[1]}_mlups": round(cells / best[1], 1),
+                          f"speedup_{names[1]}": round(best[0] / best[1], 3)}), flush=True)
         del u, pair
         torch.cuda.empty_cache()
 

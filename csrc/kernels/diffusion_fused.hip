@@ -1025,8 +1025,9 @@ static int step_f32_tile() {
 // FD2 tile (ADVDIFF_STEP_FD2_TILE / advdiff_set_step_fd2_tile, round-5 A/B): 0 = 12 waves
 // x 3 rows (36 stage-1 rows, 114 KB of LDS: one workgroup per CU, 3 waves per SIMD); 1 =
 // 8 waves x 3 rows (24 rows, 77 KB: TWO workgroups per CU, 4 waves per SIMD — one
-// workgroup's barrier and LDS waits overlap the other's arithmetic, for 3.5 % more
-// stage work and shorter tiles' halo re-reads).
+// workgroup's barrier and LDS waits could overlap the other's arithmetic, for 3.5 % more
+// stage work and more halo re-reads).  Measured: 8 x 3 is 5-13 % SLOWER at 384^3-768^3
+// and 1.7 % faster at 1024^3 (profiles/r5/ab/step_tile_ab.log) — the default stays 12 x 3.
 static int g_step_fd2_tile = -1;
 static int step_fd2_tile() {
   if (g_step_fd2_tile < 0) g_step_fd2_tile = knob("STEP_FD2_TILE", 0);
