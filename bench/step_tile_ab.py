@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Fused FD2 heat step: tile A/B (advdiff_set_step_fd2_tile: 0 = 12 waves x 3 rows, one
-workgroup per CU; 1 = 8 waves x 3 rows, two per CU), fp64, per size; interleaved rounds
+workgroup per CU; --alt 1 = 8 waves x 3 rows, two per CU; --alt 2 = 12 waves x 4 rows,
+48-row tiles), fp64, per size; interleaved rounds
 of back-to-back launches after a settling burst, min over rounds; bitwise comparison of
 one step across the tiles.  (An FD4 8 x 2 / 8 x 3 / 12 x 2 counterpart was not built:
 8 x 3 and 12 x 2 spill 86 / 102 VGPRs at two workgroups per CU, and 8 x 2 carries 29 %
@@ -23,6 +24,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="384,512,640,768,1024")
     ap.add_argument("--dtype", default="float64")
+    ap.add_argument("--alt", type=int, default=1, help="tile to compare with 12 x 3: 1 = 8 x 3, "
+                    "2 = 12 x 4")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=8)
     a = ap.parse_args()
@@ -30,15 +33,15 @@ def main():
     dtype = getattr(torch, a.dtype)
     setter = lib.advdiff_set_step_fd2_tile
     R = 1
-    names = ("tile12x3", "tile8x3")
+    names = ("tile12x3", {1: "tile8x3", 2: "tile12x4"}[a.alt])
     for n in (int(v) for v in a.sizes.split(",")):
         u = torch.rand((n, n, n), dtype=dtype, device="cuda")
         pair = [u, u.clone()]
         kw = dict(nx=n, ny=n, k0=R, k1=n - R, zlo=R, zhi=n - R, border=R, cx=1.0, cy=1.0,
                   cz=1.0, dt=0.05, order=2, exclusive=True)
         outs = {}
-        for t in (0, 1):
-            old = setter(t)
+        for t, tv in ((0, 0), (1, a.alt)):
+            old = setter(tv)
             o = u.clone()
             stencil.diffusion3d_step(u, o, **kw)
             torch.cuda.synchronize()
@@ -55,8 +58,8 @@ def main():
         for _ in range(30):
             step()
         for _ in range(a.rounds):
-            for t in (0, 1):
-                old = setter(t)
+            for t, tv in ((0, 0), (1, a.alt)):
+                old = setter(tv)
                 try:
                     for _ in range(2):
                         step()

@@ -183,7 +183,12 @@ __device__ __forceinline__ void v3_march(
   constexpr int E = (int)sizeof(T);
   constexpr int USETB = G::USET * E, ASETB = G::ASET * E, ABB = (G::OFF_B - G::OFF_A) * E;
   static_assert(TY > 0, "tile too small");
-  static_assert(ASETB + ABB + (2 * R * W + 2 * R) * E < 65536, "A/B offsets must fit the 16-bit DS offset");
+  // The A -> B plane distance rides in the 16-bit DS immediate together with the buffer
+  // set offset; a tall tile (FD2 12 x 4: 48 rows) overflows it, and then the B planes get
+  // base registers of their own (one more VGPR per row)
+  constexpr bool SPLITB = ASETB + ABB + (2 * R * W + 2 * R) * E >= 65536;
+  constexpr int ABI = SPLITB ? 0 : ABB;  // A -> B distance carried as an immediate
+  static_assert(ASETB + ABI + (2 * R * W + 2 * R) * E < 65536, "A/B offsets must fit the 16-bit DS offset");
   static_assert(USETB + (2 * R * UW + 2 * R) * E < 65536, "u offsets must fit");
 
   const int lane = threadIdx.x;
@@ -241,7 +246,7 @@ __device__ __forceinline__ void v3_march(
   // per row: global byte offset, LDS bases (u neighbourhood top-left; A own cell; A
   // neighbourhood top-left for stages 2/3), lane masks
   uint32_t goff[RPW];
-  int ub[RPW], aw[RPW], ar[RPW];
+  int ub[RPW], aw[RPW], ar[RPW], bw[RPW], br[RPW];
   bool m1[RPW], m2[RPW], m3[RPW];
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
@@ -256,6 +261,8 @@ __device__ __forceinline__ void v3_march(
     aw[q] = (G::OFF_A + R + row * W + lane) * E;               // A own cell, set 0
     const int rc = clampi(row, R, S1R - R - 1);                 // in-bounds for masked rows
     ar[q] = (G::OFF_A + R + (rc - R) * W + lane - (XS ? 0 : R)) * E;
+    bw[q] = aw[q] + (ABB - ABI);  // B own cell / B neighbourhood (set 0, minus ABI)
+    br[q] = ar[q] + (ABB - ABI);
   }
   // PAIR: the wave's first row and its A/B-plane LDS base at row row0 - R (the lowest
   // row any of its y reads touches: immediates stay non-negative)
@@ -343,7 +350,7 @@ __device__ __forceinline__ void v3_march(
   };
   // the y-axis sum of stage 3 from the B plane of buffer set AO (LDS)
   auto s3_ysum = [&](int q, int AO) {
-    const int b = ar[q] + AO + ABB;
+    const int b = br[q] + AO + ABI;
     if constexpr (R == 2)
       return fd4_sum(ld(b + 0 * W * E), ld(b + 1 * W * E), ld(b + 3 * W * E), ld(b + 4 * W * E));
     else
@@ -401,7 +408,7 @@ __device__ __forceinline__ void v3_march(
         ru[q][UIN] = un[PF0][q];
         lds_st<T>(lb, ub[q] + UO + (R * UW + R) * E, ru[q][sl(2 * R)]);
         lds_st<T>(lb, aw[q] + AO, ra[q][sl(R)]);
-        lds_st<T>(lb, aw[q] + AO + ABB, rb[q][sl(0)]);
+        lds_st<T>(lb, bw[q] + AO + ABI, rb[q][sl(0)]);
       }
 #pragma unroll
       for (int h = 0; h < NH; ++h)  // the rim of u(k+2R)
@@ -545,7 +552,7 @@ __device__ __forceinline__ void v3_march(
           T own[RPW];
 #pragma unroll
           for (int q = 0; q < RPW; ++q) own[q] = rb[q][sl(0)];
-          ywin(yb, apb + AO + ABB, W * E, own);
+          ywin(yb, apb + (ABB - ABI) + AO + ABI, W * E, own);
         }
       }
 #pragma unroll
@@ -1028,6 +1035,8 @@ static int step_f32_tile() {
 // workgroup's barrier and LDS waits could overlap the other's arithmetic, for 3.5 % more
 // stage work and more halo re-reads).  Measured: 8 x 3 is 5-13 % SLOWER at 384^3-768^3
 // and 1.7 % faster at 1024^3 (profiles/r5/ab/step_tile_ab.log) — the default stays 12 x 3.
+// 2 = 12 waves x 4 rows (48 rows, 152 KB: fewer rim rows and halo re-reads per output,
+// B planes on their own base registers: v3_march SPLITB).
 static int g_step_fd2_tile = -1;
 static int step_fd2_tile() {
   if (g_step_fd2_tile < 0) g_step_fd2_tile = knob("STEP_FD2_TILE", 0);
@@ -1045,6 +1054,7 @@ static hipError_t dispatch_step(const SArgs& a) {
     return launch_step_var<T, ORDER, 16, 2>(a);
   } else {
     if (step_fd2_tile() == 1) return launch_step<T, ORDER, 8, 3, 23>(a);
+    if (step_fd2_tile() == 2) return launch_step<T, ORDER, 12, 4, 23>(a);
     return launch_step_var<T, ORDER, 12, 3>(a);
   }
 }
@@ -1281,6 +1291,7 @@ extern "C" int advdiff_preload_diffusion_fused(void) {
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 4, 16, 2, 3>, 64 * 16);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 2, 12, 3, 23>, 64 * 12);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 2, 8, 3, 23>, 64 * 8);
+  (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 2, 12, 4, 23>, 64 * 12);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<float, 4, 16, 2, 3>, 64 * 16);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<float, 2, 12, 3, 23>, 64 * 12);
   (void)occupancy_per_cu((const void*)diffusion3d_step2x_kernel<double, 12, 2>, 64 * 12);
