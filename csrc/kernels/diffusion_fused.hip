@@ -1035,8 +1035,11 @@ static int step_f32_tile() {
 // workgroup's barrier and LDS waits could overlap the other's arithmetic, for 3.5 % more
 // stage work and more halo re-reads).  Measured: 8 x 3 is 5-13 % SLOWER at 384^3-768^3
 // and 1.7 % faster at 1024^3 (profiles/r5/ab/step_tile_ab.log) — the default stays 12 x 3.
-// 2 = 12 waves x 4 rows (48 rows, 152 KB: fewer rim rows and halo re-reads per output,
-// B planes on their own base registers: v3_march SPLITB).
+// 2 = 12 waves x 4 rows (48 rows, 152 KB, 152 VGPRs: 13 % fewer VALU instructions per
+// output row and fewer halo re-reads; B planes on their own base registers, v3_march
+// SPLITB): +3.6 / +0.5 / -7.0 / +3.0 / +10.1 % at 384 / 512 / 640 / 768 / 1024^3 — the tile
+// quantisation decides, and where 12 x 4 wins the two-step launch wins by more
+// (profiles/r5/ab/step_tile_ab_12x4.log vs step2_sizes.log), so the default stays 12 x 3.
 static int g_step_fd2_tile = -1;
 static int step_fd2_tile() {
   if (g_step_fd2_tile < 0) g_step_fd2_tile = knob("STEP_FD2_TILE", 0);
