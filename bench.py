@@ -183,8 +183,17 @@ STRIPE = 2  # relay helpers per face message of the striped ipc slab exchange
 
 
 def solver_transport(t):
-    """(transport, stripe) of a candidate name: "ipc+stripe" = ipc with relayed parts."""
-    return ("ipc", STRIPE) if t == "ipc+stripe" else (t, 0)
+    """Solver keyword arguments of a candidate name: "ipc+stripe" = ipc with relayed parts,
+    "rccl+bc" = rccl with the boundary launch on the comm stream (the ipc default schedule;
+    rccl's default is the plain one until it has run on distinct GPUs, so the tuner times
+    both and the fingerprint check vets the opt-in one)."""
+    if t is None:
+        return {}
+    if t == "ipc+stripe":
+        return {"transport": "ipc", "stripe": STRIPE}
+    if t == "rccl+bc":
+        return {"transport": "rccl", "boundary_on_comm": True}
+    return {"transport": t}
 
 
 def transports_for(comm, want: str):
@@ -193,6 +202,8 @@ def transports_for(comm, want: str):
     if comm.size == 1 or comm.device.type != "cuda":
         return [comm.transport], None
     names = comm.transports() if want == "tune" else [want]
+    if want == "tune" and "rccl" in names:
+        names.insert(names.index("rccl") + 1, "rccl+bc")
     if want == "tune" and "ipc" in names:
         from multigpu_advectiondiffusion_amd.parallel.ipc import stripe_plan
         if any(stripe_plan(comm.size, STRIPE).values()):  # 7-8 ranks: idle links exist
@@ -377,9 +388,8 @@ def run(args):
     dt = model.stable_dt()
 
     def make_heat(p, t, m=model, c=comm):
-        tr, st = solver_transport(t) if t else (None, 0)
         return Solver(m, grid, c, dtype=torch.float64, ic="sine",
-                      overlap=not args.no_overlap, decomp=p, transport=tr, stripe=st)
+                      overlap=not args.no_overlap, decomp=p, **solver_transport(t))
 
     ashape = tuple(reversed(shape))
     if args.decomp == "tune":
@@ -416,6 +426,7 @@ def run(args):
                              f"the 1-GPU solution ({rec})")
 
     link = {"ipc": "ipc device puts", "rccl": "RCCL", "host": "host-staged",
+            "rccl+bc": "RCCL, boundary launch on the comm stream",
             "ipc+stripe": "ipc device puts striped over idle links"}.get(transport, transport)
     result = {
         "metric": METRIC,
@@ -485,9 +496,8 @@ def run(args):
         bdt = bmodel.stable_dt()
 
         def make_burgers(p, t, c=comm):
-            tr, st = solver_transport(t) if t else (None, 0)
             return Solver(bmodel, bgrid, c, dtype=torch.float64, ic="gaussian",
-                          overlap=not args.no_overlap, decomp=p, transport=tr, stripe=st)
+                          overlap=not args.no_overlap, decomp=p, **solver_transport(t))
         if args.decomp == "tune":
             bgrids = candidate_proc_grids(n, tuple(reversed(bshape)), bmodel.radius, 8)
         else:
@@ -507,10 +517,9 @@ def run(args):
             # self-check (outside the timed region): every step the timed solver took,
             # again through the fp64 PyTorch reference ops on the same decomposition
             progress(comm, f"burgers: {bsolver.it} reference steps (torch ops)")
-            tr, st = solver_transport(btransport) if btransport else (None, 0)
             ref = Solver(bmodel, bgrid, comm, dtype=torch.float64, ic="gaussian",
-                         overlap=not args.no_overlap, decomp=bdecomp, transport=tr,
-                         stripe=st, kernel="torch")
+                         overlap=not args.no_overlap, decomp=bdecomp, kernel="torch",
+                         **solver_transport(btransport))
             t_ref = time.perf_counter()
             ref.run(iters=bsolver.it, dt=bdt, graph=False)
             ref.sync_halos()

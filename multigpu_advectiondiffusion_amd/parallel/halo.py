@@ -236,7 +236,8 @@ class SlabHalo:
                     field[r0:r1].copy_(hr, non_blocking=True)
                 done = torch.cuda.Event()
                 done.record(cs)
-            torch.cuda.current_stream().wait_event(done)
+            if torch.cuda.current_stream() != cs:
+                torch.cuda.current_stream().wait_event(done)
             # keep the pinned buffers alive until the copies have run
             cs.synchronize()
 

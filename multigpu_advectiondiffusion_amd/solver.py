@@ -192,9 +192,11 @@ class Solver:
                 env = os.environ.get("ADVDIFF_BCOMM") or os.environ.get("ADVDIFF_BSTREAM")
                 boundary_on_comm = (env == "1") if env else self.transport == "ipc"
             # the boundary launch on the (high-priority) comm stream, between the wait for
-            # the halo of its input and the puts of its output: _step_fused_bcomm
-            self.bcomm = bool(boundary_on_comm and overlap and exchange == "u"
-                              and self.transport in ("ipc", "rccl"))
+            # the halo of its input and the puts of its output: _step_fused_bcomm (with the
+            # host-staged transport, gloo device tests only, the host blocks on the comm
+            # stream inside the exchange: allowed, eager only, for testing the schedule
+            # with an exchange handle that carries works like RCCL's)
+            self.bcomm = bool(boundary_on_comm and overlap and exchange == "u")
         if self.cart:
             # the fused step stacks three star stencils: it needs edge/corner ghosts too
             self.halo = CartesianHalo(comm, self.cd, self.comm_stream, corners=self.fused,

@@ -28,8 +28,14 @@ def _make(kind):
 
 
 def _run(comm, kind, steps, overlap):
+    """overlap: True / False, or "bcomm" (boundary launch on the comm stream: the schedule
+    the RCCL transport opts into with ADVDIFF_BCOMM=1 — here with the host-staged exchange,
+    whose handle carries works like RCCL's)."""
     model, grid, ic = _make(kind)
-    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, overlap=overlap)
+    bc = overlap == "bcomm"
+    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, overlap=bool(overlap),
+               boundary_on_comm=bc)
+    assert s.bcomm == bc
     s.run(iters=steps)
     g = s.gather()
     return None if g is None else g.copy()
@@ -42,14 +48,15 @@ def test_gpu_multirank_bitwise(kind, monkeypatch):
     s = Solver(model, grid, dtype=torch.float64, device="cuda", ic=ic)
     s.run(iters=5)
     ref = s.gather()
-    for world, overlap in ((2, True), (3, True), (2, False)):
+    for world, overlap in ((2, True), (3, True), (2, False), (3, "bcomm")):
         out = spawn_local(world, _run, kind, 5, overlap, device="cuda", backend="gloo")[0]
         assert np.array_equal(out, ref), (kind, world, overlap, np.abs(out - ref).max())
 
 
-def _run_cart(comm, kind, steps, decomp):
+def _run_cart(comm, kind, steps, decomp, bcomm=False):
     model, grid, ic = _make(kind)
-    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, decomp=decomp)
+    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, decomp=decomp,
+               boundary_on_comm=bcomm)
     assert s.cart
     s.run(iters=steps)
     g = s.gather()
@@ -68,8 +75,10 @@ def test_gpu_cartesian_bitwise(kind, world, decomp, monkeypatch):
     s = Solver(model, grid, dtype=torch.float64, device="cuda", ic=ic)
     s.run(iters=4)
     ref = s.gather()
-    out = spawn_local(world, _run_cart, kind, 4, decomp, device="cuda", backend="gloo")[0]
-    assert np.array_equal(out, ref), (kind, decomp, np.abs(out - ref).max())
+    for bc in (False, True):  # plain schedule, boundary boxes on the comm stream
+        out = spawn_local(world, _run_cart, kind, 4, decomp, bc, device="cuda",
+                          backend="gloo")[0]
+        assert np.array_equal(out, ref), (kind, decomp, bc, np.abs(out - ref).max())
 
 
 def test_gpu_init_ic_box_matches_torch():
