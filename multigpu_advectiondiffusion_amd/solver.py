@@ -86,11 +86,12 @@ class Solver:
         transport: halo transport of this solver ("ipc", "rccl", "host"; None = the
         Comm's, Comm.transport) — solvers with different transports can coexist on one
         Comm (bench.py tunes the transport this way).
-        boundary_on_comm (N > 1 device ranks, overlap, ipc / rccl transport): the boundary
-        launch on the COMM stream, right after the wait for the halo of its input and
-        right before the puts of its output — two streams per rank, the interior launch
-        beside the whole exchange (None = ADVDIFF_BCOMM, default off).  boundary_stream is
-        its round-4 name (that version used a third stream; see _step_fused_bcomm).
+        boundary_on_comm (N > 1 device ranks, overlap): the boundary launch on the COMM
+        stream, right after the wait for the halo of its input and right before the puts
+        of its output — two streams per rank, the interior launch beside the whole
+        exchange (None = ADVDIFF_BCOMM, else on for the ipc transport and off for rccl /
+        host).  boundary_stream is its round-4 name (that version used a third stream;
+        see _step_fused_bcomm).
         stripe: ipc slab exchanges of 3-D fields relay part of every face message through
         up to this many helper ranks over otherwise idle xGMI links (parallel/halo.py
         SlabHalo; None = ADVDIFF_STRIPE, default 0 = direct only).
