@@ -3,6 +3,8 @@
 kernels read dt from memory; steps past t_end are exact no-ops): the step sequence, the
 final time and the solution are bitwise those of the host-driven loop.  The CPU tests run
 the same logic through the torch reference ops (ops/stencil.py adaptive_dt CPU branch)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -69,4 +71,33 @@ def test_device_dt_multirank_gpu_gloo(monkeypatch):
     monkeypatch.setenv("ADVDIFF_SHARE_GPU", "1")
     ref = _solve(None, "b3", "cuda", False)
     got = spawn_local(2, _solve, "b3", "cuda", True, device="cuda", backend="gloo")[0]
+    assert got[2] == ref[2] and got[1] == ref[1] and np.array_equal(got[0], ref[0])
+
+
+def _solve_ipc(comm, kind, bcomm, decomp):
+    mk, g, ic, integ = _mk(kind)
+    s = Solver(mk(), g, comm, dtype=torch.float64, ic=ic, integrator=integ, device_dt=True,
+               transport="ipc", boundary_on_comm=bcomm, decomp=decomp)
+    assert s.bcomm == bcomm
+    st = s.run(t_end=0.07)
+    assert comm.ipc().errors() == 0
+    out = s.gather()
+    return None if out is None else (out.copy(), s.t, st.steps)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,decomp", [(2, None), (4, (2, 2, 1))])
+@pytest.mark.parametrize("bcomm", [True, False])
+def test_device_dt_multirank_gpu_ipc(world, decomp, bcomm, monkeypatch):
+    """Device dt over the peer-mapped transport, with the boundary launch on the comm
+    stream (the ipc default: it reads the dt the compute stream's reduction wrote) and
+    with the plain schedule: the same steps, time and field as the 1-rank host loop.
+    Ranks share the one GPU: the hardware-queue cap and short wait timeout of
+    tests/test_ipc_gpu.py::_shared_gpu_env apply."""
+    monkeypatch.setenv("ADVDIFF_SHARE_GPU", "1")
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", os.environ.get("ADVDIFF_TEST_HW_QUEUES", "2"))
+    monkeypatch.setenv("ADVDIFF_IPC_TIMEOUT_S", os.environ.get("ADVDIFF_IPC_TIMEOUT_S", "10"))
+    ref = _solve(None, "b3", "cuda", False)
+    got = spawn_local(world, _solve_ipc, "b3", bcomm, decomp, device="cuda", transport="ipc",
+                      timeout=100)[0]
     assert got[2] == ref[2] and got[1] == ref[1] and np.array_equal(got[0], ref[0])
