@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """fp32 fused heat step: tile A/B (advdiff_set_step_f32_tile 0 = the fp64 shapes, 3 / 4 =
-16 waves x 3 / 4 rows) at 512^3, interleaved rounds of back-to-back launches after a
+16 waves x 3 / 4 rows; the default -1 = 4 for FD4, 0 for FD2) at each --n, interleaved rounds of back-to-back launches after a
 settling run, bitwise comparison of one step across the tiles.  Effective TB/s = the
 step's compulsory 8 B/cell (read u^n + write u^{n+1}, fp32) / time.
 
-    python bench/step_fp32_ab.py [--n 512] [--rounds 4]
+    python bench/step_fp32_ab.py [--n 512 384 ...] [--rounds 4]
 """
 import argparse
 import json
@@ -19,12 +19,12 @@ from multigpu_advectiondiffusion_amd.ops import _lib, stencil  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--n", type=int, nargs="+", default=[512])
     ap.add_argument("--rounds", type=int, default=4)
     a = ap.parse_args()
     lib = _lib.require()
-    n = a.n
-    for order in (4, 2):
+    default = lib.advdiff_set_step_f32_tile(-1)
+    for n, order in [(n, o) for n in a.n for o in (4, 2)]:
         R = order // 2
         u = torch.rand((n, n, n), dtype=torch.float32, device="cuda")
         v = torch.zeros_like(u)
@@ -46,7 +46,7 @@ def main():
             stencil.diffusion3d_step(pair[0], pair[1], **kw)
             pair.reverse()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        lib.advdiff_set_step_f32_tile(0)
+        lib.advdiff_set_step_f32_tile(default)
         for _ in range(60):
             fn()
         for _ in range(a.rounds):
@@ -60,7 +60,7 @@ def main():
                 e.record()
                 torch.cuda.synchronize()
                 best[t] = min(best[t], s.elapsed_time(e) * 1e3 / 16)
-        lib.advdiff_set_step_f32_tile(0)
+        lib.advdiff_set_step_f32_tile(default)
         cells = (n - 2 * R) ** 3
         print(json.dumps({"order": order, "n": n, "bitwise_equal_across_tiles": same,
                           **{f"tile{t}_us": round(best[t], 1) for t in best},

@@ -30,11 +30,14 @@
 //   66-86)  --print (the field as rows of %8.2f, a blank line between planes: Print3D)
 //   --check-every N (NaN/Inf watchdog every N steps: a non-finite field stops every rank
 //   with an error instead of running on; eager stepping)
+//   --pitch PX,PY (pitched fields: PX extra elements per row, PY extra rows per 3-D plane;
+//   default ADVDIFF_PITCH, else 64 B + 1 row on 3-D fields past 128 MiB per rank)
 // Launch one process per GPU with torchrun-style env vars (RANK/WORLD_SIZE/LOCAL_RANK/
 // MASTER_ADDR/MASTER_PORT), e.g. via `python -m multigpu_advectiondiffusion_amd.launch`.
 #include <algorithm>
 #include <cctype>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <iostream>
@@ -152,7 +155,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
                  " [--write-ghosts FILE] [--error-norms] [--geometry] [--graph|--no-graph]"
                  " [--restart PREFIX] [--checkpoint PREFIX] [--check-every N] [--ascii FILE]"
                  " [--print] [--config FILE.json] [--style multigpu|singlegpu] [--initial FILE]"
-                 " [--json] [--warmup N]\n";
+                 " [--json] [--warmup N] [--pitch PX,PY]\n";
     return 1;
   }
   Problem p;
@@ -192,6 +195,12 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   if (opt.count("--no-overlap")) p.overlap = false;
   if (opt.count("--boundary-on-comm")) p.bcomm = 1;
   if (opt.count("--no-boundary-on-comm")) p.bcomm = 0;
+  if (opt.count("--pitch")) {
+    const std::string v = opt["--pitch"];
+    if (std::sscanf(v.c_str(), "%d,%d", &p.pitch_px, &p.pitch_py) != 2 || p.pitch_px < 0 ||
+        p.pitch_py < 0)
+      throw std::runtime_error("--pitch PX,PY (extra elements per row, extra rows per plane)");
+  }
   if (opt.count("--graph")) p.graph = 1;
   if (opt.count("--no-graph")) p.graph = 0;
   if (opt.count("--check-every")) p.check_every = std::stoi(opt["--check-every"]);

@@ -9,6 +9,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <sstream>
 
@@ -43,6 +45,29 @@ void Slab::split(int border, int radius, Range& interior, Range& blo, Range& bhi
   interior = {blo.hi, bhi_start};
 }
 
+// Pitched allocation, the rule of solver.py _pitch_pads / pitch_default (64 B more per
+// row and one more row per plane on 3-D fields past 128 MiB per rank: the fused heat step
+// +3.5 % FD4 / +4.6 % FD2 at 512^3, profiles/r5/ab/pitch_solver_ab.log).  Global
+// quantities only, so every slab rank gets the same plane layout.
+void pitch_pads(const Problem& p, int world, int elem, int* px, int* py) {
+  int x = p.pitch_px, y = p.pitch_py;
+  if (x < 0 || y < 0) {
+    const char* v = std::getenv("ADVDIFF_PITCH");
+    int ex = 0, ey = 0;
+    if (v && std::sscanf(v, "%d,%d", &ex, &ey) >= 1) {
+      x = ex;
+      y = ey;
+    } else if (p.dims == 3 && p.cells() / std::max(world, 1) * elem > (int64_t)(128 << 20)) {
+      x = std::max(64 / elem, 1);
+      y = 1;
+    } else {
+      x = y = 0;
+    }
+  }
+  *px = std::max(x, 0);
+  *py = p.dims == 3 ? std::max(y, 0) : 0;
+}
+
 static double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
@@ -57,10 +82,12 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   elem_ = p.dtype == ADVDIFF_F64 ? 8 : 4;
   const int per = 256 / (int)elem_;
   const int ax = alloc_[p.dims - 1];
-  const int sx = (ax + per - 1) / per * per;  // 256-B row pitch
+  int px = 0, py = 0;
+  pitch_pads(p, env.size, (int)elem_, &px, &py);
+  const int sx = (ax + per - 1) / per * per + px;  // 256-B row pitch (+ the pitch pad)
   sy_ = sx;
   if (p.dims == 3) {
-    sz_ = (int64_t)alloc_[1] * sx;
+    sz_ = (int64_t)(alloc_[1] + py) * sx;
     plane_bytes_ = (size_t)sz_ * elem_;
   } else {
     sz_ = sx;
@@ -737,7 +764,7 @@ std::vector<V> Engine::gather_as() {
   V* dst = (V*)packed.data();
   for (int r = 0; r < rows; ++r)
     for (int i = 0; i < p_.nx; ++i) {
-      const size_t src = (size_t)r * sy_ + i;
+      const size_t src = row_offset(r) + i;
       dst[(size_t)r * p_.nx + i] = elem_ == 8 ? (V)((const double*)raw.data())[src]
                                               : (V)((const float*)raw.data())[src];
     }
@@ -786,7 +813,7 @@ std::vector<float> Engine::gather_float32_ghosts() {
   float* dst = (float*)packed.data();
   for (int r = 0; r < rows; ++r)
     for (int i = 0; i < p_.nx; ++i) {
-      const size_t src = (size_t)r * sy_ + i;
+      const size_t src = row_offset(r) + i;
       dst[(size_t)r * p_.nx + i] = elem_ == 8 ? (float)((const double*)raw.data())[src]
                                               : ((const float*)raw.data())[src];
     }

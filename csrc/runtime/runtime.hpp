@@ -310,6 +310,10 @@ struct Problem {
   // halo and the puts of its output (-1 = ADVDIFF_BCOMM, default on for the ipc transport;
   // --boundary-on-comm / --no-boundary-on-comm)
   int bcomm = -1;
+  // pitched fields (solver.py pitch_default): extra elements per row after the 256-B
+  // alignment and extra rows per 3-D plane, never read or written (-1 = ADVDIFF_PITCH,
+  // else 64 B and one row on 3-D fields past 128 MiB per rank; --pitch PX,PY)
+  int pitch_px = -1, pitch_py = -1;
   int integrator = 0;              // 0 SSP-RK3, 1 low-storage RK4(5)
   bool fused = true;               // 3-D heat + SSP-RK3: one launch per step (3R ghosts)
   int graph = -1;                  // hipGraph stepping: -1 auto (graph-safe transports), 0, 1
@@ -326,6 +330,9 @@ struct Problem {
   int n_decomposed() const { return dims == 3 ? nz : ny; }
   int64_t cells() const { return (int64_t)nx * ny * (dims == 3 ? nz : 1); }
 };
+
+// extra elements per row / rows per 3-D plane of this problem's device fields (engine.cpp)
+void pitch_pads(const Problem& p, int world, int elem, int* px, int* py);
 
 struct Stats {
   int steps = 0;
@@ -439,6 +446,12 @@ class Engine {
   ProcEnv env_;
   Slab slab_;
   int64_t sy_ = 0, sz_ = 0;  // element pitches (2-D: sz_ = row pitch of the decomposed axis)
+  // element offset of the r-th row of a slab field counted over whole planes of p_.ny rows
+  // (3-D planes may carry padding rows: sz_ >= ny sy_)
+  size_t row_offset(int r) const {
+    return p_.dims == 3 ? (size_t)(r / p_.ny) * sz_ + (size_t)(r % p_.ny) * sy_
+                        : (size_t)r * sy_;
+  }
   size_t elem_ = 8, plane_bytes_ = 0, field_bytes_ = 0;
   // SSP-RK3: u -> A -> B -> u.  Fused step / LSRK: u <-> A ping-pong (B = du for LSRK).
   void *u_ = nullptr, *A_ = nullptr, *B_ = nullptr;

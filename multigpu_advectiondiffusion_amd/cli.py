@@ -78,6 +78,10 @@ def build_parser():
                     help="overlap: boundary launch on the comm stream between the halo wait "
                          "and the puts (default on for --transport ipc; ADVDIFF_BCOMM)")
     ap.add_argument("--no-boundary-on-comm", dest="bcomm", action="store_false")
+    ap.add_argument("--pitch", default=None, metavar="PX,PY",
+                    help="pitched device fields: PX extra elements per row, PY extra rows "
+                         "per 3-D plane (default ADVDIFF_PITCH, else 64 B + 1 row on 3-D "
+                         "fields past 128 MiB per rank; 0,0 = the 256-B row pitch only)")
     ap.add_argument("--stripe", type=int, default=None,
                     help="ipc slab halos: relay part of every face message through up to N "
                          "helper ranks over idle xGMI links (default: ADVDIFF_STRIPE or 0)")
@@ -196,7 +200,8 @@ def main(argv=None) -> int:
     solver, htod_s = fenced(lambda: Solver(
         model, grid, comm, dtype=dtype, ic=ic, overlap=not ns.no_overlap, t0=t0,
         check_every=ns.check_every, decomp=ns.decomp, integrator=ns.integrator,
-        kernel=ns.kernel, exchange=ns.exchange, stripe=ns.stripe, boundary_on_comm=ns.bcomm))
+        kernel=ns.kernel, exchange=ns.exchange, stripe=ns.stripe, boundary_on_comm=ns.bcomm,
+        pitch=None if ns.pitch is None else tuple(int(v) for v in ns.pitch.split(","))))
     if ns.geometry:  # decomposition only (no steps), one JSON line per rank in rank order
         geo = {"rank": comm.rank, "world": comm.size, "pgrid": list(solver.pgrid),
                "global_box": [list(b) for b in solver.cd.global_box()],

@@ -64,6 +64,44 @@ def _row_pitch(nx: int, elem: int, align_bytes: int = 256) -> int:
     return ((nx + per - 1) // per) * per
 
 
+def _pitch_pads(pitch, dims: int, device, elem: int = 8, cells_per_rank: int = 0) -> tuple:
+    """(extra elements per row after the 256-B alignment, extra rows per plane) of a
+    device field: `pitch` = (px, py), else ADVDIFF_PITCH="px,py", else the default rule
+    (pitch_default).  The extra rows are real rows of the tensor that no kernel reads or
+    writes (like the row padding columns), so every plane range stays one dense block
+    (zero-copy halo sends) and `clone()` keeps the layout.  2-D fields take px only; CPU
+    fields none.  The result depends on global quantities only, so every slab rank gets
+    the same plane layout (RCCL sends whole plane ranges between equal layouts)."""
+    import os
+    if torch.device(device).type != "cuda":
+        return 0, 0
+    if pitch is None:
+        env = os.environ.get("ADVDIFF_PITCH")
+        pitch = (tuple(int(v) for v in env.split(",")) if env
+                 else pitch_default(dims, elem, cells_per_rank))
+    px, py = (int(pitch[0]), int(pitch[1]) if len(pitch) > 1 else 0)
+    if px < 0 or py < 0:
+        raise ValueError(f"pitch pads must be >= 0, got {pitch}")
+    return px, (py if dims == 3 else 0)
+
+
+# Pitched allocation of 3-D device fields.  Rows of 2^k-ish byte lengths put every row of a
+# tile, and every plane of the z march, on the same HBM channels; 64 B more per row and one
+# more row per plane spread them: fused heat step at 512^3 +3.5 % (FD4) / +4.6 % (FD2),
+# 384^3-768^3 FD2 +14-22 %, bitwise the same solution (bench/pitch_ab.py,
+# bench/pitch_solver_ab.py; profiles/r5/ab/pitch_*.log).  Not below MALL_FIELD_BYTES per
+# field: at 256^3 (128 MiB fields) the two heat fields share the 256 MB Infinity Cache and
+# the padding that pushes them past it costs FD2 10 %.  Burgers: neutral (+-0.6 %).
+PITCH_PAD_BYTES = 64
+MALL_FIELD_BYTES = 128 << 20
+
+
+def pitch_default(dims: int, elem: int, cells_per_rank: int) -> tuple:
+    if dims != 3 or cells_per_rank * elem <= MALL_FIELD_BYTES:
+        return 0, 0
+    return max(PITCH_PAD_BYTES // elem, 1), 1
+
+
 class Solver:
     def __init__(self, model: Model, grid: Grid, comm: Comm | None = None, *,
                  dtype=torch.float64, device=None, ic: str = "sine", ic_params=None,
@@ -72,7 +110,8 @@ class Solver:
                  integrator: str = "ssprk3", kernel: str = "native",
                  device_dt: bool | None = None, exchange: str = "u",
                  transport: str | None = None, stripe: int | None = None,
-                 boundary_stream: bool | None = None, boundary_on_comm: bool | None = None):
+                 boundary_stream: bool | None = None, boundary_on_comm: bool | None = None,
+                 pitch=None):
         """decomp: process grid — None/"slab" (split the slowest axis only, the
         reference's layout), "auto" (smallest halo surface) or "PZxPYxPX" / a tuple in
         array axis order ((pz, py, px) in 3-D, (py, px) in 2-D).
@@ -92,6 +131,11 @@ class Solver:
         exchange (None = ADVDIFF_BCOMM, else on for the ipc transport and off for rccl /
         host).  boundary_stream is its round-4 name (that version used a third stream;
         see _step_fused_bcomm).
+        pitch: (px, py) — device fields get rows of align256(nx) + px elements and, in
+        3-D, planes of ny + py rows (the extra rows and columns are never read or written;
+        the reference's pitched-memory variants, SingleGPU/*_PitchedMem); None =
+        ADVDIFF_PITCH="px,py", else pitch_default() (64 B and one row on 3-D fields past
+        128 MiB per rank).  pad_rows=False: no padding at all.
         stripe: ipc slab exchanges of 3-D fields relay part of every face message through
         up to this many helper ranks over otherwise idle xGMI links (parallel/halo.py
         SlabHalo; None = ADVDIFF_STRIPE, default 0 = direct only).
@@ -149,7 +193,9 @@ class Solver:
         self.d = self.cd.axis(0)
         elem = torch.empty((), dtype=dtype).element_size()
         ax = self.cd.alloc[-1]
-        self.sx = _row_pitch(ax, elem) if pad_rows else ax
+        px, self.ypad = (_pitch_pads(pitch, grid.dims, self.device, elem,
+                                     grid.cells // comm.size) if pad_rows else (0, 0))
+        self.sx = _row_pitch(ax, elem) + px if pad_rows else ax
         self.ic_name, self.ic_params = ic, ic_params
         if self._ipc_multi():
             # BEFORE allocating: the peers close their mappings of any field freed since
@@ -243,7 +289,8 @@ class Solver:
         if self.device.type == "cuda":
             p = params if params is not None else ics.IC_DEFAULT_PARAMS.get(ic, (0.0, 0.0))
             if g.dims == 3:
-                u = torch.zeros((self.d.alloc, g.ny, self.sx), dtype=self.dtype, device=self.device)
+                u = torch.zeros((self.d.alloc, g.ny + self.ypad, self.sx), dtype=self.dtype,
+                                device=self.device)
                 stencil.init_ic_device(u, ics.ic_code(ic), nx=g.nx, ny=g.ny, nzl=self.d.alloc,
                                        kg0=self.d.start - G, NX=g.nx, NY=g.ny, NZ=g.nz,
                                        dx=g.spacing[0], dy=g.spacing[1], dz=g.spacing[2],
@@ -264,7 +311,9 @@ class Solver:
         ext = list(cd.alloc)
         if self.device.type == "cuda":
             p = params if params is not None else ics.IC_DEFAULT_PARAMS.get(ic, (0.0, 0.0))
-            u = torch.zeros(tuple(ext[:-1]) + (self.sx,), dtype=self.dtype, device=self.device)
+            pad = (0, self.ypad, 0) if g.dims == 3 else (0, 0)
+            u = torch.zeros(tuple(e + p for e, p in zip(ext[:-1], pad)) + (self.sx,),
+                            dtype=self.dtype, device=self.device)
             if g.dims == 3:
                 stencil.init_ic_box_device(u, ics.ic_code(ic), nx=ext[2], ny=ext[1], nzl=ext[0],
                                            ig0=offs[2], jg0=offs[1], kg0=offs[0], NX=g.nx,
@@ -900,6 +949,10 @@ class Solver:
             exact = ics.exact_solution_box(self.ic_name, self.grid.shape, self.grid.spacing,
                                            tt, K, self.ic_params, offs, list(cd.alloc),
                                            self.sx, self.dtype, self.device)
+            if self.ypad:  # the plane padding rows (never read)
+                e = torch.zeros_like(self.u)
+                e[:, :exact.shape[1]] = exact
+                exact = e
         elif tuple(exact.shape) != tuple(self.u.shape):
             raise ValueError(f"exact must have the local layout {tuple(self.u.shape)}")
         r = self.reducer()

@@ -1,7 +1,7 @@
 """Per-GPU problem sizing for 288 GB of HBM3E (MI355X).
 
-Device memory of a solver = number of resident fields × local cells (ghost planes and
-256-B row padding included) × element size; everything else (reduction workspace, halo
+Device memory of a solver = number of resident fields × local cells (ghost planes, the
+256-B row padding and the pitch pads of solver.pitch_default included) × element size; everything else (reduction workspace, halo
 pack buffers of a Cartesian grid) is negligible.  Resident fields:
 
 =============================  =======  =======================================
@@ -36,10 +36,17 @@ def row_pitch(nx: int, elem: int, align: int = 256) -> int:
     return (nx + per - 1) // per * per
 
 
-def solver_bytes(shape_local_alloc, elem: int, fields: int) -> int:
-    """Bytes of the resident fields for a local allocation (array order, last axis x)."""
+def solver_bytes(shape_local_alloc, elem: int, fields: int, pitch=None) -> int:
+    """Bytes of the resident fields for a local allocation (array order, last axis x);
+    pitch = (extra elements per row, extra rows per 3-D plane), None = the solver's
+    default rule for a rank of this many cells."""
     *outer, nx = shape_local_alloc
-    return fields * math.prod(outer) * row_pitch(nx, elem) * elem
+    if pitch is None:
+        from ..solver import pitch_default
+        pitch = pitch_default(len(shape_local_alloc), elem, math.prod(shape_local_alloc))
+    if len(outer) == 2:
+        outer = [outer[0], outer[1] + pitch[1]]
+    return fields * math.prod(outer) * (row_pitch(nx, elem) + pitch[0]) * elem
 
 
 def max_cube(mem_bytes: int = HBM_BYTES_MI355X, elem: int = 8, fields: int = 2,

@@ -55,6 +55,31 @@ def test_fused_step_bitwise_equals_per_stage(dtype, order, case):
     assert (got.cpu().double() - out).abs().max().item() < tol
 
 
+@pytest.mark.parametrize("tile", [-1, 0, 3, 4])
+@pytest.mark.parametrize("order", [4, 2])
+@pytest.mark.parametrize("case", CASES)
+def test_fused_step_fp32_tiles_bitwise(tile, order, case):
+    """Every fp32 tile (advdiff_set_step_f32_tile: -1 the per-order default — FD4 16 x 4 —,
+    0 the fp64 shapes, 16 waves x 3 / 4 rows) is bitwise the per-stage path."""
+    from multigpu_advectiondiffusion_amd.ops import _lib
+    lib = _lib.require()
+    nz, ny, nx, sx, k0, k1, zlo, zhi, border = case
+    g = torch.Generator().manual_seed(13)
+    u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).float().cuda()
+    c = (0.21, 0.17, 0.13)
+    dt = 0.9 / (2 * sum(c)) if order == 2 else 0.5 / sum(c)
+    exp = _per_stage(u, nx, ny, k0, k1, zlo, zhi, border, order, c, dt)
+    old = lib.advdiff_set_step_f32_tile(tile)
+    try:
+        got = u.clone()
+        stencil.diffusion3d_step(u, got, nx=nx, ny=ny, k0=k0, k1=k1, zlo=zlo, zhi=zhi,
+                                 border=border, order=order, cx=c[0], cy=c[1], cz=c[2], dt=dt)
+        torch.cuda.synchronize()
+    finally:
+        lib.advdiff_set_step_f32_tile(old)
+    assert torch.equal(got, exp), (got - exp).abs().max().item()
+
+
 @pytest.mark.parametrize("order", [4, 2])
 @pytest.mark.parametrize("case", CASES + [
     (200, 70, 130, 136, 3, 197, 3, 197, 3),   # many z chunks

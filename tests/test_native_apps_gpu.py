@@ -525,6 +525,44 @@ def test_native_field_memory_matches_python(tmp_path, app, args, model):
     assert rec["device_field_bytes"] == (2 if app == "diffusion3d" else 3) * s.u.numel() * 8
 
 
+@pytest.mark.parametrize("app,args,shape", [
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 50, 44, 46, 21], (46, 44, 50)),
+    ("burgers3d", [0.03, 0.3, 2.0, 2.0, 2.0, 40, 36, 41], (41, 36, 40)),
+])
+def test_native_pitched_fields_bitwise(tmp_path, app, args, shape):
+    """--pitch PX,PY (extra elements per row, extra rows per plane; engine.cpp pitch_pads):
+    one rank, 2 socket ranks and 4 ipc ranks on a 2x2x1 grid all give the unpadded 1-rank
+    result, and --json reports the padded field bytes the Python solver allocates."""
+    import json
+    ref = tmp_path / "ref.bin"
+    _run(app, args, ref, extra=["--pitch", "0,0"])
+    a = np.fromfile(ref, dtype=np.float32).reshape(shape)
+    out = tmp_path / "p.bin"
+    txt = _run(app, args, out, extra=["--pitch", "8,1", "--json"])
+    assert np.array_equal(np.fromfile(out, dtype=np.float32).reshape(shape), a)
+    rec = json.loads([ln for ln in txt.splitlines() if ln.startswith("{")][-1])
+    if app == "diffusion3d":
+        m, grid, ic = Diffusion(K=1.0, order=4), Grid(tuple(args[4:7]), (1.0,) * 3), "sine"
+    else:
+        m = Burgers(viscosity=1e-5, weno="z", cfl=0.3)
+        grid, ic = Grid(tuple(args[5:8]), (2.0,) * 3), "gaussian"
+    s = Solver(m, grid, dtype=torch.float64, device="cuda", ic=ic, pitch=(8, 1))
+    assert s.sx == 72 and s.u.shape[1] == shape[1] + 1
+    assert rec["device_field_bytes"] == s.memory_bytes(), (rec, s.memory_bytes())
+    del s
+    _run(app, args, out, world=2, extra=["--pitch", "8,1", "--transport", "socket"])
+    assert np.array_equal(np.fromfile(out, dtype=np.float32).reshape(shape), a)
+    env = dict(os.environ)
+    os.environ.update(ADVDIFF_SHARE_GPU="1", GPU_MAX_HW_QUEUES="2", ADVDIFF_IPC_TIMEOUT_S="60")
+    try:
+        _run(app, args, out, world=4, extra=["--pitch", "8,1", "--transport", "ipc",
+                                             "--decomp", "1x2x2"])
+    finally:
+        os.environ.clear()
+        os.environ.update(env)
+    assert np.array_equal(np.fromfile(out, dtype=np.float32).reshape(shape), a)
+
+
 @pytest.mark.parametrize("graph", ["--graph", "--no-graph"])
 def test_native_fd2_two_step_launch_bitwise(tmp_path, monkeypatch, graph):
     """Single-rank FD2 heat: the engine pairs its steps into two-step launches
