@@ -31,7 +31,8 @@
 //   --check-every N (NaN/Inf watchdog every N steps: a non-finite field stops every rank
 //   with an error instead of running on; eager stepping)
 //   --pitch PX,PY (pitched fields: PX extra elements per row, PY extra rows per 3-D plane;
-//   default ADVDIFF_PITCH, else 64 B + 1 row on 3-D fields past 128 MiB per rank)
+//   default ADVDIFF_PITCH, else 4 fp64 / 16 fp32 elements + 1 row on 3-D fields past
+//   128 MiB per rank)
 // Launch one process per GPU with torchrun-style env vars (RANK/WORLD_SIZE/LOCAL_RANK/
 // MASTER_ADDR/MASTER_PORT), e.g. via `python -m multigpu_advectiondiffusion_amd.launch`.
 #include <algorithm>

@@ -45,10 +45,10 @@ void Slab::split(int border, int radius, Range& interior, Range& blo, Range& bhi
   interior = {blo.hi, bhi_start};
 }
 
-// Pitched allocation, the rule of solver.py _pitch_pads / pitch_default (64 B more per
-// row and one more row per plane on 3-D fields past 128 MiB per rank: the fused heat step
-// +3.5 % FD4 / +4.6 % FD2 at 512^3, profiles/r5/ab/pitch_solver_ab.log).  Global
-// quantities only, so every slab rank gets the same plane layout.
+// Pitched allocation, the rule of solver.py _pitch_pads / pitch_default (4 fp64 / 16 fp32
+// elements more per row and one more row per plane on 3-D fields past 128 MiB per rank:
+// the fused heat step +3.8 % FD4 / +5.6 % FD2 at 512^3, profiles/r5/ab/pitch_solver_c_*.log).
+// Global quantities only, so every slab rank gets the same plane layout.
 void pitch_pads(const Problem& p, int world, int elem, int* px, int* py) {
   int x = p.pitch_px, y = p.pitch_py;
   if (x < 0 || y < 0) {
@@ -58,7 +58,7 @@ void pitch_pads(const Problem& p, int world, int elem, int* px, int* py) {
       x = ex;
       y = ey;
     } else if (p.dims == 3 && p.cells() / std::max(world, 1) * elem > (int64_t)(128 << 20)) {
-      x = std::max(64 / elem, 1);
+      x = elem == 8 ? 4 : 16;
       y = 1;
     } else {
       x = y = 0;

@@ -312,7 +312,8 @@ struct Problem {
   int bcomm = -1;
   // pitched fields (solver.py pitch_default): extra elements per row after the 256-B
   // alignment and extra rows per 3-D plane, never read or written (-1 = ADVDIFF_PITCH,
-  // else 64 B and one row on 3-D fields past 128 MiB per rank; --pitch PX,PY)
+  // else 4 fp64 / 16 fp32 elements and one row on 3-D fields past 128 MiB per rank;
+  // --pitch PX,PY)
   int pitch_px = -1, pitch_py = -1;
   int integrator = 0;              // 0 SSP-RK3, 1 low-storage RK4(5)
   bool fused = true;               // 3-D heat + SSP-RK3: one launch per step (3R ghosts)

@@ -80,8 +80,9 @@ def build_parser():
     ap.add_argument("--no-boundary-on-comm", dest="bcomm", action="store_false")
     ap.add_argument("--pitch", default=None, metavar="PX,PY",
                     help="pitched device fields: PX extra elements per row, PY extra rows "
-                         "per 3-D plane (default ADVDIFF_PITCH, else 64 B + 1 row on 3-D "
-                         "fields past 128 MiB per rank; 0,0 = the 256-B row pitch only)")
+                         "per 3-D plane (default ADVDIFF_PITCH, else 4 fp64 / 16 fp32 "
+                         "elements + 1 row on 3-D fields past 128 MiB per rank; 0,0 = the "
+                         "256-B row pitch only)")
     ap.add_argument("--stripe", type=int, default=None,
                     help="ipc slab halos: relay part of every face message through up to N "
                          "helper ranks over idle xGMI links (default: ADVDIFF_STRIPE or 0)")

@@ -85,21 +85,24 @@ def _pitch_pads(pitch, dims: int, device, elem: int = 8, cells_per_rank: int = 0
     return px, (py if dims == 3 else 0)
 
 
-# Pitched allocation of 3-D device fields.  Rows of 2^k-ish byte lengths put every row of a
-# tile, and every plane of the z march, on the same HBM channels; 64 B more per row and one
-# more row per plane spread them: fused heat step at 512^3 +3.5 % (FD4) / +4.6 % (FD2),
-# 384^3-768^3 FD2 +14-22 %, bitwise the same solution (bench/pitch_ab.py,
-# bench/pitch_solver_ab.py; profiles/r5/ab/pitch_*.log).  Not below MALL_FIELD_BYTES per
-# field: at 256^3 (128 MiB fields) the two heat fields share the 256 MB Infinity Cache and
-# the padding that pushes them past it costs FD2 10 %.  Burgers: neutral (+-0.6 %).
-PITCH_PAD_BYTES = 64
+# Pitched allocation of 3-D device fields.  Rows of 2^k elements put every row of a tile,
+# and every plane of the z march, on the same HBM channels; a few more elements per row and
+# one more row per plane spread them.  Solver-level A/B at 512^3 fp64, two processes
+# (bench/pitch_solver_ab.py, profiles/r5/ab/pitch_solver_c_*.log): FD4 640.5 -> 617.2 us
+# (+3.8 %), FD2 540.4 -> 511.6 us (+5.6 %) with 4 elements + 1 row, bitwise the same
+# solution; every pad from 2 to 24 elements lands within 1 % for FD4.  384^3-768^3 FD2
+# gains 14-22 % (pitch_sweep_sizes.log).  fp32: 16 elements + 1 row (FD4 +4.8 %, FD2
+# +10.6 %, pitch_ab_fp32.log).  Not at or below MALL_FIELD_BYTES per field: at 256^3
+# (128 MiB fields) the two heat fields share the 256 MB Infinity Cache and the padding
+# that pushes them past it costs FD2 10 %.  Burgers: neutral (+-0.6 %).
+PITCH_PAD_ELEMS = {8: 4, 4: 16}
 MALL_FIELD_BYTES = 128 << 20
 
 
 def pitch_default(dims: int, elem: int, cells_per_rank: int) -> tuple:
     if dims != 3 or cells_per_rank * elem <= MALL_FIELD_BYTES:
         return 0, 0
-    return max(PITCH_PAD_BYTES // elem, 1), 1
+    return PITCH_PAD_ELEMS.get(elem, max(32 // elem, 1)), 1
 
 
 class Solver:
@@ -134,8 +137,8 @@ class Solver:
         pitch: (px, py) — device fields get rows of align256(nx) + px elements and, in
         3-D, planes of ny + py rows (the extra rows and columns are never read or written;
         the reference's pitched-memory variants, SingleGPU/*_PitchedMem); None =
-        ADVDIFF_PITCH="px,py", else pitch_default() (64 B and one row on 3-D fields past
-        128 MiB per rank).  pad_rows=False: no padding at all.
+        ADVDIFF_PITCH="px,py", else pitch_default() (4 fp64 / 16 fp32 elements and one row
+        on 3-D fields past 128 MiB per rank).  pad_rows=False: no padding at all.
         stripe: ipc slab exchanges of 3-D fields relay part of every face message through
         up to this many helper ranks over otherwise idle xGMI links (parallel/halo.py
         SlabHalo; None = ADVDIFF_STRIPE, default 0 = direct only).

@@ -563,6 +563,23 @@ def test_native_pitched_fields_bitwise(tmp_path, app, args, shape):
     assert np.array_equal(np.fromfile(out, dtype=np.float32).reshape(shape), a)
 
 
+def test_native_default_pitch_matches_python(tmp_path, monkeypatch):
+    """Past 128 MiB per field both front ends pad by the same rule (engine.cpp pitch_pads,
+    solver.py pitch_default): equal device bytes, and equal results."""
+    import json
+    monkeypatch.delenv("ADVDIFF_PITCH", raising=False)
+    args = [1.0, 1.0, 1.0, 1.0, 260, 256, 262, 2]
+    txt = _run("diffusion3d", args, tmp_path / "big.bin", extra=["--ic", "sine", "--json"])
+    rec = json.loads([ln for ln in txt.splitlines() if ln.startswith("{")][-1])
+    s = Solver(Diffusion(K=1.0, order=4), Grid((260, 256, 262), (1.0,) * 3),
+               dtype=torch.float64, device="cuda", ic="sine")
+    assert s.ypad == 1 and s.sx == 288 + 4
+    assert rec["device_field_bytes"] == s.memory_bytes(), (rec, s.memory_bytes())
+    s.run(iters=2)
+    got = np.fromfile(tmp_path / "big.bin", dtype=np.float32).reshape(262, 256, 260)
+    assert np.array_equal(got, s.gather().astype(np.float32))
+
+
 @pytest.mark.parametrize("graph", ["--graph", "--no-graph"])
 def test_native_fd2_two_step_launch_bitwise(tmp_path, monkeypatch, graph):
     """Single-rank FD2 heat: the engine pairs its steps into two-step launches
