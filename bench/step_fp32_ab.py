@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """fp32 fused heat step: tile A/B (advdiff_set_step_f32_tile 0 = the fp64 shapes, 3 / 4 =
-16 waves x 3 / 4 rows; the default -1 = 4 for FD4, 0 for FD2) at each --n, interleaved rounds of back-to-back launches after a
+16 waves x 3 / 4 rows; default 0) at each --n, interleaved rounds of back-to-back launches after a
 settling run, bitwise comparison of one step across the tiles.  Effective TB/s = the
 step's compulsory 8 B/cell (read u^n + write u^{n+1}, fp32) / time.
 
@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     a = ap.parse_args()
     lib = _lib.require()
-    default = lib.advdiff_set_step_f32_tile(-1)
+    default = lib.advdiff_set_step_f32_tile(0)
     for n, order in [(n, o) for n in a.n for o in (4, 2)]:
         R = order // 2
         u = torch.rand((n, n, n), dtype=torch.float32, device="cuda")

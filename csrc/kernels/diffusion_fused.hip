@@ -1022,12 +1022,13 @@ static hipError_t launch_step_var(const SArgs& a) {
 // fp32 tile (ADVDIFF_STEP_F32_TILE / advdiff_set_step_f32_tile): 4-B elements halve the
 // LDS planes and the register rings, so taller tiles fit: 0 = the fp64 shapes, 3 / 4 =
 // 16 waves x 3 / 4 rows (48 / 64 stage-1 rows: fewer redundant rim rows and halo re-reads
-// per output).  -1 (the default) = per order: FD4 16 x 4, FD2 the fp64 shape — the
-// round-5 A/B (profiles/r5/ab/step_fp32_ab.log, bitwise equal across the tiles): FD4 16 x 4
-// 403 us vs 420 us at 512^3, FD2 12 x 3 370 us vs 380 / 454 us.
-static int g_step_f32_tile = -2;
+// per output).  Round-5 A/B at 256^3-1024^3 (profiles/r5/ab/step_fp32_ab.log, bitwise
+// equal across the tiles): FD4 16 x 4 is 3-4 % faster at 384^3 / 512^3 but 4-6 % slower
+// at 640^3-1024^3, 16 x 3 wins at 256^3 / 640^3 only; FD2 is fastest on the fp64 shape at
+// every size but 1024^3 — so the default stays 0 (the fp64 shapes).
+static int g_step_f32_tile = -1;
 static int step_f32_tile() {
-  if (g_step_f32_tile == -2) g_step_f32_tile = knob("STEP_F32_TILE", -1);
+  if (g_step_f32_tile < 0) g_step_f32_tile = knob("STEP_F32_TILE", 0);
   return g_step_f32_tile;
 }
 
@@ -1051,7 +1052,7 @@ static int step_fd2_tile() {
 template <typename T, int ORDER>
 static hipError_t dispatch_step(const SArgs& a) {
   if constexpr (sizeof(T) == 4) {
-    const int t = step_f32_tile() >= 0 ? step_f32_tile() : (ORDER == 4 ? 4 : 0);
+    const int t = step_f32_tile();
     if (t == 3) return launch_step<T, ORDER, 16, 3, ORDER == 4 ? 3 : 23>(a);
     if (t == 4) return launch_step<T, ORDER, 16, 4, ORDER == 4 ? 3 : 23>(a);
   }

@@ -55,12 +55,12 @@ def test_fused_step_bitwise_equals_per_stage(dtype, order, case):
     assert (got.cpu().double() - out).abs().max().item() < tol
 
 
-@pytest.mark.parametrize("tile", [-1, 0, 3, 4])
+@pytest.mark.parametrize("tile", [0, 3, 4])
 @pytest.mark.parametrize("order", [4, 2])
 @pytest.mark.parametrize("case", CASES)
 def test_fused_step_fp32_tiles_bitwise(tile, order, case):
-    """Every fp32 tile (advdiff_set_step_f32_tile: -1 the per-order default — FD4 16 x 4 —,
-    0 the fp64 shapes, 16 waves x 3 / 4 rows) is bitwise the per-stage path."""
+    """Every fp32 tile (advdiff_set_step_f32_tile: 0 the fp64 shapes, the default; 16 waves
+    x 3 / 4 rows) is bitwise the per-stage path."""
     from multigpu_advectiondiffusion_amd.ops import _lib
     lib = _lib.require()
     nz, ny, nx, sx, k0, k1, zlo, zhi, border = case
