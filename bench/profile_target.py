@@ -2,6 +2,7 @@
 """Run ONE stencil kernel repeatedly (for rocprofv3 --pmc / --kernel-trace).
 
     python bench/profile_target.py {fused,fused2,step2x,stage,burgers,copy} [--n 512] [--reps 5]
+        [--pitch PX,PY]   (fields of (n, n + PY, n + PX): the solver's pitched layout)
 """
 import argparse
 import os
@@ -17,9 +18,11 @@ ap.add_argument("which", choices=["fused", "fused2", "step2x", "stage", "burgers
                                   "copy"])
 ap.add_argument("--n", type=int, default=512)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--pitch", default="0,0")
 a = ap.parse_args()
 n = a.n if a.which in ("fused", "fused2", "step2x", "stage", "copy") else min(a.n, 256)
-u = torch.rand((n, n, n), dtype=torch.float64, device="cuda") * 0.5 + 0.1
+px, py = (int(v) for v in a.pitch.split(","))
+u = torch.rand((n, n + py, n + px), dtype=torch.float64, device="cuda") * 0.5 + 0.1
 o = torch.rand_like(u)
 for _ in range(a.reps):
     if a.which == "copy":  # calibration: exactly n^3 x 8 B read and written
