@@ -27,7 +27,11 @@ def main():
     ap.add_argument("--pads", nargs="+", default=["0,0", "8,0", "64,0", "0,1", "8,1", "0,4"])
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--orders", type=int, nargs="+", default=[4, 2])
+    ap.add_argument("--dims", type=int, default=3, choices=[2, 3],
+                    help="2: the fused 2-D step on (n, n + px) fields (py ignored)")
     a = ap.parse_args()
+    if a.dims == 2:
+        return main2d(a)
     dt_ = torch.float64 if a.dtype == "fp64" else torch.float32
     pads = [tuple(int(v) for v in p.split(",")) for p in a.pads]
     for n in a.n:
@@ -74,6 +78,53 @@ def main():
                                   "py": p[1], "row_pitch": n + p[0], "rows_per_plane": n + p[1],
                                   "us": round(best[p], 1),
                                   "mlups": round(cells / best[p], 1),
+                                  "vs_unpadded": round(best[pads[0]] / best[p], 4),
+                                  "bitwise_equal": fields[p][1]}), flush=True)
+            del fields, ref
+            torch.cuda.empty_cache()
+
+
+def main2d(a):
+    dt_ = torch.float64 if a.dtype == "fp64" else torch.float32
+    pads = sorted({int(p.split(",")[0]) for p in a.pads}, key=[int(p.split(",")[0]) for p in a.pads].index)
+    for n in a.n:
+        for order in a.orders:
+            R = order // 2
+            kw = dict(nx=n, j0=R, j1=n - R, ylo=R, yhi=n - R, border=R, order=order, cx=0.1,
+                      cy=0.1, dt=0.5)
+            g = torch.Generator(device="cuda").manual_seed(3)
+            base = torch.rand((n, n), dtype=dt_, device="cuda", generator=g)
+            fields, ref = {}, None
+            for px in pads:
+                u = torch.zeros((n, n + px), dtype=dt_, device="cuda")
+                v = torch.zeros_like(u)
+                u[:, :n] = base
+                v[:, :n] = base
+                stencil.diffusion2d_step(u, v, **kw)
+                out = v[:, :n].clone()
+                ref = out if ref is None else ref
+                fields[px] = ([u, v], torch.equal(out, ref))
+            del base
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            best = {p: float("inf") for p in pads}
+
+            def run(pair, k):
+                for _ in range(k):
+                    stencil.diffusion2d_step(pair[0], pair[1], **kw)
+                    pair.reverse()
+            run(fields[pads[0]][0], 200)
+            for _ in range(a.rounds):
+                for p in pads:
+                    run(fields[p][0], 4)
+                    s.record()
+                    run(fields[p][0], 16)
+                    e.record()
+                    torch.cuda.synchronize()
+                    best[p] = min(best[p], s.elapsed_time(e) * 1e3 / 16)
+            cells = (n - 2 * R) ** 2
+            for p in pads:
+                print(json.dumps({"dims": 2, "n": n, "order": order, "dtype": a.dtype, "px": p,
+                                  "us": round(best[p], 2), "mlups": round(cells / best[p], 1),
                                   "vs_unpadded": round(best[pads[0]] / best[p], 4),
                                   "bitwise_equal": fields[p][1]}), flush=True)
             del fields, ref
