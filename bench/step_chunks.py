@@ -5,7 +5,7 @@ interior launch [12, 128)).  Each case times the automatic chunk (pick_chunk_rou
 forced chunks, interleaved over rounds (clock drift), by HIP events over a run of
 back-to-back launches after a settling run.  Per case: us per launch and MLUPS per chunk.
 
-    python bench/step_chunks.py [--rounds 3] [--cases 512,1024,slab8]
+    python bench/step_chunks.py [--rounds 3] [--cases 512,1024,slab8] [--pitch PX,PY]
 """
 import argparse
 import json
@@ -49,14 +49,17 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--cases", default="512,1024,slab8")
     ap.add_argument("--orders", default="4,2")
+    ap.add_argument("--pitch", default="0,0",
+                    help="fields of (nz, ny + PY, nx + PX): the solver's pitched layout")
     a = ap.parse_args()
+    px, py = (int(v) for v in a.pitch.split(","))
     lib = _lib.require()
     for name in a.cases.split(","):
         for order in map(int, a.orders.split(",")):
             shape, rng, cells = case_args(name, order)
-            u = torch.rand(shape, dtype=torch.float64, device="cuda")
-            v = u.clone()
             nz, ny, nx = shape
+            u = torch.rand((nz, ny + py, nx + px), dtype=torch.float64, device="cuda")
+            v = u.clone()
             kw = dict(nx=nx, ny=ny, border=order // 2, order=order, cx=1.0, cy=1.0, cz=1.0,
                       dt=0.01, **rng)
             span = rng["k1"] - rng["k0"]
@@ -76,7 +79,7 @@ def main():
                     time_launches(fn, 4)
                     best[c] = min(best[c], time_launches(fn, 12))
             lib.advdiff_set_step_zchunk(0)
-            rec = {"case": name, "order": order, "shape": list(shape),
+            rec = {"case": name, "order": order, "shape": list(shape), "pitch": [px, py],
                    "auto_us": round(best[0], 1),
                    "auto_mlups": round(cells / best[0], 1),
                    "by_chunk_us": {str(c): round(best[c], 1) for c in chunks if c}}
