@@ -207,7 +207,8 @@ def main(argv=None) -> int:
         geo = {"rank": comm.rank, "world": comm.size, "pgrid": list(solver.pgrid),
                "global_box": [list(b) for b in solver.cd.global_box()],
                "owned_box": [list(b) for b in solver.cd.owned_box()],
-               "ghost": solver.cd.ghost}
+               "ghost": solver.cd.ghost, "row_pitch": solver.sx,
+               "rows_per_plane": int(solver.u.shape[-2]) if solver.u.dim() == 3 else None}
         if solver.cart:
             geo["halo_phases"] = [
                 [{"peer": p, "send": [list(b) for b in sb], "recv": [list(b) for b in rb],
@@ -274,7 +275,7 @@ def main(argv=None) -> int:
                 "seconds": stats.compute_s,
                 "mlups": metrics.mlups(stats.compute_s, stats.steps, grid.cells),
                 "n_procs": comm.size, "dtype": ns.dtype, "t": stats.t,
-                "device_field_bytes": solver.memory_bytes()}))
+                "device_field_bytes": solver.memory_bytes(), "row_pitch": solver.sx}))
     sys.stdout.flush()
     comm.finalize()
     return 0

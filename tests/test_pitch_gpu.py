@@ -98,3 +98,22 @@ def test_pitched_fields_host_staged_bitwise(decomp, _shared_gpu):
     got = spawn_local(2, _run, "fd4", (8, 1), 8, decomp, False, device="cuda",
                       backend="gloo", timeout=100)[0]
     assert np.array_equal(got[0], ref[0])
+
+
+@pytest.mark.gpu
+def test_cli_pitch_flag(tmp_path, capsys):
+    """The Python front end's --pitch PX,PY: same result.bin, the padded row pitch and
+    field bytes in the --json line."""
+    import json
+    from multigpu_advectiondiffusion_amd import cli
+    args = ["diffusion3d", "1", "1", "1", "1", "50", "44", "46", "9", "--ic", "sine", "--json"]
+    recs = []
+    for pitch in ("0,0", "4,1"):
+        assert cli.main(args + ["--write", str(tmp_path / f"{pitch}.bin"), "--pitch", pitch]) == 0
+        out = capsys.readouterr().out
+        recs.append(json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1]))
+    a = np.fromfile(tmp_path / "0,0.bin", dtype=np.float32)
+    b = np.fromfile(tmp_path / "4,1.bin", dtype=np.float32)
+    assert np.array_equal(a, b)
+    assert recs[1]["row_pitch"] == recs[0]["row_pitch"] + 4
+    assert recs[1]["device_field_bytes"] > recs[0]["device_field_bytes"]
