@@ -4,6 +4,7 @@ alternating launch by launch, so clock and thermal drift hit both builds alike (
 runs on this pool differ by ±5 % from the clock alone).
 
     python bench/ab_step.py LIB_A LIB_B [--n 512] [--reps 20] [--rounds 8] [--orders 4,2]
+        [--pitch PX,PY]   (fields of (n, n + PY, n + PX): the solver's pitched layout)
 """
 import argparse
 import ctypes
@@ -30,9 +31,12 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--orders", default="4,2")
+    ap.add_argument("--pitch", default="0,0")
     a = ap.parse_args()
     n = a.n
-    u = torch.rand((n, n, n), dtype=torch.float64, device="cuda")
+    px, py = (int(v) for v in a.pitch.split(","))
+    u = torch.rand((n, n + py, n + px), dtype=torch.float64, device="cuda")
+    sy, sz = u.stride(1), u.stride(0)
     outs = [torch.empty_like(u), torch.empty_like(u)]
     st = torch.cuda.current_stream().cuda_stream
     fns = [load(p) for p in a.libs]
@@ -40,7 +44,7 @@ def main():
     for order in [int(o) for o in a.orders.split(",")]:
         R = order // 2
         box = (ctypes.c_int * 8)(R, n - R, R, n - R, 0, n, 0, n)
-        args = lambda o: (1, u.data_ptr(), o.data_ptr(), n, n, n, n * n, n, R, n - R, 0, 0,  # noqa
+        args = lambda o: (1, u.data_ptr(), o.data_ptr(), n, n, sy, sz, n, R, n - R, 0, 0,  # noqa
                           R, n - R, box, order, 1.0, 1.0, 1.0, 0.01, 1, st)
         ts = [[], []]
         for _ in range(a.rounds):

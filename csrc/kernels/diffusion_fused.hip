@@ -1006,9 +1006,20 @@ static int step_var() {
   return g_step_var;
 }
 
+// (build-time override of the defaults, for A/B libraries: scripts/build_ab_libs.sh with
+// -DADVDIFF_FD4_VAR=... / -DADVDIFF_FD2_VAR=....  Re-checked on the round-5 pitched layout,
+// bench/ab_step.py --pitch 4,1, one process: FD4 VAR 19 / 23 / 7 at 0.997 / 1.020 / 1.036 x
+// the VAR 3 time, FD2 VAR 7 / 19 at 1.031 / 0.993 x VAR 23 — the defaults stand;
+// profiles/r5/ab/var_pitched_ab.log.)
+#ifndef ADVDIFF_FD4_VAR
+#define ADVDIFF_FD4_VAR 3
+#endif
+#ifndef ADVDIFF_FD2_VAR
+#define ADVDIFF_FD2_VAR 23
+#endif
 template <typename T, int ORDER, int NW, int RPW>
 static hipError_t launch_step_var(const SArgs& a) {
-  constexpr int DEF = ORDER == 4 ? 3 : 23;
+  constexpr int DEF = ORDER == 4 ? ADVDIFF_FD4_VAR : ADVDIFF_FD2_VAR;
   const int v = step_var();
   if (v < 0 || v == DEF) return launch_step<T, ORDER, NW, RPW, DEF>(a);
   if (v == 0) return launch_step<T, ORDER, NW, RPW, 0>(a);
