@@ -1010,7 +1010,9 @@ class Solver:
         self.sync_halos()
         self._sync()
         nx = self.grid.shape[0]
-        local = self.u[..., :nx].contiguous()
+        # crop the row padding and, in 3-D, the plane padding rows (pitched fields)
+        local = (self.u[:, :self.grid.shape[1], :nx] if self.grid.dims == 3
+                 else self.u[..., :nx]).contiguous()
         counts = [self.cd.axis(0, r).alloc for r in range(self.comm.size)]
         g = self.comm.gather_planes(local, counts)
         return None if g is None else g.numpy()

@@ -117,3 +117,16 @@ def test_cli_pitch_flag(tmp_path, capsys):
     assert np.array_equal(a, b)
     assert recs[1]["row_pitch"] == recs[0]["row_pitch"] + 4
     assert recs[1]["device_field_bytes"] > recs[0]["device_field_bytes"]
+
+
+@pytest.mark.gpu
+def test_pitched_fields_gather_with_ghosts():
+    """The multi-GPU result.bin layout (every slab with its ghost planes) crops the plane
+    padding rows: the same array as the dense layout."""
+    m, g, ic, _ = _case("fd4")
+    a = Solver(m, g, dtype=torch.float64, ic=ic, pitch=(0, 0))
+    b = Solver(m, g, dtype=torch.float64, ic=ic, pitch=(4, 1))
+    for s in (a, b):
+        s.run(iters=3, dt=m.stable_dt())
+    ga, gb = a.gather_with_ghosts(), b.gather_with_ghosts()
+    assert ga.shape == gb.shape and np.array_equal(ga, gb)
