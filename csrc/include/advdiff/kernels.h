@@ -219,6 +219,17 @@ int advdiff_set_step_zchunk(int zc);
 // fused FD2 step tile: 0 = 12 waves x 3 rows (default), 1 = 8 x 3 (two workgroups per CU);
 // returns the previous setting
 int advdiff_set_step_fd2_tile(int t);
+// banded z schedule of the fused step: -1 (default) the measured choice per launch
+// (advdiff_diffusion3d_step_sched_pick; uniform z chunks for an unmeasured launch), 0
+// never, 1 always; returns the previous setting
+int advdiff_set_step_banded(int on);
+// measure banded vs uniform z chunks for this fused-step launch (uin -> uout, uout is
+// scratch; synchronous, outside graph capture), cache the faster, *banded = 1 if banded
+int advdiff_diffusion3d_step_sched_pick(int dtype, const void* uin, void* uout, int nx, int ny,
+                                        int64_t sy, int64_t sz, int nz_alloc, int k0, int k1,
+                                        int zlo, int zhi, const int* box, int order, double cx,
+                                        double cy, double cz, double dt, void* stream,
+                                        int* banded);
 // fp32 fused heat step tile: 0 = the fp64 shapes, 3 / 4 = 16 waves x 3 / 4 rows
 int advdiff_set_step_f32_tile(int t);
 // fp32 3-D WENO5 stage: packed pairs (1, default) or one cell per lane (0); returns the

@@ -73,6 +73,29 @@ __device__ __forceinline__ Tile3 xcd_tile() {
   return o;
 }
 
+// The same placement for a 1-D grid of `bands` x C tiles dispatched band by band (the
+// banded z schedule of the fused heat step): block b is band b / C; within its band every
+// XCD gets a CONTIGUOUS run of the band's C logical tiles (x fastest), so each XCD holds
+// its share of every band and neighbouring tiles share its L2.
+__device__ __forceinline__ Tile3 xcd_tile_banded(int C, int gx) {
+  const int b = blockIdx.x;
+  const int band = b / C;
+  const int off = band * C;
+  const int x = b & 7;
+  int start = 0;
+  for (int xp = 0; xp < x; ++xp) {  // tiles of this band on the XCDs before x
+    const int r = (xp - off) & 7;     // first k in [0, C) with (off + k) % 8 == xp
+    start += r < C ? (C - r + 7) >> 3 : 0;
+  }
+  const int r = (x - off) & 7;
+  Tile3 o;
+  const int t = start + ((b - off - r) >> 3);
+  o.x = t % gx;
+  o.y = t / gx;
+  o.z = band;
+  return o;
+}
+
 // Second-derivative stencils. `d2` returns the UNSCALED combination; the caller folds
 // 1/(12 dx²) (FD4) or 1/dx² (FD2) into a per-axis coefficient.  Written with explicit
 // fma() and contraction off, so every kernel that evaluates a Laplacian (per-stage,

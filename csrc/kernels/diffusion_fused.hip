@@ -28,6 +28,8 @@
 #include <cstdio>
 #include <map>
 #include <mutex>
+#include <queue>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -53,6 +55,8 @@ struct StepSched {
   int gx, gy;       // tiles along x / y
   int gza, zchunk;  // chunks of the first range, planes per chunk
   int edge;         // v3: boundary-anchored edge tiles (axis_tile)
+  int zfirst = 0;   // banded schedule (> 0): a 1-D grid of gza bands x gx gy tiles, band 0
+                    // of zfirst planes, the others of zchunk (one range only)
 };
 
 // Tile placement along one axis of the v3 march (span W = 64 lanes in x, S1R rows in y;
@@ -908,11 +912,19 @@ __global__ __launch_bounds__(64 * NW) __attribute__((
     int nz_alloc, int k0, int k1, int k0b, int k1b, StepSched sc, int zlo, int zhi,
     Box2 bx, FdCoef<T> q1, FdCoef<T> q2, FdCoef<T> q3) {
   __shared__ T lds[V3Geom<T, ORDER, NW, RPW>::TOTAL];
-  const Tile3 tile = xcd_tile();
-  // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
-  const bool second = tile.z >= sc.gza;
-  const int kc0 = second ? k0b + (tile.z - sc.gza) * sc.zchunk : k0 + tile.z * sc.zchunk;
-  const int kc1 = min(kc0 + sc.zchunk, second ? k1b : k1);
+  int kc0, kc1;
+  Tile3 tile;
+  if (sc.zfirst > 0) {  // banded: one long band, then short ones fill the last rounds
+    tile = xcd_tile_banded(sc.gx * sc.gy, sc.gx);
+    kc0 = k0 + (tile.z == 0 ? 0 : sc.zfirst + (tile.z - 1) * sc.zchunk);
+    kc1 = min(kc0 + (tile.z == 0 ? sc.zfirst : sc.zchunk), k1);
+  } else {
+    tile = xcd_tile();
+    // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
+    const bool second = tile.z >= sc.gza;
+    kc0 = second ? k0b + (tile.z - sc.gza) * sc.zchunk : k0 + tile.z * sc.zchunk;
+    kc1 = min(kc0 + sc.zchunk, second ? k1b : k1);
+  }
   v3_march<T, ORDER, NW, RPW, 1, 2, true, VAR>(lds, tile.x, tile.y, sc.gx, sc.gy, sc.edge, kc0, kc1,
                                            uin, uout, nx, ny, sy, sz, nz_alloc, zlo, zhi, bx,
                                            q1, q2, q3);
@@ -924,6 +936,89 @@ static int g_step_zchunk = -1;
 static int step_zchunk() {
   if (g_step_zchunk < 0) g_step_zchunk = knob("STEP_ZCHUNK", 0);
   return g_step_zchunk;
+}
+
+// Banded z schedule: with a whole number of z chunks per column the last round of
+// resident workgroups is often part-empty (8-GPU slab rank, 1024 x 1024 x 116 interior
+// planes, FD4: 817 columns x 2 chunks = 6.4 rounds of 256).  One long band of every
+// column followed by short bands lets the dispatcher fill the last round with short
+// workgroups; the band lengths come from a list-scheduling model of one XCD's slots
+// (step_bands).  The model ignores L2 locality — workgroups of different bands run side
+// by side at different z — and misjudges the memory-bound launches (bench/banded_ab.py,
+// profiles/r5/ab/banded_ab.log: 512^3 FD4 +2.5 %, FD2 -10 %; 8-GPU slab rank FD2 +5.4 %;
+// 1024 x 512 x 256 rank FD4 -4.2 %, FD2 +10.8 %), so it runs only where it was MEASURED
+// faster for that launch (advdiff_diffusion3d_step_sched_pick, at solver / engine
+// construction).  ADVDIFF_STEP_BANDED / advdiff_set_step_banded: -1 (default) the
+// measured choice (uniform chunks for an unmeasured launch), 0 never, 1 always.  Results
+// are bitwise the same for every chunking.
+static int g_step_banded = -2;
+static int step_banded() {
+  if (g_step_banded == -2) g_step_banded = knob("STEP_BANDED", -1);
+  return g_step_banded;
+}
+
+// Makespan, in plane-times, of `cols` columns cut into bands (first of `a` planes, then
+// `nb` bands of `b`) on `slots` resident workgroups of one XCD, band-major dispatch to the
+// earliest free slot; every workgroup also pays `warm` planes of pipeline fill.
+static long long band_makespan(long long cols, int a, int nb, int b, int slots, int warm) {
+  std::priority_queue<long long, std::vector<long long>, std::greater<long long>> t;
+  for (int i = 0; i < std::max(slots, 1); ++i) t.push(0);
+  long long end = 0;
+  auto run = [&](int len, long long n) {
+    for (long long i = 0; i < n; ++i) {
+      const long long f = t.top() + len + warm;
+      t.pop();
+      t.push(f);
+      end = std::max(end, f);
+    }
+  };
+  run(a, cols);
+  for (int q = 0; q < nb; ++q) run(b, cols);
+  return end;
+}
+
+// (first band, later band length, number of bands) for n planes of `tiles` columns on
+// `slots` resident workgroups (8 XCDs), minimising the model's makespan over uniform
+// chunkings and one-long-band + uniform-short-band splits; cached per shape.
+struct Bands {
+  int zfirst, zchunk, nbands;
+};
+static Bands step_bands(int n, long long tiles, long long slots, int warm, int minc) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, long long, long long, int, int>, Bands> cache;
+  const auto key = std::make_tuple(n, tiles, slots, warm, minc);
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  const int xs = (int)std::max<long long>(slots / 8, 1);
+  const long long cols = (tiles + 7) / 8;  // one XCD's share of every band
+  Bands best{n, n, 1};
+  long long bcost = -1;
+  auto consider = [&](int a, int nb, int b) {
+    const long long c = band_makespan(cols, a, nb, b, xs, warm);
+    if (bcost < 0 || c < bcost) {
+      bcost = c;
+      best = {a, nb > 0 ? b : a, 1 + nb};
+    }
+  };
+  const int cmax = std::max(1, n / std::max(minc, 1));
+  for (int C = 1; C <= std::min(cmax, 16); ++C) {  // uniform chunks (as pick_chunk_rounds)
+    const int len = (n + C - 1) / C;
+    const int nb = (n - len + len - 1) / len;
+    consider(len, nb, len);
+  }
+  const int step = std::max(1, n / 64);
+  for (int a = minc; a < n; a += step)  // one long band + 1..3 short ones
+    for (int nb = 1; nb <= 3; ++nb) {
+      const int b = (n - a + nb - 1) / nb;
+      if (b >= std::max(4, minc / 4)) consider(a, nb, b);
+    }
+  cache[key] = best;
+  static const int log = knob("STEP_BANDS_LOG", 0);
+  if (log)
+    std::fprintf(stderr, "advdiff: fused step %d planes x %lld columns on %lld slots: bands %d + %d x %d (model %lld)\n",
+                 n, tiles, slots, best.zfirst, best.nbands - 1, best.zchunk, bcost);
+  return best;
 }
 
 static int g_step_edge = -1;
@@ -945,6 +1040,27 @@ struct SArgs {
   hipStream_t st;
 };
 
+// measured schedule per launch (key: element size, order, device, geometry, range, box)
+static std::mutex g_sched_mu;
+static std::map<std::vector<int64_t>, int> g_sched;
+static std::vector<int64_t> sched_key(int esize, int order, int nx, int ny, int64_t sy,
+                                      int64_t sz, int nz_alloc, int k0, int k1, int zlo, int zhi,
+                                      const Box2& b) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  return {esize, order, dev, nx, ny, sy, sz, nz_alloc, k0, k1, zlo, zhi,
+          b.xa0, b.xa1, b.ya0, b.ya1, b.xo0, b.xo1, b.yo0, b.yo1};
+}
+static bool sched_banded(int esize, int order, const SArgs& a) {
+  const int m = step_banded();
+  if (m >= 0) return m > 0;
+  const auto key = sched_key(esize, order, a.nx, a.ny, a.sy, a.sz, a.nz_alloc, a.k0, a.k1, a.zlo,
+                             a.zhi, a.bx);
+  std::lock_guard<std::mutex> g(g_sched_mu);
+  auto it = g_sched.find(key);
+  return it != g_sched.end() && it->second > 0;
+}
+
 template <typename T, int ORDER, int NW, int RPW, int VAR>
 static hipError_t launch_step(const SArgs& a) {
   constexpr int R = ORDER / 2;
@@ -963,11 +1079,20 @@ static hipError_t launch_step(const SArgs& a) {
   const long long slots = (long long)device_cus() * per_cu;
   StepSched sc{gx, gy, 0, 0, edge};
   const int zforce = step_zchunk();
-  const int zc = zforce > 0 ? std::min(zforce, std::max(na, nb))
-                            : pick_chunk_rounds(na + nb, (long long)gx * gy, slots, 4 * R, minc);
-  sc.gza = na > 0 ? div_up(na, zc) : 0;
-  sc.zchunk = zc;
-  const dim3 grid(gx, gy, sc.gza + (nb > 0 ? div_up(nb, zc) : 0));
+  dim3 grid;
+  if (zforce <= 0 && nb == 0 && na > 0 && sched_banded((int)sizeof(T), ORDER, a)) {
+    const Bands bd = step_bands(na, (long long)gx * gy, slots, 4 * R, minc);
+    sc.zfirst = bd.zfirst;
+    sc.zchunk = bd.zchunk;
+    sc.gza = bd.nbands;
+    grid = dim3(gx * gy * bd.nbands, 1, 1);
+  } else {
+    const int zc = zforce > 0 ? std::min(zforce, std::max(na, nb))
+                              : pick_chunk_rounds(na + nb, (long long)gx * gy, slots, 4 * R, minc);
+    sc.gza = na > 0 ? div_up(na, zc) : 0;
+    sc.zchunk = zc;
+    grid = dim3(gx, gy, sc.gza + (nb > 0 ? div_up(nb, zc) : 0));
+  }
   // SSP-RK3 stage coefficients b = 1, 1/4, 2/3: exactly the per-stage path's (FdCoef)
   const FdCoef<T> q1 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 1.0, true);
   const FdCoef<T> q2 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 0.25, true);
@@ -1113,6 +1238,12 @@ extern "C" int advdiff_set_step_var(int v) {
   return old;
 }
 
+extern "C" int advdiff_set_step_banded(int on) {
+  const int old = advdiff::step_banded();
+  advdiff::g_step_banded = on;
+  return old;
+}
+
 extern "C" int advdiff_set_step_f32_tile(int t) {
   const int old = advdiff::step_f32_tile();
   advdiff::g_step_f32_tile = t;
@@ -1210,6 +1341,71 @@ extern "C" int advdiff_diffusion3d_step2x(int dtype, const void* uin, void* uout
 // (uin -> uout only: uin is untouched, uout's output box is scratch), min per step; two
 // per launch only if it is >= 3 % faster.  ADVDIFF_STEP2=0 / 1 forces the choice.
 // Synchronous (host waits on events): call it outside any graph capture.
+// Banded or uniform z schedule for this fused-step launch, measured: interleaved rounds of
+// both schedules uin -> uout (uout is scratch), banded kept only if >= 1.5 % faster; cached
+// per launch and consulted by every later launch of it.  Synchronous: call it outside a
+// graph capture.  ADVDIFF_STEP_BANDED=0/1 forces (no measurement).
+extern "C" int advdiff_diffusion3d_step_sched_pick(int dtype, const void* uin, void* uout,
+                                                   int nx, int ny, int64_t sy, int64_t sz,
+                                                   int nz_alloc, int k0, int k1, int zlo,
+                                                   int zhi, const int* box, int order, double cx,
+                                                   double cy, double cz, double dt, void* stream,
+                                                   int* banded) {
+  using namespace advdiff;
+  if (banded == nullptr || box == nullptr || k1 <= k0) return hipErrorInvalidValue;
+  const int mode = step_banded();
+  if (mode >= 0) {
+    *banded = mode;
+    return hipSuccess;
+  }
+  const Box2 bx{box[0], box[1], box[2], box[3], box[4], box[5], box[6], box[7]};
+  const auto key = sched_key(dtype == ADVDIFF_F64 ? 8 : 4, order, nx, ny, sy, sz, nz_alloc, k0,
+                             k1, zlo, zhi, bx);
+  {
+    std::lock_guard<std::mutex> g(g_sched_mu);
+    auto it = g_sched.find(key);
+    if (it != g_sched.end()) {
+      *banded = it->second;
+      return hipSuccess;
+    }
+  }
+  hipStream_t st = (hipStream_t)stream;
+  auto launch = [&](int m) {
+    g_step_banded = m;
+    const int e = advdiff_diffusion3d_step_box_ex(dtype, uin, uout, nx, ny, sy, sz, nz_alloc, k0,
+                                                  k1, 0, 0, zlo, zhi, box, order, cx, cy, cz, dt,
+                                                  ADVDIFF_EXCLUSIVE, stream);
+    g_step_banded = -1;
+    return e;
+  };
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipError_t e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  float t[2] = {1e30f, 1e30f};
+  for (int w = 0; w < 4 && e == hipSuccess; ++w) e = (hipError_t)launch(w & 1);
+  for (int r = 0; r < 4 && e == hipSuccess; ++r)
+    for (int m = 0; m < 2 && e == hipSuccess; ++m) {
+      float ms = 0.f;
+      e = hipEventRecord(e0, st);
+      for (int q = 0; q < 3 && e == hipSuccess; ++q) e = (hipError_t)launch(m);
+      if (e == hipSuccess) e = hipEventRecord(e1, st);
+      if (e == hipSuccess) e = hipEventSynchronize(e1);
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+      if (e == hipSuccess) t[m] = std::min(t[m], ms / 3.f);
+    }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (e != hipSuccess) return e;
+  *banded = t[1] < 0.985f * t[0];
+  if (std::getenv("ADVDIFF_STEP_BANDS_LOG"))
+    std::fprintf(stderr, "advdiff: fused FD%d %dx%dx%d %s: uniform %.1f us, banded %.1f us -> %s\n",
+                 order, nx, ny, k1 - k0, dtype == ADVDIFF_F64 ? "fp64" : "fp32", t[0] * 1e3f,
+                 t[1] * 1e3f, *banded ? "banded" : "uniform");
+  std::lock_guard<std::mutex> g(g_sched_mu);
+  g_sched[key] = *banded;
+  return hipSuccess;
+}
+
 extern "C" int advdiff_diffusion3d_step2_pick(int dtype, const void* uin, void* uout, int nx,
                                               int ny, int64_t sy, int64_t sz, int nz_alloc,
                                               int k0, int k1, int zlo, int zhi, const int* box,

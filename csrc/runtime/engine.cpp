@@ -199,6 +199,23 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
     HIP_CHECK(hipStreamSynchronize(compute_));
     step2_env_ = use2 != 0;
   }
+  // banded or uniform z chunks for the fused 3-D heat launch that carries most planes (one
+  // rank: the full range; slabs: the interior launch): measured, cached in the kernel
+  // library (kernels.h advdiff_diffusion3d_step_sched_pick), before any capture
+  if (fused_ && !cart_ && p_.dims == 3 && p_.physics == Physics::Diffusion) {
+    const Range r = env_.size == 1 ? full_ : interior_;
+    if (!r.empty()) {
+      const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
+      const int B = p_.border();
+      const int box[8] = {B, p_.nx - B, B, p_.ny - B, 0, p_.nx, 0, p_.ny};
+      int banded = 0;
+      HIP_CHECK((hipError_t)advdiff_diffusion3d_step_sched_pick(
+          p_.dtype, u_, A_, p_.nx, p_.ny, sy_, sz_, slab_.alloc(), r.lo, r.hi, zact_.lo,
+          zact_.hi, box, p_.order, p_.K / (dx * dx), p_.K / (dy * dy), p_.K / (dz * dz),
+          stable_dt(), compute_, &banded));
+      HIP_CHECK(hipStreamSynchronize(compute_));
+    }
+  }
 }
 
 Engine::~Engine() {

@@ -71,6 +71,17 @@ class Diffusion(Model):
                                               cx=self.coef[0], cy=self.coef[1], cz=self.coef[2],
                                               dt=dt)
 
+    def sched_pick(self, uin, uout, lo, hi, zlo, zhi, dt, nx=None, ny=None, box=None) -> bool:
+        """Banded or uniform z chunks for this 3-D fused launch, measured on the GPU
+        (stencil.diffusion3d_step_sched_pick; uout is scratch).  2-D: nothing to pick."""
+        if self.dims != 3:
+            return False
+        g = self.grid
+        return stencil.diffusion3d_step_sched_pick(
+            uin, uout, nx=g.nx if nx is None else nx, ny=g.ny if ny is None else ny, k0=lo,
+            k1=hi, zlo=zlo, zhi=zhi, border=self.border, order=self.order, cx=self.coef[0],
+            cy=self.coef[1], cz=self.coef[2], dt=dt, box=box)
+
     def step2(self, uin, uout, lo, hi, zlo, zhi, dt, stream=None):
         """Two fused RK3 steps on planes [lo, hi) of a whole (one-rank) field."""
         g = self.grid

@@ -43,6 +43,10 @@ _SIGS = {
     "advdiff_diffusion3d_step2_pick": [c_int, c_vp, c_vp, c_int, c_int, c_i64, c_i64, c_int,
                                        c_int, c_int, c_int, c_int, ctypes.POINTER(c_int), c_dbl,
                                        c_dbl, c_dbl, c_dbl, c_vp, ctypes.POINTER(c_int)],
+    "advdiff_diffusion3d_step_sched_pick": [c_int, c_vp, c_vp, c_int, c_int, c_i64, c_i64,
+                                            c_int, c_int, c_int, c_int, c_int,
+                                            ctypes.POINTER(c_int), c_int, c_dbl, c_dbl, c_dbl,
+                                            c_dbl, c_vp, ctypes.POINTER(c_int)],
     "advdiff_diffusion3d_step_box": [c_int, c_vp, c_vp, c_int, c_int, c_i64, c_i64, c_int,
                                      c_int, c_int, c_int, c_int, c_int, c_int,
                                      ctypes.POINTER(c_int), c_int, c_dbl, c_dbl, c_dbl, c_dbl,
@@ -171,6 +175,9 @@ def _load():
         lib.advdiff_set_step_f32_tile.restype = c_int
         lib.advdiff_set_step_fd2_tile.argtypes = [c_int]
         lib.advdiff_set_step_fd2_tile.restype = c_int
+        lib.advdiff_set_step_banded.argtypes = [c_int]
+        lib.advdiff_set_step_banded.restype = c_int
+
         lib.advdiff_set_step_zchunk.argtypes = [c_int]
         lib.advdiff_set_step_zchunk.restype = c_int
         lib.advdiff_set_b3_pack.argtypes = [c_int]

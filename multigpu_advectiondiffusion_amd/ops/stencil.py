@@ -158,6 +158,27 @@ def diffusion3d_step2_pick(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, cx, c
     return bool(use2.value)
 
 
+def diffusion3d_step_sched_pick(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx,
+                                cy, cz, dt, stream=None, box=None) -> bool:
+    """Measure the banded against the uniform z schedule of this fused-step launch
+    (advdiff_diffusion3d_step_sched_pick: uin -> uout, uout is scratch; synchronous, call
+    it outside a graph capture) and keep the faster for every later launch of it.  True
+    if banded.  Not a native device field: False (nothing to pick)."""
+    if not _native(uin):
+        return False
+    _check_layout(uin, uout)
+    if box is None:
+        box = (border, nx - border, border, ny - border, 0, nx, 0, ny)
+    lib = _lib.require()
+    out = ctypes.c_int(0)
+    code = lib.advdiff_diffusion3d_step_sched_pick(
+        _dtype_code(uin), _ptr(uin), _ptr(uout), nx, ny, uin.stride(1), uin.stride(0),
+        uin.shape[0], k0, k1, zlo, zhi, _int_array(box), order, cx, cy, cz, dt,
+        _stream_ptr(stream), ctypes.byref(out))
+    _lib.check(code, "diffusion3d_step_sched_pick")
+    return bool(out.value)
+
+
 def diffusion3d_step2x(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, cx, cy, cz, dt,
                        stream=None, box=None):
     """TWO FD2 SSP-RK3 steps in one launch (diffusion_fused.hip v6_march): uout[k0:k1] =

@@ -274,6 +274,7 @@ class Solver:
         self.device_dt = bool(device_dt) and model.needs_umax and exchange == "u"
         self._step2_on = False
         self._step2_on = self._pick_step2()
+        self._pick_sched()
 
     def _ipc_multi(self) -> bool:
         return (self.device.type == "cuda" and self.comm.size > 1
@@ -591,6 +592,34 @@ class Solver:
         (measured once per shape on the GPU at construction: _pick_step2)."""
         return (self.fused and self.comm.size == 1 and not self.cart and self.du is None
                 and self.model.supports_step2 and self._dt_dev is None and self._step2_on)
+
+    def _pick_sched(self) -> None:
+        """Banded or uniform z chunks for the fused 3-D launch that carries most planes (one
+        rank: the full range; several: the interior range or box), measured once per launch
+        shape on the GPU before any graph capture (diffusion_fused.hip step_bands; the
+        kernel library caches the choice; ADVDIFF_STEP_BANDED=0/1 forces)."""
+        if not (self.fused and self.grid.dims == 3 and self.kernel == "native"
+                and self.device.type == "cuda" and hasattr(self.model, "sched_pick")):
+            return
+        dt = self.model.stable_dt() if not self.model.needs_umax else 0.0
+        if self.comm.size == 1:
+            rng = self.full
+        else:
+            rng = self.interior
+        if self.cart:
+            box = rng
+            if any(hi <= lo for lo, hi in box):
+                return
+            (z0, z1), (y0, y1), (x0, x1) = box
+            (vy0, vy1), (ya0, ya1), (yo0, yo1) = self._fused_view(1, y0, y1)
+            (vx0, vx1), (xa0, xa1), (xo0, xo1) = self._fused_view(2, x0, x1)
+            sl = (slice(None), slice(vy0, vy1), slice(vx0, vx1))
+            self.model.sched_pick(self.u[sl], self.un[sl], z0, z1, self.zact[0], self.zact[1],
+                                  dt, nx=vx1 - vx0, ny=vy1 - vy0,
+                                  box=(xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1))
+        elif rng[1] > rng[0]:
+            self.model.sched_pick(self.u, self.un, rng[0], rng[1], self.zact[0], self.zact[1],
+                                  dt)
 
     def _pick_step2(self) -> bool:
         """One FD2 step or two per launch, decided before any graph capture: two per

@@ -83,6 +83,37 @@ def test_fused_step_fp32_tiles_bitwise(tile, order, case):
 @pytest.mark.parametrize("order", [4, 2])
 @pytest.mark.parametrize("case", CASES + [
     (200, 70, 130, 136, 3, 197, 3, 197, 3),   # many z chunks
+    (140, 200, 300, 304, 12, 128, 0, 140, 2),  # a slab rank's interior launch
+])
+def test_fused_step_banded_schedule_bitwise(order, case):
+    """The banded z schedule (one long band, short bands after it: advdiff_set_step_banded,
+    the default) is bitwise the uniform z chunks and the per-stage path."""
+    from multigpu_advectiondiffusion_amd.ops import _lib
+    lib = _lib.require()
+    nz, ny, nx, sx, k0, k1, zlo, zhi, border = case
+    g = torch.Generator().manual_seed(17)
+    u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).cuda()
+    c = (0.21, 0.17, 0.13)
+    dt = 0.9 / (2 * sum(c)) if order == 2 else 0.5 / sum(c)
+    exp = _per_stage(u, nx, ny, k0, k1, zlo, zhi, border, order, c, dt)
+    got = {}
+    for m in (0, 1):
+        old = lib.advdiff_set_step_banded(m)
+        try:
+            o = u.clone()
+            stencil.diffusion3d_step(u, o, nx=nx, ny=ny, k0=k0, k1=k1, zlo=zlo, zhi=zhi,
+                                     border=border, order=order, cx=c[0], cy=c[1], cz=c[2],
+                                     dt=dt)
+            torch.cuda.synchronize()
+            got[m] = o
+        finally:
+            lib.advdiff_set_step_banded(old)
+    assert torch.equal(got[0], exp) and torch.equal(got[1], exp)
+
+
+@pytest.mark.parametrize("order", [4, 2])
+@pytest.mark.parametrize("case", CASES + [
+    (200, 70, 130, 136, 3, 197, 3, 197, 3),   # many z chunks
 ])
 def test_fused_step_two_ranges_bitwise(order, case):
     """Two plane ranges in one launch (a slab rank's two boundary slabs) == two launches,
@@ -368,3 +399,30 @@ def test_step2_pick_measured_leaves_u_and_results(monkeypatch):
     s0.run(iters=9, graph=True)
     assert (s.it, s.t) == (s0.it, s0.t)
     assert torch.equal(s.owned, s0.owned), (s.owned - s0.owned).abs().max().item()
+
+
+@pytest.mark.parametrize("order", [4, 2])
+def test_sched_pick_measured_and_bitwise(order):
+    """The solver measures banded vs uniform z chunks for its fused launch at construction
+    (advdiff_diffusion3d_step_sched_pick, u -> un only; cached per launch); whichever it
+    keeps, the run equals the uniform-chunk run bitwise, and u is untouched by the pick."""
+    from multigpu_advectiondiffusion_amd.models.base import Grid
+    from multigpu_advectiondiffusion_amd.models.diffusion import Diffusion
+    from multigpu_advectiondiffusion_amd.ops import _lib
+    from multigpu_advectiondiffusion_amd.solver import Solver
+    lib = _lib.require()
+    g = Grid((131, 97, 140), (1.0, 1.0, 1.0))
+    ref = Solver(Diffusion(order=order), g, device="cuda", ic="sine")
+    u0 = ref.u.clone()
+    old = lib.advdiff_set_step_banded(0)
+    try:
+        ref.run(iters=7, graph=False)
+    finally:
+        lib.advdiff_set_step_banded(old)
+    s = Solver(Diffusion(order=order), g, device="cuda", ic="sine")
+    assert torch.equal(s.u, u0)  # the pick wrote un only
+    m = s.model
+    again = m.sched_pick(s.u, s.un, s.full[0], s.full[1], s.zact[0], s.zact[1], m.stable_dt())
+    assert isinstance(again, bool)
+    s.run(iters=7, graph=False)
+    assert torch.equal(s.owned, ref.owned)
