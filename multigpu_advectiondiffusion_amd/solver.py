@@ -499,8 +499,9 @@ class Solver:
         """View window, active and output bounds along array axis a (decomposition.fused_view)."""
         return fused_view(self.cd, self.model.radius, self.model.border, a, lo, hi)
 
-    def _launch_fused_box(self, box, dt, exclusive=False):
-        """Fused step of a Cartesian block box (array order) on a kernel VIEW."""
+    def _launch_fused_box(self, box, dt, exclusive=False, pick=False):
+        """Fused step of a Cartesian block box (array order) on a kernel VIEW.  pick: measure
+        the launch's z schedule instead of stepping (3-D; _pick_sched)."""
         if any(hi <= lo for lo, hi in box):
             return
         if self.grid.dims == 3:
@@ -508,9 +509,13 @@ class Solver:
             (vy0, vy1), (ya0, ya1), (yo0, yo1) = self._fused_view(1, y0, y1)
             (vx0, vx1), (xa0, xa1), (xo0, xo1) = self._fused_view(2, x0, x1)
             sl = (slice(None), slice(vy0, vy1), slice(vx0, vx1))
+            vbox = (xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1)
+            if pick:
+                self.model.sched_pick(self.u[sl], self.un[sl], z0, z1, self.zact[0],
+                                      self.zact[1], dt, nx=vx1 - vx0, ny=vy1 - vy0, box=vbox)
+                return
             self.model.step(self.u[sl], self.un[sl], z0, z1, self.zact[0], self.zact[1], dt,
-                            nx=vx1 - vx0, ny=vy1 - vy0,
-                            box=(xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1), exclusive=exclusive)
+                            nx=vx1 - vx0, ny=vy1 - vy0, box=vbox, exclusive=exclusive)
         else:
             (y0, y1), (x0, x1) = box
             (vx0, vx1), (xa0, xa1), (xo0, xo1) = self._fused_view(1, x0, x1)
@@ -602,21 +607,9 @@ class Solver:
                 and self.device.type == "cuda" and hasattr(self.model, "sched_pick")):
             return
         dt = self.model.stable_dt() if not self.model.needs_umax else 0.0
-        if self.comm.size == 1:
-            rng = self.full
-        else:
-            rng = self.interior
+        rng = self.full if self.comm.size == 1 else self.interior
         if self.cart:
-            box = rng
-            if any(hi <= lo for lo, hi in box):
-                return
-            (z0, z1), (y0, y1), (x0, x1) = box
-            (vy0, vy1), (ya0, ya1), (yo0, yo1) = self._fused_view(1, y0, y1)
-            (vx0, vx1), (xa0, xa1), (xo0, xo1) = self._fused_view(2, x0, x1)
-            sl = (slice(None), slice(vy0, vy1), slice(vx0, vx1))
-            self.model.sched_pick(self.u[sl], self.un[sl], z0, z1, self.zact[0], self.zact[1],
-                                  dt, nx=vx1 - vx0, ny=vy1 - vy0,
-                                  box=(xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1))
+            self._launch_fused_box(rng, dt, pick=True)
         elif rng[1] > rng[0]:
             self.model.sched_pick(self.u, self.un, rng[0], rng[1], self.zact[0], self.zact[1],
                                   dt)
