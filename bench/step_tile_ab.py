@@ -28,14 +28,16 @@ def main():
                     "2 = 12 x 4")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--pitch", default="0,0", help="fields of (n, n + PY, n + PX)")
     a = ap.parse_args()
+    px, py = (int(v) for v in a.pitch.split(","))
     lib = _lib.require()
     dtype = getattr(torch, a.dtype)
     setter = lib.advdiff_set_step_fd2_tile
     R = 1
     names = ("tile12x3", {1: "tile8x3", 2: "tile12x4"}[a.alt])
     for n in (int(v) for v in a.sizes.split(",")):
-        u = torch.rand((n, n, n), dtype=dtype, device="cuda")
+        u = torch.rand((n, n + py, n + px), dtype=dtype, device="cuda")
         pair = [u, u.clone()]
         kw = dict(nx=n, ny=n, k0=R, k1=n - R, zlo=R, zhi=n - R, border=R, cx=1.0, cy=1.0,
                   cz=1.0, dt=0.05, order=2, exclusive=True)

@@ -176,8 +176,30 @@ template <typename T, int ORDER, int NW, int RPW, int XS, int PF, bool SEP, int 
 __device__ __forceinline__ void v3_march(
     T* lds, int tx, int ty, int gx, int gy, int edge, int kc0, int kc1,
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
-    int nz_alloc, int zlo, int zhi, const Box2& bx, const FdCoef<T>& q1, const FdCoef<T>& q2,
-    const FdCoef<T>& q3) {
+    int nz_alloc, int zlo, int zhi, const Box2& bx, const FdCoef<T>& q1a, const FdCoef<T>& q2a,
+    const FdCoef<T>& q3a) {
+  // fp64: the stage-1 coefficients live in VGPRs (a "+v" asm operand makes the uniform
+  // values look divergent; 8 more VGPRs, same occupancy).  With all twelve fp64
+  // coefficients in SGPRs the kernel needs 106 SGPRs and the compiler spills them into
+  // VGPR lanes: 20 v_readlane reloads per plane of the FD4 march (148 -> 128 VALU per
+  // plane without them).  FD4 512^3 642 -> 614 us, bitwise the same (in-process A/B,
+  // profiles/r5/ab/vcoef_ab.log; stage 3 instead of 1: the same).  fp32 keeps SGPRs (no
+  // spill there, and 4 more VGPRs would cost the 16 x 2 tile its second workgroup per CU).
+  // ADVDIFF_VCOEF (build time, bit s-1 = stage s) overrides for A/B libraries.
+#ifndef ADVDIFF_VCOEF
+#define ADVDIFF_VCOEF 1
+#endif
+  FdCoef<T> q1 = q1a, q2 = q2a, q3 = q3a;
+  auto to_v = [](FdCoef<T>& c) {
+    asm volatile("" : "+v"(c.kc));
+#pragma unroll
+    for (int d = 0; d < 3; ++d) asm volatile("" : "+v"(c.k[d]));
+  };
+  if constexpr (sizeof(T) == 8) {
+    if constexpr ((ADVDIFF_VCOEF & 1) != 0) to_v(q1);
+    if constexpr ((ADVDIFF_VCOEF & 2) != 0) to_v(q2);
+    if constexpr ((ADVDIFF_VCOEF & 4) != 0) to_v(q3);
+  }
   using G = V3Geom<T, ORDER, NW, RPW>;
   constexpr int R = G::R, NR = 2 * R + 1, W = G::W, S1R = G::S1R, UW = G::UW, UH = G::UH;
   constexpr int TX = W - 4 * R, TY = S1R - 4 * R;
@@ -622,8 +644,15 @@ template <typename T, int NW, int RPW>
 __device__ __forceinline__ void v6_march(
     T* lds, int tx, int ty, int gx, int gy, int edge, int kc0, int kc1,
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
-    int nz_alloc, int zlo, int zhi, const Box2& bx, const FdCoef<T>& q1, const FdCoef<T>& q2,
+    int nz_alloc, int zlo, int zhi, const Box2& bx, const FdCoef<T>& q1a, const FdCoef<T>& q2,
     const FdCoef<T>& q3) {
+  // fp64: stage-1 coefficients in VGPRs, as in v3_march (no SGPR spill reloads)
+  FdCoef<T> q1 = q1a;
+  if constexpr (sizeof(T) == 8 && (ADVDIFF_VCOEF & 1) != 0) {
+    asm volatile("" : "+v"(q1.kc));
+#pragma unroll
+    for (int d = 0; d < 3; ++d) asm volatile("" : "+v"(q1.k[d]));
+  }
   using G = V6Geom<T, NW, RPW>;
   constexpr int R = 1, W = G::W, S1R = G::S1R, UW = G::UW, UH = G::UH, NR = 4, PF = 2;
   constexpr int SH = 5 * R;  // interior output shrink per side
