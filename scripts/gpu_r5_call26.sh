@@ -3,10 +3,10 @@
 set -o pipefail
 mkdir -p gpurun_out/r5
 L=bench/ab_libs
-: > gpurun_out/r5/vcoef_ab.log
-for v in vc1 vc4; do
+: > gpurun_out/r5/vcoef_ab2.log
+for v in vc3 vc5; do
   timeout -k 10 200 python -u bench/ab_step.py $L/base.so $L/$v.so --pitch 4,1 --rounds 10 > gpurun_out/r5/ab_$v.log 2>&1 || { cat gpurun_out/r5/ab_$v.log; exit 1; }
-  echo "$v $(tail -1 gpurun_out/r5/ab_$v.log)" >> gpurun_out/r5/vcoef_ab.log
+  echo "$v $(tail -1 gpurun_out/r5/ab_$v.log)" >> gpurun_out/r5/vcoef_ab2.log
 done
-timeout -k 10 200 python -u bench/ab_step.py $L/vc1.so $L/base.so --pitch 4,1 --rounds 10 > gpurun_out/r5/ab_vc1_rev.log 2>&1 && echo "vc1-rev $(tail -1 gpurun_out/r5/ab_vc1_rev.log)" >> gpurun_out/r5/vcoef_ab.log
-cat gpurun_out/r5/vcoef_ab.log
+
+cat gpurun_out/r5/vcoef_ab2.log
