@@ -1208,6 +1208,9 @@ static int step_f32_tile() {
 // SPLITB): +3.6 / +0.5 / -7.0 / +3.0 / +10.1 % at 384 / 512 / 640 / 768 / 1024^3 — the tile
 // quantisation decides, and where 12 x 4 wins the two-step launch wins by more
 // (profiles/r5/ab/step_tile_ab_12x4.log vs step2_sizes.log), so the default stays 12 x 3.
+// (FD4 12 waves x 3 rows re-checked after the round-5 SGPR fix: 161 VGPRs at 3 waves per
+// SIMD, 45 spill reloads left; 0.94 / 0.99 / 0.96 x the 16 x 2 speed at 384 / 512 /
+// 768^3 on pitched fields, bitwise equal — profiles/r5/ab/fd4_tile_ab.log; removed.)
 static int g_step_fd2_tile = -1;
 static int step_fd2_tile() {
   if (g_step_fd2_tile < 0) g_step_fd2_tile = knob("STEP_FD2_TILE", 0);
