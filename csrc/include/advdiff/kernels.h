@@ -223,6 +223,8 @@ int advdiff_set_step_fd2_tile(int t);
 // (advdiff_diffusion3d_step_sched_pick; uniform z chunks for an unmeasured launch), 0
 // never, 1 always; returns the previous setting
 int advdiff_set_step_banded(int on);
+// force the banded split (first band, later bands) of banded launches; first <= 0: the model
+void advdiff_set_step_bands(int first, int rest);
 // measure banded vs uniform z chunks for this fused-step launch (uin -> uout, uout is
 // scratch; synchronous, outside graph capture), cache the faster, *banded = 1 if banded
 int advdiff_diffusion3d_step_sched_pick(int dtype, const void* uin, void* uout, int nx, int ny,

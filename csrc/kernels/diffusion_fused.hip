@@ -980,6 +980,7 @@ static int step_zchunk() {
 // construction).  ADVDIFF_STEP_BANDED / advdiff_set_step_banded: -1 (default) the
 // measured choice (uniform chunks for an unmeasured launch), 0 never, 1 always.  Results
 // are bitwise the same for every chunking.
+static int g_band_force[2] = {0, 0};  // forced (first band, later bands) for sweeps; 0 = model
 static int g_step_banded = -2;
 static int step_banded() {
   if (g_step_banded == -2) g_step_banded = knob("STEP_BANDED", -1);
@@ -1110,7 +1111,12 @@ static hipError_t launch_step(const SArgs& a) {
   const int zforce = step_zchunk();
   dim3 grid;
   if (zforce <= 0 && nb == 0 && na > 0 && sched_banded((int)sizeof(T), ORDER, a)) {
-    const Bands bd = step_bands(na, (long long)gx * gy, slots, 4 * R, minc);
+    Bands bd = step_bands(na, (long long)gx * gy, slots, 4 * R, minc);
+    if (g_band_force[0] > 0) {  // forced split (advdiff_set_step_bands; band sweeps)
+      bd.zfirst = std::min(g_band_force[0], na);
+      bd.zchunk = std::max(g_band_force[1], 1);
+      bd.nbands = 1 + div_up(na - bd.zfirst, bd.zchunk);
+    }
     sc.zfirst = bd.zfirst;
     sc.zchunk = bd.zchunk;
     sc.gza = bd.nbands;
@@ -1268,6 +1274,13 @@ extern "C" int advdiff_set_step_var(int v) {
   const int old = advdiff::step_var();
   advdiff::g_step_var = v;
   return old;
+}
+
+// Force the banded split (first band, later band length) of banded launches; first <= 0
+// returns to the model's split (step_bands).  For band sweeps (bench/band_sweep.py).
+extern "C" void advdiff_set_step_bands(int first, int rest) {
+  advdiff::g_band_force[0] = first;
+  advdiff::g_band_force[1] = rest;
 }
 
 extern "C" int advdiff_set_step_banded(int on) {

@@ -175,6 +175,8 @@ def _load():
         lib.advdiff_set_step_f32_tile.restype = c_int
         lib.advdiff_set_step_fd2_tile.argtypes = [c_int]
         lib.advdiff_set_step_fd2_tile.restype = c_int
+        lib.advdiff_set_step_bands.argtypes = [c_int, c_int]
+        lib.advdiff_set_step_bands.restype = None
         lib.advdiff_set_step_banded.argtypes = [c_int]
         lib.advdiff_set_step_banded.restype = c_int
 
