@@ -225,6 +225,10 @@ int advdiff_set_step_fd2_tile(int t);
 int advdiff_set_step_banded(int on);
 // force the banded split (first band, later bands) of banded launches; first <= 0: the model
 void advdiff_set_step_bands(int first, int rest);
+// host-only band model query: out[5] = {first band, later band, bands, makespan of that
+// split, makespan of the best uniform chunking} (plane-times, one XCD's slots)
+int advdiff_step_bands_plan(int n, long long tiles, long long slots, int warm, int minc,
+                            long long* out);
 // measure banded vs uniform z chunks for this fused-step launch (uin -> uout, uout is
 // scratch; synchronous, outside graph capture), cache the faster, *banded = 1 if banded
 int advdiff_diffusion3d_step_sched_pick(int dtype, const void* uin, void* uout, int nx, int ny,

@@ -1276,6 +1276,31 @@ extern "C" int advdiff_set_step_var(int v) {
   return old;
 }
 
+// Host-only query of the band model (no GPU): out = {first band, later band length,
+// number of bands, modelled makespan in plane-times of the best split, of the best
+// uniform chunking}.  For tests and scheduling studies.
+extern "C" int advdiff_step_bands_plan(int n, long long tiles, long long slots, int warm,
+                                       int minc, long long* out) {
+  using namespace advdiff;
+  if (out == nullptr || n <= 0 || tiles <= 0 || slots <= 0) return hipErrorInvalidValue;
+  const Bands b = step_bands(n, tiles, slots, warm, minc);
+  const int xs = (int)std::max<long long>(slots / 8, 1);
+  const long long cols = (tiles + 7) / 8;
+  long long uni = -1;
+  const int cmax = std::max(1, n / std::max(minc, 1));
+  for (int C = 1; C <= std::min(cmax, 16); ++C) {
+    const int len = (n + C - 1) / C;
+    const long long c = band_makespan(cols, len, (n - len + len - 1) / len, len, xs, warm);
+    if (uni < 0 || c < uni) uni = c;
+  }
+  out[0] = b.zfirst;
+  out[1] = b.zchunk;
+  out[2] = b.nbands;
+  out[3] = band_makespan(cols, b.zfirst, b.nbands - 1, b.zchunk, xs, warm);
+  out[4] = uni;
+  return hipSuccess;
+}
+
 // Force the banded split (first band, later band length) of banded launches; first <= 0
 // returns to the model's split (step_bands).  For band sweeps (bench/band_sweep.py).
 extern "C" void advdiff_set_step_bands(int first, int rest) {

@@ -175,6 +175,9 @@ def _load():
         lib.advdiff_set_step_f32_tile.restype = c_int
         lib.advdiff_set_step_fd2_tile.argtypes = [c_int]
         lib.advdiff_set_step_fd2_tile.restype = c_int
+        lib.advdiff_step_bands_plan.argtypes = [c_int, ctypes.c_longlong, ctypes.c_longlong,
+                                                c_int, c_int, ctypes.POINTER(ctypes.c_longlong)]
+        lib.advdiff_step_bands_plan.restype = c_int
         lib.advdiff_set_step_bands.argtypes = [c_int, c_int]
         lib.advdiff_set_step_bands.restype = None
         lib.advdiff_set_step_banded.argtypes = [c_int]
