@@ -28,6 +28,14 @@ bench therefore runs --settle-ms (default 300 ms) more untimed steps of the same
 then times exactly K steps; the count is reported as `settle`.  `sustained`
 (informational, AFTER the K timed steps): --sustained-steps more steps timed the same way.
 
+Failure handling (N > 1 has never run on distinct GPUs before the driver's node): every
+(process grid, transport) candidate first runs 2 real steps in hang-isolated child
+process groups (parallel/preflight.py: a candidate that hangs, crashes or differs from
+the one-rank solution is dropped and recorded in `preflight`); the whole run has one
+deadline below the driver's limit (--deadline, default 540 s from the launcher's start):
+every rank dumps its stacks 15 s before it, and at it rank 0 prints the JSON line with
+whatever finished (`status` says where it stopped) and every rank exits 124.
+
 FD2 on one GPU runs one RK3 step per launch or two (diffusion_fused.hip v6_march;
 bit-identical), whichever the solver measured faster for the shape at construction
 (advdiff_diffusion3d_step2_pick; at 512^3 fp64 one step per launch wins by 3 %):
@@ -179,46 +187,46 @@ def tune(make, cands, dt, dev, trial_steps=8, rounds=3):
     return best[1], trials
 
 
-STRIPE = 2  # relay helpers per face message of the striped ipc slab exchange
+from multigpu_advectiondiffusion_amd.parallel.preflight import (  # noqa: E402
+    cand_key, family, run_preflight, transport_kwargs as solver_transport)
 
 
-def solver_transport(t):
-    """Solver keyword arguments of a candidate name: "ipc+stripe" = ipc with relayed parts,
-    "rccl+bc" = rccl with the boundary launch on the comm stream (the ipc default schedule;
-    rccl's default is the plain one until it has run on distinct GPUs, so the tuner times
-    both and the fingerprint check vets the opt-in one)."""
-    if t is None:
-        return {}
-    if t == "ipc+stripe":
-        return {"transport": "ipc", "stripe": STRIPE}
-    if t == "rccl+bc":
-        return {"transport": "rccl", "boundary_on_comm": True}
-    return {"transport": t}
+def planned_transports(world: int, on_gpu: bool, want: str) -> list:
+    """Halo transports the run may use (before any process group exists): with the nccl
+    backend rccl (boundary launch on the comm stream, the default schedule), rccl-plain
+    (boundary launch after the interior), ipc and, at 7-8 ranks, ipc+stripe; with ranks
+    sharing one GPU (ADVDIFF_SHARE_GPU=1, gloo) host and ipc; on the CPU host only."""
+    if world == 1:
+        return [None]
+    if not on_gpu:
+        return ["host"]
+    if want != "tune":
+        return [want]
+    if os.environ.get("ADVDIFF_SHARE_GPU", "0") == "1" or os.environ.get("ADVDIFF_BACKEND") == "gloo":
+        names = ["host", "ipc"]
+    else:
+        names = ["rccl", "rccl-plain", "ipc"]
+    from multigpu_advectiondiffusion_amd.parallel.ipc import stripe_plan
+    if any(stripe_plan(world, STRIPE).values()):  # 7-8 ranks: idle links exist
+        names.append("ipc+stripe")
+    return names
 
 
-def transports_for(comm, want: str):
-    """Halo transports to consider (N > 1 on GPUs) and the ipc preflight record.
-    want: "tune" (every transport of this Comm whose preflight passes), or one name."""
-    if comm.size == 1 or comm.device.type != "cuda":
-        return [comm.transport], None
-    names = comm.transports() if want == "tune" else [want]
-    if want == "tune" and "rccl" in names:
-        names.insert(names.index("rccl") + 1, "rccl+bc")
-    if want == "tune" and "ipc" in names:
-        from multigpu_advectiondiffusion_amd.parallel.ipc import stripe_plan
-        if any(stripe_plan(comm.size, STRIPE).values()):  # 7-8 ranks: idle links exist
-            names.append("ipc+stripe")
-    pre = None
-    if "ipc" in names:
-        try:
-            pre = comm.ipc().preflight()
-        except Exception as e:  # noqa: BLE001 - any failure rejects the transport
-            pre = f"failed: {type(e).__name__}: {e}"
-            if comm.rank == 0:
-                print(f"bench: ipc transport rejected ({pre})", file=sys.stderr, flush=True)
-            names = [t for t in names if not t.startswith("ipc")]
-            if not names:
-                raise SystemExit(f"bench: the requested ipc transport failed its preflight: {pre}")
+STRIPE = 2
+
+
+def ipc_pair_check(comm, names):
+    """The main process's own ipc pair preflight (its fields are new mappings): a failure
+    drops ipc from the candidates.  Returns (names, record)."""
+    if not any(t.startswith("ipc") for t in names) or comm.size == 1:
+        return names, None
+    try:
+        pre = comm.ipc().preflight()
+    except Exception as e:  # noqa: BLE001 - any failure rejects the transport
+        pre = f"failed: {type(e).__name__}: {e}"
+        if comm.rank == 0:
+            print(f"bench: ipc transport rejected ({pre})", file=sys.stderr, flush=True)
+        names = [t for t in names if not t.startswith("ipc")]
     return names, pre
 
 
@@ -311,8 +319,8 @@ def parse_args(argv=None):
                          "PZxPYxPX")
     ap.add_argument("--transport", default="tune",
                     help="halo transport for N > 1: 'tune' (default: every transport that "
-                         "passes its preflight, the fastest measured), 'rccl', 'ipc' or "
-                         "'host'")
+                         "passes its preflight, the fastest measured), 'rccl', 'rccl-plain', "
+                         "'ipc', 'ipc+stripe' or 'host'")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: base^3 cells per GPU (default); strong: the 8-GPU grid "
                          "(2*base)^3 on any N")
@@ -326,64 +334,176 @@ def parse_args(argv=None):
                          "'sustained' fields; 0 = off)")
     ap.add_argument("--check-steps", type=int, default=10,
                     help="N > 1: steps of the bitwise N-rank vs 1-GPU check (0 = off)")
-    ap.add_argument("--launch-timeout", type=float, default=1500.0,
-                    help="self-launch (--gpus N > 1 without WORLD_SIZE): wall-clock limit "
-                         "of the N ranks, seconds")
+    ap.add_argument("--deadline", type=float, default=540.0,
+                    help="seconds from the launcher's start (below the driver's 600 s): the "
+                         "ranks dump their stacks 15 s before; at the deadline rank 0 prints "
+                         "the JSON line with what finished and every rank exits 124")
+    ap.add_argument("--preflight", choices=["on", "off"], default="on",
+                    help="N > 1: run every (grid, transport) candidate for 2 steps in "
+                         "hang-isolated child process groups first (parallel/preflight.py)")
+    ap.add_argument("--preflight-cand-s", type=float, default=60.0,
+                    help="preflight: seconds without progress after which a candidate is "
+                         "taken to hang")
+    ap.add_argument("--preflight-total-s", type=float, default=240.0)
     return ap.parse_args(argv)
 
 
-def self_launch(args) -> int:
+def self_launch(args, deadline) -> int:
     """--gpus N > 1 without a launcher: start N ranks of this script ourselves (fresh
     subprocesses with the torchrun environment, before this process touches the GPU;
     never an exec) and return the first failing rank's exit code.  Rank 0 prints the
-    JSON line."""
+    JSON line.  The ranks keep their own deadline (this process is their launcher, so
+    they count from its start); 20 s after it the ranks still alive get SIGUSR1 (stack
+    dump) and are terminated."""
+    import signal
+
     from multigpu_advectiondiffusion_amd.launch import launch_cmd
     cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
-    rc = launch_cmd(args.gpus, cmd, timeout=args.launch_timeout)
+    rc = launch_cmd(args.gpus, cmd, timeout=max(deadline.remaining() + 20.0, 30.0),
+                    dump_signal=signal.SIGUSR1)
     if rc != 0:
         print(f"bench: {args.gpus}-rank run failed (exit {rc})", file=sys.stderr, flush=True)
     return rc
 
 
 def main(argv=None) -> int:
+    from multigpu_advectiondiffusion_amd.utils.deadline import Deadline
     args = parse_args(argv)
     # a dead peer must end an ipc wait well before the driver's clock does
     os.environ.setdefault("ADVDIFF_IPC_TIMEOUT_S", "60")
     world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    dl = Deadline(args.deadline)
     if world == 0 and args.gpus > 1:
-        return self_launch(args)
+        return self_launch(args, dl)
     if world and world != args.gpus:
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
               f"{world}-rank run as {args.gpus} GPUs", file=sys.stderr, flush=True)
         return 2
-    run(args)
-    return 0
+    # the process group's own timeout must not fire before the deadline does (with nccl a
+    # timed-out collective aborts the process: no JSON line)
+    os.environ.setdefault("ADVDIFF_COMM_TIMEOUT", str(int(max(dl.remaining(), 0) + 120)))
+    rank = int(os.environ.get("RANK", "0") or 0)
+    dl.on_expire = (lambda d: report_partial(d)) if rank == 0 else None
+    dl.arm()
+    STATE["deadline"] = dl
+    try:
+        return run(args)
+    finally:
+        dl.cancel()
 
 
-def run(args):
+# ---- what a run has finished so far (printed by rank 0 if the deadline cuts it short) --
+STATE = {"result": None, "deadline": None}
+
+
+def report_partial(dl):
+    res = dict(STATE["result"] or {"metric": METRIC, "value": None, "unit": "MLUPS"})
+    res["status"] = (f"incomplete: the {dl.seconds:g} s bench deadline was reached in phase "
+                     f"'{dl.phase}' (every rank's stack is in stderr)")
+    print(json.dumps(res), flush=True)
+
+
+def phase(comm, name):
+    """Enter a bench phase: progress line, deadline bookkeeping, fault injection
+    (ADVDIFF_FAULT=hang:phase:<name> makes the last rank sleep there: tests)."""
+    dl = STATE["deadline"]
+    if dl is not None:
+        dl.phase = name
+    progress(comm, name)
+    if (os.environ.get("ADVDIFF_FAULT", "") == f"hang:phase:{name.split(':')[0]}"
+            and comm.rank == comm.size - 1):
+        while True:
+            time.sleep(3600)
+
+
+def preflight_candidates(args, n, on_gpu, transports, heat_spec, burgers_spec):
+    """Run every (model, grid, transport) candidate in child process groups (N > 1) and
+    return ({mkey: [(pgrid, transport) that passed]}, record)."""
+    from multigpu_advectiondiffusion_amd.parallel.decomposition import candidate_proc_grids
+    grids = {}
+    for mkey, spec, ghost, corners in heat_spec + burgers_spec:
+        ashape = tuple(reversed(spec["shape"]))
+        if args.decomp == "tune":
+            grids[mkey] = candidate_proc_grids(n, ashape, ghost, 8, corners=corners)
+        else:
+            grids[mkey] = [None if args.decomp == "slab" else args.decomp]
+    models = {mkey: spec for mkey, spec, _, _ in heat_spec + burgers_spec}
+
+    def ok_for(p, t):  # striping applies to slabs only
+        return t != "ipc+stripe" or p in (None, "slab") or tuple(p)[1:] == (1, 1)
+    allc = [(m, p, t) for m in models for p in grids[m] for t in transports if ok_for(p, t)]
+    if n == 1 or args.preflight == "off":
+        return {m: [(p, t) for mm, p, t in allc if mm == m] for m in models}, None
+    verdict = {}
+    dev = "cuda" if on_gpu else "cpu"
+    for fam in ("nccl", "gloo"):
+        cs = [c for c in allc if family(c[2]) == fam]
+        if not cs:
+            continue
+        dl = STATE["deadline"]
+        budget = min(args.preflight_total_s, max(dl.remaining() - 200.0, 30.0)) if dl else \
+            args.preflight_total_s
+        t0 = time.perf_counter()
+        verdict.update(run_preflight(cs, models, device=dev, backend=fam,
+                                     cand_s=args.preflight_cand_s, total_s=budget,
+                                     init_s=max(args.preflight_cand_s, 90.0),
+                                     log=lambda m: print(m, file=sys.stderr, flush=True)))
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(f"bench [{time.perf_counter() - _T0:7.1f} s] preflight ({fam}): "
+                  f"{sum(v == 'ok' for k, v in verdict.items())} ok of {len(verdict)} "
+                  f"in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+    passed = {m: [(p, t) for mm, p, t in allc if mm == m and verdict.get(cand_key(m, p, t)) == "ok"]
+              for m in models}
+    return passed, verdict
+
+
+def run(args) -> int:
     from multigpu_advectiondiffusion_amd import Burgers, Diffusion, Grid, Solver
     from multigpu_advectiondiffusion_amd.parallel import Comm, weak_scaling_grid
-    from multigpu_advectiondiffusion_amd.parallel.decomposition import candidate_proc_grids
 
-    comm = Comm.from_env(device=args.device)
-    n = comm.size
-    if n != args.gpus:
-        raise SystemExit(f"bench: world {n} != --gpus {args.gpus}")
-    dev = comm.device
-    single = Comm(device=str(dev)) if dev.type == "cuda" else Comm(device="cpu")
-    progress(comm, f"{n} rank(s) on {comm.device_ids()}, backend {comm.backend}")
-    transports, preflight = transports_for(comm, args.transport)
-
-    def cands_of(grids):  # striping applies to slabs only
-        return [(p, t) for p in grids for t in transports
-                if t != "ipc+stripe" or p in (None, "slab") or tuple(p)[1:] == (1, 1)]
-
-    # ---- headline: 3-D heat, FD4, fp64, sine IC -------------------------------------
+    n = args.gpus
+    on_gpu = (args.device or ("cuda" if torch.cuda.device_count() > 0 else "cpu")).startswith("cuda")
     grid_of = ((lambda b: weak_scaling_grid(b, n)) if args.scaling == "weak"
                else (lambda b: weak_scaling_grid(b, 8)))
     shape = grid_of(args.base)
+    bshape = grid_of(args.burgers_base)
+    heat_kw = {"K": 1.0, "order": 4}
+    burg_kw = {"viscosity": 1e-5, "weno": "z", "cfl": 0.3}
+    heat_spec = [("heat", {"model": ("diffusion", heat_kw), "shape": list(shape),
+                           "spacing": [1.0, 1.0, 1.0], "ic": "sine", "dtype": "float64"},
+                  3 * 2, True)]
+    burgers_spec = [] if args.no_burgers else [
+        ("burgers", {"model": ("burgers", burg_kw), "shape": list(bshape),
+                     "spacing": [2.0, 2.0, 2.0], "ic": "gaussian", "dtype": "float64"}, 3, False)]
+
+    # ---- N > 1: exercise every candidate in hang-isolated child process groups first ----
+    transports = planned_transports(n, on_gpu, args.transport)
+    passed, pf = preflight_candidates(args, n, on_gpu, transports, heat_spec, burgers_spec)
+    backend = None
+    if n > 1 and on_gpu and pf is not None:
+        ok_t = {t for c in passed.values() for _, t in c}
+        if (any(family(t) == "nccl" for t in transports)
+                and not any(family(t) == "nccl" for t in ok_t)):
+            backend = "gloo"  # RCCL failed everywhere: gloo control plane + ipc puts
+    if n > 1 and not passed.get("heat"):
+        # nothing passed: last resort, the unexercised host-staged exchange (gloo)
+        if on_gpu:
+            backend = "gloo"
+        passed = {m: [(None, "host")] for m in passed}
+
+    comm = Comm.from_env(device=args.device, backend=backend)
+    if comm.size != n:
+        raise SystemExit(f"bench: world {comm.size} != --gpus {n}")
+    dev = comm.device
+    single = Comm(device=str(dev)) if dev.type == "cuda" else Comm(device="cpu")
+    phase(comm, f"{n} rank(s) on {comm.device_ids()}, backend {comm.backend}")
+    names, ipc_pre = ipc_pair_check(comm, sorted({t for c in passed.values() for _, t in c
+                                                  if t is not None}))
+    passed = {m: [(p, t) for p, t in c if t is None or t in names] for m, c in passed.items()}
+
+    # ---- headline: 3-D heat, FD4, fp64, sine IC -------------------------------------
     grid = Grid(shape, (1.0, 1.0, 1.0))
-    model = Diffusion(K=1.0, order=4)
+    model = Diffusion(**heat_kw)
     model.bind(grid)
     dt = model.stable_dt()
 
@@ -391,82 +511,73 @@ def run(args):
         return Solver(m, grid, c, dtype=torch.float64, ic="sine",
                       overlap=not args.no_overlap, decomp=p, **solver_transport(t))
 
-    ashape = tuple(reversed(shape))
-    if args.decomp == "tune":
-        grids = candidate_proc_grids(n, ashape, 3 * model.radius, 8, corners=True)
-    else:
-        grids = [None if args.decomp == "slab" else args.decomp]
-    progress(comm, f"heat: tuning {len(cands_of(grids))} (grid, transport) candidates")
-    (decomp, transport), trials = tune(make_heat, cands_of(grids), dt, dev)
-    progress(comm, f"heat: timed run ({decomp}, {transport})")
+    result = {"metric": METRIC, "value": None, "unit": "MLUPS", "n_gpus": n,
+              "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+              "scaling": args.scaling, "dtype": "fp64",
+              "data": "synthetic (sinusoidal IC sin(pi x)sin(pi y)sin(pi z), random-free "
+                      "analytic init)",
+              "config": {"model": "diffusion3d FD4 13-point + SSP-RK3", "global_batch": 1,
+                         "seq_len": grid.cells, "grid": list(shape),
+                         "cells_per_gpu": grid.cells // n}}
+    if pf is not None:
+        result["preflight"] = pf
+    STATE["result"] = result
+    phase(comm, f"heat: tuning {len(passed['heat'])} (grid, transport) candidates")
+    (decomp, transport), trials = tune(make_heat, passed["heat"], dt, dev)
+    phase(comm, f"heat: timed run ({decomp}, {transport})")
     solver = make_heat(decomp, transport)
     secs = timed(solver, args.steps, args.warmup, dt, args.settle_ms, "heat")
     mlups = grid.cells * args.steps / secs / 1e6
+    pg = solver.pgrid
+    link = {"ipc": "ipc device puts", "rccl": "RCCL, boundary launch on the comm stream",
+            "host": "host-staged", "rccl-plain": "RCCL, boundary launch after the interior",
+            "ipc+stripe": "ipc device puts striped over idle links"}.get(transport, transport)
+    result.update({
+        "value": round(mlups, 1), "settle": SETTLE.get("heat"),
+        "ms_per_step": round(secs / args.steps * 1e3, 4),
+        "vs_baseline": round(mlups / BASE_DIFFUSION, 2)})
+    result["config"]["parallelism"] = (
+        "single GPU" if n == 1 else
+        f"z-slab{n} ({link} halo, overlapped)" if pg[1:] == (1, 1) else
+        f"cartesian {'x'.join(map(str, pg))} (z,y,x; {link} halo)")
+    result["status"] = "running"
+    phase(comm, "heat: sustained window and validation")
     sust = sustained(solver, args.sustained_steps, dt, grid.cells)
     # self-validation against the exact solution (outside the timed region)
     finite = solver.check_finite()
     _, _, linf = solver.error_norms()
-    pg = solver.pgrid
     t_end = solver.t
     diag = halo_diag(solver, dt=dt)
     del solver
     _free(dev)
     bound = linf_bound(grid, model.K, t_end, 4)
+    result.update({
+        "max_abs_u": finite, **({"sustained": sust} if sust else {}),
+        "linf_vs_exact": float(f"{linf:.3e}"), "linf_bound": float(f"{bound:.3e}"),
+        "t_end": t_end, "halo_transport": transport if n > 1 else None,
+        "rccl_world": comm.rccl_world, "transport_trials_ms_per_step": trials,
+        **({"ipc_preflight": ipc_pre} if ipc_pre is not None else {}), **diag,
+        "comm_backend": comm.backend or "none (single process)",
+        "device_ids": comm.device_ids()})
     if not linf <= bound:
-        raise SystemExit(f"bench validation failed: L_inf vs exact = {linf:.3e} > {bound:.3e}")
-    checks = {}
+        return fail(comm, result, f"bench validation failed: L_inf vs exact = {linf:.3e} > "
+                                  f"{bound:.3e}")
+    if n > 1:
+        result["bitwise_vs_1gpu"] = {}
     if n > 1 and args.check_steps > 0:
-        progress(comm, "heat: bitwise check against one GPU")
+        phase(comm, "heat: bitwise check against one GPU")
         ok, rec = bitwise_vs_1gpu(lambda: make_heat(decomp, transport),
                                   lambda: make_heat(None, None, c=single),
                                   args.check_steps, dt, comm, dev)
-        checks["heat"] = {"bitwise": ok, **rec}
+        result["bitwise_vs_1gpu"]["heat"] = ok
+        result["bitwise_check"] = rec
         if not ok:
-            raise SystemExit(f"bench validation failed: {n}-rank heat solution differs from "
-                             f"the 1-GPU solution ({rec})")
-
-    link = {"ipc": "ipc device puts", "rccl": "RCCL", "host": "host-staged",
-            "rccl+bc": "RCCL, boundary launch on the comm stream",
-            "ipc+stripe": "ipc device puts striped over idle links"}.get(transport, transport)
-    result = {
-        "metric": METRIC,
-        "value": round(mlups, 1),
-        "unit": "MLUPS",
-        "n_gpus": n,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "settle": SETTLE.get("heat"),
-        "ms_per_step": round(secs / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": args.scaling,
-        "vs_baseline": round(mlups / BASE_DIFFUSION, 2),
-        "dtype": "fp64",
-        "data": "synthetic (sinusoidal IC sin(pi x)sin(pi y)sin(pi z), random-free analytic init)",
-        "config": {"model": "diffusion3d FD4 13-point + SSP-RK3", "global_batch": 1,
-                   "seq_len": grid.cells, "grid": list(shape),
-                   "parallelism": ("single GPU" if n == 1 else
-                                   f"z-slab{n} ({link} halo, overlapped)" if pg[1:] == (1, 1) else
-                                   f"cartesian {'x'.join(map(str, pg))} (z,y,x; {link} halo)"),
-                   "cells_per_gpu": grid.cells // n},
-        "max_abs_u": finite,
-        **({"sustained": sust} if sust else {}),
-        "linf_vs_exact": float(f"{linf:.3e}"),
-        "linf_bound": float(f"{bound:.3e}"),
-        "t_end": t_end,
-        "halo_transport": transport if n > 1 else None,
-        "rccl_world": comm.rccl_world,
-        "transport_trials_ms_per_step": trials,
-        **({"ipc_preflight": preflight} if preflight is not None else {}),
-        **diag,
-        "comm_backend": comm.backend or "none (single process)",
-        "device_ids": comm.device_ids(),
-    }
-    if n > 1:
-        result["bitwise_vs_1gpu"] = {"heat": checks.get("heat", {}).get("bitwise")}
+            return fail(comm, result, f"bench validation failed: {n}-rank heat solution "
+                                      f"differs from the 1-GPU solution ({rec})")
 
     # ---- the 7-point (FD2) Laplacian named by BASELINE.json, same grid ----------------
     if not args.no_fd2:
-        progress(comm, "FD2 7-point run")
+        phase(comm, "fd2: FD2 7-point run")
         m2 = Diffusion(K=1.0, order=2)
         s2 = make_heat(decomp, transport, m=m2)
         secs2 = timed(s2, args.steps, args.warmup, m2.stable_dt(), args.settle_ms, "fd2")
@@ -475,9 +586,6 @@ def run(args):
         bound2 = linf_bound(grid, m2.K, s2.t, 2)
         del s2
         _free(dev)
-        if not linf2 <= bound2:
-            raise SystemExit(f"bench validation failed: FD2 L_inf vs exact = {linf2:.3e} "
-                             f"> {bound2:.3e}")
         ml2 = grid.cells * args.steps / secs2 / 1e6
         result["fd2_7pt"] = {"value": round(ml2, 1), "unit": "MLUPS",
                              "ms_per_step": round(secs2 / args.steps * 1e3, 4),
@@ -486,37 +594,42 @@ def run(args):
                              "settle": SETTLE.get("fd2"),
                              "steps_per_launch": per_launch,
                              "model": "diffusion3d FD2 7-point + SSP-RK3"}
+        if not linf2 <= bound2:
+            return fail(comm, result, f"bench validation failed: FD2 L_inf vs exact = "
+                                      f"{linf2:.3e} > {bound2:.3e}")
 
     # ---- secondary: 3-D Burgers WENO5-Z + C∇²u, fp64 ----------------------------------
     if not args.no_burgers:
-        bshape = grid_of(args.burgers_base)
         bgrid = Grid(bshape, (2.0, 2.0, 2.0))
-        bmodel = Burgers(viscosity=1e-5, weno="z", cfl=0.3)
+        bmodel = Burgers(**burg_kw)
         bmodel.bind(bgrid)
         bdt = bmodel.stable_dt()
 
         def make_burgers(p, t, c=comm):
             return Solver(bmodel, bgrid, c, dtype=torch.float64, ic="gaussian",
                           overlap=not args.no_overlap, decomp=p, **solver_transport(t))
-        if args.decomp == "tune":
-            bgrids = candidate_proc_grids(n, tuple(reversed(bshape)), bmodel.radius, 8)
-        else:
-            bgrids = [None if args.decomp == "slab" else args.decomp]
-        progress(comm, f"burgers: tuning {len(cands_of(bgrids))} candidates")
-        (bdecomp, btransport), btrials = tune(make_burgers, cands_of(bgrids), bdt, dev)
-        progress(comm, f"burgers: timed run ({bdecomp}, {btransport})")
+        phase(comm, f"burgers: tuning {len(passed['burgers'])} candidates")
+        (bdecomp, btransport), btrials = tune(make_burgers, passed["burgers"], bdt, dev)
+        phase(comm, f"burgers: timed run ({bdecomp}, {btransport})")
         bsolver = make_burgers(bdecomp, btransport)
         bsteps = args.burgers_steps or args.steps
         bsecs = timed(bsolver, bsteps, args.warmup, bdt, args.settle_ms, "burgers")
         bml = bgrid.cells * bsteps / bsecs / 1e6
+        brec = result["burgers3d"] = {
+            "value": round(bml, 1), "unit": "MLUPS", "grid": list(bshape), "steps": bsteps,
+            "ms_per_step": round(bsecs / bsteps * 1e3, 4), "settle": SETTLE.get("burgers"),
+            "vs_baseline": round(bml / BASE_BURGERS, 2),
+            "model": "burgers3d WENO5-Z + FD4 viscous (C=1e-5) + SSP-RK3",
+            "pgrid": list(bsolver.pgrid), "halo_transport": btransport if n > 1 else None,
+            "transport_trials_ms_per_step": btrials}
         bsust = sustained(bsolver, args.sustained_steps, bdt, bgrid.cells)
+        if bsust:
+            brec["sustained"] = bsust
         bsolver.check_finite()
-        bpg = list(bsolver.pgrid)
-        bref = None
         if args.burgers_ref_bound > 0:
             # self-check (outside the timed region): every step the timed solver took,
             # again through the fp64 PyTorch reference ops on the same decomposition
-            progress(comm, f"burgers: {bsolver.it} reference steps (torch ops)")
+            phase(comm, f"burgers: {bsolver.it} reference steps (torch ops)")
             ref = Solver(bmodel, bgrid, comm, dtype=torch.float64, ic="gaussian",
                          overlap=not args.no_overlap, decomp=bdecomp, kernel="torch",
                          **solver_transport(btransport))
@@ -528,36 +641,44 @@ def run(args):
                     "steps": bsolver.it, "t": bsolver.t,
                     "torch_s": round(time.perf_counter() - t_ref, 1)}
             del ref
+            brec["linf_vs_torch"] = bref["linf_vs_torch"]
+            brec["reference_check"] = bref
         del bsolver
         _free(dev)
-        if bref is not None and not bref["linf_vs_torch"] <= args.burgers_ref_bound:
-            raise SystemExit(f"bench validation failed: Burgers L_inf vs the torch reference "
-                             f"= {bref['linf_vs_torch']:.3e} > {args.burgers_ref_bound:.1e}")
-        result["burgers3d"] = {"value": round(bml, 1), "unit": "MLUPS", "grid": list(bshape),
-                               "steps": bsteps, "ms_per_step": round(bsecs / bsteps * 1e3, 4),
-                               "settle": SETTLE.get("burgers"),
-                               "vs_baseline": round(bml / BASE_BURGERS, 2),
-                               "model": "burgers3d WENO5-Z + FD4 viscous (C=1e-5) + SSP-RK3",
-                               "pgrid": bpg,
-                               **({"linf_vs_torch": bref["linf_vs_torch"],
-                                   "reference_check": bref} if bref else {}),
-                               "halo_transport": btransport if n > 1 else None,
-                               "transport_trials_ms_per_step": btrials,
-                               **({"sustained": bsust} if bsust else {})}
+        if "reference_check" in brec and not brec["linf_vs_torch"] <= args.burgers_ref_bound:
+            return fail(comm, result, f"bench validation failed: Burgers L_inf vs the torch "
+                                      f"reference = {brec['linf_vs_torch']:.3e} > "
+                                      f"{args.burgers_ref_bound:.1e}")
         if n > 1 and args.check_steps > 0:
-            progress(comm, "burgers: bitwise check against one GPU")
+            phase(comm, "burgers: bitwise check against one GPU")
             ok, rec = bitwise_vs_1gpu(lambda: make_burgers(bdecomp, btransport),
                                       lambda: make_burgers(None, None, c=single),
                                       args.check_steps, bdt, comm, dev)
-            result["burgers3d"]["bitwise_check"] = rec
+            brec["bitwise_check"] = rec
             result["bitwise_vs_1gpu"]["burgers3d"] = ok
             if not ok:
-                raise SystemExit(f"bench validation failed: {n}-rank Burgers solution "
-                                 f"differs from the 1-GPU solution ({rec})")
+                return fail(comm, result, f"bench validation failed: {n}-rank Burgers "
+                                          f"solution differs from the 1-GPU solution ({rec})")
 
+    result["status"] = "ok"
+    if STATE["deadline"] is not None:
+        STATE["deadline"].cancel()
     if comm.rank == 0:
         print(json.dumps(result), flush=True)
     comm.finalize()
+    return 0
+
+
+def fail(comm, result, msg) -> int:
+    """A validation failure: no result line (the numbers are not valid), the reason on
+    stderr, exit 1 on every rank."""
+    STATE["result"] = None
+    if STATE["deadline"] is not None:
+        STATE["deadline"].cancel()
+    if comm.rank == 0:
+        print(msg, file=sys.stderr, flush=True)
+    comm.finalize()
+    return 1
 
 
 if __name__ == "__main__":

@@ -1345,6 +1345,20 @@ extern "C" int advdiff_burgers2d_stage_ls(int dtype, const void* in, void* du, v
                                     vx, vy, dt, A, B, 1, nullptr, stream);
 }
 
+namespace advdiff {
+template <typename T, bool PK>
+static void preload_w5s_occupancies() {
+  [&]<int... I>(std::integer_sequence<int, I...>) {
+    // I = WZ | VISC << 1 | MODE << 2 | (TXL == 32) << 4
+    ((void)occupancy_per_cu(
+         (const void*)burgers3d_w5s_kernel<T, (I & 1) != 0, (I & 2) != 0, (I >> 2) & 3,
+                                           (I & 16) ? 32 : 64, PK>,
+         512),
+     ...);
+  }(std::make_integer_sequence<int, 32>{});
+}
+}  // namespace advdiff
+
 // Code-object preload (see advdiff_preload in aux.hip): the attributes query makes the
 // runtime load this translation unit's code object now instead of at the first launch.
 extern "C" int advdiff_preload_burgers(void) {
@@ -1352,13 +1366,12 @@ extern "C" int advdiff_preload_burgers(void) {
   hipFuncAttributes a;
   const hipError_t e =
       hipFuncGetAttributes(&a, (const void*)burgers3d_w5s_kernel<double, true, true, 1>);
-  // occupancies of the default 3-D stage instances (launch.hpp occupancy_per_cu): WENO5-Z
-  // viscous, RK3 modes 0-2, both tile rows
-  (void)occupancy_per_cu((const void*)burgers3d_w5s_kernel<double, true, true, 0, 64>, 512);
-  (void)occupancy_per_cu((const void*)burgers3d_w5s_kernel<double, true, true, 1, 64>, 512);
-  (void)occupancy_per_cu((const void*)burgers3d_w5s_kernel<double, true, true, 2, 64>, 512);
-  (void)occupancy_per_cu((const void*)burgers3d_w5s_kernel<double, true, true, 0, 32>, 512);
-  (void)occupancy_per_cu((const void*)burgers3d_w5s_kernel<double, true, true, 1, 32>, 512);
-  (void)occupancy_per_cu((const void*)burgers3d_w5s_kernel<double, true, true, 2, 32>, 512);
+  // occupancies of every 3-D stage instance the default dispatch can select (launch.hpp
+  // occupancy_per_cu caches them), so no first launch — possibly inside a hipGraph capture
+  // — queries the runtime: fp64 and fp32 (one cell or packed pairs per lane), WENO5-JS
+  // and -Z, inviscid and viscous, every stage epilogue, both tile rows
+  preload_w5s_occupancies<double, false>();
+  preload_w5s_occupancies<float, false>();
+  preload_w5s_occupancies<float, true>();
   return e;
 }

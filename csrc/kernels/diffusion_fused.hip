@@ -27,6 +27,7 @@
 
 #include <cstdio>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <queue>
 #include <tuple>
@@ -981,10 +982,19 @@ static int step_zchunk() {
 // measured choice (uniform chunks for an unmeasured launch), 0 never, 1 always.  Results
 // are bitwise the same for every chunking.
 static int g_band_force[2] = {0, 0};  // forced (first band, later bands) for sweeps; 0 = model
-static int g_step_banded = -2;
+// process-wide setting (atomic: the C API is callable from any host thread); the pick's
+// own forced schedule is THREAD-local, so a launch from another thread during a
+// measurement keeps its own choice and a concurrent advdiff_set_step_banded survives
+static std::atomic<int> g_step_banded{-2};
+static thread_local int t_sched_force = -1;  // advdiff_diffusion3d_step_sched_pick only
 static int step_banded() {
-  if (g_step_banded == -2) g_step_banded = knob("STEP_BANDED", -1);
-  return g_step_banded;
+  int v = g_step_banded.load(std::memory_order_relaxed);
+  if (v == -2) {
+    int fresh = knob("STEP_BANDED", -1);
+    g_step_banded.compare_exchange_strong(v, fresh);
+    v = g_step_banded.load(std::memory_order_relaxed);
+  }
+  return v;
 }
 
 // Makespan, in plane-times, of `cols` columns cut into bands (first of `a` planes, then
@@ -1082,6 +1092,7 @@ static std::vector<int64_t> sched_key(int esize, int order, int nx, int ny, int6
           b.xa0, b.xa1, b.ya0, b.ya1, b.xo0, b.xo1, b.yo0, b.yo1};
 }
 static bool sched_banded(int esize, int order, const SArgs& a) {
+  if (t_sched_force >= 0) return t_sched_force > 0;
   const int m = step_banded();
   if (m >= 0) return m > 0;
   const auto key = sched_key(esize, order, a.nx, a.ny, a.sy, a.sz, a.nz_alloc, a.k0, a.k1, a.zlo,
@@ -1310,7 +1321,7 @@ extern "C" void advdiff_set_step_bands(int first, int rest) {
 
 extern "C" int advdiff_set_step_banded(int on) {
   const int old = advdiff::step_banded();
-  advdiff::g_step_banded = on;
+  advdiff::g_step_banded.store(on);
   return old;
 }
 
@@ -1440,12 +1451,12 @@ extern "C" int advdiff_diffusion3d_step_sched_pick(int dtype, const void* uin, v
     }
   }
   hipStream_t st = (hipStream_t)stream;
-  auto launch = [&](int m) {
-    g_step_banded = m;
+  auto launch = [&](int m) {  // this thread's launches only (t_sched_force)
+    t_sched_force = m;
     const int e = advdiff_diffusion3d_step_box_ex(dtype, uin, uout, nx, ny, sy, sz, nz_alloc, k0,
                                                   k1, 0, 0, zlo, zhi, box, order, cx, cy, cz, dt,
                                                   ADVDIFF_EXCLUSIVE, stream);
-    g_step_banded = -1;
+    t_sched_force = -1;
     return e;
   };
   hipEvent_t e0 = nullptr, e1 = nullptr;

@@ -9,7 +9,7 @@
 // plus named options (runtime replacements of the reference's #defines, §2.7):
 //   --ic NAME  --order 2|4  --safety S  --weno js|z|js7  --visc C  --fp32  --no-overlap
 //   --[no-]boundary-on-comm (overlap: the boundary launch on the comm stream; default on
-//   for --transport ipc; ADVDIFF_BCOMM=0/1)
+//   for --transport rccl and ipc; ADVDIFF_BCOMM=0/1)
 //   --integrator ssprk3|lsrk45  --no-fused  --transport rccl|ipc|socket  --write FILE
 //   --write-ghosts FILE (the reference's multi-GPU result.bin: every rank's slab WITH its
 //   ghost planes, MultiGPU/Diffusion3d_Baseline/main.c:341)  --error-norms

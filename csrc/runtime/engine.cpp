@@ -171,9 +171,10 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
   if (const char* s2 = std::getenv("ADVDIFF_STEP2")) step2_env_ = std::atoi(s2) != 0;
   {
     int bc = p.bcomm;
-    if (bc < 0) {  // default: on for ipc (profiles/r5/overlap.md), off for rccl / socket
+    if (bc < 0) {  // default: on for ipc (profiles/r5/overlap.md) and rccl (stream-ordered
+                   // ncclSend/Recv on comm_, the same two-stream order), off for socket
       const char* v = std::getenv("ADVDIFF_BCOMM");
-      bc = v ? std::atoi(v) : std::string(tr_->name()) == "ipc";
+      bc = v ? std::atoi(v) : std::string(tr_->name()) != "socket";
     }
     // the exchange must be stream-ordered device work on comm_ (a host-staged transport
     // blocks the host on comm_ inside start_halo: keep its boundary on compute_)

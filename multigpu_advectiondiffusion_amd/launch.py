@@ -83,12 +83,16 @@ def profiled(cmd: list, profile_dir: str, rank: int) -> list:
 
 def launch_cmd(np_: int, cmd, cpu: bool = False, timeout: float | None = None,
                poll_s: float = 0.2, port: int | None = None,
-               profile_dir: str | None = None, extra_env: dict | None = None) -> int:
+               profile_dir: str | None = None, extra_env: dict | None = None,
+               dump_signal: int | None = None) -> int:
     """Run `cmd` (a list, or a callable rank -> list) as P ranks with the torchrun
     environment; fail fast: the first rank that exits non-zero (or the wall-clock
     `timeout`, rc 124) terminates the others, so a crashed rank never leaves its peers
-    blocked in a halo exchange until the collective timeout.  Returns the first non-zero
-    exit code (0 if all succeed).  The ranks are fresh subprocesses (never an exec)."""
+    blocked in a halo exchange until the collective timeout.  dump_signal (e.g.
+    signal.SIGUSR1 for ranks that registered faulthandler on it, as bench.py's do): sent
+    to the ranks still alive before they are terminated, so their stacks — where each
+    one was stuck — reach the shared stderr.  Returns the first non-zero exit code (0 if
+    all succeed).  The ranks are fresh subprocesses (never an exec)."""
     import time
     port = port or free_port()
     procs = []
@@ -119,6 +123,14 @@ def launch_cmd(np_: int, cmd, cpu: bool = False, timeout: float | None = None,
                 break
             time.sleep(poll_s)
     finally:
+        alive = [p for p in procs if p.poll() is None]
+        if alive and dump_signal is not None:
+            for p in alive:
+                try:
+                    p.send_signal(dump_signal)
+                except OSError:
+                    pass
+            time.sleep(2.0)  # the stack dumps are written by a C-level handler
         for p in procs:
             if p.poll() is None:
                 p.terminate()

@@ -47,10 +47,12 @@ INTEGRATORS = ("ssprk3", "lsrk45")
 
 def _fault_from_env():
     """Fault injection for failure-handling tests: ADVDIFF_FAULT="RANK:STEP" raises on
-    that rank right after that step (eager stepping path)."""
+    that rank right after that step (eager stepping path).  (The "hang:..." forms belong
+    to bench.py and parallel/preflight.py.)"""
     import os
+    import re
     v = os.environ.get("ADVDIFF_FAULT")
-    if not v:
+    if not v or not re.fullmatch(r"\d+:\d+", v):
         return None
     r, st = v.split(":")
     return int(r), int(st)
@@ -131,8 +133,8 @@ class Solver:
         boundary_on_comm (N > 1 device ranks, overlap): the boundary launch on the COMM
         stream, right after the wait for the halo of its input and right before the puts
         of its output — two streams per rank, the interior launch beside the whole
-        exchange (None = ADVDIFF_BCOMM, else on for the ipc transport and off for rccl /
-        host).  boundary_stream is its round-4 name (that version used a third stream;
+        exchange (None = ADVDIFF_BCOMM, else on for the ipc and rccl transports and off
+        for host).  boundary_stream is its round-4 name (that version used a third stream;
         see _step_fused_bcomm).
         pitch: (px, py) — device fields get rows of align256(nx) + px elements and, in
         3-D, planes of ny + py rows (the extra rows and columns are never read or written;
@@ -237,10 +239,15 @@ class Solver:
                 import os
                 # default: on for the ipc transport (every exchange step is a kernel on
                 # the comm stream; 2 ranks on one GPU: 90-100 % of the put time beside the
-                # interior launch instead of 8-33 %, profiles/r5/overlap.md), off for rccl
-                # until it has run on distinct GPUs
+                # interior launch instead of 8-33 %, profiles/r5/overlap.md) and for rccl
+                # (the grouped send/recv is issued from the comm stream, so RCCL's stream
+                # waits for the boundary launch and the next boundary launch waits for
+                # RCCL — the same two-stream order; the reference's boundary-on-send-stream
+                # concurrency, MultiGPU/Diffusion3d_Baseline/main.c:118-122,209-260);
+                # off for the host-staged exchange, which blocks the host inside start
                 env = os.environ.get("ADVDIFF_BCOMM") or os.environ.get("ADVDIFF_BSTREAM")
-                boundary_on_comm = (env == "1") if env else self.transport == "ipc"
+                boundary_on_comm = ((env == "1") if env
+                                    else self.transport in ("ipc", "rccl"))
             # the boundary launch on the (high-priority) comm stream, between the wait for
             # the halo of its input and the puts of its output: _step_fused_bcomm (with the
             # host-staged transport, gloo device tests only, the host blocks on the comm
@@ -272,7 +279,24 @@ class Solver:
         if device_dt is None:
             device_dt = self.device.type == "cuda" and kernel == "native"
         self.device_dt = bool(device_dt) and model.needs_umax and exchange == "u"
+        # launch-shape measurements (FD2 steps per launch, z schedule): tune_launches(),
+        # on the first run() or explicitly — not here, so building the solver (the CLI's
+        # barrier-fenced HtD time) does not include them (the native engine also picks
+        # after its init timer)
         self._step2_on = False
+        self._picked = False
+
+    def _pick2(self) -> bool:
+        self.tune_launches()
+        return self._step2_on
+
+    def tune_launches(self) -> None:
+        """Measure the launch choices that depend on the shape once (before any graph
+        capture): one FD2 step per launch or two (_pick_step2), banded or uniform z chunks
+        (_pick_sched).  Idempotent; run() calls it first."""
+        if self._picked:
+            return
+        self._picked = True
         self._step2_on = self._pick_step2()
         self._pick_sched()
 
@@ -596,7 +620,7 @@ class Solver:
         bit-identical to two steps) — where that is the faster launch for this shape
         (measured once per shape on the GPU at construction: _pick_step2)."""
         return (self.fused and self.comm.size == 1 and not self.cart and self.du is None
-                and self.model.supports_step2 and self._dt_dev is None and self._step2_on)
+                and self.model.supports_step2 and self._dt_dev is None and self._pick2())
 
     def _pick_sched(self) -> None:
         """Banded or uniform z chunks for the fused 3-D launch that carries most planes (one
@@ -735,6 +759,7 @@ class Solver:
 
     def _graph_for(self, dt: float | None, t_end: float | None = None):
         """dt=None: a graph of device-dt (adaptive CFL) steps towards t_end."""
+        self.tune_launches()  # never inside the capture
         # A graph bakes in the buffer addresses: the fused / LSRK paths ping-pong u <-> un,
         # so after an odd number of eager steps the other parity needs its own graph.
         # multi-rank ipc: the graph also bakes in the peers' receive addresses, valid for the
@@ -846,6 +871,7 @@ class Solver:
         process, fixed dt, no per-step callback/watchdog)."""
         if iters is None and t_end is None:
             raise ValueError("give iters or t_end")
+        self.tune_launches()  # outside the timed region, before any capture
         fixed_dt = dt if dt is not None else (None if self.model.needs_umax else self.dt())
         dev_dt = (fixed_dt is None and self.device_dt and callback is None
                   and not self.check_every and _FAULT is None)

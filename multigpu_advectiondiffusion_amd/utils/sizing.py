@@ -36,14 +36,20 @@ def row_pitch(nx: int, elem: int, align: int = 256) -> int:
     return (nx + per - 1) // per * per
 
 
-def solver_bytes(shape_local_alloc, elem: int, fields: int, pitch=None) -> int:
+def solver_bytes(shape_local_alloc, elem: int, fields: int, pitch=None,
+                 cells_per_rank: int | None = None) -> int:
     """Bytes of the resident fields for a local allocation (array order, last axis x);
     pitch = (extra elements per row, extra rows per 3-D plane), None = the solver's
-    default rule for a rank of this many cells."""
+    default rule (solver.pitch_default), which the Solver applies to the GLOBAL cells per
+    rank (grid.cells // world, ghosts excluded): pass that as cells_per_rank.  Without
+    it the owned cells are taken as the allocation minus nothing — callers that size a
+    ghost-inclusive block should pass cells_per_rank, or the rule can flip near its
+    threshold."""
     *outer, nx = shape_local_alloc
     if pitch is None:
         from ..solver import pitch_default
-        pitch = pitch_default(len(shape_local_alloc), elem, math.prod(shape_local_alloc))
+        n = math.prod(shape_local_alloc) if cells_per_rank is None else int(cells_per_rank)
+        pitch = pitch_default(len(shape_local_alloc), elem, n)
     if len(outer) == 2:
         outer = [outer[0], outer[1] + pitch[1]]
     return fields * math.prod(outer) * (row_pitch(nx, elem) + pitch[0]) * elem
@@ -56,7 +62,7 @@ def max_cube(mem_bytes: int = HBM_BYTES_MI355X, elem: int = 8, fields: int = 2,
     budget = headroom * mem_bytes
     n = multiple
     while solver_bytes((n + multiple + 2 * ghost, n + multiple, n + multiple), elem,
-                       fields) <= budget:
+                       fields, cells_per_rank=(n + multiple) ** 3) <= budget:
         n += multiple
     return n
 
@@ -72,7 +78,7 @@ def main(argv=None):
                                  ("Burgers WENO7 + LSRK4(5) (fp64)", 3, 4)):
         n = max_cube(mem, 8, fields, ghost)
         print(f"{label:42s}: {n}^3 per GPU ({fields} fields, "
-              f"{solver_bytes((n + 2 * ghost, n, n), 8, fields) / 1e9:.0f} GB); "
+              f"{solver_bytes((n + 2 * ghost, n, n), 8, fields, cells_per_rank=n ** 3) / 1e9:.0f} GB); "
               f"{a.gpus} GPUs (z-slabs): {n}x{n}x{n * a.gpus}")
 
 
