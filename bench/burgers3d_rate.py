@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """In-solver rate of the bench's 3-D Burgers case (WENO5-Z + FD4 viscous, 256^3, fp64,
-SSP-RK3) under the current ADVDIFF_* launch knobs — one JSON line per process, for
-interleaved A/B runs of a knob (knobs are read once per process):
+SSP-RK3) — one JSON line per process, for interleaved A/B runs of two builds or
+settings (ADVDIFF_B3_PACK / B3_TX / B3_VER; knobs are read once per process):
 
-    ADVDIFF_TARGET_BLOCKS=512 python bench/burgers3d_rate.py
+    python bench/burgers3d_rate.py
 """
 import json
 import os

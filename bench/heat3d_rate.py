@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """In-solver rate of the fused 3-D FD4 heat step on the reference's 3-D heat grids and the
-bench grid under the current ADVDIFF_* launch knobs — one JSON line per process, for
-interleaved A/B runs of a knob (knobs are read once per process):
+bench grid — one JSON line per process, for interleaved A/B runs of two builds or of
+ADVDIFF_STEP_BANDED=0/1 (knobs are read once per process):
 
-    ADVDIFF_STEP_MIN_CHUNK=16 python bench/heat3d_rate.py [order: 4 (default) | 2]
+    python bench/heat3d_rate.py [order: 4 (default) | 2]
 """
 import json
 import os

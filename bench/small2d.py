@@ -1,12 +1,11 @@
 #!/usr/bin/env python3
 """Small 2-D grids (the reference's MultiGPU 2-D rows, 400x406, and 1001^2): MLUPS of the
 2-D Burgers (WENO5-JS inviscid) and 2-D heat (FD4) solvers, one MI355X, fp64.  These
-grids hold 0.16-1 M cells, so a stage is a few microseconds and latency-bound: the
-row-chunk length per workgroup (ADVDIFF_B2_MINC for the Burgers stage kernel) sets how
-many rows one wave walks in sequence.  Run once per knob setting (knobs are read once
-per process):
+grids hold 0.16-1 M cells, so a stage is a few microseconds and latency-bound (the
+Burgers stage walks one row per wave in sequence at these sizes: the chunk floor of 1
+row measured best, profiles/archive/small2d_r2.log).
 
-    ADVDIFF_B2_MINC=2 python bench/small2d.py
+    python bench/small2d.py
 """
 import json
 import os

@@ -192,12 +192,6 @@ int advdiff_debug_print(int dtype, const void* u, int64_t sy, int64_t sz, int i0
 int advdiff_device_info(int dev, int64_t* out, int n);
 // Peer topology: can_access (hipDeviceCanAccessPeer), HSA link type (4 = xGMI), hop count.
 int advdiff_peer_info(int a, int b, int* can_access, int* link_type, int* hops);
-// fused 3-D step: phase-overlap variant (-1 = the per-order default; 0 plain, 3 graded wave
-// priority, 7 graded priority + the second wave half deferring its stage 3; bit-identical)
-// — A/B knob, returns the previous value
-int advdiff_set_step_var(int v);
-// v3 fused step: boundary-anchored edge tiles (1, default) or the plain partition (0)
-int advdiff_set_step_edge(int on);
 // 3-D WENO5 stage kernel version (9 = default, 3 = the v3 fallback used for planes of
 // 2 GiB and more); returns the previous value.  Results agree to rounding (tests).
 int advdiff_set_b3_ver(int v);
@@ -214,17 +208,10 @@ int advdiff_diffusion3d_step2_pick(int dtype, const void* uin, void* uout, int n
                                    int64_t sy, int64_t sz, int nz_alloc, int k0, int k1,
                                    int zlo, int zhi, const int* box, double cx, double cy,
                                    double cz, double dt, void* stream, int* use2);
-// fused heat step: forced z-chunk length (0 = automatic); returns the previous setting
-int advdiff_set_step_zchunk(int zc);
-// fused FD2 step tile: 0 = 12 waves x 3 rows (default), 1 = 8 x 3 (two workgroups per CU);
-// returns the previous setting
-int advdiff_set_step_fd2_tile(int t);
 // banded z schedule of the fused step: -1 (default) the measured choice per launch
 // (advdiff_diffusion3d_step_sched_pick; uniform z chunks for an unmeasured launch), 0
 // never, 1 always; returns the previous setting
 int advdiff_set_step_banded(int on);
-// force the banded split (first band, later bands) of banded launches; first <= 0: the model
-void advdiff_set_step_bands(int first, int rest);
 // host-only band model query: out[5] = {first band, later band, bands, makespan of that
 // split, makespan of the best uniform chunking} (plane-times, one XCD's slots)
 int advdiff_step_bands_plan(int n, long long tiles, long long slots, int warm, int minc,
@@ -236,8 +223,6 @@ int advdiff_diffusion3d_step_sched_pick(int dtype, const void* uin, void* uout, 
                                         int zlo, int zhi, const int* box, int order, double cx,
                                         double cy, double cz, double dt, void* stream,
                                         int* banded);
-// fp32 fused heat step tile: 0 = the fp64 shapes, 3 / 4 = 16 waves x 3 / 4 rows
-int advdiff_set_step_f32_tile(int t);
 // fp32 3-D WENO5 stage: packed pairs (1, default) or one cell per lane (0); returns the
 // previous setting.  Bit-identical either way.
 int advdiff_set_b3_pack(int on);

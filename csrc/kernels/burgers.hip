@@ -1034,26 +1034,25 @@ static int g_b3_zchunk = 0;
 
 template <typename T, bool WZ, bool VISC, int MODE, int TXL, bool PK = false>
 static hipError_t launch_b3_v9_tx(const BArgs& p) {
-  // XCD-contiguous tile order (default): 256^3 WENO5-Z + viscous step 0.584 -> 0.564 ms
-  // (+3.7 %, 3 interleaved rounds, bitwise identical; profiles/archive/burgers3d_xcd_r2.log)
-  static const int xcdmap = knob("B3_XCD", 1);
+  // XCD-contiguous tile order (always, its switch removed in round 6): 256^3 WENO5-Z +
+  // viscous step 0.584 -> 0.564 ms (+3.7 %, 3 interleaved rounds, bitwise identical;
+  // profiles/archive/burgers3d_xcd_r2.log)
+  constexpr int xcdmap = 1;
   constexpr int TY = 8 * (64 / TXL);
   const int gx = div_up(std::max(p.nx - 2 * p.border, 1), TXL - 1);
   const int gy = div_up(std::max(p.ny - 2 * p.border, 1), TY);
   const int na = std::max(p.hi - p.lo, 0), nb = std::max(p.hi2 - p.lo2, 0);
   // z chunks by the rounds model of the fused heat step (launch.hpp pick_chunk_rounds:
   // resident workgroups = CUs x occupancy, cost = rounds x (chunk + warm-up)).  The old
-  // target-count rule (ADVDIFF_B3_CHUNKS=0) gave 512^3 two chunks of 253 planes = 1088
+  // target-count rule (removed in round 6) gave 512^3 two chunks of 253 planes = 1088
   // workgroups for 512 resident slots: a third round with 64 workgroups alone on the chip.
-  static const int rounds_model = knob("B3_CHUNKS", 1);
   const int per_cu =
       occupancy_per_cu((const void*)burgers3d_w5s_kernel<T, WZ, VISC, MODE, TXL, PK>, 512);
   // PK: a workgroup marches two half chunks side by side — choose the half length
   const int nm = PK ? div_up(na + nb, 2) : na + nb;
   const int zm = g_b3_zchunk > 0 ? std::max(1, PK ? div_up(g_b3_zchunk, 2) : g_b3_zchunk)
-                 : rounds_model ? pick_chunk_rounds(nm, (long long)gx * gy,
-                                                    (long long)device_cus() * per_cu, 4, 8)
-                                : pick_chunk(nm, (long long)gx * gy, 8, 256);
+                                 : pick_chunk_rounds(nm, (long long)gx * gy,
+                                                     (long long)device_cus() * per_cu, 4, 8);
   const int zc = PK ? 2 * zm : zm;
   const int gza = div_up(na, zc);
   const int gz = gza + div_up(nb, zc);
@@ -1133,8 +1132,7 @@ template <typename T, bool WZ, bool VISC, int MODE>
 static hipError_t launch_b2_w5(const BArgs& p) {
   const int strips = div_up(std::max(p.nx - 2 * p.border, 1), 63);
   const int gx = div_up(strips, 4);
-  static const int minc = std::max(knob("B2_MINC", 1), 1);
-  const int yc = pick_chunk(p.hi - p.lo, gx, minc, 256);
+  const int yc = pick_chunk(p.hi - p.lo, gx, 1, 256);
   const int gy = div_up(p.hi - p.lo, yc);
   const double s = 1.0 / 12.0;
   hipLaunchKernelGGL((burgers2d_w5_kernel<T, WZ, VISC, MODE>), dim3(gx, gy, 1), dim3(256, 1, 1),
@@ -1156,8 +1154,7 @@ static hipError_t launch_b2(const BArgs& p) {
   // bound, and a wave walking fewer rows in sequence wins there (400x406 WENO5-JS step
   // 23.4 -> 20.4 us with 4 -> 1, profiles/archive/small2d_r2.log); from ~1000^2 up the chunk
   // comes from the block target and this floor is inactive
-  static const int minc = std::max(knob("B2_MINC", 1), 1);
-  const int yc = pick_chunk(p.hi - p.lo, gx, minc, 256);
+  const int yc = pick_chunk(p.hi - p.lo, gx, 1, 256);
   const int gy = div_up(p.hi - p.lo, yc);
   const double s = 1.0 / 12.0;
   hipLaunchKernelGGL((burgers2d_stage_kernel<T, W, WZ, VISC, MODE, kBTX2>), dim3(gx, gy, 1),

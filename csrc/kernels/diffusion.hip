@@ -204,12 +204,8 @@ static hipError_t launch_d3_ty(const DArgs& p) {
 
 template <typename T, int ORDER, int MODE>
 static hipError_t launch_d3(const DArgs& p) {
-  static const int ty = knob("D3_TY", kTY3);
-  switch (ty) {
-    case 4: return launch_d3_ty<T, ORDER, 4, MODE>(p);
-    case 16: return launch_d3_ty<T, ORDER, 16, MODE>(p);
-    default: return launch_d3_ty<T, ORDER, 8, MODE>(p);
-  }
+  // (the 4- and 16-row tiles and their ADVDIFF_D3_TY switch were removed in round 6)
+  return launch_d3_ty<T, ORDER, kTY3, MODE>(p);
 }
 
 template <typename T, int ORDER, int MODE>

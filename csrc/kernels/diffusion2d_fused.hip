@@ -166,8 +166,8 @@ static hipError_t launch_step2d(const void* uin, void* uout, int nx, int64_t sy,
   // 4R warm-up) x max(1, waves / wave slots), wave slots ~ 4 per SIMD (fitted on 400² ..
   // 16384²: profiles/heat2d_sizes.log).  Small grids get short chunks (more waves), large
   // grids long ones (less warm-up).
-  static const int slots = knob("STEP2D_SLOTS", 4 * 4 * device_cus());
-  static const int minc = knob("STEP2D_MIN_CHUNK", 2);
+  static const int slots = 4 * 4 * device_cus();
+  constexpr int minc = 2;
   const int n = j1 - j0;
   int chunks = 1;
   double best = -1.0;

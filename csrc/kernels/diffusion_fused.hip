@@ -186,21 +186,13 @@ __device__ __forceinline__ void v3_march(
   // plane without them).  FD4 512^3 642 -> 614 us, bitwise the same (in-process A/B,
   // profiles/r5/ab/vcoef_ab.log; stage 3 instead of 1: the same).  fp32 keeps SGPRs (no
   // spill there, and 4 more VGPRs would cost the 16 x 2 tile its second workgroup per CU).
-  // ADVDIFF_VCOEF (build time, bit s-1 = stage s) overrides for A/B libraries.
-#ifndef ADVDIFF_VCOEF
-#define ADVDIFF_VCOEF 1
-#endif
   FdCoef<T> q1 = q1a, q2 = q2a, q3 = q3a;
   auto to_v = [](FdCoef<T>& c) {
     asm volatile("" : "+v"(c.kc));
 #pragma unroll
     for (int d = 0; d < 3; ++d) asm volatile("" : "+v"(c.k[d]));
   };
-  if constexpr (sizeof(T) == 8) {
-    if constexpr ((ADVDIFF_VCOEF & 1) != 0) to_v(q1);
-    if constexpr ((ADVDIFF_VCOEF & 2) != 0) to_v(q2);
-    if constexpr ((ADVDIFF_VCOEF & 4) != 0) to_v(q3);
-  }
+  if constexpr (sizeof(T) == 8) to_v(q1);
   using G = V3Geom<T, ORDER, NW, RPW>;
   constexpr int R = G::R, NR = 2 * R + 1, W = G::W, S1R = G::S1R, UW = G::UW, UH = G::UH;
   constexpr int TX = W - 4 * R, TY = S1R - 4 * R;
@@ -649,7 +641,7 @@ __device__ __forceinline__ void v6_march(
     const FdCoef<T>& q3) {
   // fp64: stage-1 coefficients in VGPRs, as in v3_march (no SGPR spill reloads)
   FdCoef<T> q1 = q1a;
-  if constexpr (sizeof(T) == 8 && (ADVDIFF_VCOEF & 1) != 0) {
+  if constexpr (sizeof(T) == 8) {
     asm volatile("" : "+v"(q1.kc));
 #pragma unroll
     for (int d = 0; d < 3; ++d) asm volatile("" : "+v"(q1.k[d]));
@@ -960,14 +952,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((
                                            q1, q2, q3);
 }
 
-// forced z-chunk length (ADVDIFF_STEP_ZCHUNK / advdiff_set_step_zchunk; 0 = the
-// pick_chunk_rounds model) — for chunk sweeps (bench/step_chunks.py)
-static int g_step_zchunk = -1;
-static int step_zchunk() {
-  if (g_step_zchunk < 0) g_step_zchunk = knob("STEP_ZCHUNK", 0);
-  return g_step_zchunk;
-}
-
 // Banded z schedule: with a whole number of z chunks per column the last round of
 // resident workgroups is often part-empty (8-GPU slab rank, 1024 x 1024 x 116 interior
 // planes, FD4: 817 columns x 2 chunks = 6.4 rounds of 256).  One long band of every
@@ -981,7 +965,6 @@ static int step_zchunk() {
 // construction).  ADVDIFF_STEP_BANDED / advdiff_set_step_banded: -1 (default) the
 // measured choice (uniform chunks for an unmeasured launch), 0 never, 1 always.  Results
 // are bitwise the same for every chunking.
-static int g_band_force[2] = {0, 0};  // forced (first band, later bands) for sweeps; 0 = model
 // process-wide setting (atomic: the C API is callable from any host thread); the pick's
 // own forced schedule is THREAD-local, so a launch from another thread during a
 // measurement keeps its own choice and a concurrent advdiff_set_step_banded survives
@@ -1061,11 +1044,13 @@ static Bands step_bands(int n, long long tiles, long long slots, int warm, int m
   return best;
 }
 
-static int g_step_edge = -1;
-static int step_edge() {  // v3 edge tiles (axis_tile): ADVDIFF_STEP_EDGE / advdiff_set_step_edge
-  if (g_step_edge < 0) g_step_edge = knob("STEP_EDGE", 1);
-  return g_step_edge;
-}
+// v3 edge tiles (axis_tile): always on since round 2 (the plain partition, their A/B
+// loser, was removed in round 6 with the other A/B-only knobs)
+constexpr int kStepEdge = 1;
+// fewest planes per z chunk: 16 (was 32) lets small grids fill one round of CUs
+// (201x199x200 FD4: 6 -> 7 chunks, 216 -> 252 groups, 51.6 -> 45.1 us per step); 512^3 and
+// 400x200x206 pick the same chunking either way (profiles/archive/heat3d_min_chunk_r2.log)
+constexpr int kStepMinChunk = 16;
 
 struct SArgs {
   const void* uin;
@@ -1105,36 +1090,26 @@ static bool sched_banded(int esize, int order, const SArgs& a) {
 template <typename T, int ORDER, int NW, int RPW, int VAR>
 static hipError_t launch_step(const SArgs& a) {
   constexpr int R = ORDER / 2;
-  const int edge = step_edge();
+  constexpr int edge = kStepEdge;
   const int gx = axis_tile_count(64, R, a.bx.xa0, a.bx.xa1, a.bx.xo0, a.bx.xo1, a.nx, edge);
   const int gy = axis_tile_count(NW * RPW, R, a.bx.ya0, a.bx.ya1, a.bx.yo0, a.bx.yo1, a.ny, edge);
   // z chunks: minimise (rounds of resident workgroups) x (chunk + 4R warm-up planes);
   // resident workgroups = CUs x occupancy of this instance (LDS / VGPR bound: 1-2 per CU)
   const int per_cu =
       occupancy_per_cu((const void*)diffusion3d_step_kernel<T, ORDER, NW, RPW, VAR>, 64 * NW);
-  // chunk floor 16 (was 32): lets small grids fill one round of CUs (201x199x200 FD4:
-  // 6 -> 7 chunks, 216 -> 252 groups, 51.6 -> 45.1 us per step); 512^3 and 400x200x206
-  // pick the same chunking either way (profiles/archive/heat3d_min_chunk_r2.log)
-  static const int minc = knob("STEP_MIN_CHUNK", 16);
+  constexpr int minc = kStepMinChunk;
   const int na = std::max(a.k1 - a.k0, 0), nb = std::max(a.k1b - a.k0b, 0);
   const long long slots = (long long)device_cus() * per_cu;
   StepSched sc{gx, gy, 0, 0, edge};
-  const int zforce = step_zchunk();
   dim3 grid;
-  if (zforce <= 0 && nb == 0 && na > 0 && sched_banded((int)sizeof(T), ORDER, a)) {
-    Bands bd = step_bands(na, (long long)gx * gy, slots, 4 * R, minc);
-    if (g_band_force[0] > 0) {  // forced split (advdiff_set_step_bands; band sweeps)
-      bd.zfirst = std::min(g_band_force[0], na);
-      bd.zchunk = std::max(g_band_force[1], 1);
-      bd.nbands = 1 + div_up(na - bd.zfirst, bd.zchunk);
-    }
+  if (nb == 0 && na > 0 && sched_banded((int)sizeof(T), ORDER, a)) {
+    const Bands bd = step_bands(na, (long long)gx * gy, slots, 4 * R, minc);
     sc.zfirst = bd.zfirst;
     sc.zchunk = bd.zchunk;
     sc.gza = bd.nbands;
     grid = dim3(gx * gy * bd.nbands, 1, 1);
   } else {
-    const int zc = zforce > 0 ? std::min(zforce, std::max(na, nb))
-                              : pick_chunk_rounds(na + nb, (long long)gx * gy, slots, 4 * R, minc);
+    const int zc = pick_chunk_rounds(na + nb, (long long)gx * gy, slots, 4 * R, minc);
     sc.gza = na > 0 ? div_up(na, zc) : 0;
     sc.zchunk = zc;
     grid = dim3(gx, gy, sc.gza + (nb > 0 ? div_up(nb, zc) : 0));
@@ -1167,87 +1142,31 @@ static hipError_t launch_step(const SArgs& a) {
 // Also rejected: prefetching NR planes ahead instead of 2 (FD4 equal, FD2 +1.6 %,
 // profiles/prefetch_ab_r3.log) and pacing the workgroups of an XCD so co-XCD tiles read
 // their shared halo rows together (no gain, profiles/pace_ab_r3.log).
-// Built instances: the order's default (FD4 VAR 3, FD2 VAR 23) and the plain kernel
-// (VAR 0) as the fallback; ADVDIFF_STEP_VAR / advdiff_set_step_var picks -1 (default) or 0.
-// VAR 7 and the cross-order variants (FD4 23, FD2 3) were removed after their A/Bs; the
-// template still takes any VAR for a new experiment.
-static int g_step_var = -2;
-static int step_var() {
-  if (g_step_var == -2) g_step_var = knob("STEP_VAR", -1);
-  return g_step_var;
-}
-
-// (build-time override of the defaults, for A/B libraries: scripts/build_ab_libs.sh with
-// -DADVDIFF_FD4_VAR=... / -DADVDIFF_FD2_VAR=....  Re-checked on the round-5 pitched layout,
-// bench/ab_step.py --pitch 4,1, one process: FD4 VAR 19 / 23 / 7 at 0.997 / 1.020 / 1.036 x
-// the VAR 3 time, FD2 VAR 7 / 19 at 1.031 / 0.993 x VAR 23 — the defaults stand;
-// profiles/r5/ab/var_pitched_ab.log.)
-#ifndef ADVDIFF_FD4_VAR
-#define ADVDIFF_FD4_VAR 3
-#endif
-#ifndef ADVDIFF_FD2_VAR
-#define ADVDIFF_FD2_VAR 23
-#endif
-template <typename T, int ORDER, int NW, int RPW>
-static hipError_t launch_step_var(const SArgs& a) {
-  constexpr int DEF = ORDER == 4 ? ADVDIFF_FD4_VAR : ADVDIFF_FD2_VAR;
-  const int v = step_var();
-  if (v < 0 || v == DEF) return launch_step<T, ORDER, NW, RPW, DEF>(a);
-  if (v == 0) return launch_step<T, ORDER, NW, RPW, 0>(a);
-  return hipErrorInvalidValue;
-}
+// Built instances: the order's default only (FD4 VAR 3, FD2 VAR 23; the plain kernel,
+// VAR 0, and the ADVDIFF_STEP_VAR switch were removed in round 6 — re-checked on the
+// round-5 pitched layout, one process: FD4 VAR 19 / 23 / 7 at 0.997 / 1.020 / 1.036 x the
+// VAR 3 time, FD2 VAR 7 / 19 at 1.031 / 0.993 x VAR 23, profiles/r5/ab/var_pitched_ab.log).
+// The template still takes any VAR for a new experiment.
+template <int ORDER>
+constexpr int kStepVar = ORDER == 4 ? 3 : 23;
 
 // Tile shape per order.  With the edge tiles (axis_tile), interleaved medians at 512^3:
 // FD4 16 waves x 2 rows (32 stage-1 rows) 662 us vs 715 us for 12 x 3; FD2 12 x 3 rows
 // 535 us vs 549 us for 16 x 2 (profiles/archive/step_cfgs_edge_r2.log).  48 rows overflow the
 // 16-bit DS offsets, 10 x 4 spills at 168 VGPRs.
-// fp32 tile (ADVDIFF_STEP_F32_TILE / advdiff_set_step_f32_tile): 4-B elements halve the
-// LDS planes and the register rings, so taller tiles fit: 0 = the fp64 shapes, 3 / 4 =
-// 16 waves x 3 / 4 rows (48 / 64 stage-1 rows: fewer redundant rim rows and halo re-reads
-// per output).  Round-5 A/B at 256^3-1024^3 (profiles/r5/ab/step_fp32_ab.log, bitwise
-// equal across the tiles): FD4 16 x 4 is 3-4 % faster at 384^3 / 512^3 but 4-6 % slower
-// at 640^3-1024^3, 16 x 3 wins at 256^3 / 640^3 only; FD2 is fastest on the fp64 shape at
-// every size but 1024^3 — so the default stays 0 (the fp64 shapes).
-static int g_step_f32_tile = -1;
-static int step_f32_tile() {
-  if (g_step_f32_tile < 0) g_step_f32_tile = knob("STEP_F32_TILE", 0);
-  return g_step_f32_tile;
-}
-
-// FD2 tile (ADVDIFF_STEP_FD2_TILE / advdiff_set_step_fd2_tile, round-5 A/B): 0 = 12 waves
-// x 3 rows (36 stage-1 rows, 114 KB of LDS: one workgroup per CU, 3 waves per SIMD); 1 =
-// 8 waves x 3 rows (24 rows, 77 KB: TWO workgroups per CU, 4 waves per SIMD — one
-// workgroup's barrier and LDS waits could overlap the other's arithmetic, for 3.5 % more
-// stage work and more halo re-reads).  Measured: 8 x 3 is 5-13 % SLOWER at 384^3-768^3
-// and 1.7 % faster at 1024^3 (profiles/r5/ab/step_tile_ab.log) — the default stays 12 x 3.
-// 2 = 12 waves x 4 rows (48 rows, 152 KB, 152 VGPRs: 13 % fewer VALU instructions per
-// output row and fewer halo re-reads; B planes on their own base registers, v3_march
-// SPLITB): +3.6 / +0.5 / -7.0 / +3.0 / +10.1 % at 384 / 512 / 640 / 768 / 1024^3 — the tile
-// quantisation decides, and where 12 x 4 wins the two-step launch wins by more
-// (profiles/r5/ab/step_tile_ab_12x4.log vs step2_sizes.log), so the default stays 12 x 3.
-// (FD4 12 waves x 3 rows re-checked after the round-5 SGPR fix: 161 VGPRs at 3 waves per
-// SIMD, 45 spill reloads left; 0.94 / 0.99 / 0.96 x the 16 x 2 speed at 384 / 512 /
-// 768^3 on pitched fields, bitwise equal — profiles/r5/ab/fd4_tile_ab.log; removed.)
-static int g_step_fd2_tile = -1;
-static int step_fd2_tile() {
-  if (g_step_fd2_tile < 0) g_step_fd2_tile = knob("STEP_FD2_TILE", 0);
-  return g_step_fd2_tile;
-}
-
+// fp32 uses the fp64 tile shapes.  Round-5 A/B at 256^3-1024^3 of taller fp32 tiles (16 x
+// 3 / 4 rows; profiles/r5/ab/step_fp32_ab.log, bitwise equal): FD4 16 x 4 3-4 % faster at
+// 384^3 / 512^3 but 4-6 % slower at 640^3-1024^3, FD2 fastest on the fp64 shape.  FD2 8 x 3
+// (two workgroups per CU) 5-13 % slower at 384^3-768^3; 12 x 4 (152 VGPRs) +3.6 / +0.5 /
+// -7.0 / +3.0 / +10.1 % at 384 / 512 / 640 / 768 / 1024^3, where the two-step launch wins by
+// more (profiles/r5/ab/step_tile_ab*.log); FD4 12 x 3 0.94-0.99 x (fd4_tile_ab.log).  The
+// alternatives and their switches were removed in round 6.
 template <typename T, int ORDER>
 static hipError_t dispatch_step(const SArgs& a) {
-  if constexpr (sizeof(T) == 4) {
-    const int t = step_f32_tile();
-    if (t == 3) return launch_step<T, ORDER, 16, 3, ORDER == 4 ? 3 : 23>(a);
-    if (t == 4) return launch_step<T, ORDER, 16, 4, ORDER == 4 ? 3 : 23>(a);
-  }
-  if constexpr (ORDER == 4) {
-    return launch_step_var<T, ORDER, 16, 2>(a);
-  } else {
-    if (step_fd2_tile() == 1) return launch_step<T, ORDER, 8, 3, 23>(a);
-    if (step_fd2_tile() == 2) return launch_step<T, ORDER, 12, 4, 23>(a);
-    return launch_step_var<T, ORDER, 12, 3>(a);
-  }
+  if constexpr (ORDER == 4)
+    return launch_step<T, ORDER, 16, 2, kStepVar<4>>(a);
+  else
+    return launch_step<T, ORDER, 12, 3, kStepVar<2>>(a);
 }
 
 // two-step FD2 launch (v6_march): 12 waves x 2 rows (24 stage-1 rows, 14 output rows;
@@ -1255,19 +1174,16 @@ static hipError_t dispatch_step(const SArgs& a) {
 template <typename T, int NW, int RPW>
 static hipError_t launch_step2x(const SArgs& a) {
   constexpr int R = 1, SH = 5 * R;
-  const int edge = step_edge();
+  constexpr int edge = kStepEdge;
   const int gx = axis_tile_count(64, R, a.bx.xa0, a.bx.xa1, a.bx.xo0, a.bx.xo1, a.nx, edge, SH);
   const int gy = axis_tile_count(NW * RPW, R, a.bx.ya0, a.bx.ya1, a.bx.yo0, a.bx.yo1, a.ny, edge,
                                  SH);
   const int per_cu =
       occupancy_per_cu((const void*)diffusion3d_step2x_kernel<T, NW, RPW>, 64 * NW);
-  static const int minc = knob("STEP_MIN_CHUNK", 16);
   const int na = std::max(a.k1 - a.k0, 0);
   const long long slots = (long long)device_cus() * per_cu;
   StepSched sc{gx, gy, 0, 0, edge};
-  const int zforce = step_zchunk();
-  const int zc = zforce > 0 ? std::min(zforce, na)
-                            : pick_chunk_rounds(na, (long long)gx * gy, slots, 10 * R, minc);
+  const int zc = pick_chunk_rounds(na, (long long)gx * gy, slots, 10 * R, kStepMinChunk);
   sc.gza = div_up(na, zc);
   sc.zchunk = zc;
   const FdCoef<T> q1 = fd_coef<T>(2, a.cx, a.cy, a.cz, a.dt, 1.0, true);
@@ -1280,12 +1196,6 @@ static hipError_t launch_step2x(const SArgs& a) {
 }
 
 }  // namespace advdiff
-
-extern "C" int advdiff_set_step_var(int v) {
-  const int old = advdiff::step_var();
-  advdiff::g_step_var = v;
-  return old;
-}
 
 // Host-only query of the band model (no GPU): out = {first band, later band length,
 // number of bands, modelled makespan in plane-times of the best split, of the best
@@ -1312,40 +1222,9 @@ extern "C" int advdiff_step_bands_plan(int n, long long tiles, long long slots, 
   return hipSuccess;
 }
 
-// Force the banded split (first band, later band length) of banded launches; first <= 0
-// returns to the model's split (step_bands).  For band sweeps (bench/band_sweep.py).
-extern "C" void advdiff_set_step_bands(int first, int rest) {
-  advdiff::g_band_force[0] = first;
-  advdiff::g_band_force[1] = rest;
-}
-
 extern "C" int advdiff_set_step_banded(int on) {
   const int old = advdiff::step_banded();
   advdiff::g_step_banded.store(on);
-  return old;
-}
-
-extern "C" int advdiff_set_step_f32_tile(int t) {
-  const int old = advdiff::step_f32_tile();
-  advdiff::g_step_f32_tile = t;
-  return old;
-}
-
-extern "C" int advdiff_set_step_fd2_tile(int t) {
-  const int old = advdiff::step_fd2_tile();
-  advdiff::g_step_fd2_tile = t;
-  return old;
-}
-
-extern "C" int advdiff_set_step_zchunk(int zc) {
-  const int old = advdiff::step_zchunk();
-  advdiff::g_step_zchunk = zc > 0 ? zc : 0;
-  return old;
-}
-
-extern "C" int advdiff_set_step_edge(int on) {
-  const int old = advdiff::step_edge();
-  advdiff::g_step_edge = on ? 1 : 0;
   return old;
 }
 
@@ -1584,8 +1463,6 @@ extern "C" int advdiff_preload_diffusion_fused(void) {
       hipFuncGetAttributes(&a, (const void*)diffusion3d_step_kernel<double, 4, 16, 2, 3>);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 4, 16, 2, 3>, 64 * 16);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 2, 12, 3, 23>, 64 * 12);
-  (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 2, 8, 3, 23>, 64 * 8);
-  (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 2, 12, 4, 23>, 64 * 12);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<float, 4, 16, 2, 3>, 64 * 16);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<float, 2, 12, 3, 23>, 64 * 12);
   (void)occupancy_per_cu((const void*)diffusion3d_step2x_kernel<double, 12, 2>, 64 * 12);

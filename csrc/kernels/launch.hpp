@@ -23,7 +23,7 @@ inline int knob(const char* name, int def);
 
 inline int pick_chunk(int nrange, long long xyblocks, int minc, int maxc) {
   if (nrange <= 0) return 1;
-  static const long long target = knob("TARGET_BLOCKS", (int)kTargetBlocks);
+  constexpr long long target = kTargetBlocks;
   long long want_chunks = (target + xyblocks - 1) / std::max<long long>(xyblocks, 1);
   long long c = (nrange + want_chunks - 1) / std::max<long long>(want_chunks, 1);
   c = std::max<long long>(c, minc);

@@ -165,26 +165,13 @@ def _load():
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = c_int
-        lib.advdiff_set_step_var.argtypes = [c_int]
-        lib.advdiff_set_step_var.restype = c_int
-        lib.advdiff_set_step_edge.argtypes = [c_int]
-        lib.advdiff_set_step_edge.restype = c_int
         lib.advdiff_set_b3_ver.argtypes = [c_int]
         lib.advdiff_set_b3_ver.restype = c_int
-        lib.advdiff_set_step_f32_tile.argtypes = [c_int]
-        lib.advdiff_set_step_f32_tile.restype = c_int
-        lib.advdiff_set_step_fd2_tile.argtypes = [c_int]
-        lib.advdiff_set_step_fd2_tile.restype = c_int
         lib.advdiff_step_bands_plan.argtypes = [c_int, ctypes.c_longlong, ctypes.c_longlong,
                                                 c_int, c_int, ctypes.POINTER(ctypes.c_longlong)]
         lib.advdiff_step_bands_plan.restype = c_int
-        lib.advdiff_set_step_bands.argtypes = [c_int, c_int]
-        lib.advdiff_set_step_bands.restype = None
         lib.advdiff_set_step_banded.argtypes = [c_int]
         lib.advdiff_set_step_banded.restype = c_int
-
-        lib.advdiff_set_step_zchunk.argtypes = [c_int]
-        lib.advdiff_set_step_zchunk.restype = c_int
         lib.advdiff_set_b3_pack.argtypes = [c_int]
         lib.advdiff_set_b3_pack.restype = c_int
         lib.advdiff_set_b3_tx.argtypes = [c_int]

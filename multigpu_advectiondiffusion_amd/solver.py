@@ -245,7 +245,7 @@ class Solver:
                 # RCCL — the same two-stream order; the reference's boundary-on-send-stream
                 # concurrency, MultiGPU/Diffusion3d_Baseline/main.c:118-122,209-260);
                 # off for the host-staged exchange, which blocks the host inside start
-                env = os.environ.get("ADVDIFF_BCOMM") or os.environ.get("ADVDIFF_BSTREAM")
+                env = os.environ.get("ADVDIFF_BCOMM")
                 boundary_on_comm = ((env == "1") if env
                                     else self.transport in ("ipc", "rccl"))
             # the boundary launch on the (high-priority) comm stream, between the wait for

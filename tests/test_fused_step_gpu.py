@@ -55,31 +55,6 @@ def test_fused_step_bitwise_equals_per_stage(dtype, order, case):
     assert (got.cpu().double() - out).abs().max().item() < tol
 
 
-@pytest.mark.parametrize("tile", [0, 3, 4])
-@pytest.mark.parametrize("order", [4, 2])
-@pytest.mark.parametrize("case", CASES)
-def test_fused_step_fp32_tiles_bitwise(tile, order, case):
-    """Every fp32 tile (advdiff_set_step_f32_tile: 0 the fp64 shapes, the default; 16 waves
-    x 3 / 4 rows) is bitwise the per-stage path."""
-    from multigpu_advectiondiffusion_amd.ops import _lib
-    lib = _lib.require()
-    nz, ny, nx, sx, k0, k1, zlo, zhi, border = case
-    g = torch.Generator().manual_seed(13)
-    u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).float().cuda()
-    c = (0.21, 0.17, 0.13)
-    dt = 0.9 / (2 * sum(c)) if order == 2 else 0.5 / sum(c)
-    exp = _per_stage(u, nx, ny, k0, k1, zlo, zhi, border, order, c, dt)
-    old = lib.advdiff_set_step_f32_tile(tile)
-    try:
-        got = u.clone()
-        stencil.diffusion3d_step(u, got, nx=nx, ny=ny, k0=k0, k1=k1, zlo=zlo, zhi=zhi,
-                                 border=border, order=order, cx=c[0], cy=c[1], cz=c[2], dt=dt)
-        torch.cuda.synchronize()
-    finally:
-        lib.advdiff_set_step_f32_tile(old)
-    assert torch.equal(got, exp), (got - exp).abs().max().item()
-
-
 @pytest.mark.parametrize("order", [4, 2])
 @pytest.mark.parametrize("case", CASES + [
     (200, 70, 130, 136, 3, 197, 3, 197, 3),   # many z chunks
@@ -195,35 +170,26 @@ def test_fused_step_box_bounds_match_reference():
         assert (got.cpu() - out).abs().max().item() < 1e-12, box
 
 
-@pytest.mark.parametrize("var", [-1, 0])
 @pytest.mark.parametrize("order", [4, 2])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_fused_step_odd_subrange_bitwise(var, order, dtype):
-    """The step kernel of each order (FD4: 16 waves x 2 rows, FD2: 12 x 3), both built
-    variants (advdiff_set_step_var: -1 the order's phase-overlap default, 0 the plain
-    kernel), is bit-identical to the per-stage path on a sub-range with frozen planes,
-    odd sizes and chunk lengths that are not a multiple of the march unroll."""
-    from multigpu_advectiondiffusion_amd.ops import _lib
-    lib = _lib.require()
+def test_fused_step_odd_subrange_bitwise(order, dtype):
+    """The step kernel of each order (FD4: 16 waves x 2 rows, FD2: 12 x 3) is bit-identical
+    to the per-stage path on a sub-range with frozen planes, odd sizes and chunk lengths
+    that are not a multiple of the march unroll."""
     nz, ny, nx, sx, k0, k1, zlo, zhi, border = (77, 53, 133, 136, 5, 70, 2, 74, 2)
     g = torch.Generator().manual_seed(5)
     u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).to(dtype).cuda()
     c = (0.21, 0.17, 0.13)
     dt = 0.9 / (2 * sum(c)) if order == 2 else 0.5 / sum(c)
     exp = _per_stage(u, nx, ny, k0, k1, zlo, zhi, border, order, c, dt)
-    old = lib.advdiff_set_step_var(var)
-    try:
-        for kk in ((k0, k1), (k0, k0 + 1), (k0, k0 + 11), (k0 + 3, k1)):
-            got = u.clone()
-            stencil.diffusion3d_step(u, got, nx=nx, ny=ny, k0=kk[0], k1=kk[1], zlo=zlo, zhi=zhi,
-                                     border=border, order=order, cx=c[0], cy=c[1], cz=c[2],
-                                     dt=dt)
-            torch.cuda.synchronize()
-            want = u.clone()
-            want[kk[0]:kk[1]] = exp[kk[0]:kk[1]]
-            assert torch.equal(got, want), (kk, (got - want).abs().max().item())
-    finally:
-        lib.advdiff_set_step_var(old)
+    for kk in ((k0, k1), (k0, k0 + 1), (k0, k0 + 11), (k0 + 3, k1)):
+        got = u.clone()
+        stencil.diffusion3d_step(u, got, nx=nx, ny=ny, k0=kk[0], k1=kk[1], zlo=zlo, zhi=zhi,
+                                 border=border, order=order, cx=c[0], cy=c[1], cz=c[2], dt=dt)
+        torch.cuda.synchronize()
+        want = u.clone()
+        want[kk[0]:kk[1]] = exp[kk[0]:kk[1]]
+        assert torch.equal(got, want), (kk, (got - want).abs().max().item())
 
 
 @pytest.mark.parametrize("order", [4, 2])
@@ -248,12 +214,11 @@ def test_fused_step_production_size_bitwise(order):
 @pytest.mark.parametrize("boxkind", ["slab", "interior", "edge_hi_x_lo_y", "edge_lo_x_hi_y"])
 @pytest.mark.parametrize("shape", [(40, 44, 70, 72), (24, 130, 300, 320), (20, 37, 61, 64)])
 def test_fused_step_edge_tiles_bitwise(order, boxkind, shape):
-    """Boundary-anchored edge tiles (axis_tile, the default) vs the plain partition: the
-    same values on every cell, no cell written twice or left out (output initialised with
-    a sentinel), for slab and Cartesian-view boxes (output >= 3R inside view edges that
-    are not global boundaries, as the solver's boxes are)."""
-    from multigpu_advectiondiffusion_amd.ops import _lib
-    lib = _lib.require()
+    """Boundary-anchored edge tiles (axis_tile): every cell of the output box written
+    exactly once with the reference value (output initialised with a sentinel), for slab
+    and Cartesian-view boxes (output >= 3R inside view edges that are not global
+    boundaries, as the solver's boxes are).  (Round 6 removed the plain-partition switch
+    this test used to compare against: the CPU reference box step is the oracle.)"""
     nz, ny, nx, sx = shape
     box = {"slab": None,
            "interior": (0, nx, 0, ny, 6, nx - 6, 6, ny - 6),
@@ -265,26 +230,16 @@ def test_fused_step_edge_tiles_bitwise(order, boxkind, shape):
     dt = 0.9 / (2 * sum(c)) if order == 2 else 0.5 / sum(c)
     kw = dict(nx=nx, ny=ny, k0=3, k1=nz - 3, zlo=2, zhi=nz - 2, border=3, order=order,
               cx=c[0], cy=c[1], cz=c[2], dt=dt, box=box)
-    outs = []
-    old = lib.advdiff_set_step_edge(1)
-    try:
-        for edge in (1, 0):
-            lib.advdiff_set_step_edge(edge)
-            got = torch.full_like(u, float("nan"))
-            stencil.diffusion3d_step(u, got, **kw)
-            torch.cuda.synchronize()
-            outs.append(got)
-    finally:
-        lib.advdiff_set_step_edge(old)
-    assert torch.equal(outs[0].isnan(), outs[1].isnan())
-    assert torch.equal(torch.nan_to_num(outs[0], 7.0), torch.nan_to_num(outs[1], 7.0))
-    if box is not None:
-        cpu = u.cpu()
-        ref_out = torch.full_like(cpu, float("nan"))
-        ref.diffusion3d_step_box(cpu, ref_out, nx, ny, 3, nz - 3, 2, nz - 2, box, order, *c, dt)
-        written = ~outs[0].isnan().cpu()
-        assert torch.equal(written, ~ref_out.isnan())
-        assert (outs[0].cpu()[written] - ref_out[written]).abs().max().item() < 1e-12
+    got = torch.full_like(u, float("nan"))
+    stencil.diffusion3d_step(u, got, **kw)
+    torch.cuda.synchronize()
+    cpu = u.cpu()
+    ref_out = torch.full_like(cpu, float("nan"))
+    rbox = box if box is not None else (3, nx - 3, 3, ny - 3, 0, nx, 0, ny)
+    ref.diffusion3d_step_box(cpu, ref_out, nx, ny, 3, nz - 3, 2, nz - 2, rbox, order, *c, dt)
+    written = ~got.isnan().cpu()
+    assert torch.equal(written, ~ref_out.isnan())
+    assert (got.cpu()[written] - ref_out[written]).abs().max().item() < 1e-12
 
 
 # ---- two steps per launch (v6_march, FD2): == two one-step launches, bit for bit ----
@@ -324,28 +279,20 @@ def test_two_step_kernel_bitwise_equals_two_steps(dtype, case):
     assert torch.equal(got, exp), (got - exp).abs().max().item()
 
 
-@pytest.mark.parametrize("edge", [1, 0])
-def test_two_step_kernel_box_and_tiles(edge):
-    """An explicit active / output box (a Cartesian block's view) and both tile partitions
-    (boundary-anchored edge tiles and the plain one)."""
-    from multigpu_advectiondiffusion_amd.ops import _lib
-    lib = _lib.require()
-    old = lib.advdiff_set_step_edge(edge)
-    try:
-        nz, ny, nx, sx = 60, 70, 150, 160
-        g = torch.Generator().manual_seed(9)
-        u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).cuda()
-        c = (0.21, 0.17, 0.13)
-        dt = 0.9 / (2 * sum(c))
-        box = (3, 140, 2, 66, 10, 120, 7, 60)
-        exp = _two_steps(u, nx, ny, 6, 54, 1, 59, 1, c, dt, box=box)
-        got = u.clone()
-        stencil.diffusion3d_step2x(u, got, nx=nx, ny=ny, k0=6, k1=54, zlo=1, zhi=59, border=1,
-                                   cx=c[0], cy=c[1], cz=c[2], dt=dt, box=box)
-        torch.cuda.synchronize()
-        assert torch.equal(got, exp), (got - exp).abs().max().item()
-    finally:
-        lib.advdiff_set_step_edge(old)
+def test_two_step_kernel_box_and_tiles():
+    """An explicit active / output box (a Cartesian block's view), edge tiles."""
+    nz, ny, nx, sx = 60, 70, 150, 160
+    g = torch.Generator().manual_seed(9)
+    u = torch.rand((nz, ny, sx), generator=g, dtype=torch.float64).cuda()
+    c = (0.21, 0.17, 0.13)
+    dt = 0.9 / (2 * sum(c))
+    box = (3, 140, 2, 66, 10, 120, 7, 60)
+    exp = _two_steps(u, nx, ny, 6, 54, 1, 59, 1, c, dt, box=box)
+    got = u.clone()
+    stencil.diffusion3d_step2x(u, got, nx=nx, ny=ny, k0=6, k1=54, zlo=1, zhi=59, border=1,
+                               cx=c[0], cy=c[1], cz=c[2], dt=dt, box=box)
+    torch.cuda.synchronize()
+    assert torch.equal(got, exp), (got - exp).abs().max().item()
 
 
 def test_solver_two_step_path_bitwise(monkeypatch):
