@@ -192,11 +192,15 @@ class Solver:
         thin = any(n // p < 3 * model.radius for n, p in zip(ashape, self.pgrid) if p > 1)
         if self.fused and (integrator != "ssprk3" or thin):
             self.fused = False  # LSRK, or blocks thinner than the wide (3R) halo
-        G = 3 * model.radius if self.fused else model.radius
+        elem = torch.empty((), dtype=dtype).element_size()
+        # multi-rank FD2 slabs: two RK3 steps per launch with a 6R-plane halo every second
+        # step (the same bytes per step as 3R every step, half the messages and launches);
+        # decided before the fields exist, since it sets the ghost width
+        self._mr2 = self._choose_multirank_step2(ashape, elem, pitch, pad_rows, exchange)
+        G = (6 if self._mr2 else 3) * model.radius if self.fused else model.radius
         self.ghost = G
         self.cd = CartesianDecomposition(ashape, self.pgrid, comm.rank, G)
         self.d = self.cd.axis(0)
-        elem = torch.empty((), dtype=dtype).element_size()
         ax = self.cd.alloc[-1]
         px, self.ypad = (_pitch_pads(pitch, grid.dims, self.device, elem,
                                      grid.cells // comm.size) if pad_rows else (0, 0))
@@ -299,6 +303,45 @@ class Solver:
         self._picked = True
         self._step2_on = self._pick_step2()
         self._pick_sched()
+
+    def _choose_multirank_step2(self, ashape, elem, pitch, pad_rows, exchange) -> bool:
+        """Several slab ranks, 3-D FD2 fused step: one step per launch (3R ghost planes,
+        one exchange per step) or two (diffusion_fused.hip v6_march on the interior and on
+        each boundary slab, 6R ghost planes, one exchange per two steps — bit-identical).
+        ADVDIFF_STEP2=0/1 forces; otherwise, on the GPU, the rank's interior launch is
+        timed both ways once per shape on scratch fields (advdiff_diffusion3d_step2_pick,
+        two per launch only if >= 3 % faster) and rank 0's answer is every rank's (the
+        ghost width must agree).  CPU runs default to one per launch."""
+        import os
+        m, comm = self.model, self.comm
+        if not (self.fused and comm.size > 1 and not self.cart and m.supports_step2
+                and self.integrator == "ssprk3" and exchange == "u"):
+            return False
+        G2 = 6 * m.radius
+        if ashape[0] // comm.size < G2:
+            return False  # a neighbour must own the 6R planes it sends
+        env = os.environ.get("ADVDIFF_STEP2")
+        if env in ("0", "1"):
+            return env == "1"
+        on = False
+        if self.device.type == "cuda" and self.kernel == "native" and comm.rank == 0:
+            cd = CartesianDecomposition(ashape, self.pgrid, 0, G2)
+            d = cd.axis(0)
+            inter, _, _ = d.split_ranges(m.border, G2)
+            if inter[1] > inter[0]:
+                px, ypad = (_pitch_pads(pitch, self.grid.dims, self.device, elem,
+                                        self.grid.cells // comm.size) if pad_rows else (0, 0))
+                sx = _row_pitch(cd.alloc[-1], elem) + px if pad_rows else cd.alloc[-1]
+                a = torch.zeros((d.alloc, self.grid.ny + ypad, sx), dtype=self.dtype,
+                                device=self.device)
+                b = torch.zeros_like(a)
+                off = d.start - G2
+                zlo = max(0, m.border - off)
+                zhi = min(d.alloc, self.grid.n_decomposed - m.border - off)
+                on = m.step2_preferred(a, b, inter[0], inter[1], zlo, zhi, m.stable_dt())
+                del a, b
+                torch.cuda.empty_cache()
+        return comm.allreduce_max(1.0 if on else 0.0) > 0.5
 
     def _ipc_multi(self) -> bool:
         return (self.device.type == "cuda" and self.comm.size > 1
@@ -616,10 +659,13 @@ class Solver:
         self.it += 1
 
     def step2_capable(self) -> bool:
-        """Two fixed-dt steps in one launch (single-rank 3-D FD2 heat: the model's step2,
-        bit-identical to two steps) — where that is the faster launch for this shape
-        (measured once per shape on the GPU at construction: _pick_step2)."""
-        return (self.fused and self.comm.size == 1 and not self.cart and self.du is None
+        """Two fixed-dt steps in one launch (3-D FD2 heat: the model's step2, bit-identical
+        to two steps) — where that is the faster launch for this shape (one rank: measured
+        once per shape on the GPU before the first run, _pick_step2; several slab ranks:
+        decided at construction, _choose_multirank_step2)."""
+        if self.comm.size > 1:
+            return self._mr2 and self._dt_dev is None
+        return (self.fused and not self.cart and self.du is None
                 and self.model.supports_step2 and self._dt_dev is None and self._pick2())
 
     def _pick_sched(self) -> None:
@@ -660,12 +706,69 @@ class Solver:
             self.step(dt)
             return
         ctx = stencil.use_torch_reference() if self.kernel == "torch" else contextlib.nullcontext()
+        if self.comm.size > 1:
+            with ctx:
+                self._step2_multi(dt)
+            return
         with ctx:
             self._pending.pop(id(self.u), None)
             lo, hi = self.full
             self.model.step2(self.u, self.un, lo, hi, self.zact[0], self.zact[1], dt)
             trace.sync_check(f"{self.model.name} fused 2-step [{lo},{hi})", self.device)
         self.u, self.un = self.un, self.u
+        for _ in range(2):  # same rounding as two steps
+            self.t += dt
+        self.it += 2
+
+    def _step2_multi(self, dt: float) -> None:
+        """Two steps of a slab rank in two-step launches (6R ghost planes): the interior
+        (owned planes >= 6R from a rank face: no ghost in their dependency cone) beside the
+        halo, then each boundary slab, then ONE exchange of 6R planes — the schedule of
+        _step_fused / _step_fused_bcomm with v6_march launches."""
+        pend = self._pending.pop(id(self.u), None)
+        z0, z1 = self.zact
+
+        def launch(rng):
+            lo, hi = rng
+            if hi > lo:
+                self.model.step2(self.u, self.un, lo, hi, z0, z1, dt)
+                trace.sync_check(f"{self.model.name} fused 2-step [{lo},{hi})", self.device)
+
+        if self.bcomm:
+            cur = torch.cuda.current_stream(self.device)
+            cs = self.comm_stream
+            cs.wait_stream(cur)
+            with trace.range_("interior"):
+                launch(self.interior)
+            with torch.cuda.stream(cs):
+                if pend is not None:
+                    pend.wait()
+                with trace.range_("boundary"):
+                    for rng in self.boundary:
+                        launch(rng)
+                bdone = torch.cuda.Event()
+                bdone.record(cs)
+                self.u, self.un = self.un, self.u
+                with trace.range_("halo_start"):
+                    self._pending[id(self.u)] = self.halo.start(self.u, after_event=False)
+            cur.wait_event(bdone)
+        else:
+            if self.overlap:
+                with trace.range_("interior"):
+                    launch(self.interior)
+                with trace.range_("halo_wait"):
+                    if pend is not None:
+                        pend.wait()
+                with trace.range_("boundary"):
+                    for rng in self.boundary:
+                        launch(rng)
+            else:
+                if pend is not None:
+                    pend.wait()
+                launch(self.full)
+            self.u, self.un = self.un, self.u
+            with trace.range_("halo_start"):
+                self._pending[id(self.u)] = self.halo.start(self.u)
         for _ in range(2):  # same rounding as two steps
             self.t += dt
         self.it += 2

@@ -315,3 +315,40 @@ def test_ipc_boundary_on_comm_bitwise(kind, world, decomp):
         out = spawn_local(world, _run_bcomm, kind, 17, decomp, graph, device="cuda",
                           transport="ipc", timeout=240)[0]
         assert np.array_equal(out, ref), (kind, world, decomp, graph, np.abs(out - ref).max())
+
+
+def _run_step2(comm, steps, overlap, graph, flag):  # noqa: D103
+    if flag is None:
+        os.environ.pop("ADVDIFF_STEP2", None)
+    else:
+        os.environ["ADVDIFF_STEP2"] = flag
+    model, grid, ic = _make("diff3o2")
+    bc = None
+    if overlap == "plain":
+        overlap, bc = True, False
+    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, overlap=overlap,
+               boundary_on_comm=bc)
+    if flag == "1":
+        assert s._mr2 and s.ghost == 6 and s.step2_capable()
+    s.run(iters=steps, graph=graph)
+    g = s.gather()
+    assert comm.ipc().errors() == 0
+    return s._mr2, (None if g is None else g.copy())
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("overlap", [True, "plain", False])
+def test_ipc_multirank_two_step_bitwise(world, overlap):
+    """Multi-rank FD2 with two steps per launch (v6_march on the interior and on each
+    boundary slab, 6R ghost planes exchanged every second step): bitwise the one-rank run,
+    odd step count (a one-step launch in the 6R layout at the end), eager and graph-
+    replayed, all three schedules; and the measured choice (ADVDIFF_STEP2 unset) agrees on
+    every rank."""
+    ref = _reference("diff3o2", 17)
+    for graph in (False, True):
+        for flag in ("1", None):
+            out = spawn_local(world, _run_step2, 17, overlap, graph, flag, device="cuda",
+                              transport="ipc", timeout=240)
+            assert len({o[0] for o in out}) == 1
+            g = out[0][1]
+            assert np.array_equal(g, ref), (world, overlap, graph, flag, np.abs(g - ref).max())
