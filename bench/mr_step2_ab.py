@@ -17,6 +17,8 @@ the rank shape (advdiff_diffusion3d_step2_pick on the interior, the rule
 Solver._choose_multirank_step2 applies).
 
     python bench/mr_step2_ab.py [--owned 128] [--nx 1024] [--rounds 5] [--steps 20]
+    python bench/mr_step2_ab.py --order 4   # the FD4 slab rank's step (one per launch,
+                                            # 3R = 6 ghost planes): interior + boundary
 """
 import argparse
 import json
@@ -36,7 +38,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--pitch", default="4,1")
+    ap.add_argument("--order", type=int, default=2, choices=[2, 4])
     a = ap.parse_args()
+    if a.order == 4:
+        return fd4_rank(a)
     px, py = (int(v) for v in a.pitch.split(","))
     n, own = a.nx, a.owned
     c = (1.0, 1.0, 1.0)
@@ -113,6 +118,62 @@ def main():
            "solver_pick_two_step": bool(inter),
            "one_gpu_512_us": round(t5, 1), "one_gpu_512_mlups": round(m ** 3 / t5, 1)}
     print(json.dumps(out), flush=True)
+
+
+def fd4_rank(a):
+    """FD4 slab rank per step: interior launch + one launch of both 3R-plane boundary
+    slabs, vs the same cells in one launch (what the rank would cost without the overlap
+    split) and the one-GPU 512^3 step."""
+    px, py = (int(v) for v in a.pitch.split(","))
+    n, own, G = a.nx, a.owned, 6
+    nz = own + 2 * G
+    kw = dict(nx=n, ny=n, border=2, order=4, cx=1.0, cy=1.0, cz=1.0, dt=0.01)
+    pair = [torch.rand((nz, n + py, n + px), dtype=torch.float64, device="cuda")]
+    pair.append(pair[0].clone())
+
+    def split(k):
+        for _ in range(k):
+            stencil.diffusion3d_step(pair[0], pair[1], k0=2 * G, k1=nz - 2 * G, zlo=0, zhi=nz, **kw)
+            stencil.diffusion3d_step(pair[0], pair[1], k0=G, k1=2 * G, k0b=nz - 2 * G,
+                                     k1b=nz - G, zlo=0, zhi=nz, **kw)
+            pair.reverse()
+
+    def whole(k):
+        for _ in range(k):
+            stencil.diffusion3d_step(pair[0], pair[1], k0=G, k1=nz - G, zlo=0, zhi=nz, **kw)
+            pair.reverse()
+
+    def inter(k):
+        for _ in range(k):
+            stencil.diffusion3d_step(pair[0], pair[1], k0=2 * G, k1=nz - 2 * G, zlo=0, zhi=nz, **kw)
+            pair.reverse()
+
+    def bnd(k):
+        for _ in range(k):
+            stencil.diffusion3d_step(pair[0], pair[1], k0=G, k1=2 * G, k0b=nz - 2 * G,
+                                     k1b=nz - G, zlo=0, zhi=nz, **kw)
+            pair.reverse()
+
+    def timed(fn):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn(a.steps)
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / a.steps
+
+    fns = {"split": split, "whole": whole, "interior": inter, "boundary": bnd}
+    for f in fns.values():
+        f(10)
+    best = {k: 1e30 for k in fns}
+    for _ in range(a.rounds):
+        for k, f in fns.items():
+            best[k] = min(best[k], timed(f))
+    cells = own * n * n
+    print(json.dumps({"order": 4, "rank_block": [n, n, own],
+                      **{f"{k}_us": round(v, 1) for k, v in best.items()},
+                      "split_mlups": round(cells / best["split"], 1),
+                      "whole_mlups": round(cells / best["whole"], 1)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -14,5 +14,12 @@ case "$1" in
       "pytest_gpu|900|$PT -m gpu tests" \
       "smoke|300|python -c 'import __graft_entry__ as g; g.smoke()'" \
       "bench|600|python -u bench.py" ;;
+  shapes)  # multi-rank FD2 two-step (tests + slab-rank A/B), FD4 per-rank shapes (A/B + PMC)
+    bash scripts/gpu_steps.sh r6/shapes \
+      "mr2_tests|600|$PT tests/test_ipc_gpu.py -k 'two_step'" \
+      "mr2_ab|300|python -u bench/mr_step2_ab.py" \
+      "fd4_rank|300|python -u bench/mr_step2_ab.py --order 4" \
+      "banded_fd4|400|python -u bench/banded_ab.py --cases 512,slab8,r4x2,1024 --orders 4" \
+      "pmc_shapes|600|PMC_OUT=gpurun_out/r6/pmc_shapes PMC_TARGETS='fused slab8_int slab8_bnd r4x2_int cube1024' PMC_ARGS='--pitch 4,1' bash scripts/pmc_r5.sh" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
