@@ -454,7 +454,7 @@ def preflight_candidates(args, n, on_gpu, transports, heat_spec, burgers_spec):
         return {m: [(p, t) for mm, p, t in allc if mm == m] for m in models}, None
     verdict = {}
     dev = "cuda" if on_gpu else "cpu"
-    for fam in ("nccl", "gloo"):
+    for fam in ("gloo", "nccl"):  # ipc first: its pair preflight bounds itself
         cs = [c for c in allc if family(c[2]) == fam]
         if not cs:
             continue

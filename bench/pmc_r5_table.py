@@ -16,10 +16,22 @@ import sys
 
 # compulsory bytes read per dispatch by profile_target.py (n^3 fp64 fields)
 COMPULSORY = {"copy": 512 ** 3 * 8, "fused": 512 ** 3 * 8, "fused2": 512 ** 3 * 8,
-              "step2x": 512 ** 3 * 8, "burgers": 2 * 256 ** 3 * 8}
+              "step2x": 512 ** 3 * 8, "burgers": 2 * 256 ** 3 * 8,
+              # round 6, per-rank shapes of the 8-GPU run (profile_target.py): the planes
+              # each launch reads (its outputs +- 3R)
+              "slab8_int": 128 * 1024 * 1024 * 8, "slab8_bnd": 36 * 1024 * 1024 * 8,
+              "r4x2_int": 256 * 518 * 1024 * 8, "cube1024": 1024 ** 3 * 8}
 WHAT = {"copy": "copy_box 512³ (calibration)", "fused": "fused FD4 step 512³",
         "fused2": "fused FD2 step 512³", "step2x": "FD2 two steps per launch 512³",
-        "burgers": "WENO5-Z + viscous stage 256³"}
+        "burgers": "WENO5-Z + viscous stage 256³",
+        "slab8_int": "FD4, 8-GPU slab rank 1024²×(128+12), interior launch (116 planes)",
+        "slab8_bnd": "FD4, 8-GPU slab rank, both 6-plane boundary slabs (one launch)",
+        "r4x2_int": "FD4, 4×2×1 rank 1024×518×268, interior launch (244 planes)",
+        "cube1024": "FD4, 1024³ (one launch)"}
+# output cells per dispatch (for instructions per cell)
+CELLS = {"copy": 512 ** 3, "fused": 508 ** 3, "fused2": 510 ** 3, "step2x": 510 ** 3,
+         "burgers": 250 ** 3, "slab8_int": 116 * 1020 * 1020, "slab8_bnd": 12 * 1020 * 1020,
+         "r4x2_int": 244 * 514 * 1020, "cube1024": 1020 ** 3}
 
 
 def counters(root, tgt):
@@ -57,9 +69,10 @@ def times(root, tgt):
 def main():
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_r5"
     print("| kernel | µs min / median (trace) | clock GHz | VALU busy | issuing | parked (waitcnt / barrier) "
-          "| ready, not issued | VALU instr | LDS instr | SALU instr | read B / compulsory |")
-    print("|---|---|---|---|---|---|---|---|---|---|---|")
-    for tgt in ("copy", "fused", "fused2", "step2x", "burgers"):
+          "| ready, not issued | VALU instr | LDS instr | SALU instr | read B / compulsory "
+          "| VALU lane-ops / cell | µs per M cells |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|")
+    for tgt in WHAT:
         c = counters(root, tgt)
         if not c:
             continue
@@ -72,7 +85,8 @@ def main():
               f"{clock_ghz(root, tgt):.2f} | {busy:.0%} | {c.get('SQ_ACTIVE_INST_ANY', 0) / wc:.0%} | "
               f"{c.get('SQ_WAIT_ANY', 0) / wc:.0%} | {c.get('SQ_WAIT_INST_ANY', 0) / wc:.0%} | "
               f"{c.get('SQ_INSTS_VALU', 0):.3g} | {c.get('SQ_INSTS_LDS', 0):.3g} | "
-              f"{c.get('SQ_INSTS_SALU', 0):.3g} | {rd / COMPULSORY[tgt]:.2f} |")
+              f"{c.get('SQ_INSTS_SALU', 0):.3g} | {rd / COMPULSORY[tgt]:.2f} | "
+              f"{c.get('SQ_INSTS_VALU', 0) * 64 / CELLS[tgt]:.0f} | {tmin / CELLS[tgt] * 1e6:.2f} |")
 
 
 if __name__ == "__main__":

@@ -330,7 +330,8 @@ def _run_session(spec, rank, world, session, init_s, cand_s, log):
 
 def run_preflight(cands, models, *, device: str, backend: str, steps: int = 2,
                   cand_s: float = 60.0, init_s: float = 90.0, total_s: float = 300.0,
-                  op_timeout: float = 120.0, check: bool = True, log=None) -> dict:
+                  op_timeout: float = 120.0, check: bool = True, log=None,
+                  max_hangs: int = 2) -> dict:
     """Exercise every candidate in hang-isolated child sessions (module doc).
 
     cands: [(mkey, pgrid, transport)] — mkey names an entry of `models`:
@@ -338,7 +339,9 @@ def run_preflight(cands, models, *, device: str, backend: str, steps: int = 2,
     children's process-group backend ("nccl" for rccl candidates, "gloo" otherwise).
     Returns {key: "ok" | failure text} for every candidate, the same on every rank (the
     children agree over their control group; a candidate that hung is failed on every
-    rank, because every rank's session ends at it).  Call it on every rank, before the
+    rank, because every rank's session ends at it).  After `max_hangs` hangs the family's
+    remaining candidates are not run (a transport that deadlocks twice is not trusted,
+    and each hang costs cand_s of the run's budget).  Call it on every rank, before the
     caller touches the GPU."""
     log = log or (lambda m: print(m, file=sys.stderr, flush=True))
     rank = int(os.environ.get("RANK", "0"))
@@ -366,9 +369,11 @@ def run_preflight(cands, models, *, device: str, backend: str, steps: int = 2,
             verdict[k] = v
             if v != "ok":
                 failed[k] = v
-        if dead_at_start or time.monotonic() > t_end:
+        hangs = sum(v.startswith("hang") for v in verdict.values())
+        if dead_at_start or time.monotonic() > t_end or hangs >= max_hangs:
             why = ("the preflight process group did not start" if dead_at_start
-                   else f"preflight budget of {total_s:g} s spent")
+                   else f"preflight budget of {total_s:g} s spent" if hangs < max_hangs
+                   else f"{hangs} candidates of this transport family hung")
             for c in todo:
                 if c["key"] not in verdict:
                     verdict[c["key"]] = f"not run: {why}"
