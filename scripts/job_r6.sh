@@ -21,5 +21,8 @@ case "$1" in
       "fd4_rank|300|python -u bench/mr_step2_ab.py --order 4" \
       "banded_fd4|400|python -u bench/banded_ab.py --cases 512,slab8,r4x2,1024 --orders 4" \
       "pmc_shapes|600|PMC_OUT=gpurun_out/r6/pmc_shapes PMC_TARGETS='fused slab8_int slab8_bnd r4x2_int cube1024' PMC_ARGS='--pitch 4,1' bash scripts/pmc_r5.sh" ;;
+  reh8)  # the whole N = 8 flow (preflight, tuning, checks, deadline) with 8 ipc ranks on one GPU
+    bash scripts/gpu_steps.sh r6/reh8 \
+      "reh8|600|$SH $R --nproc-per-node 8 --master-port 29608 bench.py --gpus 8 --steps 10 --warmup 3" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
