@@ -384,6 +384,7 @@ def main(argv=None) -> int:
     os.environ.setdefault("ADVDIFF_COMM_TIMEOUT", str(int(max(dl.remaining(), 0) + 120)))
     rank = int(os.environ.get("RANK", "0") or 0)
     dl.on_expire = (lambda d: report_partial(d)) if rank == 0 else None
+    dl.heartbeat_s = 60.0 if rank == 0 else 0.0
     dl.arm()
     STATE["deadline"] = dl
     try:

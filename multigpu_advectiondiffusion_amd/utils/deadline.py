@@ -11,7 +11,10 @@ rank arms a deadline below the driver's:
 * `deadline`: a Python timer thread runs `on_expire` (rank 0 prints the partial result)
   and ends the process with `exit_code` via os._exit — no teardown that could block;
 * SIGUSR1 also dumps the stacks (`launch.launch_cmd` sends it to ranks that are still
-  alive when it gives up on a run).
+  alive when it gives up on a run);
+* heartbeat (optional, rank 0): one stderr line every `heartbeat_s` naming the phase, so
+  a long phase (the Burgers torch self-check: minutes with 8 ranks on one GPU) is not
+  mistaken for a hang by a supervisor that watches the output.
 
 The clock starts when the launcher started, not this process: under torchrun (or
 bench.py's own self-launch) the parent's creation time, so the deadline is measured the
@@ -49,14 +52,16 @@ class Deadline:
     """Arm with `arm()`; `remaining()` in seconds; `phase` names what runs now."""
 
     def __init__(self, seconds: float, start: float | None = None, on_expire=None,
-                 exit_code: int = 124, dump_s: float = 15.0):
+                 exit_code: int = 124, dump_s: float = 15.0, heartbeat_s: float = 0.0):
         self.seconds = float(seconds)
         self.start = launch_start_time() if start is None else float(start)
         self.on_expire = on_expire
         self.exit_code = int(exit_code)
         self.dump_s = float(dump_s)
         self.phase = "start"
+        self.heartbeat_s = float(heartbeat_s)
         self._timer = None
+        self._stop = threading.Event()
 
     @property
     def at(self) -> float:
@@ -76,9 +81,17 @@ class Deadline:
         self._timer = threading.Timer(max(left, 1.0), self._fire)
         self._timer.daemon = True
         self._timer.start()
+        if self.heartbeat_s > 0:
+            threading.Thread(target=self._beat, daemon=True).start()
         return self
 
+    def _beat(self):
+        while not self._stop.wait(self.heartbeat_s):
+            print(f"[deadline] {time.time() - self.start:6.0f} s since launch, phase "
+                  f"'{self.phase}', {self.remaining():.0f} s left", file=sys.stderr, flush=True)
+
     def cancel(self):
+        self._stop.set()
         faulthandler.cancel_dump_traceback_later()
         if self._timer is not None:
             self._timer.cancel()

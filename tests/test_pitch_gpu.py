@@ -130,3 +130,16 @@ def test_pitched_fields_gather_with_ghosts():
         s.run(iters=3, dt=m.stable_dt())
     ga, gb = a.gather_with_ghosts(), b.gather_with_ghosts()
     assert ga.shape == gb.shape and np.array_equal(ga, gb)
+
+
+@pytest.mark.parametrize("shape", [(256, 256, 256), (257, 256, 256), (256, 256, 257)])
+def test_sizing_matches_solver_memory_at_the_pitch_threshold(shape):
+    """utils/sizing.solver_bytes applies the pitch rule to the same quantity the Solver
+    does (global cells per rank, ghosts excluded): equal to Solver.memory_bytes() at,
+    and just above, the 128 MiB field threshold (round-5 advisor finding)."""
+    from multigpu_advectiondiffusion_amd.utils.sizing import solver_bytes
+    grid = Grid(shape, (1.0,) * 3)
+    s = Solver(Diffusion(K=1.0, order=4), grid, dtype=torch.float64, device="cuda",
+               ic="sine")
+    alloc = (s.d.alloc, grid.ny, grid.nx)
+    assert s.memory_bytes() == solver_bytes(alloc, 8, 2, cells_per_rank=grid.cells)
