@@ -424,12 +424,14 @@ def skip_note(comm, what, need_s):
 
 def phase(comm, name):
     """Enter a bench phase: progress line, deadline bookkeeping, fault injection
-    (ADVDIFF_FAULT=hang:phase:<name> makes the last rank sleep there: tests)."""
+    (ADVDIFF_FAULT=hang:phase:<prefix> makes the last rank sleep in the first phase whose
+    name starts with <prefix>: tests)."""
     dl = STATE["deadline"]
     if dl is not None:
         dl.phase = name
     progress(comm, name)
-    if (os.environ.get("ADVDIFF_FAULT", "") == f"hang:phase:{name.split(':')[0]}"
+    f = os.environ.get("ADVDIFF_FAULT", "")
+    if (f.startswith("hang:phase:") and name.startswith(f[len("hang:phase:"):])
             and comm.rank == comm.size - 1):
         while True:
             time.sleep(3600)

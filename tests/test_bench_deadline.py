@@ -4,9 +4,11 @@
   the last rank's child sleeps, its peers block in the exchange) is dropped with a
   recorded reason and the run completes on the remaining candidates — within the
   preflight's per-candidate limit, not the process group's timeout.
-* A run that hangs after the headline phase (ADVDIFF_FAULT=hang:phase:fd2) ends at the
-  bench deadline: rank 0 prints the JSON line with the finished heat result and the
-  phase it stopped in, every rank dumps its stacks, and the exit code is non-zero.
+* A run that hangs after the headline window (ADVDIFF_FAULT=hang:phase:heat: bitwise, the
+  N-rank vs one-GPU check) ends at the bench deadline: rank 0 prints the JSON line with
+  the timed heat result and the phase it stopped in, every rank dumps its stacks, and the
+  exit code is non-zero.  (Optional phases that the time left cannot cover are skipped:
+  the 45 s deadline of the test skips FD2 and Burgers.)
 * The preflight itself: verdicts agree on every rank and a candidate whose ranks compute
   a wrong solution is rejected against the one-rank hash.
 """
@@ -56,14 +58,15 @@ def test_hanging_candidate_is_dropped_and_reported():
 
 def test_deadline_prints_partial_result_and_fails():
     r, secs = _bench(["--gpus", "2", "--no-burgers", "--deadline", "45"] + SMALL,
-                     {"ADVDIFF_FAULT": "hang:phase:fd2"}, timeout=200)
+                     {"ADVDIFF_FAULT": "hang:phase:heat: bitwise"}, timeout=200)
     assert r.returncode != 0
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout
     res = lines[0]
-    assert res["status"].startswith("incomplete") and "'fd2" in res["status"], res["status"]
-    assert res["value"] > 0 and res["n_gpus"] == 2          # the heat phase had finished
-    assert res["bitwise_vs_1gpu"]["heat"] is True
+    assert res["status"].startswith("incomplete") and "'heat: bitwise" in res["status"], \
+        res["status"]
+    assert res["value"] > 0 and res["n_gpus"] == 2          # the timed window had finished
+    assert res["linf_vs_exact"] <= res["linf_bound"]
     assert "fd2_7pt" not in res
     # every rank dumped its stacks before the end (faulthandler)
     assert r.stderr.count("Most recent call first") >= 2 or r.stderr.count("Thread 0x") >= 2, \
