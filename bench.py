@@ -471,9 +471,10 @@ def preflight_candidates(args, n, on_gpu, transports, heat_spec, burgers_spec):
                                      log=lambda m: print(m, file=sys.stderr, flush=True)))
         if int(os.environ.get("RANK", "0")) == 0:
             print(f"bench [{time.perf_counter() - _T0:7.1f} s] preflight ({fam}): "
-                  f"{sum(v == 'ok' for k, v in verdict.items())} ok of {len(verdict)} "
+                  f"{sum(v.startswith('ok') for v in verdict.values())} ok of {len(verdict)} "
                   f"in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
-    passed = {m: [(p, t) for mm, p, t in allc if mm == m and verdict.get(cand_key(m, p, t)) == "ok"]
+    passed = {m: [(p, t) for mm, p, t in allc
+                  if mm == m and str(verdict.get(cand_key(m, p, t))).startswith("ok")]
               for m in models}
     return passed, verdict
 

@@ -217,7 +217,7 @@ def _port_file(session: int) -> str:
     return os.path.join(tempfile.gettempdir(), f"advdiff_preflight_{os.getuid()}_{tag}.port")
 
 
-def _shared_port(rank: int, session: int, wait_s: float = 60.0) -> int:
+def _shared_port(rank: int, session: int, wait_s: float = 180.0) -> int:
     """Rendezvous port of a child session: rank 0 picks a free one and publishes it in a
     file (atomic rename) that the other ranks of this launch poll."""
     path = _port_file(session)
@@ -346,6 +346,19 @@ def run_preflight(cands, models, *, device: str, backend: str, steps: int = 2,
     log = log or (lambda m: print(m, file=sys.stderr, flush=True))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    try:
+        return _preflight(cands, models, device, backend, steps, cand_s, init_s, total_s,
+                          op_timeout, check, log, max_hangs, rank, world)
+    except (OSError, TimeoutError) as e:
+        # the preflight machinery itself failed (no rendezvous file from rank 0, no port):
+        # nothing was learnt about the candidates — the caller keeps them all, as before
+        # the preflight existed, and records why
+        log(f"preflight: unavailable ({type(e).__name__}: {e}); candidates kept unverified")
+        return {cand_key(m, p, t): "ok (unverified: preflight unavailable)" for m, p, t in cands}
+
+
+def _preflight(cands, models, device, backend, steps, cand_s, init_s, total_s, op_timeout,
+               check, log, max_hangs, rank, world) -> dict:
     todo = [{"key": cand_key(m, p, t), "mkey": m, "pgrid": p, "transport": t}
             for m, p, t in cands]
     verdict, failed = {}, {}
