@@ -24,5 +24,8 @@ case "$1" in
   reh8)  # the whole N = 8 flow (preflight, tuning, checks, deadline) with 8 ipc ranks on one GPU
     bash scripts/gpu_steps.sh r6/reh8 \
       "reh8|600|$SH $R --nproc-per-node 8 --master-port 29608 bench.py --gpus 8 --steps 10 --warmup 3" ;;
+  rcclfail)  # RCCL refuses two ranks on one GPU: the real RCCL error path of the preflight
+    bash scripts/gpu_steps.sh r6/rcclfail \
+      "reh2_rccl|400|$SH $R --nproc-per-node 2 --master-port 29612 bench.py --gpus 2 --steps 10 --warmup 3 --sustained-steps 0 --transport rccl --no-burgers" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac

@@ -503,4 +503,3 @@ def test_burgers3d_fp32_packed_pairs(tx, weno_z, visc, mode, ranges):
     if not ls:
         scale = _burgers_scale(inp, u0, a, b, 1e-3, rd, vv)
         assert err <= _fp32_bound(scale, 64), (err, scale)
-
