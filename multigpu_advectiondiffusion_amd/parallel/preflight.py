@@ -169,11 +169,16 @@ def _child_main(spec_path: str) -> int:
             # one-rank solution of the same grid (rank 0, single-process solver)
             h1 = None
             if rank == 0:
-                single = Comm(device=str(comm.device))
-                s1 = _solver(spec["models"][mkey], single, None, None)
-                s1.run(iters=spec["steps"], dt=s1.model.stable_dt())
-                h1 = int(s1.bit_hash())
-                del s1
+                try:
+                    single = Comm(device=str(comm.device))
+                    s1 = _solver(spec["models"][mkey], single, None, None)
+                    s1.run(iters=spec["steps"], dt=s1.model.stable_dt())
+                    h1 = int(s1.bit_hash())
+                    del s1
+                except Exception as e:  # noqa: BLE001 - e.g. the whole grid does not fit
+                    print(f"preflight: no one-rank reference for {mkey} "
+                          f"({type(e).__name__}: {e}); ranks are still compared with each "
+                          "other", file=sys.stderr, flush=True)
                 if comm.device.type == "cuda":
                     torch.cuda.empty_cache()
             ref_hash[mkey] = agree(h1)[0]
@@ -252,7 +257,9 @@ def _reader(stream, q):
 
 
 def _run_session(spec, rank, world, session, init_s, cand_s, log):
-    """One child session.  Returns (closed_keys: {key: verdict}, agreed: dict | None)."""
+    """One child session.  Returns (closed: {key: verdict} of the candidates it finished,
+    agreed: the children's merged failure records, or None if the session did not end
+    cleanly, dead_at_start: it ended before any candidate began)."""
     port = _shared_port(rank, session)
     fd, path = tempfile.mkstemp(prefix="advdiff_pf_", suffix=".json")
     with os.fdopen(fd, "w") as f:
