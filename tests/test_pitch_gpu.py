@@ -132,6 +132,7 @@ def test_pitched_fields_gather_with_ghosts():
     assert ga.shape == gb.shape and np.array_equal(ga, gb)
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("shape", [(256, 256, 256), (257, 256, 256), (256, 256, 257)])
 def test_sizing_matches_solver_memory_at_the_pitch_threshold(shape):
     """utils/sizing.solver_bytes applies the pitch rule to the same quantity the Solver
