@@ -623,7 +623,9 @@ def run(args) -> int:
                                       f"{linf2:.3e} > {bound2:.3e}")
 
     # ---- secondary: 3-D Burgers WENO5-Z + C∇²u, fp64 ----------------------------------
-    if not args.no_burgers and (note := skip_note(comm, "the Burgers run", 150.0)):
+    if not args.no_burgers and not passed.get("burgers"):
+        result["burgers3d"] = {"skipped": "no (grid, transport) candidate passed the preflight"}
+    elif not args.no_burgers and (note := skip_note(comm, "the Burgers run", 150.0)):
         result["burgers3d"] = {"skipped": note}
     elif not args.no_burgers:
         bgrid = Grid(bshape, (2.0, 2.0, 2.0))
