@@ -33,6 +33,7 @@ master port and the world size (all ranks run on one node: bench.py's contract).
 """
 from __future__ import annotations
 
+import glob
 import json
 import os
 import queue
@@ -282,11 +283,19 @@ def _run_session(spec, rank, world, session, init_s, cand_s, log):
     closed, agreed, open_key = {}, None, None
     limit = time.monotonic() + init_s
     why = None
+    ready = False
+    # a child that dies before its process group is up leaves a marker next to the port
+    # file, so the other ranks' children (blocked in the rendezvous) are ended at once
+    # instead of after init_s
+    dead_mark = f"{_port_file(session)}.dead"
     try:
         while True:
             try:
                 msg = q.get(timeout=max(0.05, min(1.0, limit - time.monotonic())))
             except queue.Empty:
+                if not ready and glob.glob(dead_mark + ".*"):
+                    why = "another rank's preflight child died starting the process group"
+                    break
                 if time.monotonic() > limit:
                     why = (f"no progress within {cand_s if open_key else init_s:g} s "
                            f"({'in the exchange' if open_key else 'starting the process group'})")
@@ -296,9 +305,13 @@ def _run_session(spec, rank, world, session, init_s, cand_s, log):
                 rc = p.wait()
                 if agreed is None:
                     why = f"preflight child exited with {rc}"
+                    if not ready:
+                        with open(f"{dead_mark}.{rank}", "w") as f:
+                            f.write(str(rc))
                 break
             kind = msg[0]
             if kind == "ready":
+                ready = True
                 limit = time.monotonic() + cand_s
             elif kind == "begin":
                 open_key = msg[1]
@@ -322,10 +335,11 @@ def _run_session(spec, rank, world, session, init_s, cand_s, log):
             p.wait()
         os.unlink(path)
         if rank == 0:
-            try:
-                os.unlink(_port_file(session))
-            except OSError:
-                pass
+            for f in [_port_file(session)] + glob.glob(dead_mark + ".*"):
+                try:
+                    os.unlink(f)
+                except OSError:
+                    pass
     if agreed is None:
         if open_key is not None:
             closed[open_key] = f"hang or crash: {why}"

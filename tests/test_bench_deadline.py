@@ -119,3 +119,27 @@ def test_preflight_under_torchrun():
     assert r.returncode == 0, r.stderr[-4000:]
     (res,) = _json_lines(r.stdout)
     assert res["preflight"] == {"heat:2x1x1/host": "ok"}, res["preflight"]
+
+
+def _dead_at_init(comm, models):
+    from multigpu_advectiondiffusion_amd.parallel.preflight import run_preflight
+    import time as _t
+    if comm.rank == 1:  # this rank's child cannot start (a bad backend name)
+        os.environ["ADVDIFF_BACKEND"] = "no-such-backend"
+    t0 = _t.monotonic()
+    v = run_preflight([("heat", None, "host")], models, device="cpu", backend="gloo"
+                      if comm.rank != 1 else "no-such-backend", cand_s=10, init_s=120,
+                      total_s=200, log=lambda m: None)
+    return v, _t.monotonic() - t0
+
+
+def test_preflight_child_dying_at_init_ends_every_rank_fast():
+    """One rank's child dies starting its process group: the other ranks' children, blocked
+    in the rendezvous, are ended through the marker file well before init_s."""
+    from multigpu_advectiondiffusion_amd.launch import spawn_local
+    models = {"heat": {"model": ("diffusion", {"K": 1.0, "order": 4}), "shape": [16, 14, 24],
+                       "spacing": [1.0, 1.0, 1.0], "ic": "sine", "dtype": "float64"}}
+    out = spawn_local(2, _dead_at_init, models, timeout=200)
+    for v, secs in out:
+        assert v["heat:slab/host"].startswith("not run"), v
+        assert secs < 60, secs
