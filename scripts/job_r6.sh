@@ -27,5 +27,13 @@ case "$1" in
   rcclfail)  # RCCL refuses two ranks on one GPU: the real RCCL error path of the preflight
     bash scripts/gpu_steps.sh r6/rcclfail \
       "reh2_rccl|400|$SH $R --nproc-per-node 2 --master-port 29612 bench.py --gpus 2 --steps 10 --warmup 3 --sustained-steps 0 --transport rccl --no-burgers" ;;
+  final)  # round-end tiers + evidence: GPU tests, smoke, bench, kernel-trace stats of the bench,
+          # the slab-rank step schedules
+    bash scripts/gpu_steps.sh r6/final \
+      "pytest_gpu|900|$PT -m gpu tests" \
+      "smoke|300|python -c 'import __graft_entry__ as g; g.smoke()'" \
+      "bench|600|python -u bench.py" \
+      "bench_prof|600|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6/final/prof -o p -- python3 bench.py --steps 20 --no-burgers --sustained-steps 0" \
+      "rank_steps|300|python -u bench/mr_step2_ab.py --order 4 && python -u bench/mr_step2_ab.py" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
