@@ -35,5 +35,15 @@ case "$1" in
       "bench|600|python -u bench.py" \
       "bench_prof|600|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6/final/prof -o p -- python3 bench.py --steps 20 --no-burgers --sustained-steps 0" \
       "rank_steps|300|python -u bench/mr_step2_ab.py --order 4 && python -u bench/mr_step2_ab.py" ;;
+  own)  # WENO5 v9 staging the own cell from the register column: kernel A/B (two builds in
+        # one process, bitwise compared) and in-solver rates (alternating processes)
+    A=bench/ab_libs/libadvdiff_base.so; B=bench/ab_libs/libadvdiff_own.so
+    RATE="ADVDIFF_ALLOW_STALE=1 python -u bench/burgers3d_rate.py"
+    bash scripts/gpu_steps.sh r6/own \
+      "kernel256|300|python -u bench/ab_burgers.py $A $B --n 256 --rounds 7" \
+      "kernel512|300|python -u bench/ab_burgers.py $A $B --n 512 --rounds 5 --reps 20" \
+      "kernel256_fp32|300|python -u bench/ab_burgers.py $A $B --n 256 --rounds 7 --fp32" \
+      "solver256|600|for r in 1 2 3; do ADVDIFF_LIB=$A $RATE 256 && ADVDIFF_LIB=$B $RATE 256 || exit 1; done" \
+      "solver512|600|for r in 1 2; do ADVDIFF_LIB=$A $RATE 512 && ADVDIFF_LIB=$B $RATE 512 || exit 1; done" ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
