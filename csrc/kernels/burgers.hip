@@ -434,7 +434,11 @@ __device__ __forceinline__ T w5_combine6(T n1, T S1, T n2, T S2) {
 //     to its last plane, so no branch and no phi copies (v_mov_b64) around the loads;
 //     the extra tile staged after the last plane lands in the idle buffer set;
 //   * x and y faces use w5_side_h (common.hpp): 37 instead of 41 fp64 ops per side,
-//     carried as 3 x the flux; z faces keep w5_side on the z rings (6 x the flux).
+//     carried as 3 x the flux; z faces keep w5_side on the z rings (6 x the flux);
+//   * (round 6) a lane stages its OWN cell of the next tile from its z rings (f+, f-, u of
+//     plane k+1 are already there) and only the tile's halo is loaded and split: half the
+//     tile loads, one split per lane instead of two — bitwise the same, +1.2-1.7 % in the
+//     solver at 256^3 / 512^3 (profiles/r6/ab/burgers_own_cell_ab.log).
 // Requires a plane below 2^31 bytes (v9_fits); TY = 8 only (offsets < 64 KiB).
 // ------------------------------------------------------------------------------
 //
@@ -457,7 +461,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
   constexpr int NW = 8, RW = 64 / TXL;  // waves per workgroup, tile rows per wave
   constexpr int TY = NW * RW, R = 3, NR = 5, TX = TXL, TXO = TX - 1;
   constexpr int LX = TX + 2 * R, LY = TY + 2 * R, NT = 64 * NW, LT = LX * LY;
-  constexpr int NPT = (LT + NT - 1) / NT;
   constexpr int E = (int)sizeof(V), EG = (int)sizeof(T);  // LDS / global element bytes
   constexpr int NARR = VISC ? 3 : 2;                 // staged arrays: f+, f- [, u]
   constexpr int SET = NARR * LT + (TY + 1) * TX;     // elements per buffer set (+ y faces)
@@ -517,45 +520,84 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
     }
   };
 
-  uint32_t toff[NPT];
+  // Tile staging: a lane's OWN cell of the staged plane comes from its register z column
+  // (the rings already hold f+, f- and u of planes k-2..k+2 — the same loads and the same
+  // split, so the same bits); only the tile's halo — NHALO = LX LY - TX TY cells, 468 of
+  // 980 for the 64 x 8 tile — is loaded and split, by the first NHALO lanes: half the tile
+  // loads and one split per lane instead of two (the round-5 kernel staged every cell)
+  constexpr int NHALO = LT - TX * TY;
+  constexpr int NH = (NHALO + NT - 1) / NT;
+  uint32_t hoff[NH];
+  int hl[NH];
 #pragma unroll
-  for (int r = 0; r < NPT; ++r) {
-    const int idx = min(tid + r * NT, LT - 1);
-    const int ly = idx / LX, lx = idx - ly * LX;
-    toff[r] = (uint32_t)(clampi(jb - R + ly, 0, ny - 1) * (int)sy +
-                         clampi(ib - R + lx, 0, nx - 1)) * (uint32_t)EG;
+  for (int h = 0; h < NH; ++h) {
+    int idx = tid + h * NT;
+    hl[h] = -1;
+    hoff[h] = 0;
+    if (idx < NHALO) {
+      int ly, lx;
+      if (idx < R * LX) {  // the R rows below the tile
+        ly = idx / LX;
+        lx = idx - ly * LX;
+      } else if ((idx -= R * LX) < R * LX) {  // the R rows above it
+        ly = TY + R + idx / LX;
+        lx = idx % LX;
+      } else {  // the R columns left and right of each tile row
+        idx -= R * LX;
+        ly = R + idx / (2 * R);
+        const int c = idx % (2 * R);
+        lx = c < R ? c : TX + c;
+      }
+      hl[h] = (ly * LX + lx) * E;
+      hoff[h] = (uint32_t)(clampi(jb - R + ly, 0, ny - 1) * (int)sy +
+                           clampi(ib - R + lx, 0, nx - 1)) * (uint32_t)EG;
+    }
   }
   // loop-invariant LDS lane bases (byte addresses); everything else is an immediate
-  const int lrb = ((row + R) * LX + col + R) * E - XO;  // own-cell reads
+  const int lrb = ((row + R) * LX + col + R) * E - XO;  // own-cell reads (and own-cell staging)
   const int brb = col * E;                              // bottom y faces (row R-1) + its store
   const int fyb = ((row + 1) * TX + col) * E;           // y face above the own cell
-  const int stb = tid * E;                           // tile staging
-  V pre[NPT];
-  auto fetch_tile = [&](int k) {
+  V pre[NH];
+  auto fetch_tile = [&](int k) {  // the halo of plane k
 #pragma unroll
-    for (int r = 0; r < NPT; ++r) pre[r] = gl(in, k, toff[r]);
+    for (int h = 0; h < NH; ++h) pre[h] = gl(in, k, hoff[h]);
   };
-  auto stage_tile = [&]<int SB>() {  // SB: byte offset of the buffer set
+  // SB: byte offset of the buffer set; op, om, ou: the own cell's f+, f-, u (ring values)
+  auto stage_tile = [&]<int SB>(V op, V om, V ou) {
+    lds_st<V>(lb + lrb, SB + XO, op);
+    lds_st<V>(lb + lrb, SB + OM + XO, om);
+    if constexpr (VISC) lds_st<V>(lb + lrb, SB + OU + XO, ou);
 #pragma unroll
-    for (int r = 0; r < NPT; ++r) {
-      const int idx = tid + r * NT;
-      if (NPT * NT == LT || idx < LT) {
+    for (int h = 0; h < NH; ++h) {
+      if (hl[h] >= 0) {
         V p, m;
-        lf_split(pre[r], p, m);
-        lds_st<V>(lb + stb, SB + r * NT * E, p);
-        lds_st<V>(lb + stb, SB + OM + r * NT * E, m);
-        if constexpr (VISC) lds_st<V>(lb + stb, SB + OU + r * NT * E, pre[r]);
+        lf_split(pre[h], p, m);
+        lds_st<V>(lb + hl[h], SB, p);
+        lds_st<V>(lb + hl[h], SB + OM, m);
+        if constexpr (VISC) lds_st<V>(lb + hl[h], SB + OU, pre[h]);
       }
     }
   };
   // 3 x flux at the face to the right of the cell at immediate offset c (relative to the
-  // base pointer bp) along stride st
+  // base pointer bp) along stride st.  own_face3: the cell is the lane's own, whose f+ and
+  // f- (op, om: the ring values) need no LDS read
   auto lds_face3 = [&](const char* bp, int c, int st) {
     V pv[5], mv[5];
 #pragma unroll
     for (int d = 0; d < 5; ++d) {
       pv[d] = lds_ld<V>(bp, c + (d - 2) * st);
       mv[d] = lds_ld<V>(bp, c + OM + (d - 1) * st);
+    }
+    V n1, S1, n2, S2;
+    w5_face3_sides<V, WZ>(pv, mv, n1, S1, n2, S2, kk);
+    return w5_combine6(n1, S1, n2, S2);
+  };
+  auto own_face3 = [&](const char* bp, int c, int st, V op, V om) {
+    V pv[5], mv[5];
+#pragma unroll
+    for (int d = 0; d < 5; ++d) {
+      pv[d] = d == 2 ? op : lds_ld<V>(bp, c + (d - 2) * st);
+      mv[d] = d == 1 ? om : lds_ld<V>(bp, c + OM + (d - 1) * st);
     }
     V n1, S1, n2, S2;
     w5_face3_sides<V, WZ>(pv, mv, n1, S1, n2, S2, kk);
@@ -593,7 +635,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
     for (int q = 2; q < 2 * R; ++q) rm[sl(q - R)] = fm[q];  // kc0-1 .. kc0+2
   }
   fetch_tile(kc0);
-  stage_tile.template operator()<0>();
+  stage_tile.template operator()<0>(rp[0], rm[0], ru[0]);  // plane kc0: ring slot 0
   fetch_tile(min(kc0 + 1, klast));
   V un = gl(in, kc0 + R, goff);  // u(k+3) of the current iteration
   V ax = V(0);
@@ -612,14 +654,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
     V axk = ax;
     if constexpr (reads_aux<MODE>()) ax = gl(aux, min(k + 1, klast), goff);
 
-    const V fy = lds_face3(lb + lrb, SB + XO, LX * E);  // y face j+½
+    const V fy = own_face3(lb + lrb, SB + XO, LX * E, rp[sl(0)], rm[sl(0)]);  // y face j+½
     if (w == (k - kc0) % NW)  // the tile's bottom y faces rotate over the waves
       // (TXL 32: both rows of the wave compute them; identical values, same slots)
       lds_st<V>(lb + brb, SB + OFY, lds_face3(lb + brb, SB + ((R - 1) * LX + R) * E, LX * E));
     lds_st<V>(lb + fyb, SB + OFY, fy);
     const V ctr = ru[sl(0)];
     V d2x = V(0), d2y = V(0), d2z = V(0);
-    const V fx = lds_face3(lb + lrb, SB + XO, E);  // x face i+½
+    const V fx = own_face3(lb + lrb, SB + XO, E, rp[sl(0)], rm[sl(0)]);  // x face i+½
     if constexpr (VISC) {
       const int c = SB + OU + XO;
       const char* bp = lb + lrb;
@@ -642,7 +684,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
 
     // stage tile k+1 into the other buffer set, fetch tile k+2 (past the chunk: its last
     // plane again, staged into the idle set and never read)
-    stage_tile.template operator()<SBN>();
+    stage_tile.template operator()<SBN>(rp[sl(1)], rm[sl(1)], ru[sl(1)]);
     fetch_tile(min(k + 2, klast));
     __syncthreads();  // y faces of k and tile k+1 visible
 

@@ -37,9 +37,10 @@ case "$1" in
       "rank_steps|300|python -u bench/mr_step2_ab.py --order 4 && python -u bench/mr_step2_ab.py" ;;
   own)  # WENO5 v9 staging the own cell from the register column: kernel A/B (two builds in
         # one process, bitwise compared) and in-solver rates (alternating processes)
-    A=bench/ab_libs/libadvdiff_base.so; B=bench/ab_libs/libadvdiff_own.so
+    A=bench/ab_libs/libadvdiff_base.so; B=bench/ab_libs/${OWN_LIB:-libadvdiff_own2.so}
     RATE="ADVDIFF_ALLOW_STALE=1 python -u bench/burgers3d_rate.py"
-    bash scripts/gpu_steps.sh r6/own \
+    bash scripts/gpu_steps.sh r6/${OWN_OUT:-own2} \
+      "tests|600|$PT tests/test_kernels_gpu.py tests/test_weno7_lsrk_gpu.py tests/test_pitch_gpu.py -k 'burgers or b3 or weno'" \
       "kernel256|300|python -u bench/ab_burgers.py $A $B --n 256 --rounds 7" \
       "kernel512|300|python -u bench/ab_burgers.py $A $B --n 512 --rounds 5 --reps 20" \
       "kernel256_fp32|300|python -u bench/ab_burgers.py $A $B --n 256 --rounds 7 --fp32" \
