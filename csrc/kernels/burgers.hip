@@ -437,8 +437,11 @@ __device__ __forceinline__ T w5_combine6(T n1, T S1, T n2, T S2) {
 //     carried as 3 x the flux; z faces keep w5_side on the z rings (6 x the flux);
 //   * (round 6) a lane stages its OWN cell of the next tile from its z rings (f+, f-, u of
 //     plane k+1 are already there) and only the tile's halo is loaded and split: half the
-//     tile loads, one split per lane instead of two — bitwise the same, +1.2-1.7 % in the
-//     solver at 256^3 / 512^3 (profiles/r6/ab/burgers_own_cell_ab.log).
+//     tile loads, one split per lane instead of two; the lane's own f+ / f- in its x and
+//     y faces come from the same registers (no LDS read) — bitwise the same, in the
+//     solver +2.6-3.2 % at 256^3 and +5.0-5.4 % at 512^3, where the 32 x 16 tile also
+//     stopped spilling (profiles/r6/ab/burgers_own_face_ab.log; staging alone:
+//     burgers_own_cell_ab.log, +1.2-1.7 %).
 // Requires a plane below 2^31 bytes (v9_fits); TY = 8 only (offsets < 64 KiB).
 // ------------------------------------------------------------------------------
 //
