@@ -17,6 +17,7 @@ import sys
 # compulsory bytes read per dispatch by profile_target.py (n^3 fp64 fields)
 COMPULSORY = {"copy": 512 ** 3 * 8, "fused": 512 ** 3 * 8, "fused2": 512 ** 3 * 8,
               "step2x": 512 ** 3 * 8, "burgers": 2 * 256 ** 3 * 8,
+              "burgers512": 2 * 512 ** 3 * 8,
               # round 6, per-rank shapes of the 8-GPU run (profile_target.py): the planes
               # each launch reads (its outputs +- 3R)
               "slab8_int": 128 * 1024 * 1024 * 8, "slab8_bnd": 36 * 1024 * 1024 * 8,
@@ -24,13 +25,15 @@ COMPULSORY = {"copy": 512 ** 3 * 8, "fused": 512 ** 3 * 8, "fused2": 512 ** 3 * 
 WHAT = {"copy": "copy_box 512³ (calibration)", "fused": "fused FD4 step 512³",
         "fused2": "fused FD2 step 512³", "step2x": "FD2 two steps per launch 512³",
         "burgers": "WENO5-Z + viscous stage 256³",
+        "burgers512": "WENO5-Z + viscous stage 512³",
         "slab8_int": "FD4, 8-GPU slab rank 1024²×(128+12), interior launch (116 planes)",
         "slab8_bnd": "FD4, 8-GPU slab rank, both 6-plane boundary slabs (one launch)",
         "r4x2_int": "FD4, 4×2×1 rank 1024×518×268, interior launch (244 planes)",
         "cube1024": "FD4, 1024³ (one launch)"}
 # output cells per dispatch (for instructions per cell)
 CELLS = {"copy": 512 ** 3, "fused": 508 ** 3, "fused2": 510 ** 3, "step2x": 510 ** 3,
-         "burgers": 250 ** 3, "slab8_int": 116 * 1020 * 1020, "slab8_bnd": 12 * 1020 * 1020,
+         "burgers": 250 ** 3, "burgers512": 506 ** 3,
+         "slab8_int": 116 * 1020 * 1020, "slab8_bnd": 12 * 1020 * 1020,
          "r4x2_int": 244 * 514 * 1020, "cube1024": 1020 ** 3}
 
 

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Run ONE stencil kernel repeatedly (for rocprofv3 --pmc / --kernel-trace).
 
-    python bench/profile_target.py {fused,fused2,step2x,stage,burgers,copy} [--n 512] [--reps 5]
+    python bench/profile_target.py {fused,fused2,step2x,stage,burgers,burgers512,copy} [--n 512]
+        [--reps 5]
         [--pitch PX,PY]   (fields of (n, n + PY, n + PX): the solver's pitched layout)
 
 Per-rank shapes of the 8-GPU weak-scaling run (FD4 fused step, round 6):
@@ -23,12 +24,14 @@ from multigpu_advectiondiffusion_amd.ops import stencil  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("which", choices=["fused", "fused2", "step2x", "stage", "burgers", "burgers_js",
+                                  "burgers512",
                                   "copy", "slab8_int", "slab8_bnd", "r4x2_int", "cube1024"])
 ap.add_argument("--n", type=int, default=512)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--pitch", default="0,0")
 a = ap.parse_args()
-n = a.n if a.which in ("fused", "fused2", "step2x", "stage", "copy") else min(a.n, 256)
+n = (a.n if a.which in ("fused", "fused2", "step2x", "stage", "copy") else
+     512 if a.which == "burgers512" else min(a.n, 256))
 px, py = (int(v) for v in a.pitch.split(","))
 RANK = {"slab8_int": ((140, 1024, 1024), dict(k0=12, k1=128, zlo=0, zhi=140)),
         "slab8_bnd": ((140, 1024, 1024), dict(k0=6, k1=12, k0b=128, k1b=134, zlo=0, zhi=140)),
@@ -56,7 +59,7 @@ for _ in range(a.reps):
                                   cy=1.0, cz=1.0, dt=0.01, a=0.75, b=0.25)
     else:
         stencil.burgers3d_stage(u, u, o, nx=n, ny=n, k0=3, k1=n - 3, border=3,
-                                weno_z=a.which == "burgers", rdx=n / 2.0, rdy=n / 2.0,
+                                weno_z=a.which != "burgers_js", rdx=n / 2.0, rdy=n / 2.0,
                                 rdz=n / 2.0, vx=1e-5 * n * n / 4, vy=1e-5 * n * n / 4,
                                 vz=1e-5 * n * n / 4, dt=1e-4, a=0.75, b=0.25)
 torch.cuda.synchronize()

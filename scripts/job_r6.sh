@@ -35,6 +35,9 @@ case "$1" in
       "bench|600|python -u bench.py" \
       "bench_prof|600|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6/final/prof -o p -- python3 bench.py --steps 20 --no-burgers --sustained-steps 0" \
       "rank_steps|300|python -u bench/mr_step2_ab.py --order 4 && python -u bench/mr_step2_ab.py" ;;
+  pmcb)  # counter row of the shipped WENO5-Z viscous stage (256^3 and 512^3)
+    bash scripts/gpu_steps.sh r6/pmc_burgers \
+      "pmc|600|PMC_OUT=gpurun_out/r6/pmc_burgers PMC_TARGETS='burgers burgers512' bash scripts/pmc_r5.sh" ;;
   own)  # WENO5 v9 staging the own cell from the register column: kernel A/B (two builds in
         # one process, bitwise compared) and in-solver rates (alternating processes)
     A=bench/ab_libs/libadvdiff_base.so; B=bench/ab_libs/${OWN_LIB:-libadvdiff_own2.so}
