@@ -194,8 +194,9 @@ from multigpu_advectiondiffusion_amd.parallel.preflight import (  # noqa: E402
 def planned_transports(world: int, on_gpu: bool, want: str) -> list:
     """Halo transports the run may use (before any process group exists): with the nccl
     backend rccl (boundary launch on the comm stream, the default schedule), rccl-plain
-    (boundary launch after the interior), ipc and, at 7-8 ranks, ipc+stripe; with ranks
-    sharing one GPU (ADVDIFF_SHARE_GPU=1, gloo) host and ipc; on the CPU host only."""
+    (boundary launch after the interior), ipc, ipc+fused (the heat step's halo puts inside
+    its one launch; slabs) and, at 7-8 ranks, ipc+stripe; with ranks sharing one GPU
+    (ADVDIFF_SHARE_GPU=1, gloo) host, ipc and ipc+fused; on the CPU host only."""
     if world == 1:
         return [None]
     if not on_gpu:
@@ -203,9 +204,9 @@ def planned_transports(world: int, on_gpu: bool, want: str) -> list:
     if want != "tune":
         return [want]
     if os.environ.get("ADVDIFF_SHARE_GPU", "0") == "1" or os.environ.get("ADVDIFF_BACKEND") == "gloo":
-        names = ["host", "ipc"]
+        names = ["host", "ipc", "ipc+fused"]
     else:
-        names = ["rccl", "rccl-plain", "ipc"]
+        names = ["rccl", "rccl-plain", "ipc", "ipc+fused"]
     from multigpu_advectiondiffusion_amd.parallel.ipc import stripe_plan
     if any(stripe_plan(world, STRIPE).values()):  # 7-8 ranks: idle links exist
         names.append("ipc+stripe")
@@ -450,9 +451,13 @@ def preflight_candidates(args, n, on_gpu, transports, heat_spec, burgers_spec):
             grids[mkey] = [None if args.decomp == "slab" else args.decomp]
     models = {mkey: spec for mkey, spec, _, _ in heat_spec + burgers_spec}
 
-    def ok_for(p, t):  # striping applies to slabs only
-        return t != "ipc+stripe" or p in (None, "slab") or tuple(p)[1:] == (1, 1)
-    allc = [(m, p, t) for m in models for p in grids[m] for t in transports if ok_for(p, t)]
+    def ok_for(m, p, t):  # striping and fused puts: slabs only; fused puts: the heat step
+        slab = p in (None, "slab") or tuple(p)[1:] == (1, 1)
+        if t == "ipc+fused":
+            return slab and m == "heat"
+        return t != "ipc+stripe" or slab
+    allc = [(m, p, t) for m in models for p in grids[m] for t in transports
+            if ok_for(m, p, t)]
     if n == 1 or args.preflight == "off":
         return {m: [(p, t) for mm, p, t in allc if mm == m] for m in models}, None
     verdict = {}
@@ -551,7 +556,8 @@ def run(args) -> int:
     secs = timed(solver, args.steps, args.warmup, dt, args.settle_ms, "heat")
     mlups = grid.cells * args.steps / secs / 1e6
     pg = solver.pgrid
-    link = {"ipc": "ipc device puts", "rccl": "RCCL, boundary launch on the comm stream",
+    link = {"ipc": "ipc device puts", "ipc+fused": "ipc puts inside the step launch",
+            "rccl": "RCCL, boundary launch on the comm stream",
             "host": "host-staged", "rccl-plain": "RCCL, boundary launch after the interior",
             "ipc+stripe": "ipc device puts striped over idle links"}.get(transport, transport)
     result.update({

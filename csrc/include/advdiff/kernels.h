@@ -76,6 +76,15 @@ int advdiff_diffusion3d_step_box_ex(int dtype, const void* uin, void* uout, int 
                                     int k0b, int k1b, int zlo, int zhi, const int* box,
                                     int order, double cx, double cy, double cz, double dt,
                                     int flags, void* stream);
+// A full-range slab step (planes [k0, k1), active box from `border`) whose output planes
+// [lo_k0, lo_k1) / [hi_k0, hi_k1) are also stored, system scope, into the peer planes at
+// dst_lo / dst_hi (IPC mappings of the neighbours' output fields: the peer plane of local
+// plane lo_k0 / hi_k0; same row pitch and plane stride).  Null / empty: no peer that side.
+int advdiff_diffusion3d_step_put(int dtype, const void* uin, void* uout, int nx, int ny,
+                                 int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int zlo,
+                                 int zhi, int border, int order, double cx, double cy,
+                                 double cz, double dt, void* dst_lo, int lo_k0, int lo_k1,
+                                 void* dst_hi, int hi_k0, int hi_k1, void* stream);
 // 2-D heat: ONE FULL SSP-RK3 step per launch on rows [j0, j1) (intermediate stages on
 // the active rows [ylo, yhi)); reads rows j0-3R .. j1+3R-1 (clamped to [0, ny_alloc)).
 // Wave-independent y-march, no LDS; bit-identical to three advdiff_diffusion2d_stage.

@@ -131,6 +131,17 @@ __device__ __forceinline__ AxisTile axis_tile(int t, int n, int W, int R, int a0
   return axis_tile(t, n, W, R, a0, a1, o0, o1, nmax, edge, 2 * R);
 }
 
+// Fused halo puts (slab ranks, ipc transport): the output planes [k0[s], k1[s]) of a
+// launch are ALSO stored into a peer's ghost planes — dst[s] is the peer's plane for local
+// plane k0[s] (an IPC mapping of the peer's output field, same row pitch and plane stride)
+// — so the exchange rides inside the step launch over xGMI instead of a boundary launch
+// plus a put launch after it.  Every such store is a system-scope store (as ipc_put_kernel's);
+// the signal kernel after the launch publishes them (ipc.hip link 2).
+struct StepPut {
+  char* dst[2];
+  int k0[2], k1[2];
+};
+
 // ---------------------------------------------------------------------------------
 // v3 march: the same algorithm (compact rings, trapezoid, one barrier per plane) with
 // the code shaped for the gfx950 issue model:
@@ -173,12 +184,13 @@ struct V3Geom {
 // — LDS traffic and VALU work of the two groups overlap instead of alternating in lockstep
 // (MI355X_MICROARCH.md "Two waves per SIMD", items 4 and 9).  Same arithmetic, bit-
 // identical results.
-template <typename T, int ORDER, int NW, int RPW, int XS, int PF, bool SEP, int VAR = 0>
+template <typename T, int ORDER, int NW, int RPW, int XS, int PF, bool SEP, int VAR = 0,
+          bool PUT = false>
 __device__ __forceinline__ void v3_march(
     T* lds, int tx, int ty, int gx, int gy, int edge, int kc0, int kc1,
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
     int nz_alloc, int zlo, int zhi, const Box2& bx, const FdCoef<T>& q1a, const FdCoef<T>& q2a,
-    const FdCoef<T>& q3a) {
+    const FdCoef<T>& q3a, const StepPut& put = StepPut{}) {
   // fp64: the stage-1 coefficients live in VGPRs (a "+v" asm operand makes the uniform
   // values look divergent; 8 more VGPRs, same occupancy).  With all twelve fp64
   // coefficients in SGPRs the kernel needs 106 SGPRs and the compiler spills them into
@@ -366,6 +378,16 @@ __device__ __forceinline__ void v3_march(
     acc = fd_apply(acc, q3.k[1], ys);
     acc = pin(acc);
     if (m3[q]) gst<T>(plane_rsrc((char*)uout + (int64_t)kp * szb), goff[q], acc);
+    if constexpr (PUT) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        if (kp >= put.k0[s] && kp < put.k1[s] && m3[q]) {  // kp scalar: a scalar branch
+          using U = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>;
+          U* d = (U*)(put.dst[s] + (int64_t)(kp - put.k0[s]) * szb + goff[q]);
+          __hip_atomic_store(d, __builtin_bit_cast(U, acc), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
   };
   // the y-axis sum of stage 3 from the B plane of buffer set AO (LDS)
   auto s3_ysum = [&](int q, int AO) {
@@ -602,6 +624,8 @@ __device__ __forceinline__ void v3_march(
       (void)((kb + P < kend ? (body.template operator()<P>(kb + P), true) : false) && ...);
     }(std::make_integer_sequence<int, 2 * NR>{});
   }
+  // every peer store of this wave acknowledged before the wave (and the dispatch) ends
+  if constexpr (PUT) __builtin_amdgcn_s_waitcnt(0);
 }
 
 // ---------------------------------------------------------------------------------
@@ -927,12 +951,12 @@ constexpr int step_min_waves() {
 // The march variant: DPP x neighbours in stages 2/3 (XS = 1), prefetch distance 2,
 // unmerged LDS reads (SEP).  The other (XS, PF, SEP) combinations measured 1-9 % slower
 // at 512^3 (profiles/archive/step_variants_r2.log, step_cfgs_edge_r2.log) and were removed.
-template <typename T, int ORDER, int NW, int RPW, int VAR>
+template <typename T, int ORDER, int NW, int RPW, int VAR, bool PUT = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((
     amdgpu_waves_per_eu(step_min_waves<T, ORDER, NW, RPW>()))) void diffusion3d_step_kernel(
     const T* __restrict__ uin, T* __restrict__ uout, int nx, int ny, int64_t sy, int64_t sz,
     int nz_alloc, int k0, int k1, int k0b, int k1b, StepSched sc, int zlo, int zhi,
-    Box2 bx, FdCoef<T> q1, FdCoef<T> q2, FdCoef<T> q3) {
+    Box2 bx, FdCoef<T> q1, FdCoef<T> q2, FdCoef<T> q3, StepPut put) {
   __shared__ T lds[V3Geom<T, ORDER, NW, RPW>::TOTAL];
   int kc0, kc1;
   Tile3 tile;
@@ -947,9 +971,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((
     kc0 = second ? k0b + (tile.z - sc.gza) * sc.zchunk : k0 + tile.z * sc.zchunk;
     kc1 = min(kc0 + sc.zchunk, second ? k1b : k1);
   }
-  v3_march<T, ORDER, NW, RPW, 1, 2, true, VAR>(lds, tile.x, tile.y, sc.gx, sc.gy, sc.edge, kc0, kc1,
-                                           uin, uout, nx, ny, sy, sz, nz_alloc, zlo, zhi, bx,
-                                           q1, q2, q3);
+  v3_march<T, ORDER, NW, RPW, 1, 2, true, VAR, PUT>(lds, tile.x, tile.y, sc.gx, sc.gy, sc.edge,
+                                                  kc0, kc1, uin, uout, nx, ny, sy, sz, nz_alloc,
+                                                  zlo, zhi, bx, q1, q2, q3, put);
 }
 
 // Banded z schedule: with a whole number of z chunks per column the last round of
@@ -1087,8 +1111,8 @@ static bool sched_banded(int esize, int order, const SArgs& a) {
   return it != g_sched.end() && it->second > 0;
 }
 
-template <typename T, int ORDER, int NW, int RPW, int VAR>
-static hipError_t launch_step(const SArgs& a) {
+template <typename T, int ORDER, int NW, int RPW, int VAR, bool PUT = false>
+static hipError_t launch_step(const SArgs& a, const StepPut& put = StepPut{}) {
   constexpr int R = ORDER / 2;
   constexpr int edge = kStepEdge;
   const int gx = axis_tile_count(64, R, a.bx.xa0, a.bx.xa1, a.bx.xo0, a.bx.xo1, a.nx, edge);
@@ -1096,13 +1120,17 @@ static hipError_t launch_step(const SArgs& a) {
   // z chunks: minimise (rounds of resident workgroups) x (chunk + 4R warm-up planes);
   // resident workgroups = CUs x occupancy of this instance (LDS / VGPR bound: 1-2 per CU)
   const int per_cu =
-      occupancy_per_cu((const void*)diffusion3d_step_kernel<T, ORDER, NW, RPW, VAR>, 64 * NW);
+      occupancy_per_cu((const void*)diffusion3d_step_kernel<T, ORDER, NW, RPW, VAR, PUT>, 64 * NW);
   constexpr int minc = kStepMinChunk;
   const int na = std::max(a.k1 - a.k0, 0), nb = std::max(a.k1b - a.k0b, 0);
   const long long slots = (long long)device_cus() * per_cu;
   StepSched sc{gx, gy, 0, 0, edge};
   dim3 grid;
-  if (nb == 0 && na > 0 && sched_banded((int)sizeof(T), ORDER, a)) {
+  // (PUT: uniform chunks — the banded grid dispatches the top band last, which would
+  // bunch the upper peer's stores at the end of the launch; with uniform chunks
+  // xcd_tile spreads the chunks of a column over the XCDs, so both faces' stores run
+  // through the whole launch)
+  if (!PUT && nb == 0 && na > 0 && sched_banded((int)sizeof(T), ORDER, a)) {
     const Bands bd = step_bands(na, (long long)gx * gy, slots, 4 * R, minc);
     sc.zfirst = bd.zfirst;
     sc.zchunk = bd.zchunk;
@@ -1118,9 +1146,10 @@ static hipError_t launch_step(const SArgs& a) {
   const FdCoef<T> q1 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 1.0, true);
   const FdCoef<T> q2 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 0.25, true);
   const FdCoef<T> q3 = fd_coef<T>(ORDER, a.cx, a.cy, a.cz, a.dt, 2.0 / 3.0, true);
-  hipLaunchKernelGGL((diffusion3d_step_kernel<T, ORDER, NW, RPW, VAR>), grid, dim3(64, NW, 1), 0,
-                     a.st, (const T*)a.uin, (T*)a.uout, a.nx, a.ny, a.sy, a.sz, a.nz_alloc,
-                     a.k0, a.k1, a.k0b, a.k1b, sc, a.zlo, a.zhi, a.bx, q1, q2, q3);
+  hipLaunchKernelGGL((diffusion3d_step_kernel<T, ORDER, NW, RPW, VAR, PUT>), grid,
+                     dim3(64, NW, 1), 0, a.st, (const T*)a.uin, (T*)a.uout, a.nx, a.ny, a.sy,
+                     a.sz, a.nz_alloc, a.k0, a.k1, a.k0b, a.k1b, sc, a.zlo, a.zhi, a.bx, q1, q2,
+                     q3, put);
   return hipGetLastError();
 }
 
@@ -1161,12 +1190,12 @@ constexpr int kStepVar = ORDER == 4 ? 3 : 23;
 // -7.0 / +3.0 / +10.1 % at 384 / 512 / 640 / 768 / 1024^3, where the two-step launch wins by
 // more (profiles/r5/ab/step_tile_ab*.log); FD4 12 x 3 0.94-0.99 x (fd4_tile_ab.log).  The
 // alternatives and their switches were removed in round 6.
-template <typename T, int ORDER>
-static hipError_t dispatch_step(const SArgs& a) {
+template <typename T, int ORDER, bool PUT = false>
+static hipError_t dispatch_step(const SArgs& a, const StepPut& put = StepPut{}) {
   if constexpr (ORDER == 4)
-    return launch_step<T, ORDER, 16, 2, kStepVar<4>>(a);
+    return launch_step<T, ORDER, 16, 2, kStepVar<4>, PUT>(a, put);
   else
-    return launch_step<T, ORDER, 12, 3, kStepVar<2>>(a);
+    return launch_step<T, ORDER, 12, 3, kStepVar<2>, PUT>(a, put);
 }
 
 // two-step FD2 launch (v6_march): 12 waves x 2 rows (24 stage-1 rows, 14 output rows;
@@ -1453,6 +1482,43 @@ extern "C" int advdiff_diffusion3d_step(int dtype, const void* uin, void* uout, 
                                    zhi, border, order, cx, cy, cz, dt, stream);
 }
 
+// One full-range slab step whose output planes [lo_k0, lo_k1) / [hi_k0, hi_k1) are also
+// stored into the peer planes at dst_lo / dst_hi (the peer's plane for local plane lo_k0 /
+// hi_k0; null or an empty range: no peer on that side).  The peer fields must have this
+// field's row pitch and plane stride (slab ranks of one grid).  Uniform z chunks.
+extern "C" int advdiff_diffusion3d_step_put(int dtype, const void* uin, void* uout, int nx,
+                                            int ny, int64_t sy, int64_t sz, int nz_alloc, int k0,
+                                            int k1, int zlo, int zhi, int border, int order,
+                                            double cx, double cy, double cz, double dt,
+                                            void* dst_lo, int lo_k0, int lo_k1, void* dst_hi,
+                                            int hi_k0, int hi_k1, void* stream) {
+  using namespace advdiff;
+  if (k1 <= k0) return hipSuccess;
+  if (nx <= 0 || ny <= 0 || uin == uout || k0 < 0 || k1 > nz_alloc) return hipErrorInvalidValue;
+  if (sy * (int64_t)ny >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+  StepPut put{};
+  void* dsts[2] = {dst_lo, dst_hi};
+  const int pk0[2] = {lo_k0, hi_k0}, pk1[2] = {lo_k1, hi_k1};
+  for (int s = 0; s < 2; ++s) {
+    const bool on = dsts[s] != nullptr && pk1[s] > pk0[s];
+    if (on && (pk0[s] < 0 || pk1[s] > nz_alloc)) return hipErrorInvalidValue;
+    put.dst[s] = on ? (char*)dsts[s] : nullptr;
+    put.k0[s] = on ? pk0[s] : 0;
+    put.k1[s] = on ? pk1[s] : 0;
+  }
+  const Box2 bx{border, nx - border, border, ny - border, 0, nx, 0, ny};
+  const SArgs a{uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, 0, 0, zlo, zhi, bx,
+                cx, cy, cz, dt, (hipStream_t)stream};
+  if (dtype == ADVDIFF_F64) {
+    if (order == 4) return dispatch_step<double, 4, true>(a, put);
+    if (order == 2) return dispatch_step<double, 2, true>(a, put);
+  } else if (dtype == ADVDIFF_F32) {
+    if (order == 4) return dispatch_step<float, 4, true>(a, put);
+    if (order == 2) return dispatch_step<float, 2, true>(a, put);
+  }
+  return hipErrorInvalidValue;
+}
+
 // Code-object preload (see advdiff_preload in aux.hip).
 // The default kernels' occupancies are cached here too (launch.hpp occupancy_per_cu), so
 // no launch inside a hipGraph capture is the first to query one.
@@ -1465,6 +1531,10 @@ extern "C" int advdiff_preload_diffusion_fused(void) {
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 2, 12, 3, 23>, 64 * 12);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<float, 4, 16, 2, 3>, 64 * 16);
   (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<float, 2, 12, 3, 23>, 64 * 12);
+  (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 4, 16, 2, 3, true>, 64 * 16);
+  (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<double, 2, 12, 3, 23, true>, 64 * 12);
+  (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<float, 4, 16, 2, 3, true>, 64 * 16);
+  (void)occupancy_per_cu((const void*)diffusion3d_step_kernel<float, 2, 12, 3, 23, true>, 64 * 12);
   (void)occupancy_per_cu((const void*)diffusion3d_step2x_kernel<double, 12, 2>, 64 * 12);
   (void)occupancy_per_cu((const void*)diffusion3d_step2x_kernel<float, 12, 2>, 64 * 12);
   return e;

@@ -86,6 +86,10 @@ def build_parser():
     ap.add_argument("--stripe", type=int, default=None,
                     help="ipc slab halos: relay part of every face message through up to N "
                          "helper ranks over idle xGMI links (default: ADVDIFF_STRIPE or 0)")
+    ap.add_argument("--fused-put", action="store_true", default=None,
+                    help="ipc slab halos of the fused 3-D heat step: the step launch stores "
+                         "its boundary planes into the neighbours' ghost planes itself "
+                         "(default: ADVDIFF_FUSED_PUT)")
     ap.add_argument("--decomp", default=None,
                     help="process grid: slab (default), auto, or PZxPYxPX / PYxPX")
     ap.add_argument("--transport", choices=["rccl", "ipc", "host"], default=None,
@@ -202,7 +206,8 @@ def main(argv=None) -> int:
         model, grid, comm, dtype=dtype, ic=ic, overlap=not ns.no_overlap, t0=t0,
         check_every=ns.check_every, decomp=ns.decomp, integrator=ns.integrator,
         kernel=ns.kernel, exchange=ns.exchange, stripe=ns.stripe, boundary_on_comm=ns.bcomm,
-        pitch=None if ns.pitch is None else tuple(int(v) for v in ns.pitch.split(","))))
+        pitch=None if ns.pitch is None else tuple(int(v) for v in ns.pitch.split(",")),
+        fused_put=ns.fused_put))
     # the shape-dependent launch picks (GPU measurements) after the fenced HtD, as the
     # native engine does after init_s_
     solver.tune_launches()

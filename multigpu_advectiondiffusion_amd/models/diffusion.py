@@ -90,11 +90,12 @@ class Diffusion(Model):
                                    cz=self.coef[2], dt=dt, stream=stream)
 
     def step(self, uin, uout, lo, hi, zlo, zhi, dt, stream=None, lo2=0, hi2=0, nx=None,
-             ny=None, box=None, exclusive=False):
+             ny=None, box=None, exclusive=False, put=None):
         """Fused RK3 step on planes [lo, hi) (and [lo2, hi2) in the same launch).
         nx/ny/box: extents and explicit active/output bounds of a view (Cartesian blocks).
         exclusive: the launch has the GPU to itself (3-D: persistent schedule; the 2-D
-        step has one grid schedule — its y-march waves are independent — and ignores it)."""
+        step has one grid schedule — its y-march waves are independent — and ignores it).
+        put: fused halo puts of a 3-D slab rank (stencil.diffusion3d_step)."""
         g = self.grid
         nx = g.nx if nx is None else nx
         ny = g.ny if ny is None else ny
@@ -109,7 +110,7 @@ class Diffusion(Model):
         stencil.diffusion3d_step(uin, uout, nx=nx, ny=ny, k0=lo, k1=hi, zlo=zlo, zhi=zhi,
                                  border=self.border, order=self.order, cx=self.coef[0],
                                  cy=self.coef[1], cz=self.coef[2], dt=dt, stream=stream,
-                                 k0b=lo2, k1b=hi2, box=box, exclusive=exclusive)
+                                 k0b=lo2, k1b=hi2, box=box, exclusive=exclusive, put=put)
 
     def stable_dt(self, umax=None) -> float:
         return self.safety / (2.0 * sum(self.coef))

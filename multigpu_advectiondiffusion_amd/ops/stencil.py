@@ -106,17 +106,35 @@ EXCLUSIVE = 1  # ADVDIFF_EXCLUSIVE (kernels.h)
 
 
 def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, cy, cz, dt,
-                     stream=None, k0b=0, k1b=0, box=None, exclusive=False):
+                     stream=None, k0b=0, k1b=0, box=None, exclusive=False, put=None):
     """A FULL SSP-RK3 step in one launch (temporal blocking): uout[k0:k1] = RK3(uin), and
     uout[k0b:k1b] too when a second range is given (one launch for both).
     box = (xa0, xa1, ya0, ya1, xo0, xo1, yo0, yo1): explicit active / output x-y bounds
     (Cartesian blocks launched on a view); default from `border`.
     exclusive=True: nothing else runs on the GPU meanwhile (single rank / full-range
     launch) -> one round of persistent workgroups; False (an interior launch overlapping
-    RCCL) keeps the dynamically balanced grid of z chunks.  Results are bit-identical."""
+    RCCL) keeps the dynamically balanced grid of z chunks.  Results are bit-identical.
+    put = ((dst_lo, lo_k0, lo_k1), (dst_hi, hi_k0, hi_k1)): the output planes [lo_k0, lo_k1)
+    / [hi_k0, hi_k1) are also stored at the peer addresses dst_lo / dst_hi (the peer plane
+    of local plane lo_k0 / hi_k0; 0 = no peer) — the ipc transport's fused halo puts
+    (advdiff_diffusion3d_step_put; one plane range, default box, native device fields)."""
     _check_layout(uin, uout)
     if uin.data_ptr() == uout.data_ptr():
         raise ValueError("the fused step needs distinct input/output buffers")
+    if put is not None:
+        if not _native(uin) or box is not None or k1b > k0b:
+            raise ValueError("fused halo puts: native device fields, one range, default box")
+        lib = _lib.require()
+        nz = uin.shape[0]
+        assert 0 <= k0 and k1 <= nz and 0 <= zlo and zhi <= nz
+        assert nx <= uin.shape[2] and ny <= uin.shape[1]
+        (dlo, lo0, lo1), (dhi, hi0, hi1) = put
+        code = lib.advdiff_diffusion3d_step_put(
+            _dtype_code(uin), _ptr(uin), _ptr(uout), nx, ny, uin.stride(1), uin.stride(0), nz,
+            k0, k1, zlo, zhi, border, order, cx, cy, cz, dt, dlo or None, lo0, lo1,
+            dhi or None, hi0, hi1, _stream_ptr(stream))
+        _lib.check(code, "diffusion3d_step_put")
+        return
     if box is None:
         box = (border, nx - border, border, ny - border, 0, nx, 0, ny)
     if _native(uin):

@@ -83,15 +83,16 @@ def _start_ipc_routed(comm, comm_stream, phases, after_event=None, tag=None) -> 
     return _joinable(cs)
 
 
-def _start_ipc(comm, comm_stream, phases, after_event=None) -> PendingExchange:
+def _start_ipc(comm, comm_stream, phases, after_event=None, puts=True) -> PendingExchange:
     """Device puts into the peers' ghost cells (parallel/ipc.py) on the comm stream after
-    `after_event`, phases in order; the returned handle joins the current stream."""
+    `after_event`, phases in order; the returned handle joins the current stream.
+    puts=False: the producing kernel stored the boxes itself — signal and wait only."""
     cur = torch.cuda.current_stream()
     cs = comm_stream or cur
     _order_after(cs, cur, after_event)
     ipc = comm.ipc()
     for msgs in phases:
-        ipc.exchange(msgs, cs)
+        ipc.exchange(msgs, cs, puts=puts)
     return _joinable(cs)
 
 
@@ -265,14 +266,42 @@ class SlabHalo:
         elif _ipc_on(self, field):
             self.comm.ipc()._resolve(self._ipc_msgs(field))
 
-    def start(self, field: torch.Tensor, after_event=None) -> PendingExchange | None:
+    def put_targets(self, field: torch.Tensor):
+        """Fused halo puts (ipc, direct, 3-D): ((dst_lo, k0, k1), (dst_hi, k0, k1)) — the
+        peer address of my send planes [k0, k1) of `field` towards the lower / upper
+        neighbour (dst 0: no neighbour), for a step kernel that stores its output planes
+        there itself (stencil.diffusion3d_step put=).  The peers' receive boxes must have
+        this field's strides (slab ranks of one grid); start(field, puts=False) then only
+        signals and waits."""
+        if not _ipc_on(self, field) or self._use_stripes(field) or field.dim() != 3:
+            raise ValueError("fused halo puts: the direct ipc transport of a 3-D slab")
+        msgs = self._ipc_msgs(field)
+        dests = self.comm.ipc().targets(msgs)
+        d = self.d
+        out = [(0, 0, 0), (0, 0, 0)]
+        for (peer, send, _), (ptr, rsy, rsz) in zip(msgs, dests):
+            if (rsy, rsz) != (field.stride(1), field.stride(0)):
+                raise ValueError(f"fused halo puts: peer {peer} field strides {(rsy, rsz)} "
+                                 f"!= {(field.stride(1), field.stride(0))}")
+            s0, s1 = d.send_lower() if peer == d.lower else d.send_upper()
+            out[0 if peer == d.lower else 1] = (ptr, s0, s1)
+        return tuple(out)
+
+    def start(self, field: torch.Tensor, after_event=None,
+              puts: bool = True) -> PendingExchange | None:
         """Begin exchanging the ghost planes of `field` (axis 0).
 
         On device: the transfers are issued on the comm stream after `after_event`
         (None: after all work currently queued on the current stream; False: the field's
-        producer ran on the comm stream itself)."""
+        producer ran on the comm stream itself).  puts=False (ipc, direct): the producer
+        already stored the send planes into the peers (put_targets) — signal and wait."""
         if self.comm.size == 1:
             return None
+        if not puts:
+            if not _ipc_on(self, field) or self._use_stripes(field):
+                raise ValueError("puts=False: the direct ipc transport only")
+            return _start_ipc(self.comm, self.comm_stream, [self._ipc_msgs(field)],
+                              after_event, puts=False)
         if _ipc_on(self, field) and self._use_stripes(field):
             par = self.parity
             p1, p2 = self._stripe_phases(field, par)

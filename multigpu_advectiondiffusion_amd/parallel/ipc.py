@@ -179,18 +179,25 @@ class IpcPeers:
             out[peer] = d
         return out
 
-    def exchange(self, msgs, stream) -> None:
+    def exchange(self, msgs, stream, puts: bool = True) -> None:
         """Enqueue on `stream`: put every send box into its peer's matching receive box,
         signal the peers, wait for their puts into ours.  msgs = [(peer, send_view,
-        recv_view)] with distinct peers."""
+        recv_view)] with distinct peers.  puts=False: the boxes were already stored by a
+        kernel earlier on `stream` (the fused step's halo puts, targets()): signal + wait."""
         if not msgs:
             return
         peers = [m[0] for m in msgs]
         if len(set(peers)) != len(peers):
             raise ValueError("ipc: one message per peer and exchange")
-        self.route({peer: (send, recv) for peer, send, recv in msgs}, stream, 0)
+        self.route({peer: (send, recv) for peer, send, recv in msgs}, stream, 0, puts=puts)
 
-    def route(self, pairs, stream, ch: int, tag=None) -> None:
+    def targets(self, msgs) -> list:
+        """Peer receive (pointer, sy, sz) of every message of a symmetric exchange — for a
+        kernel that stores the send boxes itself (then exchange(..., puts=False)).  The
+        same handshake and cache as exchange()."""
+        return self._resolve(msgs)
+
+    def route(self, pairs, stream, ch: int, tag=None, puts: bool = True) -> None:
         """One exchange phase on flag channel `ch`: pairs = {peer: (send_view | None,
         recv_view | None)}.  Enqueues the puts of every send box into the peer's receive
         box, the signal of the peers I sent to, and the wait for the peers that send to
@@ -202,7 +209,7 @@ class IpcPeers:
         sp = stream.cuda_stream
         to = sorted(p for p, (snd, _) in pairs.items() if snd is not None)
         frm = sorted(p for p, (_, rcv) in pairs.items() if rcv is not None)
-        for peer in to:
+        for peer in (to if puts else ()):
             send = pairs[peer][0]
             dptr, dsy, dsz = dests[peer]
             ni, nj, nk, ssy, ssz = _box_geom(send)

@@ -116,7 +116,7 @@ class Solver:
                  device_dt: bool | None = None, exchange: str = "u",
                  transport: str | None = None, stripe: int | None = None,
                  boundary_stream: bool | None = None, boundary_on_comm: bool | None = None,
-                 pitch=None):
+                 pitch=None, fused_put: bool | None = None):
         """decomp: process grid — None/"slab" (split the slowest axis only, the
         reference's layout), "auto" (smallest halo surface) or "PZxPYxPX" / a tuple in
         array axis order ((pz, py, px) in 3-D, (py, px) in 2-D).
@@ -149,7 +149,13 @@ class Solver:
         exchange the boundary planes of the RHS L(u) and advance the ghost planes
         redundantly with the RK update).  "lu" is a slab, per-stage, PyTorch-ops mode kept
         for semantic parity; its results equal the "u" mode's bit for bit
-        (tests/test_lu_exchange.py)."""
+        (tests/test_lu_exchange.py).
+        fused_put (3-D fused heat step, slab ranks, direct ipc transport): ONE launch per
+        step over all owned planes that also stores its boundary output planes straight
+        into the neighbours' ghost planes over xGMI (advdiff_diffusion3d_step_put), then
+        signal + wait — no boundary launch and no put launch (_step_fused_put).  None =
+        ADVDIFF_FUSED_PUT=1; ignored where it does not apply (per-stage models, Cartesian
+        grids, striped or non-ipc transports, the multi-rank FD2 two-step launch)."""
         if kernel not in ("native", "torch"):
             raise ValueError("kernel must be 'native' or 'torch'")
         if exchange not in ("u", "lu"):
@@ -193,6 +199,10 @@ class Solver:
         if self.fused and (integrator != "ssprk3" or thin):
             self.fused = False  # LSRK, or blocks thinner than the wide (3R) halo
         elem = torch.empty((), dtype=dtype).element_size()
+        if fused_put is None:
+            import os
+            fused_put = os.environ.get("ADVDIFF_FUSED_PUT") == "1"
+        self._want_put = bool(fused_put)
         # multi-rank FD2 slabs: two RK3 steps per launch with a 6R-plane halo every second
         # step (the same bytes per step as 3R every step, half the messages and launches);
         # decided before the fields exist, since it sets the ghost width
@@ -273,6 +283,14 @@ class Solver:
             self.full = self.d.compute_range(model.border)
             self.interior, blo, bhi = self.d.split_ranges(model.border, G)
             self.boundary = [blo, bhi]
+        # fused halo puts: the step launch stores the send planes into the peers itself
+        self.fput = bool(self._want_put and self.fused and not self.cart and grid.dims == 3
+                         and comm.size > 1 and self.transport == "ipc"
+                         and self.device.type == "cuda" and kernel == "native"
+                         and exchange == "u" and not self._mr2 and not self.halo.striped)
+        self._put_cache = {}
+        if self.fput:
+            self.bcomm = False
         # planes (local, ghosts included) whose intermediate stages are updated
         off = self.d.start - G
         self.zact = (max(0, model.border - off), min(self.d.alloc, grid.n_decomposed - model.border - off))
@@ -315,7 +333,7 @@ class Solver:
         import os
         m, comm = self.model, self.comm
         if not (self.fused and comm.size > 1 and not self.cart and m.supports_step2
-                and self.integrator == "ssprk3" and exchange == "u"):
+                and self.integrator == "ssprk3" and exchange == "u" and not self._want_put):
             return False
         G2 = 6 * m.radius
         if ashape[0] // comm.size < G2:
@@ -591,8 +609,55 @@ class Solver:
                             nx=vx1 - vx0, box=(xa0, xa1, xo0, xo1), exclusive=exclusive)
         trace.sync_check(f"{self.model.name} fused step box {box}", self.device)
 
+    def _put_targets(self, field):
+        """(cached per field and ipc epoch) the peer addresses of the fused step's halo
+        puts into `field`'s counterparts.  First use: the device drains first, so every
+        rank's fields are initialised (the IC, the partner clone) before a peer's store can
+        land in them — the handshake in put_targets is pairwise, so the peer has drained
+        too.  Never called for the first time inside a graph capture (_prepare_graph_halos
+        resolves both fields before it)."""
+        key = (field.data_ptr(), self._ipc_epoch())
+        t = self._put_cache.get(key)
+        if t is None:
+            torch.cuda.synchronize(self.device)
+            t = self.halo.put_targets(field)
+            self._put_cache[key] = t
+        return t
+
+    def _step_fused_put(self, dt: float, pend) -> None:
+        """One launch over every owned plane whose boundary output planes also go straight
+        into the neighbours' ghost planes (the peers' output fields, IPC-mapped), then
+        signal + wait on the comm stream:
+
+            compute : [wait halo n-1 (join)][step n + puts] ------------> [step n+1 ...
+            comm    :                                    [signal n, wait halo n]
+
+        The wait for halo n-1 also orders this step's stores into a peer's field after the
+        peer's step n-1, the last reader of that buffer (ping-pong: the peer's output of
+        step n is its input of step n-1), so no acknowledgement is needed.  No boundary
+        launch (its 4R-plane z warm-up per slab) and no put launch; the puts run beside
+        the compute of every other workgroup."""
+        if pend is not None:
+            pend.wait()
+        put = self._put_targets(self.un)
+        with trace.range_("step+puts"):
+            lo, hi = self.full
+            if hi > lo:
+                self.model.step(self.u, self.un, lo, hi, self.zact[0], self.zact[1], dt,
+                                put=put)
+                trace.sync_check(f"{self.model.name} fused step + puts [{lo},{hi})",
+                                 self.device)
+        self.u, self.un = self.un, self.u
+        with trace.range_("halo_signal"):
+            self._pending[id(self.u)] = self.halo.start(self.u, puts=False)
+        self.t += dt
+        self.it += 1
+
     def _step_fused(self, dt: float) -> None:
         pend = self._pending.pop(id(self.u), None)
+        if self.fput:
+            self._step_fused_put(dt, pend)
+            return
         if self.bcomm and self.comm.size > 1:
             self._step_fused_bcomm(dt, pend)
             return
@@ -674,7 +739,8 @@ class Solver:
         shape on the GPU before any graph capture (diffusion_fused.hip step_bands; the
         kernel library caches the choice; ADVDIFF_STEP_BANDED=0/1 forces)."""
         if not (self.fused and self.grid.dims == 3 and self.kernel == "native"
-                and self.device.type == "cuda" and hasattr(self.model, "sched_pick")):
+                and self.device.type == "cuda" and hasattr(self.model, "sched_pick")
+                and not self.fput):  # the put launch always takes uniform chunks
             return
         dt = self.model.stable_dt() if not self.model.needs_umax else 0.0
         rng = self.full if self.comm.size == 1 else self.interior
@@ -859,6 +925,9 @@ class Solver:
             self.sync_halos()
             for f in self.fields():
                 self.halo.prepare(f)
+            if self.fput:
+                for f in (self.u, self.un):
+                    self._put_targets(f)
 
     def _graph_for(self, dt: float | None, t_end: float | None = None):
         """dt=None: a graph of device-dt (adaptive CFL) steps towards t_end."""

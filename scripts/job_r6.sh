@@ -38,6 +38,14 @@ case "$1" in
   pmcb)  # counter row of the shipped WENO5-Z viscous stage (256^3 and 512^3)
     bash scripts/gpu_steps.sh r6/pmc_burgers \
       "pmc|600|PMC_OUT=gpurun_out/r6/pmc_burgers PMC_TARGETS='burgers burgers512' bash scripts/pmc_r5.sh" ;;
+  fput)  # fused halo puts: bitwise tests (2-4 ipc ranks on the GPU), kernel-side A/B at the
+         # slab-rank shapes, the N = 4 bench flow with the new candidate
+    bash scripts/gpu_steps.sh r6/fput \
+      "tests|600|$PT tests/test_ipc_gpu.py -k 'fused_put or slab_bitwise'" \
+      "ab|300|python -u bench/fused_put_ab.py" \
+      "reh4|450|$SH $R --nproc-per-node 4 --master-port 29604 bench.py --gpus 4 --steps 10 --warmup 3 --sustained-steps 0 --no-burgers" ;;
+  gap)  # the bench's Burgers window vs the rate tool: build path or thermal state
+    bash scripts/gpu_steps.sh r6/burgers_gap "gap|300|python -u bench/burgers_bench_gap.py" ;;
   own)  # WENO5 v9 staging the own cell from the register column: kernel A/B (two builds in
         # one process, bitwise compared) and in-solver rates (alternating processes)
     A=bench/ab_libs/libadvdiff_base.so; B=bench/ab_libs/${OWN_LIB:-libadvdiff_own2.so}

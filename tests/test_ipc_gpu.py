@@ -352,3 +352,42 @@ def test_ipc_multirank_two_step_bitwise(world, overlap):
             assert len({o[0] for o in out}) == 1
             g = out[0][1]
             assert np.array_equal(g, ref), (world, overlap, graph, flag, np.abs(g - ref).max())
+
+
+def _run_fused_put(comm, kind, steps, graph, dtype):  # noqa: D103
+    model, grid, ic = _make(kind)
+    s = Solver(model, grid, comm, dtype=dtype, ic=ic, transport="ipc", fused_put=True)
+    assert s.fput and not s.bcomm and not s._mr2 and s.ghost == 3 * model.radius
+    s.run(iters=steps, graph=graph)
+    g = s.gather()
+    assert comm.ipc().errors() == 0
+    return None if g is None else g.copy()
+
+
+@pytest.mark.parametrize("kind,dtype", [("diff3", torch.float64), ("diff3o2", torch.float64),
+                                        ("diff3", torch.float32)])
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_ipc_fused_put_bitwise(kind, dtype, world):
+    """Fused halo puts (transport "ipc+fused"): ONE step launch over every owned plane that
+    stores its boundary output planes straight into the neighbours' ghost planes
+    (advdiff_diffusion3d_step_put), then signal + wait — uneven slabs (41 planes over 2-4
+    ranks), FD4 and FD2, fp64 and fp32, eager and graph-replayed, odd step count: bitwise
+    equal to the one-rank run."""
+    model, grid, ic = _make(kind)
+    r = Solver(model, grid, dtype=dtype, device="cuda", ic=ic)
+    r.run(iters=17, graph=False)
+    ref = r.gather()
+    for graph in (False, True):
+        out = spawn_local(world, _run_fused_put, kind, 17, graph, dtype, device="cuda",
+                          transport="ipc", timeout=240)[0]
+        assert np.array_equal(out, ref), (kind, dtype, world, graph, np.abs(out - ref).max())
+
+
+def test_fused_put_needs_direct_ipc_slab():
+    """fused_put is ignored where it does not apply (one rank, per-stage Burgers)."""
+    model, grid, ic = _make("diff3")
+    assert not Solver(model, grid, dtype=torch.float64, device="cuda", ic=ic,
+                      fused_put=True).fput
+    model, grid, ic = _make("burg3")
+    assert not Solver(model, grid, dtype=torch.float64, device="cuda", ic=ic,
+                      fused_put=True).fput
