@@ -1,0 +1,82 @@
+"""Host-side logic of the fused halo puts (transport "ipc+fused", round 6): the bench's
+candidate list, the solver switch, and the peer-address plan SlabHalo.put_targets hands
+the step kernel (the kernel itself: tests/test_ipc_gpu.py::test_ipc_fused_put_bitwise)."""
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+from multigpu_advectiondiffusion_amd import Diffusion, Grid, Solver
+from multigpu_advectiondiffusion_amd.parallel import halo as halo_mod
+from multigpu_advectiondiffusion_amd.parallel.decomposition import SlabDecomposition
+from multigpu_advectiondiffusion_amd.parallel.preflight import transport_kwargs
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def test_candidates_and_kwargs(monkeypatch):
+    import bench
+    monkeypatch.delenv("ADVDIFF_SHARE_GPU", raising=False)
+    monkeypatch.delenv("ADVDIFF_BACKEND", raising=False)
+    assert "ipc+fused" in bench.planned_transports(4, True, "tune")
+    assert bench.planned_transports(4, False, "tune") == ["host"]
+    monkeypatch.setenv("ADVDIFF_SHARE_GPU", "1")
+    assert bench.planned_transports(2, True, "tune") == ["host", "ipc", "ipc+fused"]
+    assert transport_kwargs("ipc+fused") == {"transport": "ipc", "fused_put": True}
+
+
+def test_solver_ignores_fused_put_off_device():
+    """CPU (and any non-ipc / non-slab setting): the switch is ignored, the step is the
+    ordinary one."""
+    g = Grid((20, 18, 16), (1.0, 1.0, 1.0))
+    s = Solver(Diffusion(K=1.0, order=4), g, dtype=torch.float64, device="cpu",
+               fused_put=True)
+    assert not s.fput
+    s.run(iters=2)
+
+
+class _FakeIpc:
+    def __init__(self, strides):
+        self.strides = strides
+        self.seen = None
+
+    def targets(self, msgs):
+        self.seen = msgs
+        # the peer's receive box address: an arbitrary distinct value per peer
+        return [(1000 * (peer + 1), self.strides[0], self.strides[1]) for peer, _, _ in msgs]
+
+
+class _FakeComm:
+    def __init__(self, rank, size, ipc):
+        self.rank, self.size, self._ipc = rank, size, ipc
+        self.transport = "ipc"
+
+    def ipc(self):
+        return self._ipc
+
+
+@pytest.mark.parametrize("rank,size", [(0, 3), (1, 3), (2, 3), (1, 2)])
+def test_put_targets_plan(rank, size, monkeypatch):
+    """Each neighbour gets (its receive-box address, my send planes): lower <- planes
+    [o0, o0 + G), upper <- [o1 - G, o1); no neighbour: (0, 0, 0); a peer field with other
+    strides is refused (the kernel addresses the peer with the own in-plane offset)."""
+    monkeypatch.setattr(halo_mod, "_ipc_on", lambda h, f: True)
+    d = SlabDecomposition(41, size, rank, 6)
+    f = torch.zeros((d.alloc, 9, 12), dtype=torch.float64)
+    ipc = _FakeIpc((f.stride(1), f.stride(0)))
+    h = halo_mod.SlabHalo(_FakeComm(rank, size, ipc), d, transport="ipc")
+    lo, hi = h.put_targets(f)
+    if d.lower is None:
+        assert lo == (0, 0, 0)
+    else:
+        assert lo == (1000 * (d.lower + 1),) + tuple(d.send_lower())
+    if d.upper is None:
+        assert hi == (0, 0, 0)
+    else:
+        assert hi == (1000 * (d.upper + 1),) + tuple(d.send_upper())
+    if d.lower is not None or d.upper is not None:
+        bad = halo_mod.SlabHalo(_FakeComm(rank, size, _FakeIpc((f.stride(1) + 1, f.stride(0)))),
+                                d, transport="ipc")
+        with pytest.raises(ValueError):
+            bad.put_targets(f)
