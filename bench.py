@@ -451,11 +451,9 @@ def preflight_candidates(args, n, on_gpu, transports, heat_spec, burgers_spec):
             grids[mkey] = [None if args.decomp == "slab" else args.decomp]
     models = {mkey: spec for mkey, spec, _, _ in heat_spec + burgers_spec}
 
-    def ok_for(m, p, t):  # striping and fused puts: slabs only; fused puts: the heat step
+    def ok_for(m, p, t):  # striping and fused puts: slabs only
         slab = p in (None, "slab") or tuple(p)[1:] == (1, 1)
-        if t == "ipc+fused":
-            return slab and m == "heat"
-        return t != "ipc+stripe" or slab
+        return t not in ("ipc+stripe", "ipc+fused") or slab
     allc = [(m, p, t) for m in models for p in grids[m] for t in transports
             if ok_for(m, p, t)]
     if n == 1 or args.preflight == "off":
@@ -556,7 +554,7 @@ def run(args) -> int:
     secs = timed(solver, args.steps, args.warmup, dt, args.settle_ms, "heat")
     mlups = grid.cells * args.steps / secs / 1e6
     pg = solver.pgrid
-    link = {"ipc": "ipc device puts", "ipc+fused": "ipc puts inside the step launch",
+    link = {"ipc": "ipc device puts", "ipc+fused": "ipc puts inside the step launches",
             "rccl": "RCCL, boundary launch on the comm stream",
             "host": "host-staged", "rccl-plain": "RCCL, boundary launch after the interior",
             "ipc+stripe": "ipc device puts striped over idle links"}.get(transport, transport)

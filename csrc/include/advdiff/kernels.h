@@ -126,6 +126,15 @@ int advdiff_burgers3d_stage2_dt(int dtype, const void* in, void* aux, void* out,
                                 int border, int weno, double rdx, double rdy, double rdz,
                                 double vx, double vy, double vz, double dt, double a, double b,
                                 int ls, const double* dt_dev, void* stream);
+// One full-range stage of a slab rank whose output planes [lo_k0, lo_k1) / [hi_k0, hi_k1)
+// also go, system scope, to the peer planes at dst_lo / dst_hi (fused halo puts; fp64,
+// WENO5-JS / -Z, SSP-RK3 epilogues; see advdiff_diffusion3d_step_put).
+int advdiff_burgers3d_stage_put(int dtype, const void* in, void* aux, void* out, int nx, int ny,
+                                int64_t sy, int64_t sz, int k0, int k1, int border, int weno,
+                                double rdx, double rdy, double rdz, double vx, double vy,
+                                double vz, double dt, double a, double b, const double* dt_dev,
+                                void* dst_lo, int lo_k0, int lo_k1, void* dst_hi, int hi_k0,
+                                int hi_k1, void* stream);
 int advdiff_burgers2d_stage_dt(int dtype, const void* in, void* aux, void* out, int nx,
                                int64_t sy, int j0, int j1, int border, int weno, double rdx,
                                double rdy, double vx, double vy, double dt, double a, double b,

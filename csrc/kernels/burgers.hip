@@ -453,13 +453,19 @@ __device__ __forceinline__ T w5_combine6(T n1, T S1, T n2, T S2) {
 // The 32 x 16 tile also stages fewer halo cells per output (38 x 22 / (31 x 16) = 1.69
 // vs 70 x 14 / (63 x 8) = 1.94).  wave_shr1 hands lane 32 the face of lane 31 — lane 32
 // is its row's face-only lane, so the DPP shift needs no change.
-template <typename T, bool WZ, bool VISC, int MODE, int TXL = 64, bool PK = false>
+// PUT (round 6, slab ranks, ipc transport): the stage's output planes inside put's ranges
+// are also stored into the neighbours' ghost planes (common.hpp halo_put) — one launch per
+// stage over every owned plane instead of interior + boundary + put launches.
+template <typename T, bool WZ, bool VISC, int MODE, int TXL = 64, bool PK = false,
+          bool PUT = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void burgers3d_w5s_kernel(
     const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
     int k1, int k0b, int k1b, int gza, int zchunk, int border, T rdx3, T rdy3, T rdz6, T vx,
-    T vy, T vz, T dt, T a, T b, const double* __restrict__ dtp, int xcdmap) {
+    T vy, T vz, T dt, T a, T b, const double* __restrict__ dtp, int xcdmap,
+    HaloPut put = HaloPut{}) {
   static_assert(TXL == 64 || TXL == 32, "tile row: 64 or 32 lanes");
   static_assert(!PK || std::is_same_v<T, float>, "packed pairs: fp32");
+  static_assert(!(PK && PUT), "halo puts: one cell per lane");
   using V = std::conditional_t<PK, f32x2, T>;  // a lane's value: one cell or a z pair
   constexpr int NW = 8, RW = 64 / TXL;  // waves per workgroup, tile rows per wave
   constexpr int TY = NW * RW, R = 3, NR = 5, TX = TXL, TXO = TX - 1;
@@ -503,7 +509,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
   };
   if (dtp != nullptr && !device_dt(dtp, dt)) {  // adaptive run at t_end: out = in
     if (active)
-      for (int k = kc0; k < kc1; ++k) gst<T>(plane(out, k), goff, gld<T>(plane(in, k), goff));
+      for (int k = kc0; k < kc1; ++k) {
+        const T v = gld<T>(plane(in, k), goff);
+        gst<T>(plane(out, k), goff, v);
+        if constexpr (PUT) halo_put<T>(put, k, szb, goff, v);
+      }
+    if constexpr (PUT) __builtin_amdgcn_s_waitcnt(0);
     return;
   }
   // global load of plane k (PK: and of plane k + H, clamped to the last plane the
@@ -706,6 +717,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
     const V v = stage_value<V, MODE>(axk, ctr, L, V(dt), V(a), V(b), dnew);
     if (active) {
       gs(out, k, v);
+      if constexpr (PUT) halo_put<V>(put, k, szb, goff, v);
       if constexpr (MODE == kLs1 || MODE == kLs) gs(aux, k, dnew);
     }
     rp[sl(3)] = pn;  // f+(k+3), u(k+3) replace f+(k-2), u(k-2)
@@ -716,6 +728,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
       (void)((kb + P < kce ? (body.template operator()<P>(kb + P), true) : false) && ...);
     }(std::make_integer_sequence<int, 2 * NR>{});
   }
+  // every peer store of this wave acknowledged before the wave (and the dispatch) ends
+  if constexpr (PUT) __builtin_amdgcn_s_waitcnt(0);
 }
 
 template <typename T, int W, bool WZ, bool VISC, int MODE, int TX>
@@ -1077,8 +1091,8 @@ static int b3_tile_row(int nx, int ny, int border) {
 // the bit-reproducibility tests move the chunk boundaries with it
 static int g_b3_zchunk = 0;
 
-template <typename T, bool WZ, bool VISC, int MODE, int TXL, bool PK = false>
-static hipError_t launch_b3_v9_tx(const BArgs& p) {
+template <typename T, bool WZ, bool VISC, int MODE, int TXL, bool PK = false, bool PUT = false>
+static hipError_t launch_b3_v9_tx(const BArgs& p, const HaloPut& put = HaloPut{}) {
   // XCD-contiguous tile order (always, its switch removed in round 6): 256^3 WENO5-Z +
   // viscous step 0.584 -> 0.564 ms (+3.7 %, 3 interleaved rounds, bitwise identical;
   // profiles/archive/burgers3d_xcd_r2.log)
@@ -1092,7 +1106,7 @@ static hipError_t launch_b3_v9_tx(const BArgs& p) {
   // target-count rule (removed in round 6) gave 512^3 two chunks of 253 planes = 1088
   // workgroups for 512 resident slots: a third round with 64 workgroups alone on the chip.
   const int per_cu =
-      occupancy_per_cu((const void*)burgers3d_w5s_kernel<T, WZ, VISC, MODE, TXL, PK>, 512);
+      occupancy_per_cu((const void*)burgers3d_w5s_kernel<T, WZ, VISC, MODE, TXL, PK, PUT>, 512);
   // PK: a workgroup marches two half chunks side by side — choose the half length
   const int nm = PK ? div_up(na + nb, 2) : na + nb;
   const int zm = g_b3_zchunk > 0 ? std::max(1, PK ? div_up(g_b3_zchunk, 2) : g_b3_zchunk)
@@ -1102,12 +1116,20 @@ static hipError_t launch_b3_v9_tx(const BArgs& p) {
   const int gza = div_up(na, zc);
   const int gz = gza + div_up(nb, zc);
   const double s = 1.0 / 12.0;
-  hipLaunchKernelGGL((burgers3d_w5s_kernel<T, WZ, VISC, MODE, TXL, PK>), dim3(gx, gy, gz),
+  hipLaunchKernelGGL((burgers3d_w5s_kernel<T, WZ, VISC, MODE, TXL, PK, PUT>), dim3(gx, gy, gz),
                      dim3(64, 8, 1), 0, p.st, (const T*)p.in, (T*)p.aux, (T*)p.out, p.nx, p.ny,
                      p.sy, p.sz, p.lo, p.hi, p.lo2, p.hi2, gza, zc, p.border, T(p.rdx / 3.0),
                      T(p.rdy / 3.0), T(p.rdz / 6.0), T(p.vx * s), T(p.vy * s), T(p.vz * s),
-                     T(p.dt), T(p.a), T(p.b), p.dtp, xcdmap);
+                     T(p.dt), T(p.a), T(p.b), p.dtp, xcdmap, put);
   return hipGetLastError();
+}
+
+// the stage with fused halo puts: fp64, WENO5 (JS / Z), SSP-RK3 epilogues, one range
+template <bool WZ, bool VISC, int MODE>
+static hipError_t launch_b3_put(const BArgs& p, const HaloPut& put) {
+  if (b3_tile_row(p.nx, p.ny, p.border) == 32)
+    return launch_b3_v9_tx<double, WZ, VISC, MODE, 32, false, true>(p, put);
+  return launch_b3_v9_tx<double, WZ, VISC, MODE, 64, false, true>(p, put);
 }
 
 // fp32: packed pairs (two z half chunks per lane, v_pk_* arithmetic) by default;
@@ -1339,6 +1361,47 @@ extern "C" int advdiff_burgers3d_stage2_dt(int dtype, const void* in, void* aux,
   return run_b(dtype, true, weno, ls != 0, p);
 }
 
+// One full-range stage of a slab rank whose output planes [lo_k0, lo_k1) / [hi_k0, hi_k1)
+// are also stored, system scope, into the peer planes at dst_lo / dst_hi (IPC mappings of
+// the neighbours' output fields: the peer plane of local plane lo_k0 / hi_k0; same row pitch
+// and plane stride; null / empty: no peer that side).  fp64, WENO5-JS / -Z (weno 0 / 1),
+// SSP-RK3 epilogues (a == 0: first stage), the v9 kernel (planes below 2 GiB).
+extern "C" int advdiff_burgers3d_stage_put(int dtype, const void* in, void* aux, void* out,
+                                           int nx, int ny, int64_t sy, int64_t sz, int k0,
+                                           int k1, int border, int weno, double rdx, double rdy,
+                                           double rdz, double vx, double vy, double vz,
+                                           double dt, double a, double b, const double* dt_dev,
+                                           void* dst_lo, int lo_k0, int lo_k1, void* dst_hi,
+                                           int hi_k0, int hi_k1, void* stream) {
+  using namespace advdiff;
+  const BArgs p{in, aux, out, nx, ny, sy, sz, k0, k1, border, rdx, rdy, rdz,
+                vx, vy, vz, dt, a, b, (hipStream_t)stream, dt_dev};
+  if (k1 <= k0) return hipSuccess;
+  if (dtype != ADVDIFF_F64 || (weno != 0 && weno != 1) || k0 < 3 || border < 3 || nx <= 0 ||
+      ny <= 0 || in == out || b3_ver() != 9 || !v9_fits<double>(p))
+    return hipErrorInvalidValue;
+  HaloPut put{};
+  void* dsts[2] = {dst_lo, dst_hi};
+  const int pk0[2] = {lo_k0, hi_k0}, pk1[2] = {lo_k1, hi_k1};
+  for (int s = 0; s < 2; ++s) {
+    const bool on = dsts[s] != nullptr && pk1[s] > pk0[s];
+    put.dst[s] = on ? (char*)dsts[s] : nullptr;
+    put.k0[s] = on ? pk0[s] : 0;
+    put.k1[s] = on ? pk1[s] : 0;
+  }
+  const bool visc = vx != 0.0 || vy != 0.0 || vz != 0.0;
+  const int mode = a != 0.0 ? kSsp : kSsp1;
+#define BP(WZ, V) \
+  return mode == kSsp ? launch_b3_put<WZ, V, kSsp>(p, put) : launch_b3_put<WZ, V, kSsp1>(p, put)
+  if (weno == 1) {
+    if (visc) BP(true, true);
+    BP(true, false);
+  }
+  if (visc) BP(false, true);
+  BP(false, false);
+#undef BP
+}
+
 extern "C" int advdiff_burgers2d_stage_dt(int dtype, const void* in, void* aux, void* out,
                                           int nx, int64_t sy, int j0, int j1, int border,
                                           int weno, double rdx, double rdy, double vx,
@@ -1399,6 +1462,16 @@ static void preload_w5s_occupancies() {
      ...);
   }(std::make_integer_sequence<int, 32>{});
 }
+// the fused-put instances: fp64, SSP-RK3 epilogues (MODE 0 / 1), I as above
+static void preload_w5s_put_occupancies() {
+  [&]<int... I>(std::integer_sequence<int, I...>) {
+    ((void)occupancy_per_cu(
+         (const void*)burgers3d_w5s_kernel<double, (I & 1) != 0, (I & 2) != 0, (I >> 2) & 1,
+                                           (I & 8) ? 32 : 64, false, true>,
+         512),
+     ...);
+  }(std::make_integer_sequence<int, 16>{});
+}
 }  // namespace advdiff
 
 // Code-object preload (see advdiff_preload in aux.hip): the attributes query makes the
@@ -1415,5 +1488,6 @@ extern "C" int advdiff_preload_burgers(void) {
   preload_w5s_occupancies<double, false>();
   preload_w5s_occupancies<float, false>();
   preload_w5s_occupancies<float, true>();
+  preload_w5s_put_occupancies();
   return e;
 }

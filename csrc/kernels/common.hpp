@@ -21,6 +21,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace advdiff {
 
@@ -718,6 +719,38 @@ __device__ __forceinline__ void gst(__amdgpu_buffer_rsrc_t r, uint32_t boff, T v
   else
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)boff, 0, 0);
 }
+
+// Fused halo puts of a slab rank (ipc transport, round 6): the output planes [k0[s], k1[s])
+// of a launch are ALSO stored into a peer's ghost planes — dst[s] is the peer's plane for
+// local plane k0[s] (an IPC mapping of the peer's field with this field's row pitch and
+// plane stride), so the in-plane byte offset is the own one.  System-scope stores, as
+// ipc.hip's put kernel; the signal kernel after the launch publishes them.
+struct HaloPut {
+  char* dst[2];
+  int k0[2], k1[2];
+};
+// The store: a buffer store on a scalar plane base (no 64-bit per-lane address — as a
+// flat pointer the loop-invariant part dst + off was hoisted into VGPRs and spilled) with
+// cache policy sc0 sc1 (aux 1 | 16), the code gfx942's memory model gives a relaxed
+// system-scope atomic store: written through this XCD's L2 to the peer.
+constexpr int kSysScopeStore = 1 | 16;
+template <typename T>
+__device__ __forceinline__ void halo_put(const HaloPut& put, int k, int64_t plane_bytes,
+                                         uint32_t off, T v) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+    if (k >= put.k0[s] && k < put.k1[s]) {  // k is scalar: a scalar branch
+      const auto r = __builtin_amdgcn_make_buffer_rsrc(
+          put.dst[s] + (int64_t)(k - put.k0[s]) * plane_bytes, (short)0, -1, 0x00020000);
+      if constexpr (sizeof(T) == 8)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)off, 0,
+                                              kSysScopeStore);
+      else
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)off, 0,
+                                              kSysScopeStore);
+    }
+}
+
 // keep a value computed on every lane (no exec-masked skip of the computation): the
 // frozen-cell choice below it must be a v_cndmask, not a branch around the stencil
 template <typename T>

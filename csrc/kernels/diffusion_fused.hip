@@ -131,16 +131,9 @@ __device__ __forceinline__ AxisTile axis_tile(int t, int n, int W, int R, int a0
   return axis_tile(t, n, W, R, a0, a1, o0, o1, nmax, edge, 2 * R);
 }
 
-// Fused halo puts (slab ranks, ipc transport): the output planes [k0[s], k1[s]) of a
-// launch are ALSO stored into a peer's ghost planes — dst[s] is the peer's plane for local
-// plane k0[s] (an IPC mapping of the peer's output field, same row pitch and plane stride)
-// — so the exchange rides inside the step launch over xGMI instead of a boundary launch
-// plus a put launch after it.  Every such store is a system-scope store (as ipc_put_kernel's);
-// the signal kernel after the launch publishes them (ipc.hip link 2).
-struct StepPut {
-  char* dst[2];
-  int k0[2], k1[2];
-};
+// Fused halo puts (slab ranks, ipc transport; common.hpp HaloPut): the exchange rides
+// inside the step launch over xGMI instead of a boundary launch plus a put launch after it.
+using StepPut = HaloPut;
 
 // ---------------------------------------------------------------------------------
 // v3 march: the same algorithm (compact rings, trapezoid, one barrier per plane) with
@@ -379,14 +372,7 @@ __device__ __forceinline__ void v3_march(
     acc = pin(acc);
     if (m3[q]) gst<T>(plane_rsrc((char*)uout + (int64_t)kp * szb), goff[q], acc);
     if constexpr (PUT) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        if (kp >= put.k0[s] && kp < put.k1[s] && m3[q]) {  // kp scalar: a scalar branch
-          using U = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>;
-          U* d = (U*)(put.dst[s] + (int64_t)(kp - put.k0[s]) * szb + goff[q]);
-          __hip_atomic_store(d, __builtin_bit_cast(U, acc), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+      if (m3[q]) halo_put<T>(put, kp, szb, goff[q], acc);  // kp scalar: scalar branches
     }
   };
   // the y-axis sum of stage 3 from the B plane of buffer set AO (LDS)

@@ -66,6 +66,10 @@ class Model:
     bytes_per_cell_step = 64.0  # HBM traffic estimate of the fused path (metric only)
     needs_umax = False
     supports_fused = False   # one launch per full RK3 step (ghost width 3R)
+
+    def stage_put_ok(self, dtype) -> bool:
+        """The per-stage launch can carry fused halo puts (slab ranks, ipc)."""
+        return False
     supports_step2 = False   # one launch per TWO RK3 steps (single rank)
 
     def bind(self, grid: Grid) -> None:

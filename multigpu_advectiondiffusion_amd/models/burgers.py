@@ -21,6 +21,8 @@ i < Ny only — quirk #6); frozen Dirichlet border of 3 cells on every face.
 """
 from __future__ import annotations
 
+import torch
+
 from ..ops import stencil
 from .base import Model
 
@@ -76,8 +78,12 @@ class Burgers(Model):
     # slabs of a slab rank in one launch
     two_range_stage = True
 
+    def stage_put_ok(self, dtype) -> bool:
+        """The stage can carry fused halo puts (advdiff_burgers3d_stage_put)."""
+        return self.dims == 3 and self.weno in ("js", "z") and dtype == torch.float64
+
     def stage(self, inp, u0, out, lo, hi, dt, a, b, stream=None, nx=None, ny=None,
-              border=None, ls=False, dt_dev=None, lo2=0, hi2=0):
+              border=None, ls=False, dt_dev=None, lo2=0, hi2=0, put=None):
         g = self.grid
         nx = g.nx if nx is None else nx
         ny = g.ny if ny is None else ny
@@ -88,7 +94,8 @@ class Burgers(Model):
                                     border=border, weno_z=z, rdx=self.rd[0],
                                     rdy=self.rd[1], rdz=self.rd[2], vx=self.visc[0],
                                     vy=self.visc[1], vz=self.visc[2], dt=dt, a=a, b=b,
-                                    stream=stream, ls=ls, dt_dev=dt_dev, k0b=lo2, k1b=hi2)
+                                    stream=stream, ls=ls, dt_dev=dt_dev, k0b=lo2, k1b=hi2,
+                                    put=put)
         else:
             for j0, j1 in ((lo, hi), (lo2, hi2)):
                 if j1 > j0:

@@ -76,6 +76,10 @@ _SIGS = {
                                     c_int, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_dbl,
                                     c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_int, c_vp,
                                     c_vp],
+    "advdiff_burgers3d_stage_put": [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_i64, c_i64, c_int,
+                                    c_int, c_int, c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl,
+                                    c_dbl, c_dbl, c_dbl, c_dbl, c_vp, c_vp, c_int, c_int, c_vp,
+                                    c_int, c_int, c_vp],
     "advdiff_burgers2d_stage_dt": [c_int, c_vp, c_vp, c_vp, c_int, c_i64, c_int, c_int, c_int,
                                    c_int, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl, c_int,
                                    c_vp, c_vp],

@@ -275,16 +275,32 @@ def _dt_of(dt, dt_dev):
 
 def burgers3d_stage(inp, u0, out, *, nx, ny, k0, k1, border, weno_z, rdx, rdy, rdz,
                     vx=0.0, vy=0.0, vz=0.0, dt, a, b, stream=None, ls=False, dt_dev=None,
-                    k0b=0, k1b=0):
+                    k0b=0, k1b=0, put=None):
     """weno_z: scheme — bool (WENO5 Z / JS) or "js" | "z" | "js7" (WENO7).
     dt_dev: float64 device scalar holding dt (adaptive CFL: written on the device by
     adaptive_dt, read by the kernel — no host sync); 0 there makes the stage out = in.
     [k0b, k1b): an optional second plane range (a slab rank's other boundary slab),
-    served by the same launch (advdiff_burgers3d_stage2_dt)."""
+    served by the same launch (advdiff_burgers3d_stage2_dt).
+    put = ((dst_lo, lo_k0, lo_k1), (dst_hi, hi_k0, hi_k1)): fused halo puts of a slab rank
+    (advdiff_burgers3d_stage_put: native fp64 fields, WENO5, SSP-RK3, one range)."""
     _check_layout(inp, u0, out)
     code_s, R = ref.scheme_code(weno_z), ref.scheme_radius(weno_z)
     if border < R:
         raise ValueError(f"WENO needs a frozen border of at least {R} cells")
+    if put is not None:
+        if (not _native(inp) or inp.dtype != torch.float64 or code_s not in (0, 1) or ls
+                or k1b > k0b):
+            raise ValueError("fused halo puts: native fp64 WENO5 SSP-RK3 stages, one range")
+        lib = _lib.require()
+        assert k0 >= R and k1 + R <= inp.shape[0], "stencil planes out of bounds"
+        (dlo, lo0, lo1), (dhi, hi0, hi1) = put
+        code = lib.advdiff_burgers3d_stage_put(
+            _dtype_code(inp), _ptr(inp), _aux_ptr(u0, a, ls), _ptr(out), nx, ny,
+            inp.stride(1), inp.stride(0), k0, k1, border, code_s, rdx, rdy, rdz, vx, vy, vz,
+            dt, a, b, None if dt_dev is None else dt_dev.data_ptr(), dlo or None, lo0, lo1,
+            dhi or None, hi0, hi1, _stream_ptr(stream))
+        _lib.check(code, "burgers3d_stage_put")
+        return
     ranges = [(lo, hi) for lo, hi in ((k0, k1), (k0b, k1b)) if hi > lo]
     if _native(inp):
         lib = _lib.require()

@@ -150,12 +150,14 @@ class Solver:
         redundantly with the RK update).  "lu" is a slab, per-stage, PyTorch-ops mode kept
         for semantic parity; its results equal the "u" mode's bit for bit
         (tests/test_lu_exchange.py).
-        fused_put (3-D fused heat step, slab ranks, direct ipc transport): ONE launch per
-        step over all owned planes that also stores its boundary output planes straight
-        into the neighbours' ghost planes over xGMI (advdiff_diffusion3d_step_put), then
-        signal + wait — no boundary launch and no put launch (_step_fused_put).  None =
-        ADVDIFF_FUSED_PUT=1; ignored where it does not apply (per-stage models, Cartesian
-        grids, striped or non-ipc transports, the multi-rank FD2 two-step launch)."""
+        fused_put (3-D slab ranks, direct ipc transport): ONE launch per step (fused heat
+        step) or per stage (WENO5 fp64, SSP-RK3) over all owned planes that also stores its
+        boundary output planes straight into the neighbours' ghost planes over xGMI
+        (advdiff_diffusion3d_step_put / advdiff_burgers3d_stage_put), then signal + wait —
+        no boundary launch and no put launch (_step_fused_put, _stage_put).  None =
+        ADVDIFF_FUSED_PUT=1; ignored where it does not apply (other models / dtypes /
+        integrators, Cartesian grids, striped or non-ipc transports, the multi-rank FD2
+        two-step launch)."""
         if kernel not in ("native", "torch"):
             raise ValueError("kernel must be 'native' or 'torch'")
         if exchange not in ("u", "lu"):
@@ -283,8 +285,10 @@ class Solver:
             self.full = self.d.compute_range(model.border)
             self.interior, blo, bhi = self.d.split_ranges(model.border, G)
             self.boundary = [blo, bhi]
-        # fused halo puts: the step launch stores the send planes into the peers itself
-        self.fput = bool(self._want_put and self.fused and not self.cart and grid.dims == 3
+        # fused halo puts: the step launch (fused heat step) or every stage launch (3-D
+        # WENO5 fp64 SSP-RK3) stores the send planes into the peers itself
+        puts_fit = self.fused or (integrator == "ssprk3" and model.stage_put_ok(dtype))
+        self.fput = bool(self._want_put and puts_fit and not self.cart and grid.dims == 3
                          and comm.size > 1 and self.transport == "ipc"
                          and self.device.type == "cuda" and kernel == "native"
                          and exchange == "u" and not self._mr2 and not self.halo.striped)
@@ -504,8 +508,31 @@ class Solver:
                 self._pending[id(out)] = self.halo.start(out, after_event=False)
         cur.wait_event(bdone)
 
+    def _stage_put(self, inp, u0, out, a, b, dt, ls, pend):
+        """Per-stage counterpart of _step_fused_put: one launch over every owned plane that
+        also stores the boundary planes of `out` into the neighbours' ghost planes, then
+        signal + wait.  Ordering (SSP-RK3, out = A, B, u): the peer last read the ghosts of
+        its A in its stage 2 of the previous step, of its B in its stage 3, of its u in its
+        stage 1 of this step — each before the signal this stage's wait follows — and none
+        of the peer's concurrent stage reads its own output's ghosts (stage 3 reads u as
+        the aux operand on owned cells only)."""
+        if pend is not None:
+            pend.wait()
+        put = self._put_targets(out)
+        lo, hi = self.full
+        if hi > lo:
+            kw = {} if self._dt_dev is None else {"dt_dev": self._dt_dev}
+            with trace.range_("stage+puts"):
+                self.model.stage(inp, u0, out, lo, hi, dt, a, b, ls=ls, put=put, **kw)
+                trace.sync_check(f"{self.model.name} stage + puts [{lo},{hi})", self.device)
+        with trace.range_("halo_signal"):
+            self._pending[id(out)] = self.halo.start(out, puts=False)
+
     def _stage(self, inp, u0, out, a, b, dt, ls=False):
         pend = self._pending.pop(id(inp), None)
+        if self.fput:
+            self._stage_put(inp, u0, out, a, b, dt, ls, pend)
+            return
         if self.bcomm and self.comm.size > 1:
             self._stage_bcomm(inp, u0, out, a, b, dt, ls, pend)
             return
@@ -926,7 +953,7 @@ class Solver:
             for f in self.fields():
                 self.halo.prepare(f)
             if self.fput:
-                for f in (self.u, self.un):
+                for f in self.fields():
                     self._put_targets(f)
 
     def _graph_for(self, dt: float | None, t_end: float | None = None):

@@ -44,6 +44,16 @@ case "$1" in
       "tests|600|$PT tests/test_ipc_gpu.py -k 'fused_put or slab_bitwise'" \
       "ab|300|python -u bench/fused_put_ab.py" \
       "reh4|450|$SH $R --nproc-per-node 4 --master-port 29604 bench.py --gpus 4 --steps 10 --warmup 3 --sustained-steps 0 --no-burgers" ;;
+  bsplit)  # the Burgers stage's split cost at the slab-rank blocks; fused-put A/B re-check
+    bash scripts/gpu_steps.sh r6/bsplit \
+      "bsplit|300|python -u bench/burgers_split_ab.py" \
+      "fput_ab|300|python -u bench/fused_put_ab.py" ;;
+  fput2)  # fused halo puts in the WENO5 stage too: tests, kernel-side A/Bs, the N = 4 flow
+    bash scripts/gpu_steps.sh r6/fput2 \
+      "tests|600|$PT tests/test_ipc_gpu.py -k 'fused_put'" \
+      "bsplit|300|python -u bench/burgers_split_ab.py" \
+      "fput_ab|300|python -u bench/fused_put_ab.py" \
+      "reh4|500|$SH $R --nproc-per-node 4 --master-port 29604 bench.py --gpus 4 --steps 10 --warmup 3 --sustained-steps 0" ;;
   gap)  # the bench's Burgers window vs the rate tool: build path or thermal state
     bash scripts/gpu_steps.sh r6/burgers_gap "gap|300|python -u bench/burgers_bench_gap.py" ;;
   own)  # WENO5 v9 staging the own cell from the register column: kernel A/B (two builds in

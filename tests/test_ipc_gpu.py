@@ -357,7 +357,8 @@ def test_ipc_multirank_two_step_bitwise(world, overlap):
 def _run_fused_put(comm, kind, steps, graph, dtype):  # noqa: D103
     model, grid, ic = _make(kind)
     s = Solver(model, grid, comm, dtype=dtype, ic=ic, transport="ipc", fused_put=True)
-    assert s.fput and not s.bcomm and not s._mr2 and s.ghost == 3 * model.radius
+    assert s.fput and not s.bcomm and not s._mr2
+    assert s.ghost == (3 if s.fused else 1) * model.radius
     s.run(iters=steps, graph=graph)
     g = s.gather()
     assert comm.ipc().errors() == 0
@@ -365,14 +366,15 @@ def _run_fused_put(comm, kind, steps, graph, dtype):  # noqa: D103
 
 
 @pytest.mark.parametrize("kind,dtype", [("diff3", torch.float64), ("diff3o2", torch.float64),
-                                        ("diff3", torch.float32)])
+                                        ("diff3", torch.float32), ("burg3", torch.float64)])
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_ipc_fused_put_bitwise(kind, dtype, world):
-    """Fused halo puts (transport "ipc+fused"): ONE step launch over every owned plane that
-    stores its boundary output planes straight into the neighbours' ghost planes
-    (advdiff_diffusion3d_step_put), then signal + wait — uneven slabs (41 planes over 2-4
-    ranks), FD4 and FD2, fp64 and fp32, eager and graph-replayed, odd step count: bitwise
-    equal to the one-rank run."""
+    """Fused halo puts (transport "ipc+fused"): ONE launch per step (heat) or per stage
+    (WENO5-Z + viscous, adaptive device dt) over every owned plane that stores its boundary
+    output planes straight into the neighbours' ghost planes (advdiff_diffusion3d_step_put
+    / advdiff_burgers3d_stage_put), then signal + wait — uneven slabs (41 / 40 planes over
+    2-4 ranks), FD4 and FD2, fp64 and fp32, eager and graph-replayed, odd step count:
+    bitwise equal to the one-rank run."""
     model, grid, ic = _make(kind)
     r = Solver(model, grid, dtype=dtype, device="cuda", ic=ic)
     r.run(iters=17, graph=False)
@@ -384,10 +386,29 @@ def test_ipc_fused_put_bitwise(kind, dtype, world):
 
 
 def test_fused_put_needs_direct_ipc_slab():
-    """fused_put is ignored where it does not apply (one rank, per-stage Burgers)."""
-    model, grid, ic = _make("diff3")
-    assert not Solver(model, grid, dtype=torch.float64, device="cuda", ic=ic,
-                      fused_put=True).fput
+    """fused_put is ignored where it does not apply (one rank)."""
+    for kind in ("diff3", "burg3"):
+        model, grid, ic = _make(kind)
+        assert not Solver(model, grid, dtype=torch.float64, device="cuda", ic=ic,
+                          fused_put=True).fput
+
+
+def _run_fused_put_fp32_burgers(comm, steps):  # noqa: D103
     model, grid, ic = _make("burg3")
-    assert not Solver(model, grid, dtype=torch.float64, device="cuda", ic=ic,
-                      fused_put=True).fput
+    s = Solver(model, grid, comm, dtype=torch.float32, ic=ic, transport="ipc", fused_put=True)
+    assert not s.fput  # fp32 WENO5 runs packed pairs: the ordinary ipc exchange
+    s.run(iters=steps)
+    g = s.gather()
+    return None if g is None else g.copy()
+
+
+def test_fused_put_falls_back_for_fp32_burgers():
+    """Where the stage cannot carry the puts (fp32 WENO5: packed pairs), "ipc+fused" is the
+    plain ipc exchange — still bitwise equal to one rank."""
+    model, grid, ic = _make("burg3")
+    r = Solver(model, grid, dtype=torch.float32, device="cuda", ic=ic)
+    r.run(iters=5)
+    ref = r.gather()
+    out = spawn_local(2, _run_fused_put_fp32_burgers, 5, device="cuda", transport="ipc",
+                      timeout=240)[0]
+    assert np.array_equal(out, ref)
