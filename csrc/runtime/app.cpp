@@ -10,6 +10,8 @@
 //   --ic NAME  --order 2|4  --safety S  --weno js|z|js7  --visc C  --fp32  --no-overlap
 //   --[no-]boundary-on-comm (overlap: the boundary launch on the comm stream; default on
 //   for --transport rccl and ipc; ADVDIFF_BCOMM=0/1)
+//   --fused-put (--transport ipc slabs: the step / stage launch stores its boundary planes
+//   into the neighbours' ghost planes itself; ADVDIFF_FUSED_PUT=0/1)
 //   --integrator ssprk3|lsrk45  --no-fused  --transport rccl|ipc|socket  --write FILE
 //   --write-ghosts FILE (the reference's multi-GPU result.bin: every rank's slab WITH its
 //   ghost planes, MultiGPU/Diffusion3d_Baseline/main.c:341)  --error-norms
@@ -132,7 +134,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
     std::string a = argv[q];
     if (a.rfind("--", 0) == 0) {
       const bool flag = a == "--fp32" || a == "--no-overlap" || a == "--boundary-on-comm" ||
-                        a == "--no-boundary-on-comm" ||
+                        a == "--no-boundary-on-comm" || a == "--fused-put" ||
                         a == "--error-norms" || a == "--no-fused" || a == "--geometry" || a == "--graph" ||
                         a == "--no-graph" || a == "--print" || a == "--json";
       if (flag || q + 1 >= argc) {
@@ -151,7 +153,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
     std::cerr << "usage: " << argv[0]
               << (diff ? (dims == 3 ? " K L W H Nx Ny Nz iters [bx by bz]" : " K L W Nx Ny iters [bx by]")
                        : (dims == 3 ? " tEnd CFL L W H Nx Ny Nz [bx by bz]" : " tEnd CFL L W Nx Ny [bx by]"))
-              << " [--ic NAME] [--order 2|4] [--weno js|z|js7] [--integrator ssprk3|lsrk45] [--no-fused] [--visc C] [--fp32] [--no-overlap] [--[no-]boundary-on-comm]"
+              << " [--ic NAME] [--order 2|4] [--weno js|z|js7] [--integrator ssprk3|lsrk45] [--no-fused] [--visc C] [--fp32] [--no-overlap] [--[no-]boundary-on-comm] [--fused-put]"
                  " [--transport rccl|ipc|socket] [--decomp slab|PZxPYxPX|PYxPX] [--write FILE]"
                  " [--write-ghosts FILE] [--error-norms] [--geometry] [--graph|--no-graph]"
                  " [--restart PREFIX] [--checkpoint PREFIX] [--check-every N] [--ascii FILE]"
@@ -196,6 +198,7 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
   if (opt.count("--no-overlap")) p.overlap = false;
   if (opt.count("--boundary-on-comm")) p.bcomm = 1;
   if (opt.count("--no-boundary-on-comm")) p.bcomm = 0;
+  if (opt.count("--fused-put")) p.fused_put = 1;
   if (opt.count("--pitch")) {
     const std::string v = opt["--pitch"];
     if (std::sscanf(v.c_str(), "%d,%d", &p.pitch_px, &p.pitch_py) != 2 || p.pitch_px < 0 ||
@@ -247,7 +250,8 @@ int run_app(int argc, char** argv, Physics phys, int dims) {
       std::string(diff ? "Diffusion-" : "Burgers-") + (dims == 3 ? "3D" : "2D") +
       (diff ? (p.order == 4 ? " MI355X-FD4" : " MI355X-FD2") : (p.weno == 1 ? " MI355X-WENO5Z" : p.weno == 0 ? " MI355X-WENO5JS" : " MI355X-WENO7JS"));
   std::string optname = std::string("Fused LDS z-march + RK3 (gfx950), transport=") + tr->name() +
-                        (eng.graphs() ? ", hipGraph steps" : "");
+                        (eng.graphs() ? ", hipGraph steps" : "") +
+                        (eng.fused_puts() ? ", halo puts in the launch" : "");
   if (eng.cartesian()) {
     optname += ", decomp=" + std::to_string(eng.cart().pgrid[0]) + "x" +
                std::to_string(eng.cart().pgrid[1]);

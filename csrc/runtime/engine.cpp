@@ -180,6 +180,27 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
     // blocks the host on comm_ inside start_halo: keep its boundary on compute_)
     bcomm_ = bc != 0 && env.size > 1 && p.overlap && std::string(tr_->name()) != "socket";
   }
+  {
+    // fused halo puts (solver.py _step_fused_put / _stage_put): ipc slabs, the 3-D fused
+    // heat step or the fp64 WENO5 SSP-RK3 stage; every rank must address the peer planes
+    // with its own row pitch and plane stride, so those must agree across the ranks
+    int fp = p.fused_put;
+    if (fp < 0) {
+      const char* v = std::getenv("ADVDIFF_FUSED_PUT");
+      fp = v ? std::atoi(v) : 0;
+    }
+    const bool stage_ok = p_.physics == Physics::Burgers && p_.dims == 3 &&
+                          (p_.weno == 0 || p_.weno == 1) && p_.dtype == ADVDIFF_F64 &&
+                          p_.integrator == 0;
+    fput_ = fp != 0 && env.size > 1 && !cart_ && p_.dims == 3 &&
+            std::string(tr_->name()) == "ipc" && (fused_ || stage_ok);
+    if (fput_) {
+      const double z1 = tr_->allreduce_max((double)sz_), z0 = -tr_->allreduce_max(-(double)sz_);
+      const double y1 = tr_->allreduce_max((double)sy_), y0 = -tr_->allreduce_max(-(double)sy_);
+      fput_ = z1 == z0 && y1 == y0;
+      if (fput_) bcomm_ = false;  // no boundary launch left to move
+    }
+  }
   if (sync_debug_enabled() || p.check_every > 0 || fault_rank_ >= 0)
     graph_ = false;  // per-launch / per-step host checks
   if (graph_ && std::string(tr_->name()) == "socket")
@@ -325,9 +346,43 @@ void Engine::launch_fused(Range r, double dt, Range r2, bool exclusive) {
       dt, exclusive ? ADVDIFF_EXCLUSIVE : 0, ls_));
 }
 
+void Engine::put_targets(void* f, void** dlo, void** dhi) {
+  const int G = slab_.ghost, c = slab_.count();
+  if (!tr_->halo_targets(plane(f, G), plane(f, 0), plane(f, G + c - G), plane(f, G + c),
+                         (size_t)G * plane_bytes_, slab_.lower(), slab_.upper(), dlo, dhi))
+    throw std::runtime_error("fused halo puts: the transport has no peer addresses");
+}
+
+// the exchange of a field whose send planes the producing launch already stored into the
+// peers: signal + wait on comm_, after the launch (start_halo without the puts)
+void Engine::signal_halo(void* f) {
+  const int G = slab_.ghost, c = slab_.count();
+  HIP_CHECK(hipEventRecord(ready_, compute_));
+  HIP_CHECK(hipStreamWaitEvent(comm_, ready_, 0));
+  tr_->halo_signal(plane(f, G), plane(f, 0), plane(f, G + c - G), plane(f, G + c),
+                   (size_t)G * plane_bytes_, slab_.lower(), slab_.upper(), comm_);
+  HIP_CHECK(hipEventRecord(halo_done_, comm_));
+  halo_pending_ = true;
+}
+
 void Engine::step_fused(double dt) {
   if (cart_) {
     step_fused_cart(dt);
+    return;
+  }
+  if (fput_) {  // one launch; its boundary planes go straight into the neighbours' ghosts
+    if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
+    void *dlo = nullptr, *dhi = nullptr;
+    put_targets(A_, &dlo, &dhi);
+    const int G = slab_.ghost, c = slab_.count();
+    const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
+    KERNEL_CHECK(advdiff_diffusion3d_step_put(
+        p_.dtype, u_, A_, p_.nx, p_.ny, sy_, sz_, slab_.alloc(), full_.lo, full_.hi, zact_.lo,
+        zact_.hi, p_.border(), p_.order, p_.K / (dx * dx), p_.K / (dy * dy), p_.K / (dz * dz),
+        dt, dlo, G, 2 * G, dhi, c, c + G, compute_));
+    halo_pending_ = false;
+    std::swap(u_, A_);
+    signal_halo(u_);
     return;
   }
   if (env_.size == 1) {
@@ -417,6 +472,20 @@ void Engine::stage(void* in, void* aux, void* out, double a, double b, double dt
   }
   if (env_.size == 1) {
     launch(in, aux, out, full_, dt, a, b, ls);
+    return;
+  }
+  if (fput_ && !ls) {  // the fp64 WENO5 stage with its halo puts inside (_stage_put)
+    if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(compute_, halo_done_, 0));
+    void *dlo = nullptr, *dhi = nullptr;
+    put_targets(out, &dlo, &dhi);
+    const int G = slab_.ghost, c = slab_.count();
+    const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
+    KERNEL_CHECK(advdiff_burgers3d_stage_put(
+        p_.dtype, in, aux, out, p_.nx, p_.ny, sy_, sz_, full_.lo, full_.hi, p_.border(),
+        p_.weno, 1.0 / dx, 1.0 / dy, 1.0 / dz, p_.C / (dx * dx), p_.C / (dy * dy),
+        p_.C / (dz * dz), dt, a, b, nullptr, dlo, G, 2 * G, dhi, c, c + G, compute_));
+    halo_pending_ = false;
+    signal_halo(out);
     return;
   }
   if (p_.overlap) {

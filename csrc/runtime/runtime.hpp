@@ -114,6 +114,18 @@ class Transport {
   // (-1 = none) on `stream`: send_lo -> lower's recv_hi, send_hi -> upper's recv_lo.
   virtual void halo(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
                     size_t bytes, int lower, int upper, hipStream_t stream) = 0;
+  // Fused halo puts (ipc): the peer address of the receive slab matching each send slab
+  // of halo() — the same handshake and cache — so a step kernel can store the send planes
+  // itself (dst_lo / dst_hi: nullptr where there is no neighbour); halo_signal() then
+  // enqueues only the signal + wait of that halo.  false: the transport cannot.
+  virtual bool halo_targets(const void* /*send_lo*/, void* /*recv_lo*/, const void* /*send_hi*/,
+                            void* /*recv_hi*/, size_t /*bytes*/, int /*lower*/, int /*upper*/,
+                            void** /*dst_lo*/, void** /*dst_hi*/) {
+    return false;
+  }
+  virtual void halo_signal(const void* /*send_lo*/, void* /*recv_lo*/, const void* /*send_hi*/,
+                           void* /*recv_hi*/, size_t /*bytes*/, int /*lower*/, int /*upper*/,
+                           hipStream_t /*stream*/) {}
   virtual double allreduce_max(double v) = 0;
   virtual double allreduce_sum(double v) = 0;
   virtual void barrier() = 0;
@@ -310,6 +322,10 @@ struct Problem {
   // halo and the puts of its output (-1 = ADVDIFF_BCOMM, default on for the ipc transport;
   // --boundary-on-comm / --no-boundary-on-comm)
   int bcomm = -1;
+  // fused halo puts (ipc slabs, 3-D fused heat step or fp64 WENO5 SSP-RK3 stages): the
+  // step / stage launch stores its boundary planes into the neighbours' ghost planes
+  // itself, then signal + wait (-1 = ADVDIFF_FUSED_PUT; --fused-put)
+  int fused_put = -1;
   // pitched fields (solver.py pitch_default): extra elements per row after the 256-B
   // alignment and extra rows per 3-D plane, never read or written (-1 = ADVDIFF_PITCH,
   // else 4 fp64 / 16 fp32 elements and one row on 3-D fields past 128 MiB per rank;
@@ -368,6 +384,7 @@ class Engine {
   // graph of the current buffer parity, OUTSIDE the timed loop (captures run no work)
   void prepare_graphs(double dt);
   bool graphs() const { return graph_; }
+  bool fused_puts() const { return fput_; }
   static constexpr int kGraphSteps = 8;  // even: the u/A ping-pong returns to its start
   Stats run_iters(int iters);
   // n untimed steps, then the state exactly as before them (fields, buffer roles, t, it):
@@ -419,6 +436,9 @@ class Engine {
   void launch_fused(Range r, double dt, Range r2 = Range{}, bool exclusive = false);
   void step_fused(double dt);
   void start_halo(void* field, bool on_comm = false);
+  // fused halo puts: the peer planes of `field`'s send slabs / the signal + wait after
+  void put_targets(void* field, void** dlo, void** dhi);
+  void signal_halo(void* field);
   void* plane(void* base, int l) const { return (char*)base + (size_t)l * plane_bytes_; }
   // checkpoint views: array order padded to three axes (2-D: axis 0 is a unit axis whose
   // one "plane" is the whole field)
@@ -484,6 +504,7 @@ class Engine {
   hipEvent_t ready_ = nullptr, halo_done_ = nullptr;
   hipEvent_t cready_ = nullptr, bdone_ = nullptr;  // bcomm_: compute_ -> comm_, comm_ -> compute_
   bool bcomm_ = false;
+  bool fput_ = false;  // fused halo puts (engine.cpp step_fused / stage)
   void bcomm_begin();
   void bcomm_end();
   bool halo_pending_ = false;

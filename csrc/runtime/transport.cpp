@@ -577,6 +577,27 @@ class IpcTransport final : public Transport {
             size_t bytes, int lower, int upper, hipStream_t s) override {
     exchange(neighbour_msgs(send_lo, recv_lo, send_hi, recv_hi, bytes, lower, upper), s);
   }
+  bool halo_targets(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
+                    size_t bytes, int lower, int upper, void** dst_lo, void** dst_hi) override {
+    const std::vector<BoxMsg> b = halo_boxes(send_lo, recv_lo, send_hi, recv_hi, bytes, lower,
+                                             upper);
+    const std::vector<Dest> d = resolve(b);
+    *dst_lo = *dst_hi = nullptr;
+    for (size_t q = 0; q < b.size(); ++q) (b[q].peer == lower ? *dst_lo : *dst_hi) = d[q].ptr;
+    return true;
+  }
+  void halo_signal(const void* send_lo, void* recv_lo, const void* send_hi, void* recv_hi,
+                   size_t bytes, int lower, int upper, hipStream_t s) override {
+    const std::vector<BoxMsg> b = halo_boxes(send_lo, recv_lo, send_hi, recv_hi, bytes, lower,
+                                             upper);
+    if (b.empty()) return;
+    (void)resolve(b);  // the same handshake bookkeeping as a halo() with puts
+    if (dry_) return;
+    std::vector<int> peers;
+    for (const BoxMsg& m : b) peers.push_back(m.peer);
+    ipc_check(advdiff_ipc_signal(ctx_, peers.data(), (int)peers.size(), s), "advdiff_ipc_signal");
+    ipc_check(advdiff_ipc_wait(ctx_, peers.data(), (int)peers.size(), s), "advdiff_ipc_wait");
+  }
   double allreduce_max(double v) override { return star_.reduce(v, true); }
   double allreduce_sum(double v) override { return star_.reduce(v, false); }
   void barrier() override { star_.reduce(0.0, false); }
@@ -617,6 +638,13 @@ class IpcTransport final : public Transport {
     b.nj = b.nk = 1;
     b.ssy = b.rsy = b.ni;
     b.ssz = b.rsz = b.ni;
+    return b;
+  }
+  std::vector<BoxMsg> halo_boxes(const void* send_lo, void* recv_lo, const void* send_hi,
+                                 void* recv_hi, size_t bytes, int lower, int upper) {
+    std::vector<BoxMsg> b;
+    for (const Msg& m : neighbour_msgs(send_lo, recv_lo, send_hi, recv_hi, bytes, lower, upper))
+      b.push_back(flat_box(m.peer, m.send, m.recv, m.bytes));
     return b;
   }
   // The peer's receive address of every message.  First use of a (peer, send, recv,

@@ -54,6 +54,10 @@ case "$1" in
       "bsplit|300|python -u bench/burgers_split_ab.py" \
       "fput_ab|300|python -u bench/fused_put_ab.py" \
       "reh4|500|$SH $R --nproc-per-node 4 --master-port 29604 bench.py --gpus 4 --steps 10 --warmup 3 --sustained-steps 0" ;;
+  fput3)  # native-engine fused halo puts + the N = 8 flow with the new candidates
+    bash scripts/gpu_steps.sh r6/fput3 \
+      "native|600|$PT tests/test_ipc_gpu.py -k 'native_fused_put or native_plain_overlap'" \
+      "reh8|600|$SH $R --nproc-per-node 8 --master-port 29608 bench.py --gpus 8 --steps 10 --warmup 3" ;;
   gap)  # the bench's Burgers window vs the rate tool: build path or thermal state
     bash scripts/gpu_steps.sh r6/burgers_gap "gap|300|python -u bench/burgers_bench_gap.py" ;;
   own)  # WENO5 v9 staging the own cell from the register column: kernel A/B (two builds in

@@ -412,3 +412,26 @@ def test_fused_put_falls_back_for_fp32_burgers():
     out = spawn_local(2, _run_fused_put_fp32_burgers, 5, device="cuda", transport="ipc",
                       timeout=240)[0]
     assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("app,args,shape,world,extra", [
+    NATIVE_CASES[3][:4] + (["--ic", "sine"],),
+    NATIVE_CASES[3][:4] + (["--ic", "sine", "--order", "2"],),
+    ("diffusion3d", [1.0, 1.0, 1.0, 1.0, 66, 40, 45, 12], (45, 40, 66), 4, ["--ic", "sine"]),
+    NATIVE_CASES[6][:4] + ([],),
+    ("burgers3d", [0.03, 0.3, 2.0, 2.0, 2.0, 40, 36, 41], (41, 36, 40), 3, ["--weno", "js"]),
+])
+def test_native_fused_put_bitwise(tmp_path, app, args, shape, world, extra):
+    """Native engine, --transport ipc --fused-put: ONE launch per step (fused heat) or per
+    stage (fp64 WENO5) storing its boundary planes into the neighbours' ghost planes, then
+    signal + wait (engine.cpp step_fused / stage) — uneven slabs, graph-replayed, poisoned
+    allocations: bitwise equal to one rank."""
+    one, many = tmp_path / "one.bin", tmp_path / "many.bin"
+    env = {"ADVDIFF_POISON": "1"}
+    _native(app, args, one, extra=extra, env_extra=env)
+    txt = _native(app, args, many, world=world,
+                  extra=extra + ["--transport", "ipc", "--fused-put"], env_extra=env)
+    assert "halo puts in the launch" in txt, txt[-2000:]
+    a = np.fromfile(one, dtype=np.float32).reshape(shape)
+    b = np.fromfile(many, dtype=np.float32).reshape(shape)
+    assert np.isfinite(a).all() and np.array_equal(a, b), txt[-2000:]
