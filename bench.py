@@ -461,7 +461,10 @@ def preflight_candidates(args, n, on_gpu, transports, heat_spec, burgers_spec):
     verdict = {}
     dev = "cuda" if on_gpu else "cpu"
     for fam in ("gloo", "nccl"):  # ipc first: its pair preflight bounds itself
-        cs = [c for c in allc if family(c[2]) == fam]
+        # the newest transports last in their family: a family stops after two hangs, and
+        # those then cost only the candidates behind them
+        cs = sorted((c for c in allc if family(c[2]) == fam),
+                    key=lambda c: {"ipc+stripe": 1, "ipc+fused": 2}.get(c[2], 0))
         if not cs:
             continue
         dl = STATE["deadline"]
