@@ -23,7 +23,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from multigpu_advectiondiffusion_amd.ops import stencil  # noqa: E402
+from multigpu_advectiondiffusion_amd.ops import _lib, stencil  # noqa: E402
 
 # ranks -> (nx, ny, owned planes) of one slab rank of the weak-scaling grid (base 512)
 SHAPES = {8: (1024, 1024, 128), 4: (512, 1024, 256), 2: (512, 512, 512)}
@@ -77,7 +77,18 @@ def main():
             e1.synchronize()
             return e0.elapsed_time(e1) * 1e3 / a.steps
 
-        runs = {"split": seq(split), "whole": seq(whole), "put": seq(fused)}
+        lib = _lib.require()
+
+        def banded(fn):  # the same sequence with the banded z schedule forced
+            def run():
+                old = lib.advdiff_set_step_banded(1)
+                try:
+                    fn()
+                finally:
+                    lib.advdiff_set_step_banded(old)
+            return run
+        runs = {"split": seq(split), "whole": seq(whole), "put": seq(fused),
+                "whole_banded": banded(seq(whole)), "put_banded": banded(seq(fused))}
         for _ in range(3):
             for r in runs.values():
                 r()
@@ -85,21 +96,26 @@ def main():
         for _ in range(a.rounds):
             for k, r in runs.items():
                 best[k] = min(best[k], timed(r))
-        # the puts landed: the peer planes equal my boundary output planes
+        # the puts landed: the peer planes equal my boundary output planes (both schedules)
         w = torch.empty_like(u)
         stencil.diffusion3d_step(u, w, k0=G, k1=own + G, **kw)
-        peer.zero_()
-        stencil.diffusion3d_step(u, v, k0=G, k1=own + G, put=put, **kw)
-        torch.cuda.synchronize()
-        ok = (torch.equal(v[G:own + G, 2:ny - 2, 2:nx - 2], w[G:own + G, 2:ny - 2, 2:nx - 2])
-              and torch.equal(peer[G + own:2 * G + own, 2:ny - 2, 2:nx - 2],
-                              w[G:2 * G, 2:ny - 2, 2:nx - 2])
-              and torch.equal(peer[0:G, 2:ny - 2, 2:nx - 2], w[own:own + G, 2:ny - 2, 2:nx - 2]))
+        ok = True
+        for m in (0, 1):
+            peer.zero_()
+            old = lib.advdiff_set_step_banded(m)
+            stencil.diffusion3d_step(u, v, k0=G, k1=own + G, put=put, **kw)
+            lib.advdiff_set_step_banded(old)
+            torch.cuda.synchronize()
+            i = (slice(None), slice(2, ny - 2), slice(2, nx - 2))  # the interior of a plane
+            ok = (ok and torch.equal(v[G:own + G][i], w[G:own + G][i])
+                  and torch.equal(peer[G + own:2 * G + own][i], w[G:2 * G][i])
+                  and torch.equal(peer[0:G][i], w[own:own + G][i]))
         cells = nx * ny * own
         print(json.dumps({"ranks": n, "rank_block": [nx, ny, own],
                           **{f"{k}_us": round(t, 1) for k, t in best.items()},
                           **{f"{k}_mlups": round(cells / t, 1) for k, t in best.items()},
                           "put_vs_split": round(best["split"] / best["put"], 4),
+                          "put_banded_vs_split": round(best["split"] / best["put_banded"], 4),
                           "puts_exact": bool(ok)}), flush=True)
         del u, v, peer, w
         torch.cuda.empty_cache()

@@ -948,8 +948,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((
   Tile3 tile;
   if (sc.zfirst > 0) {  // banded: one long band, then short ones fill the last rounds
     tile = xcd_tile_banded(sc.gx * sc.gy, sc.gx);
-    kc0 = k0 + (tile.z == 0 ? 0 : sc.zfirst + (tile.z - 1) * sc.zchunk);
-    kc1 = min(kc0 + (tile.z == 0 ? sc.zfirst : sc.zchunk), k1);
+    if constexpr (PUT) {
+      // the long band at the TOP of the range: its workgroups store the upper face as
+      // they end and the first short band's store the lower face as they start, so both
+      // faces' puts run through the launch (bottom-up, the top band would be dispatched
+      // last and bunch the upper peer's stores at the end)
+      const int top = k1 - sc.zfirst;
+      kc0 = tile.z == 0 ? top : k0 + (tile.z - 1) * sc.zchunk;
+      kc1 = tile.z == 0 ? k1 : min(kc0 + sc.zchunk, top);
+    } else {
+      kc0 = k0 + (tile.z == 0 ? 0 : sc.zfirst + (tile.z - 1) * sc.zchunk);
+      kc1 = min(kc0 + (tile.z == 0 ? sc.zfirst : sc.zchunk), k1);
+    }
   } else {
     tile = xcd_tile();
     // z chunks of the first range [k0,k1), then (tile.z >= gza) of the second [k0b,k1b)
@@ -1112,11 +1122,10 @@ static hipError_t launch_step(const SArgs& a, const StepPut& put = StepPut{}) {
   const long long slots = (long long)device_cus() * per_cu;
   StepSched sc{gx, gy, 0, 0, edge};
   dim3 grid;
-  // (PUT: uniform chunks — the banded grid dispatches the top band last, which would
-  // bunch the upper peer's stores at the end of the launch; with uniform chunks
-  // xcd_tile spreads the chunks of a column over the XCDs, so both faces' stores run
-  // through the whole launch)
-  if (!PUT && nb == 0 && na > 0 && sched_banded((int)sizeof(T), ORDER, a)) {
+  // (PUT, banded: the long band is the top one, see the kernel; uniform chunks: xcd_tile
+  // spreads the chunks of a column over the XCDs, so both faces' stores run through the
+  // whole launch either way)
+  if (nb == 0 && na > 0 && sched_banded((int)sizeof(T), ORDER, a)) {
     const Bands bd = step_bands(na, (long long)gx * gy, slots, 4 * R, minc);
     sc.zfirst = bd.zfirst;
     sc.zchunk = bd.zchunk;

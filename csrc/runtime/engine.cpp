@@ -222,10 +222,11 @@ Engine::Engine(const Problem& p, Transport* tr, const ProcEnv& env) : p_(p), tr_
     step2_env_ = use2 != 0;
   }
   // banded or uniform z chunks for the fused 3-D heat launch that carries most planes (one
-  // rank: the full range; slabs: the interior launch): measured, cached in the kernel
-  // library (kernels.h advdiff_diffusion3d_step_sched_pick), before any capture
+  // rank, or slabs with fused puts: the full range; slabs: the interior launch): measured,
+  // cached in the kernel library (kernels.h advdiff_diffusion3d_step_sched_pick), before
+  // any capture
   if (fused_ && !cart_ && p_.dims == 3 && p_.physics == Physics::Diffusion) {
-    const Range r = env_.size == 1 ? full_ : interior_;
+    const Range r = env_.size == 1 || fput_ ? full_ : interior_;
     if (!r.empty()) {
       const double dx = p_.dx(), dy = p_.dy(), dz = p_.dz();
       const int B = p_.border();

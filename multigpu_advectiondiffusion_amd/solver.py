@@ -766,11 +766,12 @@ class Solver:
         shape on the GPU before any graph capture (diffusion_fused.hip step_bands; the
         kernel library caches the choice; ADVDIFF_STEP_BANDED=0/1 forces)."""
         if not (self.fused and self.grid.dims == 3 and self.kernel == "native"
-                and self.device.type == "cuda" and hasattr(self.model, "sched_pick")
-                and not self.fput):  # the put launch always takes uniform chunks
+                and self.device.type == "cuda" and hasattr(self.model, "sched_pick")):
             return
         dt = self.model.stable_dt() if not self.model.needs_umax else 0.0
-        rng = self.full if self.comm.size == 1 else self.interior
+        # fused puts: the one launch over every owned plane (timed without its puts: the
+        # same geometry, the same cached choice)
+        rng = self.full if self.comm.size == 1 or self.fput else self.interior
         if self.cart:
             self._launch_fused_box(rng, dt, pick=True)
         elif rng[1] > rng[0]:
