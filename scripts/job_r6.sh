@@ -58,6 +58,10 @@ case "$1" in
     bash scripts/gpu_steps.sh r6/fput3 \
       "native|600|$PT tests/test_ipc_gpu.py -k 'native_fused_put or native_plain_overlap'" \
       "reh8|600|$SH $R --nproc-per-node 8 --master-port 29608 bench.py --gpus 8 --steps 10 --warmup 3" ;;
+  fput4)  # fused puts with the top-band banded schedule: tests, A/B
+    bash scripts/gpu_steps.sh r6/fput4 \
+      "tests|600|ADVDIFF_STEP_BANDED=1 $PT tests/test_ipc_gpu.py -k 'fused_put'" \
+      "ab|300|python -u bench/fused_put_ab.py" ;;
   gap)  # the bench's Burgers window vs the rate tool: build path or thermal state
     bash scripts/gpu_steps.sh r6/burgers_gap "gap|300|python -u bench/burgers_bench_gap.py" ;;
   own)  # WENO5 v9 staging the own cell from the register column: kernel A/B (two builds in
