@@ -195,8 +195,9 @@ def planned_transports(world: int, on_gpu: bool, want: str) -> list:
     """Halo transports the run may use (before any process group exists): with the nccl
     backend rccl (boundary launch on the comm stream, the default schedule), rccl-plain
     (boundary launch after the interior), ipc, ipc+fused (the heat step's halo puts inside
-    its one launch; slabs) and, at 7-8 ranks, ipc+stripe; with ranks sharing one GPU
-    (ADVDIFF_SHARE_GPU=1, gloo) host, ipc and ipc+fused; on the CPU host only."""
+    its one launch; slabs) and, at 7-8 ranks, ipc+stripe and ipc+fused+stripe; with ranks
+    sharing one GPU (ADVDIFF_SHARE_GPU=1, gloo) host, ipc and ipc+fused (+ the striped
+    pair); on the CPU host only."""
     if world == 1:
         return [None]
     if not on_gpu:
@@ -209,7 +210,7 @@ def planned_transports(world: int, on_gpu: bool, want: str) -> list:
         names = ["rccl", "rccl-plain", "ipc", "ipc+fused"]
     from multigpu_advectiondiffusion_amd.parallel.ipc import stripe_plan
     if any(stripe_plan(world, STRIPE).values()):  # 7-8 ranks: idle links exist
-        names.append("ipc+stripe")
+        names += ["ipc+stripe", "ipc+fused+stripe"]
     return names
 
 
@@ -451,8 +452,10 @@ def preflight_candidates(args, n, on_gpu, transports, heat_spec, burgers_spec):
             grids[mkey] = [None if args.decomp == "slab" else args.decomp]
     models = {mkey: spec for mkey, spec, _, _ in heat_spec + burgers_spec}
 
-    def ok_for(m, p, t):  # striping and fused puts: slabs only
+    def ok_for(m, p, t):  # striping and fused puts: slabs only; both: the heat step only
         slab = p in (None, "slab") or tuple(p)[1:] == (1, 1)
+        if t == "ipc+fused+stripe":
+            return slab and m == "heat"
         return t not in ("ipc+stripe", "ipc+fused") or slab
     allc = [(m, p, t) for m in models for p in grids[m] for t in transports
             if ok_for(m, p, t)]
@@ -464,7 +467,8 @@ def preflight_candidates(args, n, on_gpu, transports, heat_spec, burgers_spec):
         # the newest transports last in their family: a family stops after two hangs, and
         # those then cost only the candidates behind them
         cs = sorted((c for c in allc if family(c[2]) == fam),
-                    key=lambda c: {"ipc+stripe": 1, "ipc+fused": 2}.get(c[2], 0))
+                    key=lambda c: {"ipc+stripe": 1, "ipc+fused": 2,
+                                   "ipc+fused+stripe": 3}.get(c[2], 0))
         if not cs:
             continue
         dl = STATE["deadline"]
@@ -558,6 +562,7 @@ def run(args) -> int:
     mlups = grid.cells * args.steps / secs / 1e6
     pg = solver.pgrid
     link = {"ipc": "ipc device puts", "ipc+fused": "ipc puts inside the step launches",
+            "ipc+fused+stripe": "ipc puts inside the step launches, striped over idle links",
             "rccl": "RCCL, boundary launch on the comm stream",
             "host": "host-staged", "rccl-plain": "RCCL, boundary launch after the interior",
             "ipc+stripe": "ipc device puts striped over idle links"}.get(transport, transport)

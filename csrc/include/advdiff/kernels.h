@@ -80,6 +80,15 @@ int advdiff_diffusion3d_step_box_ex(int dtype, const void* uin, void* uout, int 
 // [lo_k0, lo_k1) / [hi_k0, hi_k1) are also stored, system scope, into the peer planes at
 // dst_lo / dst_hi (IPC mappings of the neighbours' output fields: the peer plane of local
 // plane lo_k0 / hi_k0; same row pitch and plane stride).  Null / empty: no peer that side.
+// The general form (striped exchanges): part p's cells — planes [k0[p], k1[p]), rows
+// [y0[p], y1[p]) — to dst[p] + (k - k0[p]) pb[p] + the own in-plane byte offset; up to 6
+// parts, every receive box with this field's row pitch.
+int advdiff_diffusion3d_step_putv(int dtype, const void* uin, void* uout, int nx, int ny,
+                                  int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int zlo,
+                                  int zhi, int border, int order, double cx, double cy,
+                                  double cz, double dt, int nparts, void* const* dst,
+                                  const int* k0s, const int* k1s, const int* y0s,
+                                  const int* y1s, const int64_t* pb, void* stream);
 int advdiff_diffusion3d_step_put(int dtype, const void* uin, void* uout, int nx, int ny,
                                  int64_t sy, int64_t sz, int nz_alloc, int k0, int k1, int zlo,
                                  int zhi, int border, int order, double cx, double cy,

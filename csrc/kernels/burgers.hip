@@ -454,7 +454,7 @@ __device__ __forceinline__ T w5_combine6(T n1, T S1, T n2, T S2) {
 // vs 70 x 14 / (63 x 8) = 1.94).  wave_shr1 hands lane 32 the face of lane 31 — lane 32
 // is its row's face-only lane, so the DPP shift needs no change.
 // PUT (round 6, slab ranks, ipc transport): the stage's output planes inside put's ranges
-// are also stored into the neighbours' ghost planes (common.hpp halo_put) — one launch per
+// are also stored into the neighbours' ghost planes (common.hpp halo_put2) — one launch per
 // stage over every owned plane instead of interior + boundary + put launches.
 template <typename T, bool WZ, bool VISC, int MODE, int TXL = 64, bool PK = false,
           bool PUT = false>
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
     const T* __restrict__ in, T* aux, T* out, int nx, int ny, int64_t sy, int64_t sz, int k0,
     int k1, int k0b, int k1b, int gza, int zchunk, int border, T rdx3, T rdy3, T rdz6, T vx,
     T vy, T vz, T dt, T a, T b, const double* __restrict__ dtp, int xcdmap,
-    HaloPut put = HaloPut{}) {
+    HaloPut2 put = HaloPut2{}) {
   static_assert(TXL == 64 || TXL == 32, "tile row: 64 or 32 lanes");
   static_assert(!PK || std::is_same_v<T, float>, "packed pairs: fp32");
   static_assert(!(PK && PUT), "halo puts: one cell per lane");
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
       for (int k = kc0; k < kc1; ++k) {
         const T v = gld<T>(plane(in, k), goff);
         gst<T>(plane(out, k), goff, v);
-        if constexpr (PUT) halo_put<T>(put, k, szb, goff, v);
+        if constexpr (PUT) halo_put2<T>(put, k, szb, goff, v);
       }
     if constexpr (PUT) __builtin_amdgcn_s_waitcnt(0);
     return;
@@ -717,7 +717,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void b
     const V v = stage_value<V, MODE>(axk, ctr, L, V(dt), V(a), V(b), dnew);
     if (active) {
       gs(out, k, v);
-      if constexpr (PUT) halo_put<V>(put, k, szb, goff, v);
+      if constexpr (PUT) halo_put2<V>(put, k, szb, goff, v);
       if constexpr (MODE == kLs1 || MODE == kLs) gs(aux, k, dnew);
     }
     rp[sl(3)] = pn;  // f+(k+3), u(k+3) replace f+(k-2), u(k-2)
@@ -1092,7 +1092,7 @@ static int b3_tile_row(int nx, int ny, int border) {
 static int g_b3_zchunk = 0;
 
 template <typename T, bool WZ, bool VISC, int MODE, int TXL, bool PK = false, bool PUT = false>
-static hipError_t launch_b3_v9_tx(const BArgs& p, const HaloPut& put = HaloPut{}) {
+static hipError_t launch_b3_v9_tx(const BArgs& p, const HaloPut2& put = HaloPut2{}) {
   // XCD-contiguous tile order (always, its switch removed in round 6): 256^3 WENO5-Z +
   // viscous step 0.584 -> 0.564 ms (+3.7 %, 3 interleaved rounds, bitwise identical;
   // profiles/archive/burgers3d_xcd_r2.log)
@@ -1126,7 +1126,7 @@ static hipError_t launch_b3_v9_tx(const BArgs& p, const HaloPut& put = HaloPut{}
 
 // the stage with fused halo puts: fp64, WENO5 (JS / Z), SSP-RK3 epilogues, one range
 template <bool WZ, bool VISC, int MODE>
-static hipError_t launch_b3_put(const BArgs& p, const HaloPut& put) {
+static hipError_t launch_b3_put(const BArgs& p, const HaloPut2& put) {
   if (b3_tile_row(p.nx, p.ny, p.border) == 32)
     return launch_b3_v9_tx<double, WZ, VISC, MODE, 32, false, true>(p, put);
   return launch_b3_v9_tx<double, WZ, VISC, MODE, 64, false, true>(p, put);
@@ -1380,7 +1380,7 @@ extern "C" int advdiff_burgers3d_stage_put(int dtype, const void* in, void* aux,
   if (dtype != ADVDIFF_F64 || (weno != 0 && weno != 1) || k0 < 3 || border < 3 || nx <= 0 ||
       ny <= 0 || in == out || b3_ver() != 9 || !v9_fits<double>(p))
     return hipErrorInvalidValue;
-  HaloPut put{};
+  HaloPut2 put{};
   void* dsts[2] = {dst_lo, dst_hi};
   const int pk0[2] = {lo_k0, hi_k0}, pk1[2] = {lo_k1, hi_k1};
   for (int s = 0; s < 2; ++s) {

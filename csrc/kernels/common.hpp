@@ -720,26 +720,54 @@ __device__ __forceinline__ void gst(__amdgpu_buffer_rsrc_t r, uint32_t boff, T v
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)boff, 0, 0);
 }
 
-// Fused halo puts of a slab rank (ipc transport, round 6): the output planes [k0[s], k1[s])
-// of a launch are ALSO stored into a peer's ghost planes — dst[s] is the peer's plane for
-// local plane k0[s] (an IPC mapping of the peer's field with this field's row pitch and
-// plane stride), so the in-plane byte offset is the own one.  System-scope stores, as
-// ipc.hip's put kernel; the signal kernel after the launch publishes them.
+// Fused halo puts of a slab rank (ipc transport, round 6): the output planes [k0, k1) of a
+// launch, rows [y0, y1) of them, are ALSO stored into a peer — part p's cell (k, y, x)
+// goes to dst[p] + (k - k0[p]) pb[p] + the own in-plane byte offset of (y, x): dst[p] is
+// set up so that holds for the peer's receive box (the neighbour's ghost planes, or a
+// relay helper's row buffer of a striped exchange: then dst is offset by -y0 rows and pb
+// is the buffer's plane size; every receive box has this field's row pitch).  Up to
+// kHaloParts parts: the direct faces (2) or the striped ones (direct + helper parts per
+// face).  System-scope stores, as ipc.hip's put kernel; the signal kernel after the
+// launch publishes them.
+constexpr int kHaloParts = 6;
 struct HaloPut {
-  char* dst[2];
-  int k0[2], k1[2];
+  char* dst[kHaloParts];
+  int64_t pb[kHaloParts];
+  int k0[kHaloParts], k1[kHaloParts], y0[kHaloParts], y1[kHaloParts];
+  int n;  // parts in use
 };
-// The store: a buffer store on a scalar plane base (no 64-bit per-lane address — as a
-// flat pointer the loop-invariant part dst + off was hoisted into VGPRs and spilled) with
+// The store: a buffer store on a scalar base (no 64-bit per-lane address — as a flat
+// pointer the loop-invariant part dst + off was hoisted into VGPRs and spilled) with
 // cache policy sc0 sc1 (aux 1 | 16), the code gfx942's memory model gives a relaxed
 // system-scope atomic store: written through this XCD's L2 to the peer.
 constexpr int kSysScopeStore = 1 | 16;
 template <typename T>
-__device__ __forceinline__ void halo_put(const HaloPut& put, int k, int64_t plane_bytes,
-                                         uint32_t off, T v) {
+__device__ __forceinline__ void halo_put(const HaloPut& put, int k, int y, uint32_t off, T v) {
+#pragma unroll
+  for (int s = 0; s < kHaloParts; ++s)
+    if (s < put.n && k >= put.k0[s] && k < put.k1[s] && y >= put.y0[s] && y < put.y1[s]) {
+      const auto r = __builtin_amdgcn_make_buffer_rsrc(
+          put.dst[s] + (int64_t)(k - put.k0[s]) * put.pb[s], (short)0, -1, 0x00020000);
+      if constexpr (sizeof(T) == 8)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)off, 0,
+                                              kSysScopeStore);
+      else
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)off, 0,
+                                              kSysScopeStore);
+    }
+}
+// The direct two-face form (the WENO5 stage: the kernel is at its SGPR limit, and the six
+// row-ranged parts of HaloPut cost it VGPR spills): all rows, this field's plane stride.
+struct HaloPut2 {
+  char* dst[2];
+  int k0[2], k1[2];
+};
+template <typename T>
+__device__ __forceinline__ void halo_put2(const HaloPut2& put, int k, int64_t plane_bytes,
+                                          uint32_t off, T v) {
 #pragma unroll
   for (int s = 0; s < 2; ++s)
-    if (k >= put.k0[s] && k < put.k1[s]) {  // k is scalar: a scalar branch
+    if (k >= put.k0[s] && k < put.k1[s]) {
       const auto r = __builtin_amdgcn_make_buffer_rsrc(
           put.dst[s] + (int64_t)(k - put.k0[s]) * plane_bytes, (short)0, -1, 0x00020000);
       if constexpr (sizeof(T) == 8)
@@ -749,6 +777,24 @@ __device__ __forceinline__ void halo_put(const HaloPut& put, int k, int64_t plan
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)off, 0,
                                               kSysScopeStore);
     }
+}
+// host: a HaloPut of up to kHaloParts parts from arrays (null dst or empty range: skipped)
+inline bool make_halo_put(int n, void* const* dst, const int* k0, const int* k1, const int* y0,
+                          const int* y1, const int64_t* pb, int nz_alloc, HaloPut& out) {
+  out = HaloPut{};
+  if (n < 0 || n > kHaloParts) return false;
+  for (int s = 0; s < n; ++s) {
+    if (dst[s] == nullptr || k1[s] <= k0[s] || y1[s] <= y0[s]) continue;
+    if (k0[s] < 0 || k1[s] > nz_alloc || pb[s] <= 0) return false;
+    const int q = out.n++;
+    out.dst[q] = (char*)dst[s];
+    out.pb[q] = pb[s];
+    out.k0[q] = k0[s];
+    out.k1[q] = k1[s];
+    out.y0[q] = y0[s];
+    out.y1[q] = y1[s];
+  }
+  return true;
 }
 
 // keep a value computed on every lane (no exec-masked skip of the computation): the

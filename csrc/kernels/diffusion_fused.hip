@@ -372,7 +372,8 @@ __device__ __forceinline__ void v3_march(
     acc = pin(acc);
     if (m3[q]) gst<T>(plane_rsrc((char*)uout + (int64_t)kp * szb), goff[q], acc);
     if constexpr (PUT) {
-      if (m3[q]) halo_put<T>(put, kp, szb, goff[q], acc);  // kp scalar: scalar branches
+      // kp and the row are scalar: scalar branches
+      if (m3[q]) halo_put<T>(put, kp, aty.org + row_of(q), goff[q], acc);
     }
   };
   // the y-axis sum of stage 3 from the B plane of buffer set AO (LDS)
@@ -1481,26 +1482,27 @@ extern "C" int advdiff_diffusion3d_step(int dtype, const void* uin, void* uout, 
 // stored into the peer planes at dst_lo / dst_hi (the peer's plane for local plane lo_k0 /
 // hi_k0; null or an empty range: no peer on that side).  The peer fields must have this
 // field's row pitch and plane stride (slab ranks of one grid).  Uniform z chunks.
-extern "C" int advdiff_diffusion3d_step_put(int dtype, const void* uin, void* uout, int nx,
-                                            int ny, int64_t sy, int64_t sz, int nz_alloc, int k0,
-                                            int k1, int zlo, int zhi, int border, int order,
-                                            double cx, double cy, double cz, double dt,
-                                            void* dst_lo, int lo_k0, int lo_k1, void* dst_hi,
-                                            int hi_k0, int hi_k1, void* stream) {
+// One full-range slab step whose output planes also go, system scope, to peers: part p's
+// cells (planes [k0[p], k1[p]), rows [y0[p], y1[p])) to dst[p] + (k - k0[p]) pb[p] + the
+// own in-plane byte offset (common.hpp HaloPut; up to 6 parts; null dst / empty range:
+// skipped).  Every receive box has this field's row pitch.  Banded or uniform z chunks.
+extern "C" int advdiff_diffusion3d_step_putv(int dtype, const void* uin, void* uout, int nx,
+                                             int ny, int64_t sy, int64_t sz, int nz_alloc,
+                                             int k0, int k1, int zlo, int zhi, int border,
+                                             int order, double cx, double cy, double cz,
+                                             double dt, int nparts, void* const* dst,
+                                             const int* pk0, const int* pk1, const int* py0,
+                                             const int* py1, const int64_t* pb, void* stream) {
   using namespace advdiff;
   if (k1 <= k0) return hipSuccess;
   if (nx <= 0 || ny <= 0 || uin == uout || k0 < 0 || k1 > nz_alloc) return hipErrorInvalidValue;
   if (sy * (int64_t)ny >= (int64_t(1) << 31)) return hipErrorInvalidValue;
-  StepPut put{};
-  void* dsts[2] = {dst_lo, dst_hi};
-  const int pk0[2] = {lo_k0, hi_k0}, pk1[2] = {lo_k1, hi_k1};
-  for (int s = 0; s < 2; ++s) {
-    const bool on = dsts[s] != nullptr && pk1[s] > pk0[s];
-    if (on && (pk0[s] < 0 || pk1[s] > nz_alloc)) return hipErrorInvalidValue;
-    put.dst[s] = on ? (char*)dsts[s] : nullptr;
-    put.k0[s] = on ? pk0[s] : 0;
-    put.k1[s] = on ? pk1[s] : 0;
-  }
+  StepPut put;
+  if (nparts > 0 && (dst == nullptr || pk0 == nullptr || pk1 == nullptr || py0 == nullptr ||
+                     py1 == nullptr || pb == nullptr))
+    return hipErrorInvalidValue;
+  if (!make_halo_put(nparts, dst, pk0, pk1, py0, py1, pb, nz_alloc, put))
+    return hipErrorInvalidValue;
   const Box2 bx{border, nx - border, border, ny - border, 0, nx, 0, ny};
   const SArgs a{uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, 0, 0, zlo, zhi, bx,
                 cx, cy, cz, dt, (hipStream_t)stream};
@@ -1512,6 +1514,24 @@ extern "C" int advdiff_diffusion3d_step_put(int dtype, const void* uin, void* uo
     if (order == 2) return dispatch_step<float, 2, true>(a, put);
   }
   return hipErrorInvalidValue;
+}
+
+// The two-face form: output planes [lo_k0, lo_k1) / [hi_k0, hi_k1) to the peer planes at
+// dst_lo / dst_hi (the peer plane of local plane lo_k0 / hi_k0; all rows; this field's
+// plane stride).
+extern "C" int advdiff_diffusion3d_step_put(int dtype, const void* uin, void* uout, int nx,
+                                            int ny, int64_t sy, int64_t sz, int nz_alloc, int k0,
+                                            int k1, int zlo, int zhi, int border, int order,
+                                            double cx, double cy, double cz, double dt,
+                                            void* dst_lo, int lo_k0, int lo_k1, void* dst_hi,
+                                            int hi_k0, int hi_k1, void* stream) {
+  void* dst[2] = {dst_lo, dst_hi};
+  const int pk0[2] = {lo_k0, hi_k0}, pk1[2] = {lo_k1, hi_k1}, py0[2] = {0, 0};
+  const int py1[2] = {1 << 30, 1 << 30};
+  const int64_t esz = dtype == ADVDIFF_F64 ? 8 : 4, pb[2] = {sz * esz, sz * esz};
+  return advdiff_diffusion3d_step_putv(dtype, uin, uout, nx, ny, sy, sz, nz_alloc, k0, k1, zlo,
+                                       zhi, border, order, cx, cy, cz, dt, 2, dst, pk0, pk1,
+                                       py0, py1, pb, stream);
 }
 
 // Code-object preload (see advdiff_preload in aux.hip).

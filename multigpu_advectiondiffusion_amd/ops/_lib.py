@@ -55,6 +55,12 @@ _SIGS = {
                                         c_int, c_int, c_int, c_int, c_int, c_int,
                                         ctypes.POINTER(c_int), c_int, c_dbl, c_dbl, c_dbl,
                                         c_dbl, c_int, c_vp],
+    "advdiff_diffusion3d_step_putv": [c_int, c_vp, c_vp, c_int, c_int, c_i64, c_i64, c_int,
+                                      c_int, c_int, c_int, c_int, c_int, c_int, c_dbl, c_dbl,
+                                      c_dbl, c_dbl, c_int, ctypes.POINTER(c_vp),
+                                      ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                                      ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                                      ctypes.POINTER(c_i64), c_vp],
     "advdiff_diffusion3d_step_put": [c_int, c_vp, c_vp, c_int, c_int, c_i64, c_i64, c_int,
                                      c_int, c_int, c_int, c_int, c_int, c_int, c_dbl, c_dbl,
                                      c_dbl, c_dbl, c_vp, c_int, c_int, c_vp, c_int, c_int,

@@ -114,10 +114,13 @@ def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, 
     exclusive=True: nothing else runs on the GPU meanwhile (single rank / full-range
     launch) -> one round of persistent workgroups; False (an interior launch overlapping
     RCCL) keeps the dynamically balanced grid of z chunks.  Results are bit-identical.
-    put = ((dst_lo, lo_k0, lo_k1), (dst_hi, hi_k0, hi_k1)): the output planes [lo_k0, lo_k1)
-    / [hi_k0, hi_k1) are also stored at the peer addresses dst_lo / dst_hi (the peer plane
-    of local plane lo_k0 / hi_k0; 0 = no peer) — the ipc transport's fused halo puts
-    (advdiff_diffusion3d_step_put; one plane range, default box, native device fields)."""
+    put: the ipc transport's fused halo puts (one plane range, default box, native device
+    fields) — ((dst_lo, lo_k0, lo_k1), (dst_hi, hi_k0, hi_k1)): the output planes
+    [lo_k0, lo_k1) / [hi_k0, hi_k1) also go to the peer addresses dst_lo / dst_hi (the peer
+    plane of local plane lo_k0 / hi_k0; 0 = no peer; advdiff_diffusion3d_step_put); or a
+    list of parts (dst, k0, k1, y0, y1, plane_bytes): planes [k0, k1), rows [y0, y1) to
+    dst + (k - k0) plane_bytes + the own in-plane offset (striped exchanges;
+    advdiff_diffusion3d_step_putv, up to 6 parts)."""
     _check_layout(uin, uout)
     if uin.data_ptr() == uout.data_ptr():
         raise ValueError("the fused step needs distinct input/output buffers")
@@ -128,11 +131,23 @@ def diffusion3d_step(uin, uout, *, nx, ny, k0, k1, zlo, zhi, border, order, cx, 
         nz = uin.shape[0]
         assert 0 <= k0 and k1 <= nz and 0 <= zlo and zhi <= nz
         assert nx <= uin.shape[2] and ny <= uin.shape[1]
-        (dlo, lo0, lo1), (dhi, hi0, hi1) = put
-        code = lib.advdiff_diffusion3d_step_put(
-            _dtype_code(uin), _ptr(uin), _ptr(uout), nx, ny, uin.stride(1), uin.stride(0), nz,
-            k0, k1, zlo, zhi, border, order, cx, cy, cz, dt, dlo or None, lo0, lo1,
-            dhi or None, hi0, hi1, _stream_ptr(stream))
+        if len(put) == 2 and len(put[0]) == 3:  # the two-face form
+            (dlo, lo0, lo1), (dhi, hi0, hi1) = put
+            code = lib.advdiff_diffusion3d_step_put(
+                _dtype_code(uin), _ptr(uin), _ptr(uout), nx, ny, uin.stride(1), uin.stride(0),
+                nz, k0, k1, zlo, zhi, border, order, cx, cy, cz, dt, dlo or None, lo0, lo1,
+                dhi or None, hi0, hi1, _stream_ptr(stream))
+        else:
+            n = len(put)
+            if n > 6:
+                raise ValueError("fused halo puts: at most 6 parts")
+            arr = [list(col) for col in zip(*put)] if n else [[]] * 6
+            code = lib.advdiff_diffusion3d_step_putv(
+                _dtype_code(uin), _ptr(uin), _ptr(uout), nx, ny, uin.stride(1), uin.stride(0),
+                nz, k0, k1, zlo, zhi, border, order, cx, cy, cz, dt, n,
+                (ctypes.c_void_p * max(n, 1))(*arr[0]), _int_array(arr[1]),
+                _int_array(arr[2]), _int_array(arr[3]), _int_array(arr[4]),
+                (ctypes.c_int64 * max(n, 1))(*arr[5]), _stream_ptr(stream))
         _lib.check(code, "diffusion3d_step_put")
         return
     if box is None:

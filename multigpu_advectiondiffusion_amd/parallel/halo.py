@@ -70,16 +70,18 @@ def _order_after(cs, cur, after_event) -> None:
     cs.wait_event(after_event)
 
 
-def _start_ipc_routed(comm, comm_stream, phases, after_event=None, tag=None) -> PendingExchange:
+def _start_ipc_routed(comm, comm_stream, phases, after_event=None, tag=None,
+                      puts=None) -> PendingExchange:
     """Like _start_ipc for phases of one-way-capable routes: phases = [(channel, {peer:
     (send_view | None, recv_view | None)})], run in order on the comm stream; `tag`
-    keys the handshake cache (IpcPeers._resolve_pairs)."""
+    keys the handshake cache (IpcPeers._resolve_pairs); puts: per phase, whether its
+    sends are put here (False: the producing kernel stored them — fused puts)."""
     cur = torch.cuda.current_stream()
     cs = comm_stream or cur
     _order_after(cs, cur, after_event)
     ipc = comm.ipc()
-    for ch, pairs in phases:
-        ipc.route(pairs, cs, ch, tag)
+    for q, (ch, pairs) in enumerate(phases):
+        ipc.route(pairs, cs, ch, tag, puts=True if puts is None else puts[q])
     return _joinable(cs)
 
 
@@ -266,13 +268,41 @@ class SlabHalo:
         elif _ipc_on(self, field):
             self.comm.ipc()._resolve(self._ipc_msgs(field))
 
+    def put_parts(self, field: torch.Tensor) -> list:
+        """Fused halo puts of a striped exchange (ipc, 3-D; the next exchange's relay set,
+        self.parity): [(dst, k0, k1, y0, y1, plane_bytes)] — every channel-1 send box of
+        `field` (planes [k0, k1), rows [y0, y1): the direct part to a neighbour's ghost rows
+        and the relayed parts to the helpers' row buffers) with dst offset so that row y of
+        plane k lands at dst + (k - k0) plane_bytes + the own in-plane offset (each receive
+        box has this field's row pitch).  start(field, puts=False) then runs channel 1
+        without its puts and the helpers' forwards (channel 2) as usual."""
+        if not (_ipc_on(self, field) and self._use_stripes(field)):
+            raise ValueError("put_parts: the striped ipc exchange of a 3-D slab")
+        par = self.parity
+        p1, _ = self._stripe_phases(field, par)
+        dests = self.comm.ipc()._resolve_pairs(1, p1, self._tag(field, par))
+        e = field.element_size()
+        out = []
+        for peer, (send, _) in sorted(p1.items()):
+            if send is None:
+                continue
+            ptr, rsy, rsz = dests[peer]
+            if rsy != field.stride(1):
+                raise ValueError(f"fused halo puts: peer {peer} row pitch {rsy} != "
+                                 f"{field.stride(1)}")
+            off = send.storage_offset() - field.storage_offset()
+            k0, a = off // field.stride(0), (off % field.stride(0)) // field.stride(1)
+            out.append((ptr - a * rsy * e, k0, k0 + send.shape[0], a, a + send.shape[1],
+                        rsz * e))
+        return out
+
     def put_targets(self, field: torch.Tensor):
         """Fused halo puts (ipc, direct, 3-D): ((dst_lo, k0, k1), (dst_hi, k0, k1)) — the
         peer address of my send planes [k0, k1) of `field` towards the lower / upper
         neighbour (dst 0: no neighbour), for a step kernel that stores its output planes
         there itself (stencil.diffusion3d_step put=).  The peers' receive boxes must have
         this field's strides (slab ranks of one grid); start(field, puts=False) then only
-        signals and waits."""
+        signals and waits.  Striped exchanges: put_parts."""
         if not _ipc_on(self, field) or self._use_stripes(field) or field.dim() != 3:
             raise ValueError("fused halo puts: the direct ipc transport of a 3-D slab")
         msgs = self._ipc_msgs(field)
@@ -298,8 +328,15 @@ class SlabHalo:
         if self.comm.size == 1:
             return None
         if not puts:
-            if not _ipc_on(self, field) or self._use_stripes(field):
-                raise ValueError("puts=False: the direct ipc transport only")
+            if not _ipc_on(self, field):
+                raise ValueError("puts=False: the ipc transport only")
+            if self._use_stripes(field):  # channel 1 stored by the kernel, forwards as usual
+                par = self.parity
+                p1, p2 = self._stripe_phases(field, par)
+                self.parity ^= 1
+                return _start_ipc_routed(self.comm, self.comm_stream, [(1, p1), (2, p2)],
+                                         after_event, tag=self._tag(field, par),
+                                         puts=(False, True))
             return _start_ipc(self.comm, self.comm_stream, [self._ipc_msgs(field)],
                               after_event, puts=False)
         if _ipc_on(self, field) and self._use_stripes(field):

@@ -51,7 +51,8 @@ STRIPE = 2  # relay helpers per face message of the striped ipc slab exchange
 def transport_kwargs(t) -> dict:
     """Solver keyword arguments of a candidate transport name: "ipc+stripe" = ipc with
     relayed parts, "ipc+fused" = ipc with the halo puts inside the step launch (fused heat
-    step, slabs), "rccl+bc" = rccl with the boundary launch on the comm stream,
+    step, slabs), "ipc+fused+stripe" = both (the heat step's kernel stores the direct and
+    the relayed row parts), "rccl+bc" = rccl with the boundary launch on the comm stream,
     "rccl-plain" = rccl with the boundary launch after the interior on the compute
     stream (the pre-round-6 rccl default)."""
     if t is None:
@@ -60,6 +61,8 @@ def transport_kwargs(t) -> dict:
         return {"transport": "ipc", "stripe": STRIPE}
     if t == "ipc+fused":
         return {"transport": "ipc", "fused_put": True}
+    if t == "ipc+fused+stripe":
+        return {"transport": "ipc", "fused_put": True, "stripe": STRIPE}
     if t == "rccl+bc":
         return {"transport": "rccl", "boundary_on_comm": True}
     if t == "rccl-plain":

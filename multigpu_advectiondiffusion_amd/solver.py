@@ -287,11 +287,15 @@ class Solver:
             self.boundary = [blo, bhi]
         # fused halo puts: the step launch (fused heat step) or every stage launch (3-D
         # WENO5 fp64 SSP-RK3) stores the send planes into the peers itself
-        puts_fit = self.fused or (integrator == "ssprk3" and model.stage_put_ok(dtype))
+        # (striped exchanges: the fused heat step only — its kernel stores the direct and
+        # the relayed row parts, the helpers forward as usual)
+        puts_fit = self.fused or (integrator == "ssprk3" and model.stage_put_ok(dtype)
+                                  and not self.halo.striped)
         self.fput = bool(self._want_put and puts_fit and not self.cart and grid.dims == 3
                          and comm.size > 1 and self.transport == "ipc"
                          and self.device.type == "cuda" and kernel == "native"
-                         and exchange == "u" and not self._mr2 and not self.halo.striped)
+                         and exchange == "u" and not self._mr2)
+        self._primed = None  # striped fused puts: the ipc epoch whose relay sets are primed
         self._put_cache = {}
         if self.fput:
             self.bcomm = False
@@ -643,13 +647,27 @@ class Solver:
         land in them — the handshake in put_targets is pairwise, so the peer has drained
         too.  Never called for the first time inside a graph capture (_prepare_graph_halos
         resolves both fields before it)."""
-        key = (field.data_ptr(), self._ipc_epoch())
+        striped = self.halo.striped
+        key = (field.data_ptr(), self._ipc_epoch(), self.halo.parity if striped else None)
         t = self._put_cache.get(key)
         if t is None:
             torch.cuda.synchronize(self.device)
-            t = self.halo.put_targets(field)
+            t = self.halo.put_parts(field) if striped else self.halo.put_targets(field)
             self._put_cache[key] = t
         return t
+
+    def _prime_relays(self):
+        """Striped fused puts: the kernel stores only the OUTPUT cells of its send rows, and
+        the helpers forward whole rows, so every relay buffer must first hold the frozen
+        cells (Dirichlet borders, padding) of its rows: one ordinary striped exchange of u
+        per relay set, once per ipc epoch (collective; the ghost planes it writes already
+        hold those values).  Outside any graph capture (_prepare_graph_halos / first step)."""
+        if not (self.fput and self.halo.striped) or self._primed == self._ipc_epoch():
+            return
+        self.sync_halos()
+        for _ in range(2):  # both relay sets (the exchange parity alternates)
+            self.halo.start(self.u).wait()
+        self._primed = self._ipc_epoch()
 
     def _step_fused_put(self, dt: float, pend) -> None:
         """One launch over every owned plane whose boundary output planes also go straight
@@ -666,6 +684,8 @@ class Solver:
         the compute of every other workgroup."""
         if pend is not None:
             pend.wait()
+        if self.halo.striped and self._primed != self._ipc_epoch():
+            self._prime_relays()
         put = self._put_targets(self.un)
         with trace.range_("step+puts"):
             lo, hi = self.full
@@ -954,8 +974,12 @@ class Solver:
             for f in self.fields():
                 self.halo.prepare(f)
             if self.fput:
+                self._prime_relays()
                 for f in self.fields():
-                    self._put_targets(f)
+                    for _ in range(2 if self.halo.striped else 1):  # both relay sets
+                        self._put_targets(f)
+                        if self.halo.striped:
+                            self.halo.parity ^= 1
 
     def _graph_for(self, dt: float | None, t_end: float | None = None):
         """dt=None: a graph of device-dt (adaptive CFL) steps towards t_end."""

@@ -62,6 +62,10 @@ case "$1" in
     bash scripts/gpu_steps.sh r6/fput4 \
       "tests|600|ADVDIFF_STEP_BANDED=1 $PT tests/test_ipc_gpu.py -k 'fused_put'" \
       "ab|300|python -u bench/fused_put_ab.py" ;;
+  fput5)  # fused puts over the striped exchange: tests (4-5 ranks, shared links), N = 8 flow
+    bash scripts/gpu_steps.sh r6/fput5 \
+      "tests|600|$PT tests/test_ipc_gpu.py -k 'fused_put'" \
+      "reh8|600|$SH $R --nproc-per-node 8 --master-port 29608 bench.py --gpus 8 --steps 10 --warmup 3" ;;
   gap)  # the bench's Burgers window vs the rate tool: build path or thermal state
     bash scripts/gpu_steps.sh r6/burgers_gap "gap|300|python -u bench/burgers_bench_gap.py" ;;
   own)  # WENO5 v9 staging the own cell from the register column: kernel A/B (two builds in

@@ -80,3 +80,45 @@ def test_put_targets_plan(rank, size, monkeypatch):
                                 d, transport="ipc")
         with pytest.raises(ValueError):
             bad.put_targets(f)
+
+
+@pytest.mark.parametrize("rank", [0, 1, 2, 3])
+def test_put_parts_striped_plan(rank, monkeypatch):
+    """Striped fused puts: every channel-1 send box of the rank becomes one part — its
+    planes, its row range, the receive address shifted back by its first row (so the own
+    in-plane offset lands on row y - y0 of a helper's buffer), the receiver's plane size;
+    per face, the parts' rows partition the plane's rows."""
+    from multigpu_advectiondiffusion_amd.parallel.ipc import stripe_plan
+    monkeypatch.setattr(halo_mod, "_ipc_on", lambda h, f: True)
+    monkeypatch.setattr(halo_mod.SlabHalo, "_use_stripes", lambda h, f: h._plan is not None)
+    monkeypatch.setenv("ADVDIFF_STRIPE_SHARED", "1")
+    size = 4
+    d = SlabDecomposition(41, size, rank, 6)
+    f = torch.zeros((d.alloc, 20, 12), dtype=torch.float64)
+
+    class _Ipc:
+        def _resolve_pairs(self, ch, pairs, tag=None):
+            assert ch == 1
+            out = {}
+            for peer, (send, recv) in pairs.items():
+                if send is not None:  # a helper's buffer for a slice, else the ghost rows
+                    rsz = send.shape[1] * f.stride(1) if send.shape[1] != f.shape[1] else \
+                        f.stride(0)
+                    out[peer] = (10**6 * (peer + 1), f.stride(1), rsz)
+                else:
+                    out[peer] = None
+            return out
+    h = halo_mod.SlabHalo(_FakeComm(rank, size, _Ipc()), d, transport="ipc", stripe=2)
+    assert h._plan is not None and any(stripe_plan(size, 2, exclusive_links=False).values())
+    parts = h.put_parts(f)
+    e = f.element_size()
+    faces = {}
+    for dst, k0, k1, y0, y1, pb in parts:
+        assert (k0, k1) in (tuple(d.send_lower()), tuple(d.send_upper()))
+        assert (dst + y0 * f.stride(1) * e) % 10**6 == 0  # the receive address, shifted
+        faces.setdefault((k0, k1), []).append((y0, y1))
+    for rows in faces.values():
+        rows.sort()
+        assert rows[0][0] == 0 and rows[-1][1] == f.shape[1]
+        assert all(a[1] == b[0] for a, b in zip(rows, rows[1:]))
+    assert len(parts) <= 6

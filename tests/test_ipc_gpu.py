@@ -435,3 +435,31 @@ def test_native_fused_put_bitwise(tmp_path, app, args, shape, world, extra):
     a = np.fromfile(one, dtype=np.float32).reshape(shape)
     b = np.fromfile(many, dtype=np.float32).reshape(shape)
     assert np.isfinite(a).all() and np.array_equal(a, b), txt[-2000:]
+
+
+def _run_fused_striped(comm, kind, steps, graph):  # noqa: D103
+    model, grid, ic = _make(kind)
+    s = Solver(model, grid, comm, dtype=torch.float64, ic=ic, transport="ipc", stripe=2,
+               fused_put=True)
+    assert s.fput and s.halo.striped
+    s.run(iters=steps, graph=graph)
+    g = s.gather()
+    assert comm.ipc().errors() == 0
+    return None if g is None else g.copy()
+
+
+@pytest.mark.parametrize("kind", ["diff3", "diff3o2"])
+@pytest.mark.parametrize("world", [4, 5])
+def test_ipc_fused_put_striped_bitwise(kind, world, monkeypatch):
+    """Fused puts over the striped exchange ("ipc+fused+stripe"): the step kernel stores
+    its send rows' output cells straight into the neighbour's ghost rows (direct part) and
+    into the helpers' relay buffers (relayed parts; their frozen cells primed by one
+    ordinary exchange per relay set), the helpers forward as usual — eager and graph-
+    replayed, bitwise equal to one rank.  ADVDIFF_STRIPE_SHARED=1 gives 4-5 ranks
+    helpers."""
+    monkeypatch.setenv("ADVDIFF_STRIPE_SHARED", "1")
+    ref = _reference(kind, 17)
+    for graph in (False, True):
+        out = spawn_local(world, _run_fused_striped, kind, 17, graph, device="cuda",
+                          transport="ipc", timeout=240)[0]
+        assert np.array_equal(out, ref), (kind, world, graph, np.abs(out - ref).max())
