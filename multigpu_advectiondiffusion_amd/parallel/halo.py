@@ -127,6 +127,12 @@ class SlabHalo:
                                exclusive_links=os.environ.get("ADVDIFF_STRIPE_SHARED") != "1")
             if any(plan.values()):
                 self._plan = plan
+        # striped handshake tags carry the ipc epoch this halo was made in (every Solver on
+        # ipc resets the peers at construction, collectively): two striped solvers alive
+        # at once (bench.py tunes ipc+stripe and ipc+fused+stripe side by side) must not
+        # share a (field ordinal, parity) tag in the peers' address cache
+        ipc = getattr(comm, "ipc", None) if self._plan is not None else None
+        self._hid = getattr(ipc(), "epoch", 0) if ipc is not None else 0
 
     @property
     def striped(self) -> bool:
@@ -188,7 +194,7 @@ class SlabHalo:
     def _tag(self, field, parity):
         """Handshake key of a striped exchange that every rank derives alike: the field's
         ordinal (fields reach the halo in the same order on every rank) and the parity."""
-        return (self._fid.setdefault(field.data_ptr(), len(self._fid)), parity)
+        return (self._hid, self._fid.setdefault(field.data_ptr(), len(self._fid)), parity)
 
     def _ops(self, field: torch.Tensor):
         d = self.d

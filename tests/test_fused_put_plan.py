@@ -97,6 +97,8 @@ def test_put_parts_striped_plan(rank, monkeypatch):
     f = torch.zeros((d.alloc, 20, 12), dtype=torch.float64)
 
     class _Ipc:
+        epoch = 3
+
         def _resolve_pairs(self, ch, pairs, tag=None):
             assert ch == 1
             out = {}
@@ -122,3 +124,25 @@ def test_put_parts_striped_plan(rank, monkeypatch):
         assert rows[0][0] == 0 and rows[-1][1] == f.shape[1]
         assert all(a[1] == b[0] for a, b in zip(rows, rows[1:]))
     assert len(parts) <= 6
+
+
+def test_striped_tags_unique_per_solver(monkeypatch):
+    """Two striped solvers alive at once (the bench tunes ipc+stripe and ipc+fused+stripe
+    side by side) must not share a handshake tag: the tag carries the ipc epoch each was
+    made in (round-6 N = 8 rehearsal: "halo pattern (0, 0) with peer 1 changed its
+    boxes")."""
+    monkeypatch.setenv("ADVDIFF_STRIPE_SHARED", "1")
+
+    class _Ipc:
+        epoch = 0
+
+    ipc = _Ipc()
+    comm = _FakeComm(1, 4, ipc)
+    d = SlabDecomposition(41, 4, 1, 6)
+    f = torch.zeros((d.alloc, 20, 12), dtype=torch.float64)
+    ipc.epoch = 5
+    a = halo_mod.SlabHalo(comm, d, transport="ipc", stripe=2)
+    ipc.epoch = 6
+    b = halo_mod.SlabHalo(comm, d, transport="ipc", stripe=2)
+    assert a.striped and b.striped
+    assert a._tag(f, 0) != b._tag(f, 0) and a._tag(f, 0) == a._tag(f, 0)
