@@ -289,8 +289,9 @@ class Solver:
         # WENO5 fp64 SSP-RK3) stores the send planes into the peers itself
         # (striped exchanges: the fused heat step only — its kernel stores the direct and
         # the relayed row parts, the helpers forward as usual)
+        striped = getattr(self.halo, "striped", False)  # SlabHalo only
         puts_fit = self.fused or (integrator == "ssprk3" and model.stage_put_ok(dtype)
-                                  and not self.halo.striped)
+                                  and not striped)
         self.fput = bool(self._want_put and puts_fit and not self.cart and grid.dims == 3
                          and comm.size > 1 and self.transport == "ipc"
                          and self.device.type == "cuda" and kernel == "native"
